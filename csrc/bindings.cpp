@@ -1,0 +1,449 @@
+// pybind11 surface of ddp_amd._C: adapts at::Tensor to the raw-pointer kernel /
+// runtime API.  Every op validates device, dtype, contiguity and shape before it
+// launches (a wrong shape on a hand-written kernel is an out-of-bounds access on
+// the GPU), and launches on torch's current HIP stream unless stated otherwise.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <optional>
+
+#include "kernels/launchers.h"
+#include "runtime/runtime.h"
+
+namespace py = pybind11;
+using at::Tensor;
+using namespace ddp_amd;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check(const Tensor& t, const char* name, at::ScalarType st) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+}
+bf16_t* bf(const Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+const bf16_t* cbf(const Tensor& t) { return reinterpret_cast<const bf16_t*>(t.data_ptr()); }
+const bf16_t* obf(const std::optional<Tensor>& t, const char* name) {
+  if (!t) return nullptr;
+  check(*t, name, at::kBFloat16);
+  return cbf(*t);
+}
+
+BatchIdx make_bi(const std::optional<Tensor>& idx, const std::optional<Tensor>& ctr, int stride,
+                 int offset, long n_rows = 0x7fffffff) {
+  BatchIdx bi{nullptr, nullptr, stride, offset};
+  bi.n_rows = (int)std::min<long>(n_rows, 0x7fffffff);
+  if (idx) {
+    check(*idx, "idx", at::kInt);
+    bi.idx = idx->data_ptr<int>();
+    bi.n_idx = (int)idx->numel();
+    TORCH_CHECK(bi.n_idx > 0, "empty index list");
+  }
+  if (ctr) { check(*ctr, "step_ctr", at::kInt); bi.step_ctr = ctr->data_ptr<int>(); }
+  return bi;
+}
+
+void kcheck() {
+  hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, "kernel launch failed: ", hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------ ops
+void op_conv1_fwd(const Tensor& x, std::optional<Tensor> idx, std::optional<Tensor> ctr, int stride,
+                  int offset, const Tensor& w, const Tensor& b, Tensor& y, int B, int H, int W) {
+  check_cuda(x, "x");
+  const bool u8 = x.scalar_type() == at::kByte;
+  TORCH_CHECK(u8 || x.scalar_type() == at::kFloat, "x must be uint8 or float32");
+  check(w, "w", at::kFloat); check(b, "b", at::kFloat); check(y, "y", at::kBFloat16);
+  const int Cout = (int)b.numel();
+  TORCH_CHECK(Cout % 8 == 0 && 256 % (Cout / 8) == 0, "conv1: Cout must be 8..256, power of two");
+  TORCH_CHECK(w.numel() == (long)Cout * 9, "conv1: weight must be [Cout,1,3,3]");
+  TORCH_CHECK(y.numel() == (long)B * H * W * Cout, "conv1: bad output size");
+  if (!u8) {
+    TORCH_CHECK(x.numel() >= (long)B * H * W, "conv1: input too small");
+  } else {
+    TORCH_CHECK(x.numel() % ((long)H * W) == 0, "conv1: dataset must be [N,H,W]");
+  }
+  conv1_fwd(x.data_ptr(), u8, make_bi(idx, ctr, stride, offset, x.numel() / ((long)H * W)), w.data_ptr<float>(),
+            b.data_ptr<float>(), bf(y), B, H, W, Cout, cur_stream());
+  kcheck();
+}
+
+void op_conv1_wgrad(const Tensor& x, std::optional<Tensor> idx, std::optional<Tensor> ctr,
+                    int stride, int offset, const Tensor& dy, std::optional<Tensor> yact,
+                    Tensor& slab, int B, int H, int W, int Cout, int chunk) {
+  check_cuda(x, "x");
+  const bool u8 = x.scalar_type() == at::kByte;
+  check(dy, "dy", at::kBFloat16); check(slab, "slab", at::kFloat);
+  TORCH_CHECK(dy.numel() == (long)B * H * W * Cout, "conv1_wgrad: bad dy size");
+  TORCH_CHECK(Cout * 10 <= 320 * 4, "conv1_wgrad: Cout too large");
+  TORCH_CHECK(slab.numel() >= (long)conv1_wgrad_blocks(B, H, W, chunk) * Cout * 10, "slab too small");
+  conv1_wgrad(x.data_ptr(), u8, make_bi(idx, ctr, stride, offset, x.numel() / ((long)H * W)), cbf(dy), obf(yact, "yact"),
+              slab.data_ptr<float>(), B, H, W, Cout, chunk, cur_stream());
+  kcheck();
+}
+
+void op_conv3x3_fwd(const Tensor& X, const Tensor& Wt, const Tensor& bias, Tensor& Y, bool relu,
+                    std::optional<Tensor> wfc, std::optional<Tensor> fc_part, int NO, int pxt) {
+  check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(bias, "bias", at::kFloat);
+  check(Y, "Y", at::kBFloat16);
+  TORCH_CHECK(X.dim() == 4 && Y.dim() == 4, "conv3x3_fwd: X, Y must be NHWC 4-d");
+  const int B = X.size(0), H = X.size(1), W = X.size(2), Cin = X.size(3), Cout = Y.size(3);
+  TORCH_CHECK(Y.size(0) == B && Y.size(1) == H && Y.size(2) == W, "conv3x3_fwd: Y shape");
+  TORCH_CHECK(Cin % 32 == 0 && Cout % 64 == 0, "conv3x3_fwd: Cin%32, Cout%64 required");
+  TORCH_CHECK(Wt.numel() == (long)Cout * 9 * Cin && bias.numel() == Cout, "conv3x3_fwd: weight shape");
+  TORCH_CHECK(pxt == 1 || pxt == 2, "pxt must be 1 or 2");
+  const bf16_t* wf = nullptr;
+  float* part = nullptr;
+  if (wfc) {
+    check(*wfc, "wfc", at::kBFloat16);
+    TORCH_CHECK(fc_part.has_value(), "fc_part required with wfc");
+    check(*fc_part, "fc_part", at::kFloat);
+    TORCH_CHECK(Cout == 64 && (H * W) % 16 == 0 && NO <= 16, "fused fc: Cout==64, HW%16==0, NO<=16");
+    TORCH_CHECK(wfc->numel() == (long)NO * H * W * Cout, "fused fc: wfc shape");
+    TORCH_CHECK(fc_part->numel() >= (long)B * (H * W / 16) * NO, "fused fc: fc_part too small");
+    wf = cbf(*wfc);
+    part = fc_part->data_ptr<float>();
+  }
+  conv3x3_fwd(cbf(X), cbf(Wt), bias.data_ptr<float>(), bf(Y), B, H, W, Cin, Cout, relu, wf, part,
+              NO, pxt, cur_stream());
+  kcheck();
+}
+
+void op_conv3x3_dgrad(const Tensor& dY, std::optional<Tensor> Yact, const Tensor& WT,
+                      std::optional<Tensor> Xact, Tensor& dX, int pxt) {
+  check(dY, "dY", at::kBFloat16); check(WT, "WT", at::kBFloat16); check(dX, "dX", at::kBFloat16);
+  TORCH_CHECK(dY.dim() == 4 && dX.dim() == 4, "conv3x3_dgrad: NHWC 4-d");
+  const int B = dY.size(0), H = dY.size(1), W = dY.size(2), Cout = dY.size(3), Cin = dX.size(3);
+  TORCH_CHECK(dX.size(0) == B && dX.size(1) == H && dX.size(2) == W, "conv3x3_dgrad: dX shape");
+  TORCH_CHECK(Cin % 32 == 0 && Cout % 32 == 0, "conv3x3_dgrad: Cin%32, Cout%32 required");
+  TORCH_CHECK(WT.numel() == (long)Cout * 9 * Cin, "conv3x3_dgrad: WT shape");
+  if (Yact) TORCH_CHECK(Yact->sizes() == dY.sizes(), "Yact shape");
+  if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
+  BatchIdx bi{nullptr, nullptr, 0, 0};
+  conv3x3_dgrad(cbf(dY), obf(Yact, "Yact"), cbf(WT), obf(Xact, "Xact"), bf(dX), B, H, W, Cin, Cout,
+                nullptr, false, bi, nullptr, pxt, cur_stream());
+  kcheck();
+}
+
+void op_conv3x3_dgrad_fused_w1(const Tensor& dY, const Tensor& WT, const Tensor& Xact, Tensor& dX,
+                               const Tensor& x0, std::optional<Tensor> idx,
+                               std::optional<Tensor> ctr, int stride, int offset, Tensor& w1slab,
+                               int pxt) {
+  check(dY, "dY", at::kBFloat16); check(WT, "WT", at::kBFloat16); check(dX, "dX", at::kBFloat16);
+  check(Xact, "Xact", at::kBFloat16); check(w1slab, "w1slab", at::kFloat); check_cuda(x0, "x0");
+  const int B = dY.size(0), H = dY.size(1), W = dY.size(2), Cout = dY.size(3), Cin = dX.size(3);
+  TORCH_CHECK(Cin == 32, "fused conv1 wgrad requires Cin == 32");
+  TORCH_CHECK(WT.numel() == (long)Cout * 9 * Cin && Xact.sizes() == dX.sizes(), "shapes");
+  TORCH_CHECK(w1slab.numel() >= (long)conv3x3_dgrad_blocks(B, H, W, pxt) * 320, "w1slab too small");
+  const bool u8 = x0.scalar_type() == at::kByte;
+  conv3x3_dgrad(cbf(dY), nullptr, cbf(WT), cbf(Xact), bf(dX), B, H, W, Cin, Cout, x0.data_ptr(), u8,
+                make_bi(idx, ctr, stride, offset, x0.numel() / ((long)H * W)), w1slab.data_ptr<float>(), pxt, cur_stream());
+  kcheck();
+}
+
+void op_conv3x3_wgrad(const Tensor& dY, std::optional<Tensor> Yact, const Tensor& X, Tensor& slab,
+                      int R) {
+  check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(slab, "slab", at::kFloat);
+  const int B = dY.size(0), H = dY.size(1), W = dY.size(2), Cout = dY.size(3), Cin = X.size(3);
+  TORCH_CHECK(X.size(0) == B && X.size(1) == H && X.size(2) == W, "conv3x3_wgrad: X shape");
+  TORCH_CHECK(Cout % 32 == 0 && Cin % 16 == 0 && ((Cout / 32) * (Cin / 16)) % 4 == 0,
+              "conv3x3_wgrad: unsupported channel counts");
+  TORCH_CHECK(R >= 1 && R <= H, "conv3x3_wgrad: bad row chunk");
+  TORCH_CHECK(conv3x3_wgrad_lds(W, Cin, Cout, R) <= 160 * 1024, "conv3x3_wgrad: LDS too large");
+  TORCH_CHECK(slab.numel() >= (long)conv3x3_wgrad_blocks(B, H, R) * ((long)Cout * 9 * Cin + Cout),
+              "conv3x3_wgrad: slab too small");
+  if (Yact) TORCH_CHECK(Yact->sizes() == dY.sizes(), "Yact shape");
+  conv3x3_wgrad(cbf(dY), obf(Yact, "Yact"), cbf(X), slab.data_ptr<float>(), B, H, W, Cin, Cout, R,
+                cur_stream());
+  kcheck();
+}
+
+void op_fc_partial(const Tensor& X, const Tensor& Wf, Tensor& part) {
+  check(X, "X", at::kBFloat16); check(Wf, "Wf", at::kBFloat16); check(part, "part", at::kFloat);
+  TORCH_CHECK(X.dim() == 4, "fc_partial: X must be NHWC");
+  const int B = X.size(0), HW = X.size(1) * X.size(2), C = X.size(3);
+  TORCH_CHECK(HW % 16 == 0 && C % 8 == 0, "fc_partial: HW%16, C%8");
+  const int NO = (int)(Wf.numel() / ((long)HW * C));
+  TORCH_CHECK((long)NO * HW * C == Wf.numel() && NO <= 16, "fc_partial: weight shape");
+  TORCH_CHECK(part.numel() >= (long)B * (HW / 16) * NO, "fc_partial: part too small");
+  fc_partial(cbf(X), cbf(Wf), part.data_ptr<float>(), B, HW, C, NO, cur_stream());
+  kcheck();
+}
+
+void op_fc_reduce(const Tensor& part, std::optional<Tensor> bias, Tensor& out, int B, int G, int NO) {
+  check(part, "part", at::kFloat); check(out, "out", at::kFloat);
+  TORCH_CHECK(part.numel() >= (long)B * G * NO && out.numel() >= (long)B * NO, "fc_reduce sizes");
+  const float* bp = nullptr;
+  if (bias) { check(*bias, "bias", at::kFloat); bp = bias->data_ptr<float>(); }
+  fc_reduce(part.data_ptr<float>(), bp, out.data_ptr<float>(), B, G, NO, cur_stream());
+  kcheck();
+}
+
+void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, Tensor& dW,
+               double scale, bool mask) {
+  check(dL, "dL", at::kFloat); check(X, "X", at::kBFloat16); check(Wf, "Wf", at::kBFloat16);
+  check(dX, "dX", at::kBFloat16); check(dW, "dW", at::kFloat);
+  const int B = dL.size(0), NO = dL.size(1);
+  const long K = X.numel() / B;
+  TORCH_CHECK(X.numel() == (long)B * K && dX.numel() == X.numel(), "fc_bwd: X/dX shape");
+  TORCH_CHECK(Wf.numel() == (long)NO * K && dW.numel() == Wf.numel() && NO <= 16, "fc_bwd: W shape");
+  TORCH_CHECK((long)B * NO * 4 <= 64 * 1024, "fc_bwd: batch too large for LDS");
+  fc_bwd(dL.data_ptr<float>(), cbf(X), cbf(Wf), bf(dX), dW.data_ptr<float>(), (float)scale, B, K,
+         NO, mask, cur_stream());
+  kcheck();
+}
+
+void op_xent(const Tensor& part, int G, std::optional<Tensor> bias, const Tensor& labels,
+             std::optional<Tensor> logits_out, Tensor& dlogits, Tensor& loss_out,
+             std::optional<Tensor> dbias, double gscale, double dbias_scale) {
+  check(part, "part", at::kFloat); check(dlogits, "dlogits", at::kFloat);
+  check(loss_out, "loss_out", at::kFloat);
+  const int B = dlogits.size(0), C = dlogits.size(1);
+  TORCH_CHECK(C <= 1024, "xent: at most 1024 classes");
+  TORCH_CHECK(part.numel() >= (long)B * G * C, "xent: partials too small");
+  check_cuda(labels, "labels");
+  TORCH_CHECK(labels.numel() == B, "xent: labels size");
+  const long long* l64 = nullptr;
+  const int* l32 = nullptr;
+  if (labels.scalar_type() == at::kLong) l64 = reinterpret_cast<const long long*>(labels.data_ptr());
+  else { TORCH_CHECK(labels.scalar_type() == at::kInt, "labels int32/int64"); l32 = labels.data_ptr<int>(); }
+  const float* bp = nullptr;
+  if (bias) { check(*bias, "bias", at::kFloat); bp = bias->data_ptr<float>(); }
+  float* lo = nullptr;
+  if (logits_out) { check(*logits_out, "logits_out", at::kFloat); lo = logits_out->data_ptr<float>(); }
+  float* db = nullptr;
+  if (dbias) { check(*dbias, "dbias", at::kFloat); db = dbias->data_ptr<float>(); }
+  BatchIdx bi{nullptr, nullptr, 0, 0};
+  xent(part.data_ptr<float>(), G, bp, C, B, l64, l32, bi, lo, dlogits.data_ptr<float>(),
+       loss_out.data_ptr<float>(), db, (float)gscale, (float)dbias_scale, cur_stream());
+  kcheck();
+}
+
+ShadowSet make_shadows(const py::list& shadows) {
+  ShadowSet sh{};
+  TORCH_CHECK((int)shadows.size() <= MAX_SHADOWS, "too many shadow regions");
+  for (auto item : shadows) {
+    auto t = item.cast<py::tuple>();  // (off, n, dst bf16 tensor, kind, a, b, c)
+    Tensor dst = t[2].cast<Tensor>();
+    check(dst, "shadow dst", at::kBFloat16);
+    const long n = t[1].cast<long>();
+    TORCH_CHECK(dst.numel() == n, "shadow dst size mismatch");
+    sh.r[sh.count++] = ShadowRegion{t[0].cast<long>(), n, bf(dst), t[3].cast<int>(), t[4].cast<int>(),
+                                    t[5].cast<int>(), t[6].cast<int>()};
+  }
+  return sh;
+}
+
+void op_sgd(Tensor& p, const Tensor& g, std::optional<Tensor> mbuf, double lr, double momentum,
+            double dampening, double wd, bool nesterov, bool maximize, bool first_step, bool update,
+            const py::list& shadows) {
+  check(p, "params", at::kFloat); check(g, "grads", at::kFloat);
+  TORCH_CHECK(p.numel() == g.numel(), "sgd: param/grad size mismatch");
+  float* mb = nullptr;
+  if (momentum != 0.0) {
+    TORCH_CHECK(mbuf.has_value(), "sgd: momentum buffer required");
+    check(*mbuf, "momentum", at::kFloat);
+    TORCH_CHECK(mbuf->numel() == p.numel(), "sgd: momentum size");
+    mb = mbuf->data_ptr<float>();
+  }
+  SgdArgs a{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, maximize,
+            first_step, update};
+  const ShadowSet sh = make_shadows(shadows);
+  for (int r = 0; r < sh.count; ++r)
+    TORCH_CHECK(sh.r[r].off >= 0 && sh.r[r].off + sh.r[r].n <= p.numel(), "shadow out of range");
+  sgd_step(p.data_ptr<float>(), g.data_ptr<float>(), mb, p.numel(), a, sh, nullptr, cur_stream());
+  kcheck();
+}
+
+void op_grad_reduce(const py::list& segs) {
+  SlabSet ss{};
+  TORCH_CHECK(segs.size() <= 4, "at most 4 slab segments");
+  for (auto item : segs) {
+    auto t = item.cast<py::tuple>();  // (slab, row_stride, src_off, n, rows, dst, scale)
+    Tensor slab = t[0].cast<Tensor>(), dst = t[5].cast<Tensor>();
+    check(slab, "slab", at::kFloat);
+    TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst");
+    const long rs = t[1].cast<long>(), so = t[2].cast<long>(), n = t[3].cast<long>();
+    const int rows = t[4].cast<int>();
+    TORCH_CHECK(dst.numel() == n, "grad_reduce: dst size");
+    TORCH_CHECK(rows >= 1 && so + n <= rs && (long)(rows - 1) * rs + so + n <= slab.numel(),
+                "grad_reduce: slab bounds");
+    ss.s[ss.count++] = SlabSeg{slab.data_ptr<float>(), rs, so, n, rows, dst.data_ptr<float>(),
+                               (float)t[6].cast<double>()};
+  }
+  grad_reduce(ss, cur_stream());
+  kcheck();
+}
+
+void op_scale_copy(Tensor& dst, const Tensor& src, double scale) {
+  check(dst, "dst", at::kFloat); check(src, "src", at::kFloat);
+  TORCH_CHECK(dst.numel() == src.numel(), "scale_copy: size");
+  scale_copy(dst.data_ptr<float>(), src.data_ptr<float>(), dst.numel(), (float)scale, cur_stream());
+  kcheck();
+}
+
+int dtype_code(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kInt: return 2;
+    case at::kLong: return 3;
+    case at::kByte: return 4;
+    default: TORCH_CHECK(false, "unsupported dtype for RCCL: ", t.scalar_type());
+  }
+  return -1;
+}
+
+hipStream_t stream_or_current(uint64_t s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : cur_stream();
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "ddp_amd native gfx950 kernels + RCCL runtime";
+  m.def("conv1_fwd", &op_conv1_fwd);
+  m.def("conv1_wgrad", &op_conv1_wgrad);
+  m.def("conv1_wgrad_blocks", &conv1_wgrad_blocks);
+  m.def("conv3x3_fwd", &op_conv3x3_fwd);
+  m.def("conv3x3_dgrad", &op_conv3x3_dgrad);
+  m.def("conv3x3_dgrad_fused_w1", &op_conv3x3_dgrad_fused_w1);
+  m.def("conv3x3_dgrad_blocks", &conv3x3_dgrad_blocks);
+  m.def("conv3x3_wgrad", &op_conv3x3_wgrad);
+  m.def("conv3x3_wgrad_blocks", &conv3x3_wgrad_blocks);
+  m.def("fc_partial", &op_fc_partial);
+  m.def("fc_reduce", &op_fc_reduce);
+  m.def("fc_bwd", &op_fc_bwd);
+  m.def("xent", &op_xent);
+  m.def("sgd", &op_sgd);
+  m.def("grad_reduce", &op_grad_reduce);
+  m.def("scale_copy", &op_scale_copy);
+  m.def("rccl_version", []() { int v = 0; ncclGetVersion(&v); return v; });
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def_static("new_unique_id", []() { return py::bytes(Comm::new_unique_id()); })
+      .def(py::init([](py::bytes uid, int rank, int world, int device) {
+             return std::make_shared<Comm>(std::string(uid), rank, world, device);
+           }))
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def("all_reduce", [](Comm& c, Tensor& t, int op, uint64_t stream) {
+             check_cuda(t, "tensor");
+             c.all_reduce(t.data_ptr(), t.numel(), dtype_code(t), op, stream_or_current(stream));
+           }, py::arg("tensor"), py::arg("op") = 0, py::arg("stream") = 0)
+      .def("broadcast", [](Comm& c, Tensor& t, int root, uint64_t stream) {
+             check_cuda(t, "tensor");
+             c.broadcast(t.data_ptr(), t.numel(), dtype_code(t), root, stream_or_current(stream));
+           }, py::arg("tensor"), py::arg("root") = 0, py::arg("stream") = 0)
+      .def("all_gather", [](Comm& c, const Tensor& send, Tensor& recv, uint64_t stream) {
+             check_cuda(send, "send"); check_cuda(recv, "recv");
+             TORCH_CHECK(recv.numel() == send.numel() * c.world(), "all_gather: recv size");
+             c.all_gather(send.data_ptr(), recv.data_ptr(), send.numel(), dtype_code(send),
+                          stream_or_current(stream));
+           }, py::arg("send"), py::arg("recv"), py::arg("stream") = 0)
+      .def("reduce_scatter", [](Comm& c, const Tensor& send, Tensor& recv, int op, uint64_t stream) {
+             check_cuda(send, "send"); check_cuda(recv, "recv");
+             TORCH_CHECK(send.numel() == recv.numel() * c.world(), "reduce_scatter: send size");
+             c.reduce_scatter(send.data_ptr(), recv.data_ptr(), recv.numel(), dtype_code(recv), op,
+                              stream_or_current(stream));
+           }, py::arg("send"), py::arg("recv"), py::arg("op") = 0, py::arg("stream") = 0);
+
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init([](std::shared_ptr<Comm> comm, Tensor& flat, std::vector<long> poff,
+                       std::vector<long> pnum, std::vector<int> pb, std::vector<long> boff,
+                       std::vector<long> bnum, bool prescale) {
+             check(flat, "flat_grad", at::kFloat);
+             for (size_t i = 0; i < poff.size(); ++i)
+               TORCH_CHECK(poff[i] >= 0 && poff[i] + pnum[i] <= flat.numel(), "param slot OOB");
+             for (size_t i = 0; i < boff.size(); ++i)
+               TORCH_CHECK(boff[i] >= 0 && boff[i] + bnum[i] <= flat.numel(), "bucket OOB");
+             return std::make_shared<Reducer>(comm, flat.data_ptr<float>(), poff, pnum, pb, boff,
+                                              bnum, prescale);
+           }))
+      .def("mark_ready", [](Reducer& r, int param, std::optional<Tensor> grad) {
+             const float* src = nullptr;
+             if (grad) { check(*grad, "grad", at::kFloat); src = grad->data_ptr<float>(); }
+             r.mark_ready(param, src, cur_stream());
+           })
+      .def("finalize", [](Reducer& r) { r.finalize(cur_stream()); })
+      .def("reset", &Reducer::reset)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets)
+      .def_property_readonly("allreduce_calls", &Reducer::allreduce_calls);
+
+  py::class_<SimpleCNNEngine, std::shared_ptr<SimpleCNNEngine>>(m, "SimpleCNNEngine")
+      .def(py::init([](py::dict cfgd, py::dict t, py::dict offs, std::shared_ptr<Comm> comm) {
+             EngineConfig c{};
+             c.max_batch = cfgd["max_batch"].cast<int>();
+             c.H = cfgd["H"].cast<int>(); c.W = cfgd["W"].cast<int>();
+             c.C1 = cfgd["C1"].cast<int>(); c.C2 = cfgd["C2"].cast<int>(); c.NO = cfgd["NO"].cast<int>();
+             c.pxt_fwd = cfgd["pxt_fwd"].cast<int>(); c.pxt_dgrad = cfgd["pxt_dgrad"].cast<int>();
+             c.wgrad_rows = cfgd["wgrad_rows"].cast<int>();
+             c.world = cfgd["world"].cast<int>(); c.rank = cfgd["rank"].cast<int>();
+             c.lr = cfgd["lr"].cast<float>(); c.momentum = cfgd["momentum"].cast<float>();
+             c.dampening = cfgd["dampening"].cast<float>();
+             c.weight_decay = cfgd["weight_decay"].cast<float>();
+             c.nesterov = cfgd["nesterov"].cast<bool>(); c.maximize = cfgd["maximize"].cast<bool>();
+             auto T = [&](const char* k) { return t[k].cast<Tensor>(); };
+             auto need = [&](const char* k, at::ScalarType st, long n) {
+               Tensor x = T(k);
+               check(x, k, st);
+               TORCH_CHECK(x.numel() >= n, "engine buffer ", k, " too small: ", x.numel(), " < ", n);
+               return x;
+             };
+             const long B = c.max_batch, HW = (long)c.H * c.W;
+             EngineBuffers b{};
+             Tensor params = need("params", at::kFloat, 1);
+             b.params = params.data_ptr<float>();
+             b.n_params = params.numel();
+             b.grads = need("grads", at::kFloat, b.n_params).data_ptr<float>();
+             b.momentum = (c.momentum != 0.f) ? need("momentum", at::kFloat, b.n_params).data_ptr<float>() : nullptr;
+             auto O = [&](const char* k) { return offs[k].cast<long>(); };
+             b.off_w1 = O("w1"); b.off_b1 = O("b1"); b.off_w2 = O("w2"); b.off_b2 = O("b2");
+             b.off_wfc = O("wfc"); b.off_bfc = O("bfc");
+             b.bucket0_off = O("bucket0_off"); b.bucket0_n = O("bucket0_n");
+             b.bucket1_off = O("bucket1_off"); b.bucket1_n = O("bucket1_n");
+             TORCH_CHECK(b.off_wfc + (long)c.NO * HW * c.C2 <= b.n_params && b.off_w1 + 9L * c.C1 <= b.n_params &&
+                         b.bucket0_off + b.bucket0_n <= b.n_params && b.bucket1_off + b.bucket1_n <= b.n_params,
+                         "engine: parameter offsets out of range");
+             b.w2_bf16 = bf(need("w2_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
+             b.w2t_bf16 = bf(need("w2t_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
+             b.wfc_bf16 = bf(need("wfc_bf16", at::kBFloat16, (long)c.NO * HW * c.C2));
+             b.a1 = bf(need("a1", at::kBFloat16, B * HW * c.C1));
+             b.a2 = bf(need("a2", at::kBFloat16, B * HW * c.C2));
+             b.dz2 = bf(need("dz2", at::kBFloat16, B * HW * c.C2));
+             b.dz1 = bf(need("dz1", at::kBFloat16, B * HW * c.C1));
+             b.fc_part = need("fc_part", at::kFloat, B * (HW / 16) * c.NO).data_ptr<float>();
+             b.dlogits = need("dlogits", at::kFloat, B * c.NO).data_ptr<float>();
+             b.loss_hist = need("loss_hist", at::kFloat, 1).data_ptr<float>();
+             b.w2slab = need("w2slab", at::kFloat, (long)conv3x3_wgrad_blocks(B, c.H, c.wgrad_rows) * (9L * c.C1 * c.C2 + c.C2)).data_ptr<float>();
+             b.w1slab = need("w1slab", at::kFloat, (long)conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_dgrad) * 320).data_ptr<float>();
+             b.step_ctr = need("step_ctr", at::kInt, 1).data_ptr<int>();
+             Tensor images = need("images", at::kByte, HW);
+             b.images = images.data_ptr<unsigned char>();
+             Tensor labels = need("labels", at::kInt, 1);
+             b.labels = labels.data_ptr<int>();
+             Tensor idx = need("idx", at::kInt, 1);
+             b.idx = idx.data_ptr<int>();
+             b.n_idx = (int)idx.numel();
+             b.n_rows = (int)std::min<long>(images.numel() / HW, labels.numel());
+             TORCH_CHECK(conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows) <= 160 * 1024, "wgrad rows too large");
+             return std::make_shared<SimpleCNNEngine>(c, b, comm);
+           }),
+           py::arg("config"), py::arg("tensors"), py::arg("offsets"), py::arg("comm") = nullptr)
+      .def("step", &SimpleCNNEngine::step, py::arg("batch"), py::arg("batch_stride"))
+      .def("refresh_shadows", &SimpleCNNEngine::refresh_shadows)
+      .def("set_lr", &SimpleCNNEngine::set_lr)
+      .def("capture", &SimpleCNNEngine::capture)
+      .def("replay", &SimpleCNNEngine::replay)
+      .def("destroy_graph", &SimpleCNNEngine::destroy_graph)
+      .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
+      .def_property_readonly("graph_steps", &SimpleCNNEngine::graph_steps)
+      .def_property_readonly("stream", [](SimpleCNNEngine& e) { return (uint64_t)e.stream(); });
+}

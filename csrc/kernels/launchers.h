@@ -1,0 +1,76 @@
+// Host-side launch API of the gfx950 kernel library (no torch types here: the
+// runtime and the pybind layer both call these with raw pointers + a stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels/types.h"
+
+namespace ddp_amd {
+
+// ---- conv1 (Cin = 1) ---------------------------------------------------------------
+void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, bf16_t* y,
+               int B, int H, int W, int Cout, hipStream_t s);
+int conv1_wgrad_blocks(int B, int H, int W, int chunk);
+void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const bf16_t* dy, const bf16_t* yact,
+                 float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s);
+
+// ---- 3x3 / s1 / p1 NHWC conv (MFMA) --------------------------------------------------
+void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
+                 int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
+                 int pxt, hipStream_t s);
+void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
+                   bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
+                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s);
+int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
+int conv3x3_wgrad_blocks(int B, int H, int R);
+size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R);
+void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
+                   int H, int W, int Cin, int Cout, int R, hipStream_t s);
+
+// ---- Linear over NHWC-flattened activations -----------------------------------------
+void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
+                hipStream_t s);
+void fc_reduce(const float* part, const float* bias, float* out, int B, int G, int NO,
+               hipStream_t s);
+void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
+            int B, long K, int NO, bool mask, hipStream_t s);
+
+// ---- cross-entropy --------------------------------------------------------------------
+void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,
+          const int* labels32, BatchIdx bi, float* logits_out, float* dlogits, float* loss_out,
+          float* dbias, float gscale, float dbias_scale, hipStream_t s);
+
+// ---- optimizer / reductions -----------------------------------------------------------
+struct SgdArgs {
+  float lr, momentum, dampening, weight_decay;
+  int nesterov, maximize, first_step, update;
+};
+enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2 };
+constexpr int MAX_SHADOWS = 4;
+struct ShadowRegion {
+  long off, n;
+  bf16_t* dst;
+  int kind, a, b, c;  // TAPT: a = Cout, b = taps, c = Cin
+};
+struct ShadowSet {
+  ShadowRegion r[MAX_SHADOWS];
+  int count;
+};
+struct SlabSeg {
+  const float* slab;
+  long row_stride, src_off, n;
+  int rows;
+  float* dst;
+  float scale;
+};
+struct SlabSet {
+  SlabSeg s[4];
+  int count;
+};
+void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, const ShadowSet& sh,
+              int* step_ctr, hipStream_t s);
+void grad_reduce(const SlabSet& ss, hipStream_t s);
+void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s);
+
+}  // namespace ddp_amd

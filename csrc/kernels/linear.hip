@@ -1,0 +1,147 @@
+// Skinny Linear layer over an NHWC-flattened bf16 activation (SimpleCNN's fc,
+// reference model.py:16,19: nn.Linear(50176, 10)).
+//
+// The weight is kept in the activation's memory order, [out][H*W][C] (bf16
+// shadow of the fp32 master), so both passes stream it contiguously.  The
+// checkpoint still stores the reference's NCHW-flatten [out][C*H*W] order: the
+// permutation happens only at save/load (ddp_amd/models/layers.py).
+//
+//  fc_partial : per-16-pixel-tile partial logits (fixed-order split-K); the fused
+//               engine gets these from the conv2 epilogue instead.
+//  fc_reduce  : logits[b][o] = bias[o] + sum_g part[b][g][o] (fixed order).
+//  fc_bwd     : one pass over the activation computing
+//                 dX[b][k] = (MASK ? X>0 : 1) * sum_o dL[b][o] W[o][k]      (bf16)
+//                 dW[o][k] = scale * sum_b dL[b][o] X[b][k]                    (fp32)
+//               i.e. fc dgrad + fc wgrad + ReLU2 mask fused;
+//               dW is written straight into the gradient bucket, prescaled.
+#include "kernels/common.h"
+#include "kernels/launchers.h"
+
+namespace ddp_amd {
+
+constexpr int FC_MAXO = 16;
+
+__global__ __launch_bounds__(256) void fc_partial_kernel(const bf16_t* __restrict__ X,
+                                                         const bf16_t* __restrict__ Wf,
+                                                         float* __restrict__ part, int B, int HW,
+                                                         int C, int NO) {
+  const int lane = threadIdx.x & 63;
+  const long tile = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // 16-pixel tile over B*HW
+  const int G = HW / 16;
+  if (tile >= (long)B * G) return;
+  const int n = (int)(tile / G), g = (int)(tile - (long)n * G);
+  const long xoff = ((long)n * HW + g * 16) * C;
+  const long woff = (long)g * 16 * C;
+  const int te = 16 * C;
+  float s[FC_MAXO];
+#pragma unroll
+  for (int o = 0; o < FC_MAXO; ++o) s[o] = 0.f;
+  for (int e = lane * 8; e < te; e += 512) {
+    const bf16x8 xv = ld8(X + xoff + e);
+#pragma unroll
+    for (int o = 0; o < FC_MAXO; ++o) {
+      if (o < NO) {
+        const bf16x8 wv = ld8(Wf + (long)o * HW * C + woff + e);
+        float a = s[o];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a = fmaf(bf2f((bf16_t)xv[j]), bf2f((bf16_t)wv[j]), a);
+        s[o] = a;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < FC_MAXO; ++o)
+    if (o < NO) {
+      const float t = wave_sum(s[o]);
+      if (lane == 0) part[tile * NO + o] = t;
+    }
+}
+
+__global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bias,
+                                 float* __restrict__ out, int B, int G, int NO) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * NO) return;
+  const int b = i / NO, o = i - (i / NO) * NO;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[((long)b * G + g) * NO + o];
+  out[i] = s + (bias ? bias[o] : 0.f);
+}
+
+template <bool MASK>
+__global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ dL,
+                                                     const bf16_t* __restrict__ X,
+                                                     const bf16_t* __restrict__ Wf,
+                                                     bf16_t* __restrict__ dX, float* __restrict__ dW,
+                                                     float scale, int B, long K, int NO) {
+  extern __shared__ __attribute__((aligned(16))) float s_dl[];  // [B][NO]
+  for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
+  __syncthreads();
+  const long k = (long)blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  float w[FC_MAXO], dw[FC_MAXO];
+#pragma unroll
+  for (int o = 0; o < FC_MAXO; ++o) {
+    w[o] = (o < NO) ? bf2f(Wf[(long)o * K + k]) : 0.f;
+    dw[o] = 0.f;
+  }
+  int b = 0;
+  for (; b + 4 <= B; b += 4) {
+    float xa[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xa[u] = bf2f(X[(long)(b + u) * K + k]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* dl = s_dl + (b + u) * NO;
+      float dz = 0.f;
+#pragma unroll
+      for (int o = 0; o < FC_MAXO; ++o)
+        if (o < NO) {
+          dz = fmaf(dl[o], w[o], dz);
+          dw[o] = fmaf(dl[o], xa[u], dw[o]);
+        }
+      if (MASK && !(xa[u] > 0.f)) dz = 0.f;
+      dX[(long)(b + u) * K + k] = f2bf(dz);
+    }
+  }
+  for (; b < B; ++b) {
+    const float xa = bf2f(X[(long)b * K + k]);
+    const float* dl = s_dl + b * NO;
+    float dz = 0.f;
+#pragma unroll
+    for (int o = 0; o < FC_MAXO; ++o)
+      if (o < NO) {
+        dz = fmaf(dl[o], w[o], dz);
+        dw[o] = fmaf(dl[o], xa, dw[o]);
+      }
+    if (MASK && !(xa > 0.f)) dz = 0.f;
+    dX[(long)b * K + k] = f2bf(dz);
+  }
+#pragma unroll
+  for (int o = 0; o < FC_MAXO; ++o)
+    if (o < NO) dW[(long)o * K + k] = dw[o] * scale;
+}
+
+void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
+                hipStream_t s) {
+  const long tiles = (long)B * (HW / 16);
+  hipLaunchKernelGGL(fc_partial_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, X, Wf,
+                     part, B, HW, C, NO);
+}
+
+void fc_reduce(const float* part, const float* bias, float* out, int B, int G, int NO,
+               hipStream_t s) {
+  hipLaunchKernelGGL(fc_reduce_kernel, dim3((B * NO + 255) / 256), dim3(256), 0, s, part, bias, out,
+                     B, G, NO);
+}
+
+void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
+            int B, long K, int NO, bool mask, hipStream_t s) {
+  const dim3 grid((unsigned)((K + 255) / 256));
+  const size_t lds = sizeof(float) * B * NO;
+  if (mask)
+    hipLaunchKernelGGL(fc_bwd_kernel<true>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO);
+  else
+    hipLaunchKernelGGL(fc_bwd_kernel<false>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO);
+}
+
+}  // namespace ddp_amd

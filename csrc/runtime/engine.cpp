@@ -1,0 +1,160 @@
+// Fused SimpleCNN DDP training step (the MI355X-native replacement of the
+// reference's hot loop, train_ddp.py:195-200).
+//
+// One step = 8 kernels on the compute stream + 2 bucket all-reduces on the comm
+// stream, all stream-ordered so that a whole run of steps can be captured in a
+// single hipGraph and replayed (no per-step host launches):
+//
+//   conv1_fwd      u8 dataset gather (epoch index list) + /255 + conv1 + bias + ReLU -> a1
+//   conv3x3_fwd    conv2 (MFMA) + bias + ReLU -> a2, fused fc partial logits
+//   xent           split-K logits reduce + bias + softmax-xent fwd/bwd, fc bias grad
+//   fc_bwd         dZ2 = relu2'(a2) * dL.Wfc ; dWfc -> bucket 0 (prescaled 1/ws)
+//       -> event -> comm stream: all-reduce(bucket 0)  [overlaps the conv backward]
+//   conv3x3_dgrad  dZ1 = relu1'(a1) * conv2^T(dZ2) + fused conv1 wgrad slabs
+//   conv3x3_wgrad  conv2 weight/bias grad slabs (MFMA, split-K over image rows)
+//   grad_reduce    fixed-order slab sums -> bucket 1 (prescaled)
+//       -> event -> comm stream: all-reduce(bucket 1)
+//   sgd            wait both buckets; p -= lr*g over the flat buffer, bf16 shadows,
+//                  step counter += 1 (the next step's batch window)
+//
+// Buckets follow the reference DDP's rebuilt layout:
+// bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB).
+#include "runtime/runtime.h"
+
+namespace ddp_amd {
+
+SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& buf,
+                                 std::shared_ptr<Comm> comm)
+    : cfg_(cfg), b_(buf), comm_(std::move(comm)) {
+  if (cfg_.C1 != 32) throw std::runtime_error("engine: fused conv1 wgrad needs C1 == 32");
+  if (cfg_.C2 % 64 != 0) throw std::runtime_error("engine: C2 must be a multiple of 64");
+  if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
+  if (cfg_.NO > 16) throw std::runtime_error("engine: at most 16 classes");
+  if (b_.off_b2 != b_.off_w2 + (long)cfg_.C2 * 9 * cfg_.C1)
+    throw std::runtime_error("engine: conv2 bias must follow its weight in the flat buffer");
+  DDP_HIP_CHECK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
+  DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
+    DDP_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+}
+
+SimpleCNNEngine::~SimpleCNNEngine() {
+  destroy_graph();
+  for (hipEvent_t e : {e_b0_, e_b1_, e_d0_, e_d1_}) hipEventDestroy(e);
+  if (cs_) hipStreamDestroy(cs_);
+  if (ms_) hipStreamDestroy(ms_);
+}
+
+void SimpleCNNEngine::destroy_graph() {
+  if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  if (graph_) hipGraphDestroy(graph_);
+  graph_exec_ = nullptr;
+  graph_ = nullptr;
+  graph_steps_ = 0;
+}
+
+void SimpleCNNEngine::synchronize() { DDP_HIP_CHECK(hipStreamSynchronize(cs_)); }
+
+void SimpleCNNEngine::refresh_shadows() {
+  SgdArgs a{0.f, 0.f, 0.f, 0.f, 0, 0, 0, /*update=*/0};
+  ShadowSet sh{};
+  const long n_w2 = (long)cfg_.C2 * 9 * cfg_.C1;
+  sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
+  sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, cfg_.C2, 9, cfg_.C1};
+  sh.r[2] = ShadowRegion{b_.off_wfc, (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, b_.wfc_bf16,
+                         SHADOW_BF16, 0, 0, 0};
+  sh.count = 3;
+  sgd_step(b_.params, b_.grads, nullptr, b_.n_params, a, sh, nullptr, cs_);
+  DDP_HIP_CHECK(hipGetLastError());
+}
+
+void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
+  const int H = cfg_.H, W = cfg_.W, HW = H * W, C1 = cfg_.C1, C2 = cfg_.C2, NO = cfg_.NO;
+  if (B <= 0 || B > cfg_.max_batch) throw std::runtime_error("engine: bad batch size");
+  const bool dist = comm_ && comm_->world() > 1;
+  const float inv_ws = 1.f / (float)cfg_.world;
+  BatchIdx bi{b_.idx, b_.step_ctr, stride, 0};
+  bi.n_idx = b_.n_idx;
+  bi.n_rows = b_.n_rows;
+  float* P = b_.params;
+  float* G = b_.grads;
+
+  // ---- forward
+  conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
+  conv3x3_fwd(b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true, b_.wfc_bf16,
+              b_.fc_part, NO, cfg_.pxt_fwd, cs_);
+  // ---- loss + fc backward (bucket 0)
+  xent(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, nullptr, b_.labels, bi, nullptr, b_.dlogits,
+       b_.loss_hist, G + b_.off_bfc, 1.f / (float)B, inv_ws, cs_);
+  fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
+         /*mask=*/true, cs_);
+  if (dist) {
+    DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
+    comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
+    DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
+  }
+  // ---- conv backward (bucket 1)
+  conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
+                b_.w1slab, cfg_.pxt_dgrad, cs_);
+  conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_);
+  SlabSet ss{};
+  const long w2row = (long)C2 * 9 * C1 + C2;
+  ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, w2row, conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows),
+                    G + b_.off_w2, inv_ws};
+  const int dblk = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_dgrad);
+  ss.s[1] = SlabSeg{b_.w1slab, 320, 0, (long)C1 * 9, dblk, G + b_.off_w1, inv_ws};
+  ss.s[2] = SlabSeg{b_.w1slab, 320, (long)C1 * 9, (long)C1, dblk, G + b_.off_b1, inv_ws};
+  ss.count = 3;
+  grad_reduce(ss, cs_);
+  if (dist) {
+    DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
+    comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
+    DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
+  }
+  // ---- optimizer + bf16 shadows + next batch window
+  SgdArgs a{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
+            cfg_.maximize, first_momentum_step ? 1 : 0, 1};
+  ShadowSet sh{};
+  const long n_w2 = (long)C2 * 9 * C1;
+  sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
+  sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
+  sh.r[2] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
+  sh.count = 3;
+  sgd_step(P, G, b_.momentum, b_.n_params, a, sh, b_.step_ctr, cs_);
+}
+
+void SimpleCNNEngine::step(int batch, int batch_stride) {
+  const bool first = cfg_.momentum != 0.f && !momentum_started_;
+  launch_step(batch, batch_stride, first);
+  if (cfg_.momentum != 0.f) momentum_started_ = true;
+  DDP_HIP_CHECK(hipGetLastError());
+}
+
+void SimpleCNNEngine::capture(int nsteps) {
+  if (cfg_.momentum != 0.f && !momentum_started_)
+    throw std::runtime_error("engine: run one eager step before capturing (momentum init)");
+  destroy_graph();
+  DDP_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
+  try {
+    for (int i = 0; i < nsteps; ++i) launch_step(cfg_.max_batch, cfg_.max_batch, false);
+  } catch (...) {
+    hipGraph_t g = nullptr;
+    hipStreamEndCapture(cs_, &g);
+    if (g) hipGraphDestroy(g);
+    throw;
+  }
+  DDP_HIP_CHECK(hipStreamEndCapture(cs_, &graph_));
+  DDP_HIP_CHECK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+  graph_steps_ = nsteps;
+}
+
+void SimpleCNNEngine::replay() {
+  if (!graph_exec_) throw std::runtime_error("engine: no captured graph");
+  DDP_HIP_CHECK(hipGraphLaunch(graph_exec_, cs_));
+}
+
+}  // namespace ddp_amd

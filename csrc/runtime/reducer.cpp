@@ -1,0 +1,85 @@
+// Bucketed DDP gradient reducer (MI355X equivalent of torch's C++ DDP Reducer,
+// SURVEY.md §2.2 N3; reference trigger: DDP(model) at train_ddp.py:34 and
+// loss.backward() at train_ddp.py:199).
+//
+// Semantics kept from the reference DDP: gradients are averaged as
+// sum_r(g_r * 1/ws) (prescale, then SUM), buckets are launched as soon as their
+// last gradient is ready (overlapping backward), and the optimizer only runs
+// after every bucket finished.  What differs: buckets are views of one flat fp32
+// gradient buffer owned by the model, the all-reduce runs on a dedicated HIP
+// stream ordered by hipEvents (capturable), and the collective is RCCL directly.
+#include "runtime/runtime.h"
+
+namespace ddp_amd {
+
+Reducer::Reducer(std::shared_ptr<Comm> comm, float* flat_grad, std::vector<long> param_offsets,
+                 std::vector<long> param_numels, std::vector<int> param_bucket,
+                 std::vector<long> bucket_offsets, std::vector<long> bucket_numels, bool prescale)
+    : comm_(std::move(comm)),
+      flat_(flat_grad),
+      poff_(std::move(param_offsets)),
+      pnum_(std::move(param_numels)),
+      pbucket_(std::move(param_bucket)),
+      bucket_off_(std::move(bucket_offsets)),
+      bucket_num_(std::move(bucket_numels)),
+      prescale_(prescale) {
+  const int nb = (int)bucket_off_.size();
+  init_pending_.assign(nb, 0);
+  for (int b : pbucket_) {
+    if (b < 0 || b >= nb) throw std::runtime_error("reducer: parameter mapped to bad bucket");
+    init_pending_[b]++;
+  }
+  pending_ = init_pending_;
+  launched_.assign(nb, 0);
+  ready_.resize(nb);
+  done_.resize(nb);
+  for (int b = 0; b < nb; ++b) {
+    DDP_HIP_CHECK(hipEventCreateWithFlags(&ready_[b], hipEventDisableTiming));
+    DDP_HIP_CHECK(hipEventCreateWithFlags(&done_[b], hipEventDisableTiming));
+  }
+  DDP_HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
+}
+
+Reducer::~Reducer() {
+  for (auto e : ready_) hipEventDestroy(e);
+  for (auto e : done_) hipEventDestroy(e);
+  if (comm_stream_) hipStreamDestroy(comm_stream_);
+}
+
+void Reducer::reset() {
+  pending_ = init_pending_;
+  std::fill(launched_.begin(), launched_.end(), 0);
+}
+
+void Reducer::launch_bucket(int b, hipStream_t compute) {
+  DDP_HIP_CHECK(hipEventRecord(ready_[b], compute));
+  DDP_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_[b], 0));
+  if (comm_ && comm_->world() > 1) {
+    // prescaled gradients -> SUM == mean; otherwise let RCCL average
+    comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, prescale_ ? 0 : 1,
+                      comm_stream_);
+    ++calls_;
+  }
+  DDP_HIP_CHECK(hipEventRecord(done_[b], comm_stream_));
+  launched_[b] = 1;
+}
+
+void Reducer::mark_ready(int param, const float* grad_src, hipStream_t compute) {
+  if (param < 0 || param >= (int)poff_.size()) throw std::runtime_error("reducer: bad param index");
+  const int b = pbucket_[param];
+  float* dst = flat_ + poff_[param];
+  const float scale = (prescale_ && comm_) ? 1.f / (float)comm_->world() : 1.f;
+  if (grad_src != nullptr && grad_src != dst) scale_copy(dst, grad_src, pnum_[param], scale, compute);
+  else if (scale != 1.f) scale_copy(dst, dst, pnum_[param], scale, compute);
+  if (--pending_[b] == 0) launch_bucket(b, compute);
+}
+
+void Reducer::finalize(hipStream_t compute) {
+  for (int b = 0; b < (int)bucket_off_.size(); ++b) {
+    if (!launched_[b]) launch_bucket(b, compute);  // unused params: reduce what is there
+    DDP_HIP_CHECK(hipStreamWaitEvent(compute, done_[b], 0));
+  }
+  reset();
+}
+
+}  // namespace ddp_amd

@@ -1,0 +1,155 @@
+// Native host runtime of ddp_amd: RCCL communicator, bucketed gradient reducer and
+// the fused SimpleCNN training-step engine (with hipGraph capture).
+// Plain HIP host API + RCCL; no torch types (the pybind layer adapts tensors).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels/launchers.h"
+
+#define DDP_HIP_CHECK(expr)                                                              \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);  \
+  } while (0)
+
+#define DDP_NCCL_CHECK(expr)                                                             \
+  do {                                                                                   \
+    ncclResult_t _r = (expr);                                                            \
+    if (_r != ncclSuccess)                                                               \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);  \
+  } while (0)
+
+namespace ddp_amd {
+
+// ---------------------------------------------------------------- RCCL communicator
+// One communicator per process group, bootstrapped from an ncclUniqueId that rank 0
+// creates and the Python layer distributes through the c10d TCPStore.
+class Comm {
+ public:
+  static std::string new_unique_id();
+  Comm(const std::string& uid, int rank, int world, int device);
+  ~Comm();
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  // dtype: 0 = f32, 1 = bf16, 2 = i32, 3 = i64, 4 = u8; op: 0 = sum, 1 = avg, 2 = max
+  void all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t s);
+  void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s);
+  void all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t s);
+  void reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s);
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0, world_ = 1;
+};
+
+// ---------------------------------------------------------------- gradient reducer
+// DDP gradient synchronisation for an arbitrary list of parameters (the module
+// path).  Gradients live in one flat fp32 buffer cut into buckets; when the last
+// gradient of a bucket is marked ready, an event is recorded on the compute
+// stream, the comm stream waits for it and RCCL all-reduces the bucket, so
+// communication of early buckets overlaps the rest of backward.  finalize()
+// makes the compute stream wait for every bucket.  All of it is stream-ordered
+// and therefore capturable into a hipGraph.
+class Reducer {
+ public:
+  Reducer(std::shared_ptr<Comm> comm, float* flat_grad, std::vector<long> param_offsets,
+          std::vector<long> param_numels, std::vector<int> param_bucket,
+          std::vector<long> bucket_offsets, std::vector<long> bucket_numels, bool prescale);
+  ~Reducer();
+  // grad_src == nullptr: gradient already written in place (bucket view)
+  void mark_ready(int param, const float* grad_src, hipStream_t compute);
+  void finalize(hipStream_t compute);
+  void reset();
+  int num_buckets() const { return (int)bucket_off_.size(); }
+  long allreduce_calls() const { return calls_; }
+
+ private:
+  void launch_bucket(int b, hipStream_t compute);
+  std::shared_ptr<Comm> comm_;
+  float* flat_;
+  std::vector<long> poff_, pnum_;
+  std::vector<int> pbucket_;
+  std::vector<long> bucket_off_, bucket_num_;
+  std::vector<int> pending_, init_pending_;
+  std::vector<char> launched_;
+  std::vector<hipEvent_t> ready_, done_;
+  hipStream_t comm_stream_ = nullptr;
+  bool prescale_;
+  long calls_ = 0;
+};
+
+// ---------------------------------------------------------------- fused SimpleCNN engine
+struct EngineBuffers {
+  // parameters / gradients: one flat fp32 buffer each (native layouts, see layers.py)
+  float* params;
+  float* grads;
+  float* momentum;  // may be null (momentum == 0)
+  long n_params;
+  long off_w1, off_b1, off_w2, off_b2, off_wfc, off_bfc;
+  // gradient buckets (reference rebuilt order: [fl.*], [net.2.*, net.0.*])
+  long bucket0_off, bucket0_n, bucket1_off, bucket1_n;
+  // bf16 shadows
+  bf16_t *w2_bf16, *w2t_bf16, *wfc_bf16;
+  // activations / scratch (sized for max batch)
+  bf16_t *a1, *a2, *dz2, *dz1;
+  float *fc_part, *dlogits, *loss_hist, *w2slab, *w1slab;
+  int* step_ctr;
+  // data
+  const unsigned char* images;  // u8 [N][H*W]
+  const int* labels;            // i32 [N]
+  const int* idx;               // i32 epoch index list
+  int n_idx, n_rows;            // bounds for the clamped batch gather
+};
+
+struct EngineConfig {
+  int max_batch, H, W, C1, C2, NO;
+  int pxt_fwd, pxt_dgrad, wgrad_rows;
+  int world, rank;
+  float lr, momentum, dampening, weight_decay;
+  int nesterov, maximize;
+};
+
+class SimpleCNNEngine {
+ public:
+  SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& buf, std::shared_ptr<Comm> comm);
+  ~SimpleCNNEngine();
+  // eager launches of one full training step on the engine's compute stream
+  void step(int batch, int batch_stride);
+  void refresh_shadows();
+  void set_lr(float lr) { cfg_.lr = lr; }
+  // capture `nsteps` consecutive steps (batch = batch_stride = max_batch) into a graph
+  void capture(int nsteps);
+  void replay();
+  bool has_graph() const { return graph_exec_ != nullptr; }
+  int graph_steps() const { return graph_steps_; }
+  void destroy_graph();
+  hipStream_t stream() const { return cs_; }
+  void synchronize();
+  void set_momentum_started(bool v) { momentum_started_ = v; }
+
+ private:
+  void launch_step(int batch, int batch_stride, bool first_momentum_step);
+  EngineConfig cfg_;
+  EngineBuffers b_;
+  std::shared_ptr<Comm> comm_;
+  hipStream_t cs_ = nullptr, ms_ = nullptr;
+  hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
+  int graph_steps_ = 0;
+  bool momentum_started_ = false;
+};
+
+}  // namespace ddp_amd

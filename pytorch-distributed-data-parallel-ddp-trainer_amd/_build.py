@@ -1,0 +1,146 @@
+"""Native build driver for the gfx950 extension (``ddp_amd._C``).
+
+Everything native is compiled IN-TREE with the system ``hipcc`` (ROCm 7.2) for
+``--offload-arch=gfx950`` and linked against the HIP runtime / RCCL that ship
+inside the installed PyTorch wheel (``torch/lib``), so exactly one HIP runtime
+and one RCCL are mapped into the process (torch's).  No hipify step, no
+``torch.utils.cpp_extension`` JIT cache: the ``.so`` lands next to this file and
+travels with the repo snapshot to the GPU box.
+
+Layout of the native sources (``<repo>/csrc``):
+
+* ``kernels/*.hip``  - device code + thin ``extern`` launchers.  These TUs do NOT
+  include torch headers, so they compile in seconds.
+* ``runtime/*.cpp``  - host runtime (RCCL communicator, gradient reducer, fused
+  step engine + hipGraph capture).  Plain HIP host API, no torch headers.
+* ``bindings.cpp``   - the only TU that includes ``torch/extension.h``; converts
+  ``at::Tensor`` to raw pointers / streams and exposes everything via pybind11.
+
+Objects are rebuilt only when their source (or any header under ``csrc``) is
+newer than the object; the link step is skipped when the ``.so`` is newer than
+every object.
+"""
+from __future__ import annotations
+
+import concurrent.futures as _cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO_DIR, "csrc")
+BUILD_DIR = os.path.join(REPO_DIR, "build", "native")
+SO_PATH = os.path.join(PKG_DIR, "_C.so")
+ARCH = os.environ.get("DDP_AMD_ARCH", "gfx950")
+
+
+def _torch_dirs():
+    import torch
+
+    tdir = os.path.dirname(torch.__file__)
+    return tdir, os.path.join(tdir, "include"), os.path.join(tdir, "lib")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build ddp_amd._C)")
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    hs += glob.glob(os.path.join(CSRC, "**", "*.cuh"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _needs(obj: str, src: str, hdr_mtime: float) -> bool:
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return os.path.getmtime(src) > t or hdr_mtime > t
+
+
+def _compile_cmds():
+    hipcc = _hipcc()
+    _, tinc, _ = _torch_dirs()
+    rocm_inc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "include")
+    common = ["-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", rocm_inc, "-I", CSRC]
+    cmds = []
+    for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
+        obj = os.path.join(BUILD_DIR, "k_" + os.path.basename(src) + ".o")
+        cmds.append((src, obj, [hipcc, f"--offload-arch={ARCH}", *common,
+                                "-munsafe-fp-atomics", "-c", src, "-o", obj]))
+    for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
+        obj = os.path.join(BUILD_DIR, "r_" + os.path.basename(src) + ".o")
+        # host-only TUs: still driven by hipcc so hip_runtime.h resolves, but no device code
+        cmds.append((src, obj, [hipcc, *common, "-x", "c++", "-c", src, "-o", obj]))
+    bsrc = os.path.join(CSRC, "bindings.cpp")
+    bobj = os.path.join(BUILD_DIR, "bindings.o")
+    cmds.append((bsrc, bobj, [
+        hipcc, *common[:-2], "-O2", "-x", "c++", "-I", CSRC,
+        "-DUSE_ROCM", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+        f"-D_GLIBCXX_USE_CXX11_ABI={int(_cxx11_abi())}",
+        "-I", tinc, "-I", os.path.join(tinc, "torch", "csrc", "api", "include"),
+        "-I", sysconfig.get_paths()["include"], "-w", "-c", bsrc, "-o", bobj]))
+    return cmds
+
+
+def _cxx11_abi() -> bool:
+    import torch
+
+    return bool(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:
+    """Compile every HIP/C++ source for gfx950 and link ``_C.so`` in-tree.
+
+    Returns the path of the shared object.  Raises ``RuntimeError`` with the
+    compiler output on failure.
+    """
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    hdr = _headers_mtime()
+    cmds = _compile_cmds()
+    todo = [(s, o, c) for (s, o, c) in cmds if force or _needs(o, s, hdr)]
+    jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), max(1, len(todo)))
+
+    def run(item):
+        src, obj, cmd = item
+        if verbose:
+            print("[ddp_amd build]", " ".join(cmd), flush=True)
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if p.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{p.stdout}")
+        return src
+
+    if todo:
+        with _cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            for fut in _cf.as_completed([ex.submit(run, t) for t in todo]):
+                fut.result()
+
+    objs = [o for (_, o, _) in cmds]
+    if force or todo or not os.path.exists(SO_PATH) or \
+            max(os.path.getmtime(o) for o in objs) > os.path.getmtime(SO_PATH):
+        _, _, tlib = _torch_dirs()
+        # Link with the host compiler so hipcc does not add the system libamdhip64
+        # (ROCm 7.2) next to torch's bundled runtime: one HIP runtime per process.
+        tmp = SO_PATH + ".tmp"
+        cmd = ["g++", "-shared", "-fPIC", *objs, "-o", tmp, "-L", tlib,
+               "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+               "-lamdhip64", "-lrccl", f"-Wl,-rpath,{tlib}"]
+        if verbose:
+            print("[ddp_amd build]", " ".join(cmd), flush=True)
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if p.returncode != 0:
+            raise RuntimeError(f"link failed\n{p.stdout}")
+        os.replace(tmp, SO_PATH)
+    return SO_PATH
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    print(build(verbose=True, force=force))

@@ -1,0 +1,5 @@
+from .layers import Conv2d, Linear, FlatSpace, flat_space
+from .simple_cnn import SimpleCNN, reference_simple_cnn, param_count
+
+__all__ = ["Conv2d", "Linear", "FlatSpace", "flat_space", "SimpleCNN", "reference_simple_cnn",
+           "param_count"]

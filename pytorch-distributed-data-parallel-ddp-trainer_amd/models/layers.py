@@ -1,0 +1,272 @@
+"""Layers that keep MI355X-native parameter layouts but speak the reference's state_dict.
+
+Native layouts (what the gfx950 kernels read):
+
+* ``Conv2d.weight``: **OHWI** ``[Cout, KH, KW, Cin]`` - the implicit-GEMM K axis
+  (tap, ci) is contiguous, matching NHWC activations.
+* ``Linear.weight`` with ``in_layout=(C, H, W)``: ``[out, H*W, C]`` - the
+  activation's NHWC memory order, so the fc kernels stream it contiguously.
+
+The checkpoint contract is the reference's (``model.py:8-16`` + ``torch.save`` of
+``model.module.state_dict()``): OIHW conv weights and an
+NCHW-flatten ``[out, C*H*W]`` fc weight.  ``_save_to_state_dict`` /
+``_load_from_state_dict`` permute between the two, so ``state_dict()`` keys,
+shapes, ``_metadata`` and values are exactly what the reference writes, and a
+reference checkpoint loads into this model unchanged.
+
+Initialisation draws from the RNG exactly like ``torch.nn.Conv2d``/``Linear``
+(kaiming-uniform a=sqrt(5) on the reference-shaped tensor, then the bias), so
+``torch.manual_seed(s)`` gives bitwise the same initial weights as the
+reference model.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _canonical(t: torch.Tensor) -> torch.Tensor:
+    """Fresh tensor with its own storage and canonical row-major strides (incl. size-1
+    dims), so ``torch.save`` writes exactly the bytes a stock nn layer would."""
+    return t.clone(memory_format=torch.contiguous_format)
+
+
+def _kaiming_uniform_ref(shape, fan_in) -> torch.Tensor:
+    w = torch.empty(shape)
+    nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    return w
+
+
+def _bias_uniform(n, fan_in) -> torch.Tensor:
+    b = torch.empty(n)
+    bound = 1.0 / math.sqrt(fan_in) if fan_in > 0 else 0.0
+    nn.init.uniform_(b, -bound, bound)
+    return b
+
+
+class Conv2d(nn.Module):
+    """2-D convolution with an OHWI (channels-last) weight; reference-layout state_dict."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1,
+                 padding: int = 0, bias: bool = True):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        k = kernel_size
+        fan_in = in_channels * k * k
+        w_ref = _kaiming_uniform_ref((out_channels, in_channels, k, k), fan_in)
+        self.weight = nn.Parameter(w_ref.permute(0, 2, 3, 1).contiguous())
+        self.bias = nn.Parameter(_bias_uniform(out_channels, fan_in)) if bias else None
+
+    # reference (OIHW) view of the native weight; shares memory
+    def weight_oihw(self) -> torch.Tensor:
+        return self.weight.permute(0, 3, 1, 2)
+
+    def forward_nchw(self, x: torch.Tensor) -> torch.Tensor:
+        """Plain PyTorch forward on NCHW fp32 (CPU reference path)."""
+        return F.conv2d(x, self.weight_oihw(), self.bias, self.stride, self.padding)
+
+    def forward(self, x):
+        return self.forward_nchw(x)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        w = self.weight_oihw()
+        destination[prefix + "weight"] = _canonical(w if keep_vars else w.detach())
+        if self.bias is not None:
+            b = self.bias
+            destination[prefix + "bias"] = _canonical(b if keep_vars else b.detach())
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        for name in ("weight", "bias"):
+            key = prefix + name
+            p = getattr(self, name)
+            if p is None:
+                continue
+            if key not in state_dict:
+                missing_keys.append(key)
+                continue
+            v = state_dict[key]
+            if name == "weight":
+                exp = (self.out_channels, self.in_channels, self.kernel_size, self.kernel_size)
+                if tuple(v.shape) != exp:
+                    error_msgs.append(f"size mismatch for {key}: copying a param with shape "
+                                      f"{tuple(v.shape)}, the shape in current model is {exp}.")
+                    continue
+                v = v.permute(0, 2, 3, 1)
+            elif tuple(v.shape) != tuple(p.shape):
+                error_msgs.append(f"size mismatch for {key}: {tuple(v.shape)} vs {tuple(p.shape)}")
+                continue
+            with torch.no_grad():
+                p.copy_(v)
+        if strict:
+            for k in state_dict:
+                if k.startswith(prefix) and k[len(prefix):] not in ("weight", "bias") and "." not in k[len(prefix):]:
+                    unexpected_keys.append(k)
+
+    def extra_repr(self):
+        return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, "
+                f"stride={self.stride}, padding={self.padding}, layout=OHWI")
+
+
+class Linear(nn.Module):
+    """Linear layer; with ``in_layout=(C,H,W)`` it consumes NHWC-flattened activations.
+
+    Reference semantics: ``y = x_nchw_flat @ W_ref.T + b`` with ``W_ref [out, C*H*W]``.
+    Native weight: ``[out, H*W, C]`` (== W_ref permuted), so that
+    ``y = x_nhwc_flat @ W_native.reshape(out,-1).T + b`` is the same function.
+    """
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True,
+                 in_layout: tuple[int, int, int] | None = None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.in_layout = in_layout
+        w_ref = _kaiming_uniform_ref((out_features, in_features), in_features)
+        if in_layout is not None:
+            C, H, W = in_layout
+            assert C * H * W == in_features, "in_layout does not match in_features"
+            w = w_ref.view(out_features, C, H * W).permute(0, 2, 1).contiguous()
+        else:
+            w = w_ref
+        self.weight = nn.Parameter(w)
+        self.bias = nn.Parameter(_bias_uniform(out_features, in_features)) if bias else None
+
+    def weight_ref(self) -> torch.Tensor:
+        """Reference-layout ``[out, C*H*W]`` view/copy of the weight (differentiable)."""
+        if self.in_layout is None:
+            return self.weight
+        C, H, W = self.in_layout
+        return self.weight.permute(0, 2, 1).reshape(self.out_features, C * H * W)
+
+    def forward(self, x):  # x in reference (NCHW-flatten) order
+        return F.linear(x, self.weight_ref(), self.bias)
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        w = self.weight_ref()
+        destination[prefix + "weight"] = _canonical(w if keep_vars else w.detach())
+        if self.bias is not None:
+            b = self.bias
+            destination[prefix + "bias"] = _canonical(b if keep_vars else b.detach())
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        for name in ("weight", "bias"):
+            key = prefix + name
+            p = getattr(self, name)
+            if p is None:
+                continue
+            if key not in state_dict:
+                missing_keys.append(key)
+                continue
+            v = state_dict[key]
+            if name == "weight":
+                exp = (self.out_features, self.in_features)
+                if tuple(v.shape) != exp:
+                    error_msgs.append(f"size mismatch for {key}: copying a param with shape "
+                                      f"{tuple(v.shape)}, the shape in current model is {exp}.")
+                    continue
+                if self.in_layout is not None:
+                    C, H, W = self.in_layout
+                    v = v.view(self.out_features, C, H * W).permute(0, 2, 1)
+            elif tuple(v.shape) != tuple(p.shape):
+                error_msgs.append(f"size mismatch for {key}: {tuple(v.shape)} vs {tuple(p.shape)}")
+                continue
+            with torch.no_grad():
+                p.copy_(v)
+
+    def extra_repr(self):
+        lay = f", in_layout=NHWC{self.in_layout}" if self.in_layout else ""
+        return f"in_features={self.in_features}, out_features={self.out_features}{lay}"
+
+
+# ----------------------------------------------------------------------------- flat storage
+class FlatSpace:
+    """One contiguous fp32 buffer that every parameter of a module is a view into.
+
+    ``order`` lists parameters in gradient-ready order (reverse registration by
+    default, which is the order autograd produces SimpleCNN's gradients); each
+    parameter starts on a ``align``-element (256 B) boundary.  A twin buffer holds
+    the gradients, and ``param.grad`` is set to the matching view so autograd
+    accumulates in place (DDP buckets are then plain slices: no pack/unpack).
+    """
+
+    def __init__(self, module: nn.Module, align: int = 64, order: Iterable[str] | None = None):
+        named = dict(module.named_parameters())
+        names = list(order) if order is not None else list(reversed(list(named.keys())))
+        if sorted(names) != sorted(named.keys()):
+            raise ValueError("FlatSpace order must list every parameter exactly once")
+        dev = next(iter(named.values())).device
+        self.names = names
+        self.offsets, self.numels, self.shapes = {}, {}, {}
+        off = 0
+        for n in names:
+            p = named[n]
+            self.offsets[n] = off
+            self.numels[n] = p.numel()
+            self.shapes[n] = tuple(p.shape)
+            off += (p.numel() + align - 1) // align * align
+        self.numel = off
+        self.device = dev
+        self.params = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.module = module
+        # re-home every parameter into the flat buffer (same Parameter object identity is
+        # not preserved; optimizers must be built after flattening)
+        for n in names:
+            mod, attr = _resolve(module, n)
+            old = getattr(mod, attr)
+            view = self.view(self.params, n)
+            with torch.no_grad():
+                view.copy_(old.detach())
+            newp = nn.Parameter(view, requires_grad=old.requires_grad)
+            newp.grad = self.view(self.grads, n)
+            mod._parameters[attr] = newp
+        module._ddp_amd_flat = self
+
+    def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        o, n = self.offsets[name], self.numels[name]
+        return buf[o:o + n].view(self.shapes[name])
+
+    def param(self, name):
+        mod, attr = _resolve(self.module, name)
+        return getattr(mod, attr)
+
+    def reattach_grads(self):
+        """Point every ``.grad`` back at its flat view (after a set_to_none zero_grad)."""
+        for n in self.names:
+            p = self.param(n)
+            g = self.view(self.grads, n)
+            if p.grad is None:
+                p.grad = g
+            elif p.grad.data_ptr() != g.data_ptr():
+                g.copy_(p.grad)
+                p.grad = g
+
+    def zero_grad(self):
+        self.grads.zero_()
+        self.reattach_grads()
+
+
+def _resolve(module: nn.Module, name: str):
+    parts = name.split(".")
+    mod = module
+    for p in parts[:-1]:
+        mod = getattr(mod, p)
+    return mod, parts[-1]
+
+
+def flat_space(module: nn.Module, **kw) -> FlatSpace:
+    """Return the module's FlatSpace, creating it (on the module's device) if needed."""
+    fs = getattr(module, "_ddp_amd_flat", None)
+    if fs is not None:
+        cur = dict(module.named_parameters())
+        ok = all(cur[n].data_ptr() == fs.view(fs.params, n).data_ptr() for n in fs.names)
+        dev_ok = all(cur[n].device == fs.device for n in fs.names)
+        if ok and dev_ok:
+            return fs
+    return FlatSpace(module, **kw)

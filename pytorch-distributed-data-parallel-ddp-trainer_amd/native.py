@@ -1,0 +1,61 @@
+"""Loader for the in-tree gfx950 extension ``ddp_amd._C``.
+
+Policy (no silent fallbacks on the GPU): if a HIP device is visible, every op in
+``ddp_amd.ops`` runs its HIP kernel and :func:`require` raises when the
+extension cannot be imported.  The pure-PyTorch reference implementations are
+only used for tensors that live on the CPU (the CPU/gloo plumbing configuration
+and the CPU unit tests).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+_err: BaseException | None = None
+
+
+def _try_import():
+    global _mod, _err
+    with _lock:
+        if _mod is not None or _err is not None:
+            return _mod
+        try:
+            import torch  # noqa: F401  (loads torch's HIP runtime + RCCL first)
+
+            _mod = importlib.import_module(__package__ + "._C")
+        except BaseException as e:  # ImportError, OSError (bad .so), ...
+            _err = e
+        return _mod
+
+
+def available() -> bool:
+    return _try_import() is not None
+
+
+def require():
+    """Return the native module or raise a RuntimeError explaining how to build it."""
+    m = _try_import()
+    if m is None:
+        raise RuntimeError(
+            "ddp_amd native extension (_C.so) is not importable: "
+            f"{_err!r}.  Build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `python -m ddp_amd._build` (hipcc --offload-arch=gfx950).")
+    return m
+
+
+def build_if_needed(verbose: bool = False):
+    """Build the extension in-tree if sources changed (used by tests / entry points)."""
+    global _mod, _err
+    from . import _build
+
+    _build.build(verbose=verbose)
+    with _lock:
+        _mod, _err = None, None
+    return require()
+
+
+def so_path() -> str:
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")

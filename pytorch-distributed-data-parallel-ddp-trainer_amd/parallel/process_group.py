@@ -1,0 +1,100 @@
+"""Process-group runtime (reference utils.py:5-19).
+
+``setup(rank, world_size)`` keeps the reference's contract and log line but is
+explicit about the transport instead of silently auto-selecting:
+
+* GPU visible -> backend ``"nccl"`` (which *is* RCCL on ROCm) for the c10d
+  control plane, the process is bound to its **local** rank's GPU (the
+  reference used the global rank, bug B5), and a native RCCL communicator
+  (:func:`native_comm`) is bootstrapped over the same TCPStore for the data
+  plane (bucket all-reduces issued from C++ on our own HIP streams);
+* CPU only -> ``"gloo"`` (the reference's only working configuration, BASELINE
+  config 1).
+
+``MASTER_ADDR``/``MASTER_PORT`` default to 127.0.0.1 and a free port when unset
+(bug B2), and the PG timeout is configurable (``DDP_AMD_PG_TIMEOUT`` seconds).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+
+_native_comm = None
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def ensure_master_env():
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(free_port())
+
+
+def local_rank(rank: int | None = None) -> int:
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    r = rank if rank is not None else int(os.environ.get("RANK", 0))
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 1
+    return r % max(1, n)
+
+
+def default_backend() -> str:
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def setup(rank: int, world_size: int, backend: str | None = None, verbose: bool = True,
+          timeout_s: float | None = None) -> str:
+    """Join the process group; returns the backend used."""
+    backend = backend or os.environ.get("DDP_AMD_BACKEND") or default_backend()
+    if backend == "rccl":
+        backend = "nccl"
+    ensure_master_env()
+    if backend == "nccl":
+        if not torch.cuda.is_available():
+            raise RuntimeError("backend rccl/nccl requested but no HIP device is visible")
+        torch.cuda.set_device(local_rank(rank))
+    t = timeout_s or float(os.environ.get("DDP_AMD_PG_TIMEOUT", 1800))
+    kw = dict(backend=backend, world_size=world_size, rank=rank,
+              timeout=datetime.timedelta(seconds=t))
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", local_rank(rank))
+    dist.init_process_group(**kw)
+    if verbose:
+        print(f"Rank: {rank} has initialized its process group with world size {world_size}",
+              flush=True)
+    return backend
+
+
+def cleanup(verbose: bool = True):
+    global _native_comm
+    rank = dist.get_rank()
+    _native_comm = None
+    dist.destroy_process_group()
+    if verbose:
+        print(f"Rank {rank} cleaned up.", flush=True)
+
+
+def native_comm():
+    """The process-wide native RCCL communicator (created on first use, collective)."""
+    global _native_comm
+    if _native_comm is not None:
+        return _native_comm
+    from .. import native
+
+    C = native.require()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    store = dist.distributed_c10d._get_default_store()
+    key = "ddp_amd/rccl_uid"
+    if rank == 0:
+        store.set(key, C.Comm.new_unique_id())
+    uid = store.get(key)
+    _native_comm = C.Comm(uid, rank, world, torch.cuda.current_device())
+    return _native_comm
