@@ -1,0 +1,142 @@
+"""Headline benchmark: images/sec of MNIST SimpleCNN DDP training on N MI355X GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch_size 32]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric/config are BASELINE.json's: images/sec of the reference's SimpleCNN
+(520,586 params) DDP training step at the reference's default per-rank batch
+(32), weak scaling (per-GPU batch fixed), synthetic MNIST-shaped uint8 data and
+random-init weights (no network for the real dataset), bf16 compute with fp32
+master weights / gradients / optimizer.  A timed step is the complete training
+step of the reference's loop: batch gather + forward + loss + backward + DDP
+bucket all-reduce (RCCL, N>1) + SGD update - executed by the native fused
+engine (8 HIP kernels + 2 RCCL all-reduces, replayed from a hipGraph).
+
+W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
+``torch.cuda.synchronize()`` on both sides; the step time is the MAX over ranks;
+rank 0 prints one JSON line.  ``vs_baseline`` divides by the reference's
+best measured aggregate throughput at the same world size and per-rank batch 32
+(BASELINE.md survey table: ws1 2,799, ws2 2,665, ws4 3,384 img/s on the 8-core
+host - the reference publishes no numbers; ws8 at B=32 was not measured there,
+so its best measured aggregate at any batch, 3,670 img/s, is used).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec MNIST SimpleCNN DDP at 1/2/4/8 MI355X; DDP scaling efficiency"
+BASELINE_IMG_S = {1: 2799.0, 2: 2665.0, 4: 3384.0, 8: 3670.0}
+
+
+def graph_chunk(k: int, cap: int = 100) -> int:
+    for d in range(min(cap, k), 0, -1):
+        if k % d == 0:
+            return d
+    return 1
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--batch_size", type=int, default=32, help="per-rank batch (reference default 32)")
+    ap.add_argument("--graph_steps", type=int, default=None)
+    ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--lr", type=float, default=0.01)
+    args = ap.parse_args()
+
+    from ddp_amd import native
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN, param_count
+    from ddp_amd.models.layers import flat_space
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import native_comm, setup
+
+    native.require()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if ws != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    lrank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(lrank)
+    dev = torch.device("cuda", lrank)
+    comm = None
+    if ws > 1:
+        setup(rank, ws, backend="nccl", verbose=False)
+        comm = native_comm()
+
+    torch.manual_seed(0)
+    model = SimpleCNN().to(dev)
+    fs = flat_space(model)
+    if ws > 1:
+        dist.broadcast(fs.params, src=0)  # DDP construction semantics (rank-0 init)
+    opt = FusedSGD(model, lr=args.lr)
+    imgs, labels = synthetic_mnist()
+    data = DeviceMNIST(imgs, labels, dev, "synthetic")
+    k = args.graph_steps or graph_chunk(args.steps)
+    eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm,
+                               EngineOptions(graph_steps=k, use_graph=not args.no_graph))
+    eng.refresh()
+    if not args.no_graph:
+        eng.run_steps(0)           # uploads epoch 0's indices
+        eng._ensure_graph()        # capture outside the timed region
+    if args.warmup:
+        eng.run_steps(args.warmup)
+    eng.synchronize()
+
+    def barrier():
+        if ws > 1:
+            dist.barrier(device_ids=[lrank])
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    eng.run_steps(args.steps)
+    eng.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt * 1000.0 / args.steps
+    img_s = ws * args.batch_size * args.steps / dt
+    finite = bool(torch.isfinite(fs.params).all().item())
+    if rank == 0:
+        base = BASELINE_IMG_S.get(ws)
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(img_s, 1),
+            "unit": "images/sec",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / base, 2) if base else None,
+            "dtype": "bf16",
+            "data": "synthetic (MNIST-shaped uint8 60000x28x28, random-init weights)",
+            "config": {"model": f"SimpleCNN ({param_count(model):,} params)",
+                       "global_batch": ws * args.batch_size, "per_rank_batch": args.batch_size,
+                       "seq_len": None, "image": "1x28x28", "parallelism": f"dp{ws}",
+                       "engine": "fused hipGraph" if not args.no_graph else "fused eager",
+                       "graph_steps": k, "params_finite": finite},
+        }), flush=True)
+    if ws > 1:
+        dist.barrier(device_ids=[lrank])
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

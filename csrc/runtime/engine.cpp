@@ -30,8 +30,6 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   if (cfg_.C2 % 64 != 0) throw std::runtime_error("engine: C2 must be a multiple of 64");
   if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
   if (cfg_.NO > 16) throw std::runtime_error("engine: at most 16 classes");
-  if (b_.off_b2 != b_.off_w2 + (long)cfg_.C2 * 9 * cfg_.C1)
-    throw std::runtime_error("engine: conv2 bias must follow its weight in the flat buffer");
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
@@ -99,13 +97,14 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
                 b_.w1slab, cfg_.pxt_dgrad, cs_);
   conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_);
   SlabSet ss{};
-  const long w2row = (long)C2 * 9 * C1 + C2;
-  ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, w2row, conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows),
-                    G + b_.off_w2, inv_ws};
+  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
+  const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
+  ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, n_w2, wblk, G + b_.off_w2, inv_ws};
+  ss.s[1] = SlabSeg{b_.w2slab, w2row, n_w2, (long)C2, wblk, G + b_.off_b2, inv_ws};
   const int dblk = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_dgrad);
-  ss.s[1] = SlabSeg{b_.w1slab, 320, 0, (long)C1 * 9, dblk, G + b_.off_w1, inv_ws};
-  ss.s[2] = SlabSeg{b_.w1slab, 320, (long)C1 * 9, (long)C1, dblk, G + b_.off_b1, inv_ws};
-  ss.count = 3;
+  ss.s[2] = SlabSeg{b_.w1slab, 320, 0, (long)C1 * 9, dblk, G + b_.off_w1, inv_ws};
+  ss.s[3] = SlabSeg{b_.w1slab, 320, (long)C1 * 9, (long)C1, dblk, G + b_.off_b1, inv_ws};
+  ss.count = 4;
   grad_reduce(ss, cs_);
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
@@ -119,7 +118,6 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   SgdArgs a{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
             cfg_.maximize, first_momentum_step ? 1 : 0, 1};
   ShadowSet sh{};
-  const long n_w2 = (long)C2 * 9 * C1;
   sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
   sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
   sh.r[2] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};

@@ -1,0 +1,216 @@
+"""Python driver of the native fused SimpleCNN step engine (csrc/runtime/engine.cpp).
+
+The engine trains the SAME parameters as the ``SimpleCNN`` module (its flat fp32
+buffer is the engine's parameter buffer), so ``state_dict()`` / checkpoints /
+resume work unchanged; only the step itself is replaced by 8 fused HIP kernels
++ 2 RCCL bucket all-reduces, captured into one hipGraph per ``graph_steps``
+steps.
+
+Per epoch: the rank's ``DistributedSampler``-exact index list is uploaded once
+(int32, into a fixed device buffer the graph reads through a device step
+counter), full batches replay the graph, the leftover full steps and the ragged
+last batch (drop_last=False) run eagerly with their real size.  Losses are
+written on device into a per-epoch history; the host reads them one chunk
+behind the GPU (a chunk = one replay), so logging never stalls the stream.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+
+from .. import native
+from ..data.loader import DeviceMNIST
+from ..data.sampler import ShardedSampler
+from ..models.layers import flat_space
+from ..ops.functional import wgrad_rows
+from ..parallel.ddp import bucket_plan, bucket_ranges
+
+BF16 = torch.bfloat16
+
+
+@dataclasses.dataclass
+class EngineOptions:
+    graph_steps: int = 100     # steps per captured graph (one loss readback per chunk)
+    use_graph: bool = True
+    pxt_fwd: int = 2
+    pxt_dgrad: int = 2
+    wgrad_rows: int | None = None
+    bucket_cap_mb: float = 25.0
+
+
+class FusedSimpleCNNEngine:
+    def __init__(self, model, optimizer, data: DeviceMNIST, batch_size: int, world_size: int,
+                 rank: int, comm=None, opts: EngineOptions | None = None, seed: int = 0):
+        self.C = native.require()
+        self.opts = opts or EngineOptions()
+        self.model, self.opt, self.data = model, optimizer, data
+        self.B = int(batch_size)
+        self.world_size, self.rank = world_size, rank
+        self.fs = fs = flat_space(model)
+        dev = fs.params.device
+        if dev.type != "cuda":
+            raise RuntimeError("the fused engine runs on a HIP device")
+        names = {"w1": "net.0.weight", "b1": "net.0.bias", "w2": "net.2.weight",
+                 "b2": "net.2.bias", "wfc": "fl.weight", "bfc": "fl.bias"}
+        self.buckets = bucket_plan(fs, self.opts.bucket_cap_mb)
+        ranges = bucket_ranges(fs, self.buckets)
+        if len(ranges) != 2:
+            raise RuntimeError(f"expected the reference's 2 gradient buckets, got {self.buckets}")
+        offs = {k: fs.offsets[v] for k, v in names.items()}
+        offs.update(bucket0_off=ranges[0][0], bucket0_n=ranges[0][1],
+                    bucket1_off=ranges[1][0], bucket1_n=ranges[1][1])
+        self.sampler = ShardedSampler(len(data), world_size, rank, shuffle=True, seed=seed)
+        n_rank = len(self.sampler)
+        B, HW = self.B, 28 * 28
+        R = self.opts.wgrad_rows or wgrad_rows(28, B)
+        g = self.opt.param_groups[0]
+        if g["momentum"] != 0 and self.opt.momentum_buffer is None:
+            self.opt.momentum_buffer = torch.zeros_like(fs.params)
+        e = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
+        self.steps_per_epoch = math.ceil(n_rank / B)
+        self.t = dict(
+            params=fs.params, grads=fs.grads,
+            momentum=self.opt.momentum_buffer if self.opt.momentum_buffer is not None else e(1),
+            w2_bf16=e(64 * 9 * 32, dt=BF16), w2t_bf16=e(64 * 9 * 32, dt=BF16),
+            wfc_bf16=e(10 * HW * 64, dt=BF16),
+            a1=e(B * HW * 32, dt=BF16), a2=e(B * HW * 64, dt=BF16),
+            dz2=e(B * HW * 64, dt=BF16), dz1=e(B * HW * 32, dt=BF16),
+            fc_part=e(B * (HW // 16) * 10), dlogits=e(B * 10),
+            loss_hist=torch.zeros(self.steps_per_epoch + 1, device=dev),
+            w2slab=e(self.C.conv3x3_wgrad_blocks(B, 28, R) * (64 * 9 * 32 + 64)),
+            w1slab=e(self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_dgrad) * 320),
+            step_ctr=torch.zeros(1, dtype=torch.int32, device=dev),
+            images=data.images_u8.view(-1), labels=data.labels_i32,
+            idx=torch.zeros(n_rank, dtype=torch.int32, device=dev),
+        )
+        cfg = dict(max_batch=B, H=28, W=28, C1=32, C2=64, NO=10, pxt_fwd=self.opts.pxt_fwd,
+                   pxt_dgrad=self.opts.pxt_dgrad, wgrad_rows=R, world=world_size, rank=rank,
+                   lr=float(g["lr"]), momentum=float(g["momentum"]),
+                   dampening=float(g["dampening"]), weight_decay=float(g["weight_decay"]),
+                   nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]))
+        self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if world_size > 1 else None)
+        if self.opt.momentum_buffer is not None and self.opt.steps > 0:
+            self.eng.set_momentum_started(True)
+        self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)
+        self._captured = 0
+        self.steps_done = 0
+
+    # ------------------------------------------------------------------ helpers
+    def sync_from_torch(self):
+        """Order the engine stream after work queued on torch's current stream."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.stream.wait_event(ev)
+
+    def refresh(self):
+        """Re-derive bf16 shadows from the fp32 master weights (after init/load)."""
+        self.sync_from_torch()
+        self.eng.refresh_shadows()
+
+    def synchronize(self):
+        self.eng.synchronize()
+
+    def _ensure_graph(self):
+        k = self.opts.graph_steps
+        if self.opts.use_graph and self._captured != k:
+            self.eng.capture(k)
+            self._captured = k
+
+    # ------------------------------------------------------------------ epoch
+    def start_epoch(self, epoch: int):
+        self.sampler.set_epoch(epoch)
+        idx = self.sampler.indices().to(torch.int32).pin_memory()
+        with torch.cuda.stream(self.stream):
+            self.t["idx"].copy_(idx, non_blocking=True)
+            self.t["step_ctr"].zero_()
+            self.t["loss_hist"].zero_()
+        self._idx_host = idx  # keep pinned source alive until the copy ran
+
+    def run_epoch(self, epoch: int, on_loss=None, log_every: int = 100):
+        """Train one epoch; ``on_loss(batch_idx, loss)`` is called for batch_idx % log_every == 0."""
+        self.sync_from_torch()
+        self.start_epoch(epoch)
+        n = len(self.sampler)
+        B = self.B
+        nfull, rem = divmod(n, B)
+        done = 0
+        pending = []  # (first_batch, last_batch_exclusive, event)
+        if self.opt.momentum_buffer is not None and not self.opt.steps and nfull > 0:
+            self.eng.step(B, B)  # momentum buffer initialisation step (torch semantics)
+            done, self.opt.steps = 1, 1
+            pending.append((0, 1, self._event()))
+        k = self.opts.graph_steps
+        if self.opts.use_graph and nfull - done >= k:
+            self._ensure_graph()
+        while done < nfull:
+            if self.opts.use_graph and self._captured == k and nfull - done >= k:
+                self.eng.replay()
+                pending.append((done, done + k, self._event()))
+                done += k
+            else:
+                self.eng.step(B, B)
+                pending.append((done, done + 1, self._event()))
+                done += 1
+            self._drain(pending, on_loss, log_every, keep=1)
+        if rem:
+            self.eng.step(rem, B)
+            pending.append((done, done + 1, self._event()))
+            done += 1
+        self._drain(pending, on_loss, log_every, keep=0)
+        self.steps_done += done
+        self.opt.steps += done
+        return done
+
+    def run_steps(self, nsteps: int):
+        """Benchmark helper: ``nsteps`` full-batch steps (graph replays when possible).
+
+        Walks epoch 0's index list and wraps to its start when a replay would run
+        past the last full batch (the device step counter is reset on the stream).
+        """
+        if not self._bench_started:
+            self.sync_from_torch()
+            self.start_epoch(0)
+            self._bench_started = True
+        k = self.opts.graph_steps
+        n_full = len(self.sampler) // self.B
+        done = 0
+        while done < nsteps:
+            if self.opts.use_graph and nsteps - done >= k and k <= n_full:
+                self._ensure_graph()
+                self._wrap_if_needed(k, n_full)
+                self.eng.replay()
+                done += k
+            else:
+                self._wrap_if_needed(1, n_full)
+                self.eng.step(self.B, self.B)
+                done += 1
+        self.steps_done += done
+        return done
+
+    _bench_started = False
+    _bench_pos = 0
+
+    def _wrap_if_needed(self, k, n_full):
+        if self._bench_pos + k > n_full:
+            with torch.cuda.stream(self.stream):
+                self.t["step_ctr"].zero_()
+            self._bench_pos = 0
+        self._bench_pos += k
+
+    def _event(self):
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def _drain(self, pending, on_loss, log_every, keep):
+        while len(pending) > keep:
+            first, last, ev = pending.pop(0)
+            want = [b for b in range(first, last) if b % log_every == 0]
+            if not want or on_loss is None:
+                continue
+            ev.synchronize()
+            vals = self.t["loss_hist"][want].tolist()
+            for b, v in zip(want, vals):
+                on_loss(b, v)

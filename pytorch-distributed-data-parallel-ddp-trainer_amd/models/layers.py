@@ -224,7 +224,11 @@ class FlatSpace:
             with torch.no_grad():
                 view.copy_(old.detach())
             newp = nn.Parameter(view, requires_grad=old.requires_grad)
-            newp.grad = self.view(self.grads, n)
+            gview = self.view(self.grads, n)
+            if old.grad is not None:
+                with torch.no_grad():
+                    gview.copy_(old.grad)
+            newp.grad = gview
             mod._parameters[attr] = newp
         module._ddp_amd_flat = self
 

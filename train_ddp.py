@@ -1,0 +1,63 @@
+"""DDP trainer CLI - drop-in for the reference's ``train_ddp.py``.
+
+    python train_ddp.py [--epochs 10] [--batch_size 32] [--world_size N]
+    torchrun --nproc_per_node=N train_ddp.py --epochs 3 --batch_size 64
+
+Same flags and defaults as the reference (train_ddp.py:215-219: ``--epochs``
+10, per-rank ``--batch_size`` 32) plus the README's documented ``--world_size``
+(reference bug B1) and MI355X options.  Under torchrun the ranks come from the
+environment (no nested spawn, bug B3); otherwise ``--world_size`` processes are
+spawned (default: all visible GPUs, or 2 on a CPU host).  Checkpoints go to
+``./checkpoints/epoch_{N}.pt`` and a re-run resumes from the newest one.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from ddp_amd.engine.trainer import TrainOptions, ddp_train  # noqa: E402
+from ddp_amd.parallel.launcher import launch  # noqa: E402
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="DDP Training Script (MI355X-native)")
+    p.add_argument("--epochs", type=int, default=10, help="Number of training epochs")
+    p.add_argument("--batch_size", type=int, default=32, help="Batch size for training (per rank)")
+    p.add_argument("--world_size", type=int, default=None,
+                   help="processes to spawn when not under torchrun (default: #GPUs, or 2 on CPU)")
+    p.add_argument("--backend", choices=["rccl", "nccl", "gloo"], default=None,
+                   help="collective backend (default: rccl on GPU, gloo on CPU)")
+    p.add_argument("--engine", choices=["fused", "module"], default="fused",
+                   help="GPU step: fused native engine (hipGraph) or module path (autograd)")
+    p.add_argument("--data", choices=["auto", "mnist", "synthetic"], default="auto",
+                   help="MNIST IDX files under --data_root if present, else synthetic MNIST-shaped")
+    p.add_argument("--data_root", default="./data")
+    p.add_argument("--checkpoint_dir", default="./checkpoints")
+    p.add_argument("--no_save", action="store_true", help="do not write checkpoints")
+    p.add_argument("--lr", type=float, default=0.01)
+    p.add_argument("--momentum", type=float, default=0.0)
+    p.add_argument("--weight_decay", type=float, default=0.0)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--log_every", type=int, default=100)
+    p.add_argument("--graph_steps", type=int, default=100, help="steps per captured hipGraph")
+    p.add_argument("--bucket_cap_mb", type=float, default=25.0)
+    p.add_argument("--num_workers", type=int, default=2, help="CPU DataLoader workers")
+    p.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch (module/CPU path)")
+    p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse_args(argv)
+    opts = TrainOptions(lr=a.lr, momentum=a.momentum, weight_decay=a.weight_decay,
+                        backend=a.backend, engine=a.engine, data=a.data, data_root=a.data_root,
+                        checkpoint_dir=a.checkpoint_dir, save=not a.no_save, seed=a.seed,
+                        log_every=a.log_every, graph_steps=a.graph_steps,
+                        bucket_cap_mb=a.bucket_cap_mb, num_workers=a.num_workers,
+                        max_steps=a.max_steps, metrics_json=a.metrics_json)
+    launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
+
+
+if __name__ == "__main__":
+    main()
