@@ -324,6 +324,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd", &op_sgd);
   m.def("grad_reduce", &op_grad_reduce);
   m.def("scale_copy", &op_scale_copy);
+  m.def("_mark_exiting", &ddp_amd::mark_exiting);
   m.def("rccl_version", []() { int v = 0; ncclGetVersion(&v); return v; });
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")

@@ -6,11 +6,16 @@
 // ncclCommInitRank here.  Collectives are enqueued on caller-provided HIP streams
 // so they can be overlapped with compute and captured in hipGraphs.  Links
 // against the RCCL that ships inside the torch wheel (one RCCL per process).
+#include <atomic>
 #include <cstring>
 
 #include "runtime/runtime.h"
 
 namespace ddp_amd {
+
+static std::atomic<bool> g_exiting{false};
+void mark_exiting() { g_exiting.store(true); }
+bool process_exiting() { return g_exiting.load(); }
 
 static ncclDataType_t to_nccl(int dtype) {
   switch (dtype) {
@@ -48,7 +53,7 @@ Comm::Comm(const std::string& uid, int rank, int world, int device) : rank_(rank
 }
 
 Comm::~Comm() {
-  if (comm_) ncclCommDestroy(comm_);
+  if (comm_ && !process_exiting()) ncclCommDestroy(comm_);
 }
 
 void Comm::all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t s) {

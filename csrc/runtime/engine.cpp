@@ -37,10 +37,12 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
 }
 
 SimpleCNNEngine::~SimpleCNNEngine() {
+  // Streams are intentionally leaked (torch's caching allocators may still record
+  // events on a stream that touched their blocks); nothing is released at exit.
+  if (process_exiting()) return;
+  if (cs_) hipStreamSynchronize(cs_);
   destroy_graph();
   for (hipEvent_t e : {e_b0_, e_b1_, e_d0_, e_d1_}) hipEventDestroy(e);
-  if (cs_) hipStreamDestroy(cs_);
-  if (ms_) hipStreamDestroy(ms_);
 }
 
 void SimpleCNNEngine::destroy_graph() {

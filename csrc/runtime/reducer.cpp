@@ -41,9 +41,11 @@ Reducer::Reducer(std::shared_ptr<Comm> comm, float* flat_grad, std::vector<long>
 }
 
 Reducer::~Reducer() {
+  // The comm stream is intentionally never destroyed (torch does the same with its
+  // streams): torch's caching allocators may still record events on it later.
+  if (process_exiting()) return;
   for (auto e : ready_) hipEventDestroy(e);
   for (auto e : done_) hipEventDestroy(e);
-  if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
 
 void Reducer::reset() {

@@ -30,6 +30,11 @@
 
 namespace ddp_amd {
 
+// Set from Python's atexit: once the interpreter is shutting down, destructors leak
+// their HIP/RCCL handles instead of calling into a runtime that may be torn down.
+void mark_exiting();
+bool process_exiting();
+
 // ---------------------------------------------------------------- RCCL communicator
 // One communicator per process group, bootstrapped from an ncclUniqueId that rank 0
 // creates and the Python layer distributes through the c10d TCPStore.

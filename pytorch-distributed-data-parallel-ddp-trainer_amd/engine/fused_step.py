@@ -121,12 +121,13 @@ class FusedSimpleCNNEngine:
     # ------------------------------------------------------------------ epoch
     def start_epoch(self, epoch: int):
         self.sampler.set_epoch(epoch)
-        idx = self.sampler.indices().to(torch.int32).pin_memory()
+        # once per epoch, 240 KB: a synchronous pageable copy ordered on the engine stream
+        # (no pinned block is ever tied to the engine's stream)
+        idx = self.sampler.indices().to(torch.int32)
         with torch.cuda.stream(self.stream):
-            self.t["idx"].copy_(idx, non_blocking=True)
+            self.t["idx"].copy_(idx)
             self.t["step_ctr"].zero_()
             self.t["loss_hist"].zero_()
-        self._idx_host = idx  # keep pinned source alive until the copy ran
 
     def run_epoch(self, epoch: int, on_loss=None, log_every: int = 100):
         """Train one epoch; ``on_loss(batch_idx, loss)`` is called for batch_idx % log_every == 0."""

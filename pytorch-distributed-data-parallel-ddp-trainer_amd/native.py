@@ -26,6 +26,9 @@ def _try_import():
             import torch  # noqa: F401  (loads torch's HIP runtime + RCCL first)
 
             _mod = importlib.import_module(__package__ + "._C")
+            import atexit
+
+            atexit.register(_mod._mark_exiting)  # no HIP/RCCL teardown during interpreter exit
         except BaseException as e:  # ImportError, OSError (bad .so), ...
             _err = e
         return _mod
