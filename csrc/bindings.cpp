@@ -98,13 +98,14 @@ void op_conv3x3_fwd(const Tensor& X, const Tensor& Wt, const Tensor& bias, Tenso
   TORCH_CHECK(Cin % 32 == 0 && Cout % 64 == 0, "conv3x3_fwd: Cin%32, Cout%64 required");
   TORCH_CHECK(Wt.numel() == (long)Cout * 9 * Cin && bias.numel() == Cout, "conv3x3_fwd: weight shape");
   TORCH_CHECK(pxt == 1 || pxt == 2, "pxt must be 1 or 2");
+  TORCH_CHECK(conv3x3_fwd_lds(W, Cin, pxt) <= 160 * 1024, "conv3x3_fwd: LDS budget exceeded");
   const bf16_t* wf = nullptr;
   float* part = nullptr;
   if (wfc) {
     check(*wfc, "wfc", at::kBFloat16);
     TORCH_CHECK(fc_part.has_value(), "fc_part required with wfc");
     check(*fc_part, "fc_part", at::kFloat);
-    TORCH_CHECK(Cout == 64 && (H * W) % 16 == 0 && NO <= 16, "fused fc: Cout==64, HW%16==0, NO<=16");
+    TORCH_CHECK(Cout == 64 && (H * W) % 16 == 0 && NO == 10, "fused fc: Cout==64, HW%16==0, NO==10");
     TORCH_CHECK(wfc->numel() == (long)NO * H * W * Cout, "fused fc: wfc shape");
     TORCH_CHECK(fc_part->numel() >= (long)B * (H * W / 16) * NO, "fused fc: fc_part too small");
     wf = cbf(*wfc);
@@ -125,6 +126,8 @@ void op_conv3x3_dgrad(const Tensor& dY, std::optional<Tensor> Yact, const Tensor
   TORCH_CHECK(WT.numel() == (long)Cout * 9 * Cin, "conv3x3_dgrad: WT shape");
   if (Yact) TORCH_CHECK(Yact->sizes() == dY.sizes(), "Yact shape");
   if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
+  TORCH_CHECK(pxt == 1 || pxt == 2, "pxt must be 1 or 2");
+  TORCH_CHECK(conv3x3_dgrad_lds(W, Cout, pxt, false) <= 160 * 1024, "conv3x3_dgrad: LDS budget");
   BatchIdx bi{nullptr, nullptr, 0, 0};
   conv3x3_dgrad(cbf(dY), obf(Yact, "Yact"), cbf(WT), obf(Xact, "Xact"), bf(dX), B, H, W, Cin, Cout,
                 nullptr, false, bi, nullptr, pxt, cur_stream());
@@ -186,7 +189,8 @@ void op_fc_reduce(const Tensor& part, std::optional<Tensor> bias, Tensor& out, i
 }
 
 void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, Tensor& dW,
-               double scale, bool mask) {
+               double scale, bool mask, std::optional<Tensor> dbias, std::optional<Tensor> loss_rows,
+               std::optional<Tensor> loss_out) {
   check(dL, "dL", at::kFloat); check(X, "X", at::kBFloat16); check(Wf, "Wf", at::kBFloat16);
   check(dX, "dX", at::kBFloat16); check(dW, "dW", at::kFloat);
   const int B = dL.size(0), NO = dL.size(1);
@@ -194,8 +198,22 @@ void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, 
   TORCH_CHECK(X.numel() == (long)B * K && dX.numel() == X.numel(), "fc_bwd: X/dX shape");
   TORCH_CHECK(Wf.numel() == (long)NO * K && dW.numel() == Wf.numel() && NO <= 16, "fc_bwd: W shape");
   TORCH_CHECK((long)B * NO * 4 <= 64 * 1024, "fc_bwd: batch too large for LDS");
+  FcBwdExtras ex;
+  if (dbias) {
+    check(*dbias, "dbias", at::kFloat);
+    TORCH_CHECK(dbias->numel() == NO, "dbias size");
+    ex.dbias = dbias->data_ptr<float>();
+    ex.dbias_scale = (float)scale;
+  }
+  if (loss_rows) {
+    check(*loss_rows, "loss_rows", at::kFloat);
+    TORCH_CHECK(loss_out.has_value() && loss_rows->numel() >= B, "loss_rows needs loss_out");
+    check(*loss_out, "loss_out", at::kFloat);
+    ex.loss_rows = loss_rows->data_ptr<float>();
+    ex.loss_out = loss_out->data_ptr<float>();
+  }
   fc_bwd(dL.data_ptr<float>(), cbf(X), cbf(Wf), bf(dX), dW.data_ptr<float>(), (float)scale, B, K,
-         NO, mask, cur_stream());
+         NO, mask, cur_stream(), ex);
   kcheck();
 }
 
@@ -222,6 +240,20 @@ void op_xent(const Tensor& part, int G, std::optional<Tensor> bias, const Tensor
   BatchIdx bi{nullptr, nullptr, 0, 0};
   xent(part.data_ptr<float>(), G, bp, C, B, l64, l32, bi, lo, dlogits.data_ptr<float>(),
        loss_out.data_ptr<float>(), db, (float)gscale, (float)dbias_scale, cur_stream());
+  kcheck();
+}
+
+void op_xent_rows(const Tensor& part, int G, const Tensor& bias, const Tensor& labels32,
+                  std::optional<Tensor> idx, Tensor& dlogits, Tensor& loss_rows, double gscale) {
+  check(part, "part", at::kFloat); check(bias, "bias", at::kFloat); check(labels32, "labels", at::kInt);
+  check(dlogits, "dlogits", at::kFloat); check(loss_rows, "loss_rows", at::kFloat);
+  const int B = dlogits.size(0), NO = dlogits.size(1);
+  TORCH_CHECK(NO <= 16 && bias.numel() == NO, "xent_rows: at most 16 classes");
+  TORCH_CHECK(part.numel() >= (long)B * NO * G && loss_rows.numel() >= B, "xent_rows: sizes");
+  BatchIdx bi = make_bi(idx, std::nullopt, 0, 0, labels32.numel());
+  if (!idx) TORCH_CHECK(labels32.numel() >= B, "xent_rows: labels");
+  xent_rows(part.data_ptr<float>(), G, bias.data_ptr<float>(), NO, B, labels32.data_ptr<int>(), bi,
+            dlogits.data_ptr<float>(), loss_rows.data_ptr<float>(), (float)gscale, cur_stream());
   kcheck();
 }
 
@@ -319,7 +351,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_wgrad_blocks", &conv3x3_wgrad_blocks);
   m.def("fc_partial", &op_fc_partial);
   m.def("fc_reduce", &op_fc_reduce);
-  m.def("fc_bwd", &op_fc_bwd);
+  m.def("fc_bwd", &op_fc_bwd, py::arg("dL"), py::arg("X"), py::arg("Wf"), py::arg("dX"), py::arg("dW"),
+        py::arg("scale"), py::arg("mask"), py::arg("dbias") = py::none(),
+        py::arg("loss_rows") = py::none(), py::arg("loss_out") = py::none());
+  m.def("xent_rows", &op_xent_rows);
   m.def("xent", &op_xent);
   m.def("sgd", &op_sgd);
   m.def("grad_reduce", &op_grad_reduce);
@@ -421,6 +456,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.dz1 = bf(need("dz1", at::kBFloat16, B * HW * c.C1));
              b.fc_part = need("fc_part", at::kFloat, B * (HW / 16) * c.NO).data_ptr<float>();
              b.dlogits = need("dlogits", at::kFloat, B * c.NO).data_ptr<float>();
+             b.loss_rows = need("loss_rows", at::kFloat, B).data_ptr<float>();
              b.loss_hist = need("loss_hist", at::kFloat, 1).data_ptr<float>();
              b.w2slab = need("w2slab", at::kFloat, (long)conv3x3_wgrad_blocks(B, c.H, c.wgrad_rows) * (9L * c.C1 * c.C2 + c.C2)).data_ptr<float>();
              b.w1slab = need("w1slab", at::kFloat, (long)conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_dgrad) * 320).data_ptr<float>();

@@ -28,51 +28,117 @@
 
 namespace ddp_amd {
 
+// Cooperative global -> LDS copy of n 16-byte chunks: every thread keeps up to 8
+// loads in flight before its LDS writes (one memory round trip per 8 chunks instead
+// of one per chunk).  src(i) returns chunk i (zero-filled where out of range).
+template <typename SrcFn, typename DstFn>
+__device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
+  for (int base = threadIdx.x; base < n; base += 256 * 8) {
+    bf16x8 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * 256;
+      v[u] = (i < n) ? src(i) : zero8();
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * 256;
+      if (i < n) dst(i, v[u]);
+    }
+  }
+}
+
+// LDS geometry shared by fwd / dgrad: a block covers CH = 64*PXT consecutive output
+// pixels of the flattened [B*H*W] space and stages the LINEAR pixel range
+// [P0 - W - 1, P0 + CH + W + 1): every 3x3 neighbour of the block's pixels is in it
+// (neighbours in another image row/image are zeroed by the (h,w) bounds test).
+// Weight rows are padded by 8 elements so the 16 rows of an A fragment start on
+// 16 distinct 4-bank groups (conflict-free ds_read_b128).
+
 // ---------------------------------------------------------------- forward
-template <int PXT, bool RELU, bool FUSE_FC>
+template <int PXT, bool RELU, int NOF>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     bf16_t* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
-    const bf16_t* __restrict__ wfc, float* __restrict__ fc_part, int NO) {
+    const bf16_t* __restrict__ wfc, float* __restrict__ fc_part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
   const int co0 = blockIdx.y * 64;
-  const long pb = ((long)blockIdx.x * 4 + wave) * 16 * PXT;
+  const int KW = 9 * Cin, WS = KW + 8, XS = Cin + 8;
+  const int XR = CH + 2 * W + 2;
+  bf16_t* sW = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* sX = sW + 64 * WS;
+  const long P0 = (long)blockIdx.x * CH;
+  const long Pbase = P0 - W - 1;
+
+  const int wc = KW / 8;
+  stage16(64 * wc,
+          [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
+          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sW + r * WS + c) = v; });
+  const int xc = Cin / 8;
+  stage16(XR * xc,
+          [&](int i) {
+            const int r = i / xc, c = (i - r * xc) * 8;
+            const long P = Pbase + r;
+            return (P >= 0 && P < Ptot) ? ld8(X + P * Cin + c) : zero8();
+          },
+          [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
+
   const int kofs = 8 * (lane >> 4);
   const int col = lane & 15;
-
-  int n[PXT], h[PXT], w[PXT];
+  int h[PXT], w[PXT], rowc[PXT], rem[PXT];
   bool valid[PXT];
+  long Pp[PXT];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
-    const long P = pb + pt * 16 + col;
-    valid[pt] = P < Ptot;
-    const long Pc = valid[pt] ? P : 0;
-    n[pt] = (int)(Pc / HW);
-    const int rem = (int)(Pc - (long)n[pt] * HW);
-    h[pt] = rem / W;
-    w[pt] = rem - h[pt] * W;
+    const int lp = (wave * PXT + pt) * 16 + col;  // pixel within the block
+    Pp[pt] = P0 + lp;
+    valid[pt] = Pp[pt] < Ptot;
+    const long Pc = valid[pt] ? Pp[pt] : 0;
+    const int n = (int)(Pc / HW);
+    rem[pt] = (int)(Pc - (long)n * HW);
+    h[pt] = rem[pt] / W;
+    w[pt] = rem[pt] - h[pt] * W;
+    rowc[pt] = lp + W + 1;  // sX row of the pixel itself
   }
+  // fc weight prefetch (lands while the MFMAs run)
+  uint2 wv[NOF > 0 ? PXT : 1][4][NOF > 0 ? NOF : 1];
+  if (NOF > 0) {
+#pragma unroll
+    for (int pt = 0; pt < PXT; ++pt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o)
+          wv[pt][t][o] = *reinterpret_cast<const uint2*>(
+              wfc + ((long)o * HW + rem[pt]) * Cout + co0 + 16 * t + 4 * (lane >> 4));
+  }
+  __syncthreads();
+
   f32x4 acc[PXT][4];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[pt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const bf16_t* wrow = Wt + (long)(co0 + col) * 9 * Cin + kofs;
+  const bf16_t* wrow = sW + col * WS + kofs;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int dh = tap / 3 - 1, dw = tap % 3 - 1;
     for (int ci0 = 0; ci0 < Cin; ci0 += 32) {
       bf16x8 a[4], b[PXT];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = ld8(wrow + (long)16 * t * 9 * Cin + tap * Cin + ci0);
+      for (int t = 0; t < 4; ++t)
+        a[t] = *reinterpret_cast<const bf16x8*>(wrow + 16 * t * WS + tap * Cin + ci0);
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {
         const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        b[pt] = ok ? ld8(X + (((long)n[pt] * H + hh) * W + ww) * Cin + ci0 + kofs) : zero8();
+        b[pt] = ok ? *reinterpret_cast<const bf16x8*>(sX + (rowc[pt] + dh * W + dw) * XS + ci0 + kofs)
+                   : zero8();
       }
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt)
@@ -81,15 +147,12 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     }
   }
 
-  // epilogue: bias + ReLU + bf16 store (+ fc partial logits)
+  // epilogue: bias + ReLU + bf16 store (+ fc partial logits, layout [B][NOF][HW/16])
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
-    const long P = pb + pt * 16 + col;
-    float fcs[FUSE_FC ? 16 : 1];
-    if (FUSE_FC) {
+    float fcs[NOF > 0 ? NOF : 1];
 #pragma unroll
-      for (int o = 0; o < 16; ++o) fcs[o] = 0.f;
-    }
+    for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) fcs[o] = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int co = co0 + 16 * t + 4 * (lane >> 4);
@@ -98,34 +161,31 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
       float v2 = acc[pt][t][2] + bv.z, v3 = acc[pt][t][3] + bv.w;
       if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
       const uint2 pk = pack4(v0, v1, v2, v3);
-      if (valid[pt]) *reinterpret_cast<uint2*>(Y + P * Cout + co) = pk;
-      if (FUSE_FC) {
+      if (valid[pt]) *reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co) = pk;
+      if (NOF > 0) {
         float q[4];
         unpack4(pk, q);  // the bf16 values actually stored (what backward re-reads)
-        const int rem = h[pt] * W + w[pt];
 #pragma unroll
-        for (int o = 0; o < 16; ++o) {
-          if (o < NO) {
-            float wv[4];
-            unpack4(*reinterpret_cast<const uint2*>(wfc + ((long)o * HW + rem) * Cout + co), wv);
-            float s = fcs[o];
-            s = fmaf(q[0], wv[0], s); s = fmaf(q[1], wv[1], s);
-            s = fmaf(q[2], wv[2], s); s = fmaf(q[3], wv[3], s);
-            fcs[o] = valid[pt] ? s : 0.f;
-          }
+        for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
+          float wf[4];
+          unpack4(wv[pt][t][o], wf);
+          float s = fcs[o];
+          s = fmaf(q[0], wf[0], s); s = fmaf(q[1], wf[1], s);
+          s = fmaf(q[2], wf[2], s); s = fmaf(q[3], wf[3], s);
+          fcs[o] = valid[pt] ? s : 0.f;
         }
       }
     }
-    if (FUSE_FC) {
-      // whole 16-pixel tile lies in one image (HW % 16 == 0, checked on host)
-      const long g = (pb + pt * 16) / 16;
-      const bool tile_ok = (pb + pt * 16) < Ptot;
+    if (NOF > 0) {
+      // the 16-pixel tile lies in one image (HW % 16 == 0, checked on host)
+      const long tile0 = P0 + (wave * PXT + pt) * 16;
+      const int G = HW / 16;
+      const long n = tile0 / HW;
+      const int g = (int)((tile0 - n * HW) / 16);
 #pragma unroll
-      for (int o = 0; o < 16; ++o) {
-        if (o < NO) {
-          const float s = wave_sum(fcs[o]);
-          if (lane == 0 && tile_ok) fc_part[g * NO + o] = s;
-        }
+      for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
+        const float s = wave_sum(fcs[o]);
+        if (lane == 0 && tile0 < Ptot) fc_part[(n * NOF + o) * G + g] = s;
       }
     }
   }
@@ -137,46 +197,97 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
     const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab) {
-  __shared__ float s_w1[FUSE_W1 ? 4 * 320 : 1];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
   const int ci_blk = blockIdx.y * 32;
-  const long pb = ((long)blockIdx.x * 4 + wave) * 16 * PXT;
+  const int KW = 9 * Cout, WS = KW + 8, DS = Cout + 8;
+  const int XR = CH + 2 * W + 2;
+  bf16_t* sWT = reinterpret_cast<bf16_t*>(smem);        // [32 ci][9*Cout]
+  bf16_t* sDY = sWT + 32 * WS;                           // [XR][Cout]
+  float* sx0 = reinterpret_cast<float*>(sDY + XR * DS);  // [XR] conv1 input (FUSE_W1)
+  float* s_w1 = sx0 + XR;                                // [4][320] (FUSE_W1)
+  const long P0 = (long)blockIdx.x * CH;
+  const long Pbase = P0 - W - 1;
+
+  const int wc = KW / 8, cpc = Cout / 8;
+  stage16(32 * wc,
+          [&](int i) {
+            const int r = i / wc, rest = (i - r * wc) * 8;  // rest = tap*Cout + co
+            const int tap = rest / Cout, co = rest - tap * Cout;
+            return ld8(WT + ((long)tap * Cin + ci_blk + r) * Cout + co);
+          },
+          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sWT + r * WS + c) = v; });
+  stage16(XR * cpc,
+          [&](int i) {
+            const int r = i / cpc, c = (i - r * cpc) * 8;
+            const long P = Pbase + r;
+            bf16x8 v = zero8();
+            if (P >= 0 && P < Ptot) {
+              v = ld8(dY + P * Cout + c);
+              if (MASK_DY) v = mask8(v, ld8(Yact + P * Cout + c));
+            }
+            return v;
+          },
+          [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * 8; *reinterpret_cast<bf16x8*>(sDY + r * DS + c) = v; });
+  if (FUSE_W1) {
+    const int base = x0_u8 ? bi.base() : 0;
+    for (int r = threadIdx.x; r < XR; r += 256) {
+      const long P = Pbase + r;
+      float v = 0.f;
+      if (P >= 0 && P < Ptot) {
+        const int n = (int)(P / HW), rm = (int)(P - (long)n * HW);
+        if (x0_u8) v = (float)((const unsigned char*)x0)[(long)bi.row(n, base) * HW + rm] / 255.0f;
+        else v = ((const float*)x0)[P];
+      }
+      sx0[r] = v;
+    }
+  }
+
   const int kofs = 8 * (lane >> 4);
   const int col = lane & 15;
-
-  int n[PXT], h[PXT], w[PXT];
+  int h[PXT], w[PXT], rowc[PXT];
   bool valid[PXT];
+  long Pp[PXT];
+  uint2 xa[PXT][2];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
-    const long P = pb + pt * 16 + col;
-    valid[pt] = P < Ptot;
-    const long Pc = valid[pt] ? P : 0;
-    n[pt] = (int)(Pc / HW);
-    const int rem = (int)(Pc - (long)n[pt] * HW);
-    h[pt] = rem / W;
-    w[pt] = rem - h[pt] * W;
+    const int lp = (wave * PXT + pt) * 16 + col;
+    Pp[pt] = P0 + lp;
+    valid[pt] = Pp[pt] < Ptot;
+    const long Pc = valid[pt] ? Pp[pt] : 0;
+    const int n = (int)(Pc / HW);
+    const int rm = (int)(Pc - (long)n * HW);
+    h[pt] = rm / W;
+    w[pt] = rm - h[pt] * W;
+    rowc[pt] = lp + W + 1;
+    if (MASK_X) {  // prefetch the ReLU-input mask (lands during the MFMAs)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        xa[pt][t] = *reinterpret_cast<const uint2*>(Xact + Pc * Cin + ci_blk + 16 * t + 4 * (lane >> 4));
+    }
   }
+  __syncthreads();
+
   f32x4 acc[PXT][2];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) acc[pt][0] = acc[pt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
+  const bf16_t* wrow = sWT + col * WS + kofs;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int dh = 1 - tap / 3, dw = 1 - tap % 3;  // dY pixel = (h + 1 - kh, w + 1 - kw)
-    const bf16_t* wtap = WT + ((long)tap * Cin + ci_blk + col) * Cout + kofs;
     for (int co0 = 0; co0 < Cout; co0 += 32) {
-      const bf16x8 a0 = ld8(wtap + co0);
-      const bf16x8 a1 = ld8(wtap + (long)16 * Cout + co0);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(wrow + tap * Cout + co0);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wrow + 16 * WS + tap * Cout + co0);
       bf16x8 b[PXT];
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {
         const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        const long off = (((long)n[pt] * H + hh) * W + ww) * Cout + co0 + kofs;
-        b[pt] = ok ? ld8(dY + off) : zero8();
-        if (MASK_DY) b[pt] = ok ? mask8(b[pt], ld8(Yact + off)) : b[pt];
+        b[pt] = ok ? *reinterpret_cast<const bf16x8*>(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs)
+                   : zero8();
       }
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {
@@ -195,36 +306,30 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 #pragma unroll
         for (int k = 0; k < 10; ++k) w1a[t][j][k] = 0.f;
   }
-  const int base = (FUSE_W1 && x0_u8) ? bi.base() : 0;
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
-    const long P = pb + pt * 16 + col;
     float xv[9];
     if (FUSE_W1) {
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
-        const int hh = h[pt] + k / 3 - 1, ww = w[pt] + k % 3 - 1;
+        const int dh = k / 3 - 1, dw = k % 3 - 1;
+        const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        float v = 0.f;
-        if (ok) {
-          if (x0_u8) v = (float)((const unsigned char*)x0)[(long)bi.row(n[pt], base) * HW + hh * W + ww] / 255.0f;
-          else v = ((const float*)x0)[(long)n[pt] * HW + hh * W + ww];
-        }
-        xv[k] = v;
+        xv[k] = ok ? sx0[rowc[pt] + dh * W + dw] : 0.f;
       }
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int ci = ci_blk + 16 * t + 4 * (lane >> 4);
       float v[4] = {acc[pt][t][0], acc[pt][t][1], acc[pt][t][2], acc[pt][t][3]};
-      if (MASK_X && valid[pt]) {
-        float xa[4];
-        unpack4(*reinterpret_cast<const uint2*>(Xact + P * Cin + ci), xa);
+      if (MASK_X) {
+        float xm[4];
+        unpack4(xa[pt][t], xm);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = xa[j] > 0.f ? v[j] : 0.f;
+        for (int j = 0; j < 4; ++j) v[j] = xm[j] > 0.f ? v[j] : 0.f;
       }
       const uint2 pk = pack4(v[0], v[1], v[2], v[3]);
-      if (valid[pt]) *reinterpret_cast<uint2*>(dX + P * Cin + ci) = pk;
+      if (valid[pt]) *reinterpret_cast<uint2*>(dX + Pp[pt] * Cin + ci) = pk;
       if (FUSE_W1) {
         float q[4];
         unpack4(pk, q);
@@ -288,29 +393,37 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
   bf16_t* sX = sdY + (long)nslot * DS;
   const int XW = Wp + 2;
 
-  // ---- stage dY rows (masked) and X rows with halo, 16 B per thread-iteration
+  // ---- stage dY rows (masked) and X rows with halo (8 loads in flight per thread)
   const int cpy_dy = Cout / 8, cpy_x = Cin / 8;
-  for (int i = threadIdx.x; i < nslot * cpy_dy; i += 256) {
-    const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
-    const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
-    const int hh = r0 + r;
-    bf16x8 v = zero8();
-    if (r < R && hh < H && c < W) {
-      const long off = (((long)n * H + hh) * W + c) * Cout + ch;
-      v = ld8(dY + off);
-      if (MASK_DY) v = mask8(v, ld8(Yact + off));
-    }
-    *reinterpret_cast<bf16x8*>(sdY + (long)slot * DS + ch) = v;
-  }
-  for (int i = threadIdx.x; i < (R + 2) * XW * cpy_x; i += 256) {
-    const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
-    const int rr = pos / XW, cc = pos - (pos / XW) * XW;
-    const int hh = r0 - 1 + rr, ww = cc - 1;
-    bf16x8 v = zero8();
-    if ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-      v = ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch);
-    *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
-  }
+  stage16(nslot * cpy_dy,
+          [&](int i) {
+            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
+            const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
+            const int hh = r0 + r;
+            bf16x8 v = zero8();
+            if (r < R && hh < H && c < W) {
+              const long off = (((long)n * H + hh) * W + c) * Cout + ch;
+              v = ld8(dY + off);
+              if (MASK_DY) v = mask8(v, ld8(Yact + off));
+            }
+            return v;
+          },
+          [&](int i, bf16x8 v) {
+            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
+            *reinterpret_cast<bf16x8*>(sdY + (long)slot * DS + ch) = v;
+          });
+  stage16((R + 2) * XW * cpy_x,
+          [&](int i) {
+            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+            const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+            const int hh = r0 - 1 + rr, ww = cc - 1;
+            return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                       ? ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
+          },
+          [&](int i, bf16x8 v) {
+            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+            *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
+          });
   __syncthreads();
 
   // ---- wave assignment: (pair of 16-wide co tiles) x (16-wide ci tile)
@@ -375,30 +488,43 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 }
 
 // ---------------------------------------------------------------- launchers
+size_t conv3x3_fwd_lds(int W, int Cin, int pxt) {
+  return sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 8) + (size_t)(64 * pxt + 2 * W + 2) * (Cin + 8));
+}
+
+size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
+  const size_t XR = 64 * pxt + 2 * W + 2;
+  return sizeof(bf16_t) * ((size_t)32 * (9 * Cout + 8) + XR * (Cout + 8)) +
+         (fuse_w1 ? sizeof(float) * (XR + 4 * 320) : 0);
+}
+
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
                  int pxt, hipStream_t s) {
   const long P = (long)B * H * W;
-  const int per_blk = 4 * 16 * pxt;
+  const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cout / 64);
-  const bool fc = wfc != nullptr;
-#define LF(PX, RL, FC) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, FC>), grid, dim3(256), 0, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, NO)
+  const size_t lds = conv3x3_fwd_lds(W, Cin, pxt);
+  const bool fc = wfc != nullptr;  // host guarantees NO == 10 when fused
+#define LF(PX, RL, NF) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF>), grid, dim3(256), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part)
   if (pxt == 2) {
-    if (fc) LF(2, true, true); else if (relu) LF(2, true, false); else LF(2, false, false);
+    if (fc) LF(2, true, 10); else if (relu) LF(2, true, 0); else LF(2, false, 0);
   } else {
-    if (fc) LF(1, true, true); else if (relu) LF(1, true, false); else LF(1, false, false);
+    if (fc) LF(1, true, 10); else if (relu) LF(1, true, 0); else LF(1, false, 0);
   }
 #undef LF
+  (void)NO;
 }
 
 void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
                    bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
                    BatchIdx bi, float* w1slab, int pxt, hipStream_t s) {
   const long P = (long)B * H * W;
-  const int per_blk = 4 * 16 * pxt;
+  const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cin / 32);
   const bool mdy = Yact != nullptr, mx = Xact != nullptr, w1 = w1slab != nullptr;
-#define LD(PX, A, Bm, C) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C>), grid, dim3(256), 0, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab)
+  const size_t lds = conv3x3_dgrad_lds(W, Cout, pxt, w1);
+#define LD(PX, A, Bm, C) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C>), grid, dim3(256), lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab)
   if (pxt == 2) {
     if (w1) LD(2, false, true, true);
     else if (mdy && mx) LD(2, true, true, false);
@@ -417,7 +543,7 @@ void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const
 
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt) {
   const long P = (long)B * H * W;
-  const int per_blk = 4 * 16 * pxt;
+  const int per_blk = 64 * pxt;
   return (int)((P + per_blk - 1) / per_blk);
 }
 

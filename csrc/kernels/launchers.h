@@ -25,6 +25,8 @@ void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R);
+size_t conv3x3_fwd_lds(int W, int Cin, int pxt);
+size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1);
 void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
                    int H, int W, int Cin, int Cout, int R, hipStream_t s);
 
@@ -33,13 +35,25 @@ void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, i
                 hipStream_t s);
 void fc_reduce(const float* part, const float* bias, float* out, int B, int G, int NO,
                hipStream_t s);
+// Optional extras of fc_bwd's first block: fc bias gradient and the batch-mean loss
+// (from per-row losses), written at loss_out[*step_ctr] (or [0]).
+struct FcBwdExtras {
+  float* dbias = nullptr;
+  float dbias_scale = 1.f;
+  const float* loss_rows = nullptr;
+  float* loss_out = nullptr;
+  const int* step_ctr = nullptr;
+};
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
-            int B, long K, int NO, bool mask, hipStream_t s);
+            int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
 
 // ---- cross-entropy --------------------------------------------------------------------
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,
           const int* labels32, BatchIdx bi, float* logits_out, float* dlogits, float* loss_out,
           float* dbias, float gscale, float dbias_scale, hipStream_t s);
+
+void xent_rows(const float* part, int G, const float* bias, int NO, int B, const int* labels32,
+               BatchIdx bi, float* dlogits, float* loss_rows, float gscale, hipStream_t s);
 
 // ---- optimizer / reductions -----------------------------------------------------------
 struct SgdArgs {

@@ -72,10 +72,24 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ d
                                                      const bf16_t* __restrict__ X,
                                                      const bf16_t* __restrict__ Wf,
                                                      bf16_t* __restrict__ dX, float* __restrict__ dW,
-                                                     float scale, int B, long K, int NO) {
+                                                     float scale, int B, long K, int NO,
+                                                     FcBwdExtras ex) {
   extern __shared__ __attribute__((aligned(16))) float s_dl[];  // [B][NO]
   for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
   __syncthreads();
+  if (blockIdx.x == 0) {
+    // fc bias gradient (sum over the batch, fixed order) and the batch-mean loss
+    if (ex.dbias && threadIdx.x < NO) {
+      float acc = 0.f;
+      for (int b = 0; b < B; ++b) acc += s_dl[b * NO + threadIdx.x];
+      ex.dbias[threadIdx.x] = acc * ex.dbias_scale;
+    }
+    if (ex.loss_rows && threadIdx.x == 64) {
+      float acc = 0.f;
+      for (int b = 0; b < B; ++b) acc += ex.loss_rows[b];
+      ex.loss_out[ex.step_ctr ? *ex.step_ctr : 0] = acc / (float)B;
+    }
+  }
   const long k = (long)blockIdx.x * 256 + threadIdx.x;
   if (k >= K) return;
   float w[FC_MAXO], dw[FC_MAXO];
@@ -84,37 +98,27 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ d
     w[o] = (o < NO) ? bf2f(Wf[(long)o * K + k]) : 0.f;
     dw[o] = 0.f;
   }
-  int b = 0;
-  for (; b + 4 <= B; b += 4) {
-    float xa[4];
+  // 32 rows per chunk: all activation loads of the chunk are issued before any math
+  for (int b0 = 0; b0 < B; b0 += 32) {
+    const int nb = min(32, B - b0);
+    float xa[32];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) xa[u] = bf2f(X[(long)(b + u) * K + k]);
+    for (int u = 0; u < 32; ++u) xa[u] = (u < nb) ? bf2f(X[(long)(b0 + u) * K + k]) : 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float* dl = s_dl + (b + u) * NO;
-      float dz = 0.f;
+    for (int u = 0; u < 32; ++u) {
+      if (u < nb) {
+        const float* dl = s_dl + (b0 + u) * NO;
+        float dz = 0.f;
 #pragma unroll
-      for (int o = 0; o < FC_MAXO; ++o)
-        if (o < NO) {
-          dz = fmaf(dl[o], w[o], dz);
-          dw[o] = fmaf(dl[o], xa[u], dw[o]);
-        }
-      if (MASK && !(xa[u] > 0.f)) dz = 0.f;
-      dX[(long)(b + u) * K + k] = f2bf(dz);
-    }
-  }
-  for (; b < B; ++b) {
-    const float xa = bf2f(X[(long)b * K + k]);
-    const float* dl = s_dl + b * NO;
-    float dz = 0.f;
-#pragma unroll
-    for (int o = 0; o < FC_MAXO; ++o)
-      if (o < NO) {
-        dz = fmaf(dl[o], w[o], dz);
-        dw[o] = fmaf(dl[o], xa, dw[o]);
+        for (int o = 0; o < FC_MAXO; ++o)
+          if (o < NO) {
+            dz = fmaf(dl[o], w[o], dz);
+            dw[o] = fmaf(dl[o], xa[u], dw[o]);
+          }
+        if (MASK && !(xa[u] > 0.f)) dz = 0.f;
+        dX[(long)(b0 + u) * K + k] = f2bf(dz);
       }
-    if (MASK && !(xa > 0.f)) dz = 0.f;
-    dX[(long)b * K + k] = f2bf(dz);
+    }
   }
 #pragma unroll
   for (int o = 0; o < FC_MAXO; ++o)
@@ -135,13 +139,13 @@ void fc_reduce(const float* part, const float* bias, float* out, int B, int G, i
 }
 
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
-            int B, long K, int NO, bool mask, hipStream_t s) {
+            int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
   const dim3 grid((unsigned)((K + 255) / 256));
   const size_t lds = sizeof(float) * B * NO;
   if (mask)
-    hipLaunchKernelGGL(fc_bwd_kernel<true>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO);
+    hipLaunchKernelGGL(fc_bwd_kernel<true>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex);
   else
-    hipLaunchKernelGGL(fc_bwd_kernel<false>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO);
+    hipLaunchKernelGGL(fc_bwd_kernel<false>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex);
 }
 
 }  // namespace ddp_amd

@@ -55,24 +55,40 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   if (step_ctr && blockIdx.x == 0 && threadIdx.x == 0) step_ctr[0] += 1;
 }
 
+// Block = 64 consecutive outputs x 4 row groups: thread (c, g) sums rows g, g+4, ...
+// (8 loads in flight), then the 4 group sums are added in fixed order via LDS.
 __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int k = 0; k < ss.count; ++k) {
+  __shared__ float part[4][64];
+  const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  // segments are laid out back to back, each padded to a multiple of 64 outputs, so
+  // a block (64 outputs) never straddles two segments
+  long i = (long)blockIdx.x * 64 + c;
+  int k = 0;
+  for (; k < ss.count; ++k) {
+    const long padded = (ss.s[k].n + 63) / 64 * 64;
+    if (i < padded) break;
+    i -= padded;
+  }
+  const bool live = k < ss.count && i < ss.s[k].n;
+  float acc = 0.f;
+  if (live) {
     const SlabSeg& sg = ss.s[k];
-    if (i < sg.n) {
-      const float* src = sg.slab + sg.src_off + i;
-      float acc = 0.f;
-      int r = 0;
-      for (; r + 4 <= sg.rows; r += 4) {  // 4 independent loads in flight, fixed order
-        const float a0 = src[(long)r * sg.row_stride], a1 = src[(long)(r + 1) * sg.row_stride];
-        const float a2 = src[(long)(r + 2) * sg.row_stride], a3 = src[(long)(r + 3) * sg.row_stride];
-        acc = (((acc + a0) + a1) + a2) + a3;
-      }
-      for (; r < sg.rows; ++r) acc += src[(long)r * sg.row_stride];
-      sg.dst[i] = acc * sg.scale;
-      return;
+    const float* src = sg.slab + sg.src_off + i;
+    float a[8];
+    int r = grp;
+    for (; r + 28 < sg.rows; r += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = src[(long)(r + 4 * u) * sg.row_stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += a[u];
     }
-    i -= sg.n;
+    for (; r < sg.rows; r += 4) acc += src[(long)r * sg.row_stride];
+  }
+  part[grp][c] = acc;
+  __syncthreads();
+  if (grp == 0 && live) {
+    const SlabSeg& sg = ss.s[k];  // k is block-uniform
+    sg.dst[i] = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
   }
 }
 
@@ -91,10 +107,10 @@ void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, c
 }
 
 void grad_reduce(const SlabSet& ss, hipStream_t s) {
-  long total = 0;
-  for (int k = 0; k < ss.count; ++k) total += ss.s[k].n;
-  if (total == 0) return;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ss);
+  long blocks = 0;
+  for (int k = 0; k < ss.count; ++k) blocks += (ss.s[k].n + 63) / 64;
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(grad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ss);
 }
 
 void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s) {

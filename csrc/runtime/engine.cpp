@@ -29,7 +29,7 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   if (cfg_.C1 != 32) throw std::runtime_error("engine: fused conv1 wgrad needs C1 == 32");
   if (cfg_.C2 % 64 != 0) throw std::runtime_error("engine: C2 must be a multiple of 64");
   if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
-  if (cfg_.NO > 16) throw std::runtime_error("engine: at most 16 classes");
+  if (cfg_.NO != 10) throw std::runtime_error("engine: the fused fc epilogue is built for 10 classes");
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
@@ -84,10 +84,16 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   conv3x3_fwd(b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true, b_.wfc_bf16,
               b_.fc_part, NO, cfg_.pxt_fwd, cs_);
   // ---- loss + fc backward (bucket 0)
-  xent(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, nullptr, b_.labels, bi, nullptr, b_.dlogits,
-       b_.loss_hist, G + b_.off_bfc, 1.f / (float)B, inv_ws, cs_);
+  xent_rows(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits, b_.loss_rows,
+            1.f / (float)B, cs_);
+  FcBwdExtras ex;
+  ex.dbias = G + b_.off_bfc;  // fc bias grad (bucket 0), prescaled
+  ex.dbias_scale = inv_ws;
+  ex.loss_rows = b_.loss_rows;
+  ex.loss_out = b_.loss_hist;  // per-epoch history, indexed by the step counter
+  ex.step_ctr = b_.step_ctr;
   fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
-         /*mask=*/true, cs_);
+         /*mask=*/true, cs_, ex);
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));

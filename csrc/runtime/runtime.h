@@ -109,7 +109,7 @@ struct EngineBuffers {
   bf16_t *w2_bf16, *w2t_bf16, *wfc_bf16;
   // activations / scratch (sized for max batch)
   bf16_t *a1, *a2, *dz2, *dz1;
-  float *fc_part, *dlogits, *loss_hist, *w2slab, *w1slab;
+  float *fc_part, *dlogits, *loss_rows, *loss_hist, *w2slab, *w1slab;
   int* step_ctr;
   // data
   const unsigned char* images;  // u8 [N][H*W]

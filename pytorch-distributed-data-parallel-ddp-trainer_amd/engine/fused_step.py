@@ -77,7 +77,7 @@ class FusedSimpleCNNEngine:
             wfc_bf16=e(10 * HW * 64, dt=BF16),
             a1=e(B * HW * 32, dt=BF16), a2=e(B * HW * 64, dt=BF16),
             dz2=e(B * HW * 64, dt=BF16), dz1=e(B * HW * 32, dt=BF16),
-            fc_part=e(B * (HW // 16) * 10), dlogits=e(B * 10),
+            fc_part=e(B * (HW // 16) * 10), dlogits=e(B * 10), loss_rows=e(B),
             loss_hist=torch.zeros(self.steps_per_epoch + 1, device=dev),
             w2slab=e(self.C.conv3x3_wgrad_blocks(B, 28, R) * (64 * 9 * 32 + 64)),
             w1slab=e(self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_dgrad) * 320),

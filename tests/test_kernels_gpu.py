@@ -75,11 +75,26 @@ def test_conv3x3_fwd_fused_fc(C, B):
     wfc = rnd(10, H * W, 64, scale=0.01, seed=6)
     bfc = (torch.randn(10) * 0.1).to(dev)
     y = torch.empty(B, H, W, 64, dtype=BF, device=dev)
-    part = torch.full((B, H * W // 16, 10), float("nan"), device=dev)
+    part = torch.full((B, 10, H * W // 16), float("nan"), device=dev)
     C.conv3x3_fwd(x, w, b, y, True, wfc, part, 10, 2)
-    logits = part.sum(1) + bfc
+    logits = part.sum(2) + bfc
     ref = R.fc_nhwc(y.float(), wfc.float(), bfc)  # the fc of exactly the stored bf16 activation
     close(logits, ref, rtol=1e-3, atol=1e-3)
+    # engine cross-entropy over those [B][10][49] partials (+ fc bias grad / mean loss in fc_bwd)
+    labels = torch.randint(0, 10, (B,)).to(torch.int32).to(dev)
+    dl = torch.empty(B, 10, device=dev)
+    rows = torch.empty(B, device=dev)
+    C.xent_rows(part, 49, bfc, labels, None, dl, rows, 1.0 / B)
+    rl, rd = R.cross_entropy(ref, labels.long())
+    close(dl, rd, rtol=1e-4, atol=1e-6)
+    close(rows.mean(), rl, rtol=1e-5, atol=1e-5)
+    dx = torch.empty_like(y)
+    dw = torch.empty(10, 28 * 28, 64, device=dev)
+    db = torch.empty(10, device=dev)
+    loss = torch.zeros(3, device=dev)
+    C.fc_bwd(dl, y, wfc, dx, dw, 0.5, True, db, rows, loss)
+    close(db, 0.5 * rd.sum(0), rtol=1e-5, atol=1e-7)
+    close(loss[0], rl, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("mask_dy,mask_x", [(True, False), (False, True), (True, True), (False, False)])
