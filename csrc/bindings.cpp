@@ -277,12 +277,15 @@ void op_sgd(Tensor& p, const Tensor& g, std::optional<Tensor> mbuf, double lr, d
             const py::list& shadows) {
   check(p, "params", at::kFloat); check(g, "grads", at::kFloat);
   TORCH_CHECK(p.numel() == g.numel(), "sgd: param/grad size mismatch");
+  TORCH_CHECK(((uintptr_t)p.data_ptr() & 15) == 0 && ((uintptr_t)g.data_ptr() & 15) == 0,
+              "sgd: params/grads must be 16-byte aligned");
   float* mb = nullptr;
   if (momentum != 0.0) {
     TORCH_CHECK(mbuf.has_value(), "sgd: momentum buffer required");
     check(*mbuf, "momentum", at::kFloat);
     TORCH_CHECK(mbuf->numel() == p.numel(), "sgd: momentum size");
     mb = mbuf->data_ptr<float>();
+    TORCH_CHECK(((uintptr_t)mb & 15) == 0, "sgd: momentum buffer must be 16-byte aligned");
   }
   SgdArgs a{(float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, maximize,
             first_step, update};
@@ -425,6 +428,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.dampening = cfgd["dampening"].cast<float>();
              c.weight_decay = cfgd["weight_decay"].cast<float>();
              c.nesterov = cfgd["nesterov"].cast<bool>(); c.maximize = cfgd["maximize"].cast<bool>();
+             c.force_allreduce = cfgd.contains("force_allreduce") ? cfgd["force_allreduce"].cast<bool>() : false;
              auto T = [&](const char* k) { return t[k].cast<Tensor>(); };
              auto need = [&](const char* k, at::ScalarType st, long n) {
                Tensor x = T(k);

@@ -15,40 +15,84 @@
 
 namespace ddp_amd {
 
+__device__ __forceinline__ float sgd_one(float v, float d, float* mb, const SgdArgs& a) {
+  if (a.maximize) d = -d;
+  if (a.weight_decay != 0.f) d = fmaf(a.weight_decay, v, d);
+  if (a.momentum != 0.f) {
+    const float buf = a.first_step ? d : fmaf(1.f - a.dampening, d, a.momentum * (*mb));
+    *mb = buf;
+    d = a.nesterov ? fmaf(a.momentum, buf, d) : buf;
+  }
+  return fmaf(-a.lr, d, v);
+}
+
+// 4 consecutive elements per thread (16-byte loads/stores); n4 = n / 4 quads, the
+// (n % 4) tail is handled by the first threads of block 0.
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ mbuf, long n, SgdArgs a,
                                                   ShadowSet sh, int* __restrict__ step_ctr) {
+  const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float v = p[i];
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+    const long i = q << 2;
+    float4 v = reinterpret_cast<const float4*>(p)[q];
     if (a.update) {
-      float d = g[i];
-      if (a.maximize) d = -d;
-      if (a.weight_decay != 0.f) d = fmaf(a.weight_decay, v, d);
-      if (a.momentum != 0.f) {
-        float buf;
-        if (a.first_step) buf = d;
-        else buf = fmaf(1.f - a.dampening, d, a.momentum * mbuf[i]);
-        mbuf[i] = buf;
-        d = a.nesterov ? fmaf(a.momentum, buf, d) : buf;
-      }
-      v = fmaf(-a.lr, d, v);
-      p[i] = v;
+      const float4 d = reinterpret_cast<const float4*>(g)[q];
+      float4 m = {0.f, 0.f, 0.f, 0.f};
+      if (a.momentum != 0.f) m = reinterpret_cast<const float4*>(mbuf)[q];
+      v.x = sgd_one(v.x, d.x, &m.x, a);
+      v.y = sgd_one(v.y, d.y, &m.y, a);
+      v.z = sgd_one(v.z, d.z, &m.z, a);
+      v.w = sgd_one(v.w, d.w, &m.w, a);
+      reinterpret_cast<float4*>(p)[q] = v;
+      if (a.momentum != 0.f) reinterpret_cast<float4*>(mbuf)[q] = m;
     }
 #pragma unroll
     for (int r = 0; r < MAX_SHADOWS; ++r) {
       if (r < sh.count) {
         const long j = i - sh.r[r].off;
-        if (j >= 0 && j < sh.r[r].n) {
-          if (sh.r[r].kind == SHADOW_BF16) {
-            sh.r[r].dst[j] = f2bf(v);
-          } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
-            const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
-            const long co = j / ((long)T * Ci);
-            const long rr = j - co * T * Ci;
-            sh.r[r].dst[rr * Co + co] = f2bf(v);
+        if (j + 3 >= 0 && j < sh.r[r].n) {
+          const float e[4] = {v.x, v.y, v.z, v.w};
+          if (sh.r[r].kind == SHADOW_BF16 && j >= 0 && j + 3 < sh.r[r].n && ((sh.r[r].off & 3) == 0)) {
+            *reinterpret_cast<uint2*>(sh.r[r].dst + j) = pack4(e[0], e[1], e[2], e[3]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const long jj = j + u;
+              if (jj < 0 || jj >= sh.r[r].n) continue;
+              if (sh.r[r].kind == SHADOW_BF16) {
+                sh.r[r].dst[jj] = f2bf(e[u]);
+              } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
+                const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
+                const long co = jj / ((long)T * Ci);
+                const long rr = jj - co * T * Ci;
+                sh.r[r].dst[rr * Co + co] = f2bf(e[u]);
+              }
+            }
           }
         }
+      }
+    }
+  }
+  // scalar tail
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long i = (n4 << 2) + threadIdx.x;
+    float v = p[i];
+    if (a.update) {
+      float m = (a.momentum != 0.f) ? mbuf[i] : 0.f;
+      v = sgd_one(v, g[i], &m, a);
+      p[i] = v;
+      if (a.momentum != 0.f) mbuf[i] = m;
+    }
+    for (int r = 0; r < sh.count; ++r) {
+      const long j = i - sh.r[r].off;
+      if (j < 0 || j >= sh.r[r].n) continue;
+      if (sh.r[r].kind == SHADOW_BF16) {
+        sh.r[r].dst[j] = f2bf(v);
+      } else {
+        const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
+        const long co = j / ((long)T * Ci);
+        sh.r[r].dst[(j - co * T * Ci) * Co + co] = f2bf(v);
       }
     }
   }
@@ -101,7 +145,8 @@ __global__ void scale_copy_kernel(float* __restrict__ dst, const float* __restri
 
 void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, const ShadowSet& sh,
               int* step_ctr, hipStream_t s) {
-  const long blocks = (n + 255) / 256;
+  // 16-byte accesses need 16-byte-aligned buffers (torch allocations and flat views are)
+  const long blocks = ((n >> 2) + 255) / 256;
   const unsigned grid = (unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048);
   hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, s, p, g, mbuf, n, a, sh, step_ctr);
 }

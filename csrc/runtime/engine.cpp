@@ -71,7 +71,7 @@ void SimpleCNNEngine::refresh_shadows() {
 void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   const int H = cfg_.H, W = cfg_.W, HW = H * W, C1 = cfg_.C1, C2 = cfg_.C2, NO = cfg_.NO;
   if (B <= 0 || B > cfg_.max_batch) throw std::runtime_error("engine: bad batch size");
-  const bool dist = comm_ && comm_->world() > 1;
+  const bool dist = comm_ && (comm_->world() > 1 || cfg_.force_allreduce);
   const float inv_ws = 1.f / (float)cfg_.world;
   BatchIdx bi{b_.idx, b_.step_ctr, stride, 0};
   bi.n_idx = b_.n_idx;

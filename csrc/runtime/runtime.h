@@ -124,6 +124,7 @@ struct EngineConfig {
   int world, rank;
   float lr, momentum, dampening, weight_decay;
   int nesterov, maximize;
+  int force_allreduce;  // run the bucket all-reduces even at world size 1 (tests)
 };
 
 class SimpleCNNEngine {

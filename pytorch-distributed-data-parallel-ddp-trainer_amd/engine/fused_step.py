@@ -38,6 +38,7 @@ class EngineOptions:
     pxt_dgrad: int = 2
     wgrad_rows: int | None = None
     bucket_cap_mb: float = 25.0
+    force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
 
 
 class FusedSimpleCNNEngine:
@@ -89,8 +90,10 @@ class FusedSimpleCNNEngine:
                    pxt_dgrad=self.opts.pxt_dgrad, wgrad_rows=R, world=world_size, rank=rank,
                    lr=float(g["lr"]), momentum=float(g["momentum"]),
                    dampening=float(g["dampening"]), weight_decay=float(g["weight_decay"]),
-                   nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]))
-        self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if world_size > 1 else None)
+                   nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
+                   force_allreduce=bool(self.opts.force_allreduce))
+        use_comm = world_size > 1 or self.opts.force_allreduce
+        self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:
             self.eng.set_momentum_started(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)
@@ -129,13 +132,17 @@ class FusedSimpleCNNEngine:
             self.t["step_ctr"].zero_()
             self.t["loss_hist"].zero_()
 
-    def run_epoch(self, epoch: int, on_loss=None, log_every: int = 100):
-        """Train one epoch; ``on_loss(batch_idx, loss)`` is called for batch_idx % log_every == 0."""
+    def run_epoch(self, epoch: int, on_loss=None, log_every: int = 100, max_steps: int | None = None):
+        """Train one epoch; ``on_loss(batch_idx, loss)`` is called for batch_idx % log_every == 0.
+
+        ``max_steps`` truncates the epoch (smoke runs, fault injection)."""
         self.sync_from_torch()
         self.start_epoch(epoch)
         n = len(self.sampler)
         B = self.B
         nfull, rem = divmod(n, B)
+        if max_steps is not None and max_steps < nfull + (1 if rem else 0):
+            nfull, rem = max_steps, 0
         done = 0
         pending = []  # (first_batch, last_batch_exclusive, event)
         if self.opt.momentum_buffer is not None and not self.opt.steps and nfull > 0:

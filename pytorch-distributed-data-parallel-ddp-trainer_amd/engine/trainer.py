@@ -45,6 +45,7 @@ class TrainOptions:
     num_workers: int = 2
     max_steps: int | None = None      # stop each epoch early (smoke tests)
     metrics_json: str | None = None   # append per-epoch throughput records here
+    fault: tuple | None = None        # (epoch, step, rank|-1): simulate a crash there (resume tests)
 
 
 def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
@@ -109,12 +110,17 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
             if rank == 0:
                 print(f"Epoch {epoch} | Batch {batch_idx} | Loss: {loss_value:.4f}", flush=True)
 
+        fault_step = _fault_step(opts.fault, epoch, rank)
         if fused:
-            nsteps = engine.run_epoch(epoch, on_loss=log, log_every=opts.log_every)
+            nsteps = engine.run_epoch(epoch, on_loss=log, log_every=opts.log_every,
+                                      max_steps=fault_step if fault_step is not None else opts.max_steps)
             engine.synchronize()
         else:
             nsteps = _run_module_epoch(ddp_model, loader, loss_fn, opt, device, log,
-                                       opts.log_every, opts.max_steps)
+                                       opts.log_every,
+                                       fault_step if fault_step is not None else opts.max_steps)
+        if fault_step is not None:
+            _inject_fault(rank, epoch, nsteps)
         if on_gpu:
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -126,6 +132,21 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
             dist.barrier()  # B13: nobody races past a half-written checkpoint
     cleanup()
     return model
+
+
+def _fault_step(fault, epoch, rank):
+    if not fault:
+        return None
+    fe, fs_, fr = (list(fault) + [-1])[:3]
+    return int(fs_) if int(fe) == epoch and int(fr) in (-1, rank) else None
+
+
+def _inject_fault(rank, epoch, step):
+    """Simulated hard failure: the rank dies without cleanup, as a crash
+    would; the launcher tears the job down and a re-run auto-resumes from the last
+    checkpoint."""
+    print(f"Rank {rank}: injected fault at epoch {epoch} step {step}", flush=True)
+    os._exit(17)
 
 
 def _verify_and_broadcast(fs, model, world_size):

@@ -113,3 +113,32 @@ def test_train_save_and_resume_ws2(tmp_path, capfd):
     assert sorted(os.listdir(ck)) == ["epoch_0.pt", "epoch_1.pt"]
     ck1 = torch.load(os.path.join(ck, "epoch_1.pt"), weights_only=True)
     assert ck1["epoch"] == 1
+
+
+def _worker_fault(rank, ws, port, ckdir, epochs, fault):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from ddp_amd.engine.trainer import TrainOptions, ddp_train
+
+    opts = TrainOptions(backend="gloo", checkpoint_dir=ckdir, max_steps=12, num_workers=0,
+                        log_every=1000, data="synthetic", fault=fault)
+    ddp_train(rank, ws, epochs, 32, opts)
+
+
+@pytest.mark.slow
+def test_fault_then_resume_is_byte_identical(tmp_path):
+    """BASELINE config 4 on CPU/gloo: crash mid-epoch, auto-resume, final checkpoint equals
+    the uninterrupted run's (every zip record except the random serialization_id)."""
+    import zipfile
+
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    mp.start_processes(_worker_fault, args=(2, free_port(), a, 3, None), nprocs=2,
+                       start_method="spawn", join=True)
+    with pytest.raises(Exception):
+        mp.start_processes(_worker_fault, args=(2, free_port(), b, 3, (1, 5, 1)), nprocs=2,
+                           start_method="spawn", join=True)
+    assert sorted(os.listdir(b)) == ["epoch_0.pt"]
+    mp.start_processes(_worker_fault, args=(2, free_port(), b, 3, None), nprocs=2,
+                       start_method="spawn", join=True)
+    za, zb = zipfile.ZipFile(os.path.join(a, "epoch_2.pt")), zipfile.ZipFile(os.path.join(b, "epoch_2.pt"))
+    diff = [i.filename for i in za.infolist() if za.read(i.filename) != zb.read(i.filename)]
+    assert set(diff) <= {"epoch_2/.data/serialization_id"}, diff

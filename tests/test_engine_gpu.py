@@ -109,3 +109,36 @@ def test_module_ddp_world1_rccl(tmp_path):
         assert ddp.allreduce_buckets_launched == 2
     finally:
         dist.destroy_process_group()
+
+
+def test_engine_rccl_allreduce_inside_graph_world1():
+    """Bucket all-reduces on the comm stream, captured in the hipGraph with their events
+    (RCCL at world size 1 is the identity): bitwise equal to the comm-free run."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import free_port, native_comm
+
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            init_method=f"tcp://127.0.0.1:{free_port()}",
+                            device_id=torch.device("cuda", 0))
+    try:
+        comm = native_comm()
+        imgs, labels = synthetic_mnist(2048)
+        data = DeviceMNIST(imgs, labels, dev)
+        out = []
+        for force in (False, True):
+            torch.manual_seed(0)
+            m = SimpleCNN().to(dev)
+            e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01), data, 32, 1, 0, comm,
+                                     EngineOptions(graph_steps=5, force_allreduce=force))
+            e.refresh()
+            e.run_steps(10)
+            e.synchronize()
+            out.append(e.fs.params.clone())
+        assert torch.equal(out[0], out[1])
+    finally:
+        dist.destroy_process_group()

@@ -45,6 +45,8 @@ def parse_args(argv=None):
     p.add_argument("--num_workers", type=int, default=2, help="CPU DataLoader workers")
     p.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch (module/CPU path)")
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
+    p.add_argument("--fault_at", default=None, metavar="EPOCH:STEP[:RANK]",
+                   help="simulate a crash (os._exit) at that step; re-run to auto-resume")
     return p.parse_args(argv)
 
 
@@ -55,7 +57,8 @@ def main(argv=None):
                         checkpoint_dir=a.checkpoint_dir, save=not a.no_save, seed=a.seed,
                         log_every=a.log_every, graph_steps=a.graph_steps,
                         bucket_cap_mb=a.bucket_cap_mb, num_workers=a.num_workers,
-                        max_steps=a.max_steps, metrics_json=a.metrics_json)
+                        max_steps=a.max_steps, metrics_json=a.metrics_json,
+                        fault=tuple(int(v) for v in a.fault_at.split(":")) if a.fault_at else None)
     launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
 
 
