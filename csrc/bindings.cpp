@@ -257,6 +257,173 @@ void op_xent_rows(const Tensor& part, int G, const Tensor& bias, const Tensor& l
   kcheck();
 }
 
+// ------------------------------------------------------------------ ResNet ops
+ConvGeom geom_of(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, int pad) {
+  TORCH_CHECK(X.dim() == 4 && Y.dim() == 4, "NHWC 4-d tensors expected");
+  ConvGeom g{(int)X.size(0), (int)X.size(1), (int)X.size(2), (int)X.size(3), (int)Y.size(1),
+             (int)Y.size(2), (int)Y.size(3), KH, KW, stride, pad};
+  TORCH_CHECK(Y.size(0) == X.size(0), "batch mismatch");
+  TORCH_CHECK(g.OH == (g.H + 2 * pad - KH) / stride + 1 && g.OW == (g.W + 2 * pad - KW) / stride + 1,
+              "output spatial size does not match kernel/stride/pad");
+  return g;
+}
+
+void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> bias, Tensor& Y,
+                      int KH, int KW, int stride, int pad, bool relu, std::optional<Tensor> stats) {
+  check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(Y, "Y", at::kBFloat16);
+  const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
+  TORCH_CHECK(g.Cin % 32 == 0 || (g.Cin == 4 && g.Cout == 64), "conv_gemm: Cin % 32 (or stem Cin=4, Cout=64)");
+  TORCH_CHECK(g.Cout % 64 == 0, "conv_gemm: Cout % 64");
+  TORCH_CHECK(Wt.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm: weight shape");
+  const float* bp = nullptr;
+  if (bias) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == g.Cout, "bias"); bp = bias->data_ptr<float>(); }
+  float* st = nullptr;
+  if (stats) {
+    check(*stats, "stats", at::kFloat);
+    TORCH_CHECK(stats->numel() >= (long)conv_gemm_fwd_blocks(g) * 2 * g.Cout, "stats slab too small");
+    st = stats->data_ptr<float>();
+  }
+  conv_gemm_fwd(g, cbf(X), cbf(Wt), bp, bf(Y), relu, st, cur_stream());
+  kcheck();
+}
+
+void op_conv_gemm_dgrad(const Tensor& dY, const Tensor& WT, std::optional<Tensor> Xact, Tensor& dX,
+                        int KH, int KW, int stride, int pad) {
+  check(dY, "dY", at::kBFloat16); check(WT, "WT", at::kBFloat16); check(dX, "dX", at::kBFloat16);
+  const ConvGeom g = geom_of(dX, dY, KH, KW, stride, pad);
+  TORCH_CHECK(g.Cin % 64 == 0 && g.Cout % 32 == 0, "conv_gemm_dgrad: Cin % 64, Cout % 32");
+  TORCH_CHECK(WT.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm_dgrad: WT shape");
+  if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
+  conv_gemm_dgrad(g, cbf(dY), cbf(WT), obf(Xact, "Xact"), bf(dX), cur_stream());
+  kcheck();
+}
+
+int op_conv_gemm_wgrad_chunks(const Tensor& X, const Tensor& dY, int KH, int KW, int stride, int pad,
+                              int ppc) {
+  return conv_gemm_wgrad_chunks(geom_of(X, dY, KH, KW, stride, pad), ppc);
+}
+
+void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& slab, int KH, int KW, int stride,
+                        int pad, int ppc) {
+  check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(slab, "slab", at::kFloat);
+  const ConvGeom g = geom_of(X, dY, KH, KW, stride, pad);
+  TORCH_CHECK((g.Cin % 64 == 0 || g.Cin == 4) && g.Cout % 64 == 0, "conv_gemm_wgrad: Cin % 64 (or 4), Cout % 64");
+  TORCH_CHECK(ppc % 32 == 0 && ppc > 0, "pixels per chunk must be a multiple of 32");
+  TORCH_CHECK(slab.numel() >= (long)conv_gemm_wgrad_chunks(g, ppc) * g.Cout * KH * KW * g.Cin, "slab too small");
+  conv_gemm_wgrad(g, cbf(dY), cbf(X), slab.data_ptr<float>(), ppc, cur_stream());
+  kcheck();
+}
+
+void op_bn_finalize(const Tensor& slab, int nblk, int C, double count, double eps, double momentum,
+                    std::optional<Tensor> rmean, std::optional<Tensor> rvar, Tensor& mean, Tensor& invstd) {
+  check(slab, "slab", at::kFloat); check(mean, "mean", at::kFloat); check(invstd, "invstd", at::kFloat);
+  TORCH_CHECK(slab.numel() >= (long)nblk * 2 * C && mean.numel() == C && invstd.numel() == C, "bn_finalize sizes");
+  float *rm = nullptr, *rv = nullptr;
+  if (rmean) { check(*rmean, "running_mean", at::kFloat); check(*rvar, "running_var", at::kFloat); rm = rmean->data_ptr<float>(); rv = rvar->data_ptr<float>(); }
+  bn_finalize(slab.data_ptr<float>(), nblk, C, (float)count, (float)eps, (float)momentum, rm, rv,
+              mean.data_ptr<float>(), invstd.data_ptr<float>(), cur_stream());
+  kcheck();
+}
+
+void op_bn_apply(const Tensor& x, const Tensor& mean, const Tensor& invstd, const Tensor& gamma,
+                 const Tensor& beta, std::optional<Tensor> res, bool relu, Tensor& y) {
+  check(x, "x", at::kBFloat16); check(y, "y", at::kBFloat16);
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && y.sizes() == x.sizes(), "bn_apply: C % 8, y shape");
+  for (auto* t : {&mean, &invstd, &gamma, &beta}) { check(*t, "bn param", at::kFloat); TORCH_CHECK(t->numel() == C, "bn param size"); }
+  if (res) TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+  bn_apply(cbf(x), x.numel() / C, C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+           gamma.data_ptr<float>(), beta.data_ptr<float>(), obf(res, "res"), relu, bf(y), cur_stream());
+  kcheck();
+}
+
+int op_bn_bwd_blocks(long P, int rows) { return bn_bwd_blocks(P, rows); }
+
+void op_bn_bwd_reduce(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
+                      const Tensor& invstd, Tensor& slab, int rows) {
+  check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(slab, "slab", at::kFloat);
+  const int C = x.size(-1);
+  const long P = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0 && C <= 2048, "bn_bwd_reduce: C");
+  TORCH_CHECK(slab.numel() >= (long)bn_bwd_blocks(P, rows) * 2 * C, "slab too small");
+  if (out) TORCH_CHECK(out->sizes() == x.sizes(), "out shape");
+  bn_bwd_reduce(cbf(dout), obf(out, "out"), cbf(x), P, C, mean.data_ptr<float>(),
+                invstd.data_ptr<float>(), slab.data_ptr<float>(), rows, cur_stream());
+  kcheck();
+}
+
+void op_bn_bwd_apply(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
+                     const Tensor& invstd, const Tensor& gamma, const Tensor& sums, double count,
+                     Tensor& dx, std::optional<Tensor> dres) {
+  check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(dx, "dx", at::kBFloat16);
+  check(sums, "sums", at::kFloat);
+  const int C = x.size(-1);
+  TORCH_CHECK(sums.numel() == 2 * C && dx.sizes() == x.sizes(), "bn_bwd_apply sizes");
+  bf16_t* dr = nullptr;
+  if (dres) { check(*dres, "dres", at::kBFloat16); TORCH_CHECK(dres->sizes() == x.sizes(), "dres"); dr = bf(*dres); }
+  bn_bwd_apply(cbf(dout), obf(out, "out"), cbf(x), x.numel() / C, C, mean.data_ptr<float>(),
+               invstd.data_ptr<float>(), gamma.data_ptr<float>(), sums.data_ptr<float>(),
+               (float)count, bf(dx), dr, cur_stream());
+  kcheck();
+}
+
+void op_maxpool_fwd(const Tensor& x, Tensor& y, Tensor& amax) {
+  check(x, "x", at::kBFloat16); check(y, "y", at::kBFloat16); check(amax, "amax", at::kByte);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), OH = y.size(1), OW = y.size(2);
+  TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && y.size(3) == C, "maxpool 3x3/s2/p1 shape");
+  TORCH_CHECK(amax.numel() == y.numel(), "amax size");
+  maxpool_fwd(cbf(x), N, H, W, C, OH, OW, bf(y), amax.data_ptr<unsigned char>(), cur_stream());
+  kcheck();
+}
+
+void op_maxpool_bwd(const Tensor& dy, const Tensor& amax, Tensor& dx) {
+  check(dy, "dy", at::kBFloat16); check(dx, "dx", at::kBFloat16); check(amax, "amax", at::kByte);
+  const int N = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3), OH = dy.size(1), OW = dy.size(2);
+  TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && amax.numel() == dy.numel(), "maxpool bwd shape");
+  maxpool_bwd(cbf(dy), amax.data_ptr<unsigned char>(), N, H, W, C, OH, OW, bf(dx), cur_stream());
+  kcheck();
+}
+
+void op_avgpool_fwd(const Tensor& x, Tensor& y) {
+  check(x, "x", at::kBFloat16); check(y, "y", at::kFloat);
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  TORCH_CHECK(y.numel() == (long)N * C, "avgpool out size");
+  avgpool_fwd(cbf(x), N, HW, C, y.data_ptr<float>(), cur_stream());
+  kcheck();
+}
+
+void op_avgpool_bwd(const Tensor& dy, Tensor& dx) {
+  check(dy, "dy", at::kFloat); check(dx, "dx", at::kBFloat16);
+  const int N = dx.size(0), HW = dx.size(1) * dx.size(2), C = dx.size(3);
+  TORCH_CHECK(dy.numel() == (long)N * C, "avgpool dy size");
+  avgpool_bwd(dy.data_ptr<float>(), N, HW, C, bf(dx), cur_stream());
+  kcheck();
+}
+
+// C[M][N] = alpha * A(m,k) B(k,n) + bias; strides in elements (A/B: fp32 or bf16)
+void op_sgemm(int M, int N, int K, const Tensor& A, long sam, long sak, const Tensor& B, long sbk,
+              long sbn, Tensor& Cm, std::optional<Tensor> bias, double alpha) {
+  check_cuda(A, "A"); check_cuda(B, "B"); check(Cm, "C", at::kFloat);
+  const bool abf = A.scalar_type() == at::kBFloat16, bbf = B.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(abf || A.scalar_type() == at::kFloat, "A dtype");
+  TORCH_CHECK(bbf || B.scalar_type() == at::kFloat, "B dtype");
+  TORCH_CHECK((long)(M - 1) * sam + (long)(K - 1) * sak < A.numel(), "A bounds");
+  TORCH_CHECK((long)(K - 1) * sbk + (long)(N - 1) * sbn < B.numel(), "B bounds");
+  TORCH_CHECK(Cm.numel() >= (long)M * N, "C size");
+  const float* bp = nullptr;
+  if (bias) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == N, "bias"); bp = bias->data_ptr<float>(); }
+  sgemm(M, N, K, A.data_ptr(), abf, sam, sak, B.data_ptr(), bbf, sbk, sbn, Cm.data_ptr<float>(), N,
+        bp, (float)alpha, cur_stream());
+  kcheck();
+}
+
+void op_transpose_w(const Tensor& w, Tensor& wt) {
+  check(w, "w", at::kFloat); check(wt, "wt", at::kBFloat16);
+  TORCH_CHECK(w.dim() == 4 && wt.numel() == w.numel(), "transpose_w: OHWI weight expected");
+  transpose_w(w.data_ptr<float>(), w.size(0), w.size(1) * w.size(2), w.size(3), bf(wt), cur_stream());
+  kcheck();
+}
+
 ShadowSet make_shadows(const py::list& shadows) {
   ShadowSet sh{};
   TORCH_CHECK((int)shadows.size() <= MAX_SHADOWS, "too many shadow regions");
@@ -363,6 +530,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_reduce", &op_grad_reduce);
   m.def("scale_copy", &op_scale_copy);
   m.def("_mark_exiting", &ddp_amd::mark_exiting);
+  m.def("conv_gemm_fwd", &op_conv_gemm_fwd);
+  m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad);
+  m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
+  m.def("conv_gemm_wgrad", &op_conv_gemm_wgrad);
+  m.def("conv_gemm_fwd_blocks", [](const Tensor& X, const Tensor& Y, int KH, int KW, int s, int p) {
+    return conv_gemm_fwd_blocks(geom_of(X, Y, KH, KW, s, p));
+  });
+  m.def("bn_finalize", &op_bn_finalize);
+  m.def("bn_apply", &op_bn_apply);
+  m.def("bn_bwd_blocks", &op_bn_bwd_blocks);
+  m.def("bn_bwd_reduce", &op_bn_bwd_reduce);
+  m.def("bn_bwd_apply", &op_bn_bwd_apply);
+  m.def("maxpool_fwd", &op_maxpool_fwd);
+  m.def("maxpool_bwd", &op_maxpool_bwd);
+  m.def("avgpool_fwd", &op_avgpool_fwd);
+  m.def("avgpool_bwd", &op_avgpool_bwd);
+  m.def("sgemm", &op_sgemm);
+  m.def("transpose_w", &op_transpose_w);
   m.def("rccl_version", []() { int v = 0; ncclGetVersion(&v); return v; });
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")

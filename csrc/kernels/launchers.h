@@ -30,6 +30,43 @@ size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1);
 void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
                    int H, int W, int Cin, int Cout, int R, hipStream_t s);
 
+// ---- general NHWC implicit-GEMM convolution (conv_gemm.hip) ------------------------
+struct ConvGeom {
+  int N, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad;
+};
+int conv_gemm_fwd_blocks(const ConvGeom& g);
+void conv_gemm_fwd(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias,
+                   bf16_t* Y, bool relu, float* stats, hipStream_t s);
+void conv_gemm_dgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* WT, const bf16_t* Xact,
+                     bf16_t* dX, hipStream_t s);
+int conv_gemm_wgrad_chunks(const ConvGeom& g, int px_per_chunk);
+void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* slab,
+                     int px_per_chunk, hipStream_t s);
+
+// ---- ResNet ops (resnet_ops.hip) -----------------------------------------------------
+void bn_finalize(const float* slab, int nblk, int C, float count, float eps, float momentum,
+                 float* running_mean, float* running_var, float* save_mean, float* save_invstd,
+                 hipStream_t s);
+void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* invstd,
+              const float* gamma, const float* beta, const bf16_t* res, bool relu, bf16_t* y,
+              hipStream_t s);
+int bn_bwd_blocks(long P, int rows);
+void bn_bwd_reduce(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C,
+                   const float* mean, const float* invstd, float* slab, int rows, hipStream_t s);
+void bn_bwd_apply(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C,
+                  const float* mean, const float* invstd, const float* gamma, const float* sums,
+                  float count, bf16_t* dx, bf16_t* dres, hipStream_t s);
+void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
+                 unsigned char* amax, hipStream_t s);
+void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
+                 int OW, bf16_t* dx, hipStream_t s);
+void avgpool_fwd(const bf16_t* x, int N, int HW, int C, float* y, hipStream_t s);
+void avgpool_bwd(const float* dy, int N, int HW, int C, bf16_t* dx, hipStream_t s);
+void sgemm(int M, int N, int K, const void* A, bool a_bf16, long sam, long sak, const void* B,
+           bool b_bf16, long sbk, long sbn, float* C, long ldc, const float* bias, float alpha,
+           hipStream_t s);
+void transpose_w(const float* w, int Co, int T, int Ci, bf16_t* wt, hipStream_t s);
+
 // ---- Linear over NHWC-flattened activations -----------------------------------------
 void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
                 hipStream_t s);
