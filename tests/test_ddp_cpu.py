@@ -142,3 +142,25 @@ def test_fault_then_resume_is_byte_identical(tmp_path):
     za, zb = zipfile.ZipFile(os.path.join(a, "epoch_2.pt")), zipfile.ZipFile(os.path.join(b, "epoch_2.pt"))
     diff = [i.filename for i in za.infolist() if za.read(i.filename) != zb.read(i.filename)]
     assert set(diff) <= {"epoch_2/.data/serialization_id"}, diff
+
+
+@pytest.mark.slow
+def test_cli_under_torchrun_2proc(tmp_path):
+    """BASELINE config 1: `torchrun --nproc_per_node=2 train_ddp.py` on CPU/gloo.  Exactly 2
+    trainer ranks (no nested self-spawn, reference bug B3), a checkpoint, clean exit."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(repo, "train_ddp.py"), "--epochs", "1", "--batch_size", "64",
+           "--max_steps", "15", "--num_workers", "0", "--data", "synthetic", "--log_every", "5"]
+    p = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    out = p.stdout
+    assert out.count("has initialized its process group with world size 2") == 2
+    assert "Rank 0 initialized" in out and "Rank 1 initialized" in out and "Rank 2" not in out
+    assert "Epoch 0 | Batch 10 | Loss:" in out
+    assert os.path.exists(tmp_path / "checkpoints" / "epoch_0.pt")
