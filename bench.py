@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--batch_size", type=int, default=32, help="per-rank batch (reference default 32)")
     ap.add_argument("--graph_steps", type=int, default=None)
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--fuse_level", type=int, default=None,
+                    help="engine fusion level (0: 8 kernels/step, 1: 6 kernels/step); default = engine default")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
@@ -89,8 +91,10 @@ def main():
     imgs, labels = synthetic_mnist()
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
     k = args.graph_steps or graph_chunk(args.steps)
-    eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm,
-                               EngineOptions(graph_steps=k, use_graph=not args.no_graph))
+    eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph)
+    if args.fuse_level is not None:
+        eo.fuse_level = args.fuse_level
+    eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
     eng.refresh()
     if not args.no_graph:
         eng.run_steps(0)           # uploads epoch 0's indices
@@ -136,7 +140,7 @@ def main():
                        "global_batch": ws * args.batch_size, "per_rank_batch": args.batch_size,
                        "seq_len": None, "image": "1x28x28", "parallelism": f"dp{ws}",
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
-                       "graph_steps": k, "params_finite": finite},
+                       "graph_steps": k, "fuse_level": eo.fuse_level, "params_finite": finite},
         }), flush=True)
     if ws > 1:
         dist.barrier(device_ids=[lrank])

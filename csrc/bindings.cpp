@@ -614,6 +614,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.weight_decay = cfgd["weight_decay"].cast<float>();
              c.nesterov = cfgd["nesterov"].cast<bool>(); c.maximize = cfgd["maximize"].cast<bool>();
              c.force_allreduce = cfgd.contains("force_allreduce") ? cfgd["force_allreduce"].cast<bool>() : false;
+             c.fuse_level = cfgd.contains("fuse_level") ? cfgd["fuse_level"].cast<int>() : 0;
+             TORCH_CHECK(c.fuse_level == 0 || c.fuse_level == 1, "engine: fuse_level must be 0 or 1");
+             TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0) <= 160 * 1024 &&
+                             conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0) <= 160 * 1024 &&
+                             conv3x3_dgrad_lds(c.W, c.C2, c.pxt_dgrad, true) <= 160 * 1024,
+                         "engine: LDS budget exceeded for this tiling");
              auto T = [&](const char* k) { return t[k].cast<Tensor>(); };
              auto need = [&](const char* k, at::ScalarType st, long n) {
                Tensor x = T(k);

@@ -73,6 +73,16 @@ __device__ __forceinline__ bf16x8 mask8(bf16x8 g, bf16x8 y) {
   return r;
 }
 
+// SimpleCNN conv1 (Cin = 1, 3x3): relu(b1[c] + sum_k w1[c*9+k] * v[k]) with exactly the
+// FMA order of conv1_fwd_kernel, so kernels that recompute a1 instead of reading it
+// from memory reproduce the stored bf16 values bit for bit.
+__device__ __forceinline__ float conv1_eval(const float* w1, const float* b1, const float* v, int c) {
+  float acc = b1[c];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc = fmaf(w1[c * 9 + k], v[k], acc);
+  return fmaxf(acc, 0.f);
+}
+
 // fixed-order butterfly sum over all 64 lanes (every lane gets the total)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -89,6 +99,39 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
   return v;
+}
+
+// Softmax cross-entropy of one row on one wave from split-K fc partials laid out
+// [NO][G] (part_row = part + b*NO*G): 4 lanes per class, fixed summation order.
+// Writes dl_row[c] = (softmax - onehot) * gscale (lanes with j == 0) and returns
+// the row loss (valid on every lane).  Shared by xent_rows and the XENT prologue of
+// fc_bwd so both produce bit-identical values.
+__device__ __forceinline__ float xent_row_wave(const float* __restrict__ part_row, int G,
+                                               const float* __restrict__ bias, int NO, int label,
+                                               float gscale, float* dl_row) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane >> 2, j = lane & 3;
+  const bool own = c < NO;
+  float s = 0.f;
+  if (own) {
+    const float* src = part_row + (long)c * G;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int g = j;
+    for (; g + 12 < G; g += 16) {  // 4 independent loads in flight
+      a0 += src[g]; a1 += src[g + 4]; a2 += src[g + 8]; a3 += src[g + 12];
+    }
+    for (; g < G; g += 4) a0 += src[g];
+    s = ((a0 + a1) + a2) + a3;
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  const float x = own ? s + bias[c] : -INFINITY;
+  const float mx = wave_max(x);
+  const float e = (own && j == 0) ? __expf(x - mx) : 0.f;
+  const float se = wave_sum(e);
+  const float xl = wave_sum((own && j == 0 && c == label) ? x : 0.f);
+  if (own && j == 0) dl_row[c] = (e / se - (c == label ? 1.f : 0.f)) * gscale;
+  return mx + __logf(se) - xl;
 }
 
 }  // namespace ddp_amd

@@ -59,13 +59,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
   }
   float o[8];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int co = cg * 8 + c;
-    float acc = s_w[Cout * 9 + co];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) acc = fmaf(s_w[co * 9 + k], v[k], acc);
-    o[c] = fmaxf(acc, 0.f);
-  }
+  for (int c = 0; c < 8; ++c) o[c] = conv1_eval(s_w, s_w + Cout * 9, v, cg * 8 + c);
   uint4 pk;
   uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
   pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;

@@ -56,11 +56,14 @@ __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
 // 16 distinct 4-bank groups (conflict-free ds_read_b128).
 
 // ---------------------------------------------------------------- forward
-template <int PXT, bool RELU, int NOF>
+// A1X: the input X is NOT read from memory but recomputed in the staging pass as
+// relu(conv1(x)) from the uint8 dataset (x0 via the batch index list) - SimpleCNN's
+// first layer folded into the second (Cin must equal conv1's 32 output channels).
+template <int PXT, bool RELU, int NOF, bool A1X>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     bf16_t* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
-    const bf16_t* __restrict__ wfc, float* __restrict__ fc_part) {
+    const bf16_t* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -79,13 +82,54 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
           [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
           [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sW + r * WS + c) = v; });
   const int xc = Cin / 8;
-  stage16(XR * xc,
-          [&](int i) {
-            const int r = i / xc, c = (i - r * xc) * 8;
-            const long P = Pbase + r;
-            return (P >= 0 && P < Ptot) ? ld8(X + P * Cin + c) : zero8();
-          },
-          [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
+  if (!A1X) {
+    stage16(XR * xc,
+            [&](int i) {
+              const int r = i / xc, c = (i - r * xc) * 8;
+              const long P = Pbase + r;
+              return (P >= 0 && P < Ptot) ? ld8(X + P * Cin + c) : zero8();
+            },
+            [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
+  } else {
+    // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), conv1 weights, then a1
+    float* sxx = reinterpret_cast<float*>(sX + XR * XS);
+    float* sw1 = sxx + XR + 2 * W + 2;
+    const int NXX = XR + 2 * W + 2;
+    const int base = c1.bi.base();
+    for (int r = threadIdx.x; r < NXX; r += 256) {
+      const long P = Pbase - W - 1 + r;
+      float v = 0.f;
+      if (P >= 0 && P < Ptot) {
+        const int n = (int)(P / HW), rm = (int)(P - (long)n * HW);
+        v = (float)c1.x[(long)c1.bi.row(n, base) * HW + rm] / 255.0f;
+      }
+      sxx[r] = v;
+    }
+    for (int i = threadIdx.x; i < Cin * 10; i += 256) sw1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
+    __syncthreads();
+    for (int i = threadIdx.x; i < XR * xc; i += 256) {
+      const int r = i / xc, c0 = (i - r * xc) * 8;
+      const long P = Pbase + r;
+      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (P >= 0 && P < Ptot) {
+        const int rm = (int)(P % HW);
+        const int hh = rm / W, ww = rm - (rm / W) * W;
+        float v[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int dh = k / 3 - 1, dw = k % 3 - 1;
+          const bool ok = (unsigned)(hh + dh) < (unsigned)H && (unsigned)(ww + dw) < (unsigned)W;
+          v[k] = ok ? sxx[r + W + 1 + dh * W + dw] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = conv1_eval(sw1, sw1 + Cin * 9, v, c0 + j);
+      }
+      uint4 pk;
+      const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
+      pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
+      *reinterpret_cast<uint4*>(sX + r * XS + c0) = pk;
+    }
+  }
 
   const int kofs = 8 * (lane >> 4);
   const int col = lane & 15;
@@ -192,11 +236,13 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
 }
 
 // ---------------------------------------------------------------- data gradient
-template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1>
+// A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
+// being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
+template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X>
 __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
     const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
-    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab) {
+    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -251,7 +297,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
   int h[PXT], w[PXT], rowc[PXT];
   bool valid[PXT];
   long Pp[PXT];
-  uint2 xa[PXT][2];
+  uint2 xa[PXT][2] = {};
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     const int lp = (wave * PXT + pt) * 16 + col;
@@ -263,7 +309,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     h[pt] = rm / W;
     w[pt] = rm - h[pt] * W;
     rowc[pt] = lp + W + 1;
-    if (MASK_X) {  // prefetch the ReLU-input mask (lands during the MFMAs)
+    if (MASK_X && !A1X) {  // prefetch the ReLU-input mask (lands during the MFMAs)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
         xa[pt][t] = *reinterpret_cast<const uint2*>(Xact + Pc * Cin + ci_blk + 16 * t + 4 * (lane >> 4));
@@ -322,7 +368,10 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     for (int t = 0; t < 2; ++t) {
       const int ci = ci_blk + 16 * t + 4 * (lane >> 4);
       float v[4] = {acc[pt][t][0], acc[pt][t][1], acc[pt][t][2], acc[pt][t][3]};
-      if (MASK_X) {
+      if (MASK_X && A1X) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (bf2f(f2bf(conv1_eval(c1.w, c1.b, xv, ci + j))) > 0.f) ? v[j] : 0.f;
+      } else if (MASK_X) {
         float xm[4];
         unpack4(xa[pt][t], xm);
 #pragma unroll
@@ -377,10 +426,12 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // K index of a K-step (32 slots) for lane group g, element j:
 //   slot = 4g + j (j<4),  16 + 4g + (j-4) (j>=4)   (same map for both operands)
 // so the two 16-lane groups of a half-wave read 8 consecutive rows (conflict-free).
-template <bool MASK_DY>
+// A1X: the X tile (a1 rows r0-1 .. r0+R) is recomputed from the uint8 images (rows
+// r0-2 .. r0+R+1) instead of being read from a stored a1 tensor.
+template <bool MASK_DY, bool A1X>
 __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
-    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R) {
+    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nRC = (H + R - 1) / R;
@@ -412,18 +463,51 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
             const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
             *reinterpret_cast<bf16x8*>(sdY + (long)slot * DS + ch) = v;
           });
-  stage16((R + 2) * XW * cpy_x,
-          [&](int i) {
-            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
-            const int rr = pos / XW, cc = pos - (pos / XW) * XW;
-            const int hh = r0 - 1 + rr, ww = cc - 1;
-            return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                       ? ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
-          },
-          [&](int i, bf16x8 v) {
-            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
-            *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
-          });
+  if (!A1X) {
+    stage16((R + 2) * XW * cpy_x,
+            [&](int i) {
+              const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+              const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+              const int hh = r0 - 1 + rr, ww = cc - 1;
+              return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                         ? ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
+            },
+            [&](int i, bf16x8 v) {
+              const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+              *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
+            });
+  } else {
+    // uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, conv1 weights, then a1
+    const int XW2 = Wp + 4, XR2 = R + 4;
+    float* sxx = reinterpret_cast<float*>(sX + (long)(R + 2) * XW * XS);
+    float* sw1 = sxx + XR2 * XW2;
+    const long img = (long)c1.bi.row(n, c1.bi.base()) * H * W;
+    for (int i = threadIdx.x; i < XR2 * XW2; i += 256) {
+      const int rr = i / XW2, cc = i - (i / XW2) * XW2;
+      const int hh = r0 - 2 + rr, ww = cc - 2;
+      sxx[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                   ? (float)c1.x[img + hh * W + ww] / 255.0f : 0.f;
+    }
+    for (int i = threadIdx.x; i < Cin * 10; i += 256) sw1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
+    __syncthreads();
+    for (int i = threadIdx.x; i < (R + 2) * XW * cpy_x; i += 256) {
+      const int pos = i / cpy_x, c0 = (i - pos * cpy_x) * 8;
+      const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+      const int hh = r0 - 1 + rr, ww = cc - 1;
+      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) {
+        float v[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) v[k] = sxx[(rr + k / 3) * XW2 + cc + k % 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = conv1_eval(sw1, sw1 + Cin * 9, v, c0 + j);
+      }
+      uint4 pk;
+      const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
+      pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
+      *reinterpret_cast<uint4*>(sX + (long)pos * XS + c0) = pk;
+    }
+  }
   __syncthreads();
 
   // ---- wave assignment: (pair of 16-wide co tiles) x (16-wide ci tile)
@@ -488,8 +572,10 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 }
 
 // ---------------------------------------------------------------- launchers
-size_t conv3x3_fwd_lds(int W, int Cin, int pxt) {
-  return sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 8) + (size_t)(64 * pxt + 2 * W + 2) * (Cin + 8));
+size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x) {
+  const size_t XR = 64 * pxt + 2 * W + 2;
+  return sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 8) + XR * (Cin + 8)) +
+         (a1x ? sizeof(float) * ((XR + 2 * W + 2) + Cin * 10) : 0);
 }
 
 size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
@@ -500,17 +586,21 @@ size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
 
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s) {
+                 int pxt, hipStream_t s, const C1Src* c1) {
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cout / 64);
-  const size_t lds = conv3x3_fwd_lds(W, Cin, pxt);
+  const bool a1x = c1 != nullptr;
+  const size_t lds = conv3x3_fwd_lds(W, Cin, pxt, a1x);
   const bool fc = wfc != nullptr;  // host guarantees NO == 10 when fused
-#define LF(PX, RL, NF) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF>), grid, dim3(256), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part)
+  const C1Src cs = a1x ? *c1 : C1Src();
+#define LF(PX, RL, NF, AX) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF, AX>), grid, dim3(256), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs)
   if (pxt == 2) {
-    if (fc) LF(2, true, 10); else if (relu) LF(2, true, 0); else LF(2, false, 0);
+    if (fc && a1x) LF(2, true, 10, true);
+    else if (fc) LF(2, true, 10, false); else if (relu) LF(2, true, 0, false); else LF(2, false, 0, false);
   } else {
-    if (fc) LF(1, true, 10); else if (relu) LF(1, true, 0); else LF(1, false, 0);
+    if (fc && a1x) LF(1, true, 10, true);
+    else if (fc) LF(1, true, 10, false); else if (relu) LF(1, true, 0, false); else LF(1, false, 0, false);
   }
 #undef LF
   (void)NO;
@@ -518,25 +608,28 @@ void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y
 
 void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
                    bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
-                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s) {
+                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1) {
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cin / 32);
-  const bool mdy = Yact != nullptr, mx = Xact != nullptr, w1 = w1slab != nullptr;
+  const bool mdy = Yact != nullptr, mx = Xact != nullptr || c1 != nullptr, w1 = w1slab != nullptr;
   const size_t lds = conv3x3_dgrad_lds(W, Cout, pxt, w1);
-#define LD(PX, A, Bm, C) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C>), grid, dim3(256), lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab)
+  const C1Src cs = c1 ? *c1 : C1Src();
+#define LD(PX, A, Bm, C, AX) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C, AX>), grid, dim3(256), lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab, cs)
   if (pxt == 2) {
-    if (w1) LD(2, false, true, true);
-    else if (mdy && mx) LD(2, true, true, false);
-    else if (mdy) LD(2, true, false, false);
-    else if (mx) LD(2, false, true, false);
-    else LD(2, false, false, false);
+    if (w1 && c1) LD(2, false, true, true, true);
+    else if (w1) LD(2, false, true, true, false);
+    else if (mdy && mx) LD(2, true, true, false, false);
+    else if (mdy) LD(2, true, false, false, false);
+    else if (mx) LD(2, false, true, false, false);
+    else LD(2, false, false, false, false);
   } else {
-    if (w1) LD(1, false, true, true);
-    else if (mdy && mx) LD(1, true, true, false);
-    else if (mdy) LD(1, true, false, false);
-    else if (mx) LD(1, false, true, false);
-    else LD(1, false, false, false);
+    if (w1 && c1) LD(1, false, true, true, true);
+    else if (w1) LD(1, false, true, true, false);
+    else if (mdy && mx) LD(1, true, true, false, false);
+    else if (mdy) LD(1, true, false, false, false);
+    else if (mx) LD(1, false, true, false, false);
+    else LD(1, false, false, false, false);
   }
 #undef LD
 }
@@ -549,20 +642,22 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt) {
 
 int conv3x3_wgrad_blocks(int B, int H, int R) { return B * ((H + R - 1) / R); }
 
-size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R) {
+size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x) {
   const int Wp = (W + 7) & ~7;
   const int nslot = ((R * Wp + 31) / 32) * 32;
-  return sizeof(bf16_t) * ((size_t)nslot * (Cout + 16) + (size_t)(R + 2) * (Wp + 2) * (Cin + 16));
+  return sizeof(bf16_t) * ((size_t)nslot * (Cout + 16) + (size_t)(R + 2) * (Wp + 2) * (Cin + 16)) +
+         (a1x ? sizeof(float) * ((size_t)(R + 4) * (Wp + 4) + Cin * 10) : 0);
 }
 
 void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
-                   int H, int W, int Cin, int Cout, int R, hipStream_t s) {
+                   int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1) {
   const dim3 grid(conv3x3_wgrad_blocks(B, H, R), (Cout / 32) * (Cin / 16) / 4);
-  const size_t lds = conv3x3_wgrad_lds(W, Cin, Cout, R);
-  if (Yact)
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel<true>, grid, dim3(256), lds, s, dY, Yact, X, slab, B, H, W, Cin, Cout, R);
-  else
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel<false>, grid, dim3(256), lds, s, dY, Yact, X, slab, B, H, W, Cin, Cout, R);
+  const size_t lds = conv3x3_wgrad_lds(W, Cin, Cout, R, c1 != nullptr);
+  const C1Src cs = c1 ? *c1 : C1Src();
+#define LW(M, AX) hipLaunchKernelGGL((conv3x3_wgrad_kernel<M, AX>), grid, dim3(256), lds, s, dY, Yact, X, slab, B, H, W, Cin, Cout, R, cs)
+  if (c1) { if (Yact) LW(true, true); else LW(false, true); }
+  else { if (Yact) LW(true, false); else LW(false, false); }
+#undef LW
 }
 
 }  // namespace ddp_amd

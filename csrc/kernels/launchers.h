@@ -18,17 +18,17 @@ void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const bf16_t* dy, con
 // ---- 3x3 / s1 / p1 NHWC conv (MFMA) --------------------------------------------------
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s);
+                 int pxt, hipStream_t s, const C1Src* c1 = nullptr);
 void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
                    bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
-                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s);
+                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1 = nullptr);
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 int conv3x3_wgrad_blocks(int B, int H, int R);
-size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R);
-size_t conv3x3_fwd_lds(int W, int Cin, int pxt);
+size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false);
+size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x = false);
 size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1);
 void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
-                   int H, int W, int Cin, int Cout, int R, hipStream_t s);
+                   int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1 = nullptr);
 
 // ---- general NHWC implicit-GEMM convolution (conv_gemm.hip) ------------------------
 struct ConvGeom {
@@ -80,6 +80,14 @@ struct FcBwdExtras {
   const float* loss_rows = nullptr;
   float* loss_out = nullptr;
   const int* step_ctr = nullptr;
+  // XENT: compute dL (softmax cross-entropy backward) in the prologue of every block
+  // from the fused conv+fc partials [B][NO][G] instead of reading dL; loss_rows unused.
+  const float* part = nullptr;
+  int G = 0;
+  const float* fc_bias = nullptr;
+  const int* labels32 = nullptr;
+  BatchIdx bi{};
+  float gscale = 1.f;
 };
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());

@@ -67,15 +67,26 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __
   out[i] = s + (bias ? bias[o] : 0.f);
 }
 
-template <bool MASK>
+template <bool MASK, bool XENT>
 __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ dL,
                                                      const bf16_t* __restrict__ X,
                                                      const bf16_t* __restrict__ Wf,
                                                      bf16_t* __restrict__ dX, float* __restrict__ dW,
                                                      float scale, int B, long K, int NO,
                                                      FcBwdExtras ex) {
-  extern __shared__ __attribute__((aligned(16))) float s_dl[];  // [B][NO]
-  for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
+  extern __shared__ __attribute__((aligned(16))) float s_dl[];  // [B][NO] (+ [B] row losses)
+  if (XENT) {
+    // every block recomputes the (tiny) cross-entropy backward: B rows, one wave per row
+    const int base = ex.bi.base();
+    for (int b = threadIdx.x >> 6; b < B; b += 4) {
+      const int label = ex.labels32[ex.bi.row(b, base)];
+      const float l = xent_row_wave(ex.part + (long)b * NO * ex.G, ex.G, ex.fc_bias, NO, label,
+                                    ex.gscale, s_dl + b * NO);
+      if ((threadIdx.x & 63) == 0) s_dl[B * NO + b] = l;
+    }
+  } else {
+    for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
+  }
   __syncthreads();
   if (blockIdx.x == 0) {
     // fc bias gradient (sum over the batch, fixed order) and the batch-mean loss
@@ -84,9 +95,10 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ d
       for (int b = 0; b < B; ++b) acc += s_dl[b * NO + threadIdx.x];
       ex.dbias[threadIdx.x] = acc * ex.dbias_scale;
     }
-    if (ex.loss_rows && threadIdx.x == 64) {
+    if ((XENT || ex.loss_rows) && ex.loss_out && threadIdx.x == 64) {
+      const float* lr = XENT ? s_dl + B * NO : ex.loss_rows;
       float acc = 0.f;
-      for (int b = 0; b < B; ++b) acc += ex.loss_rows[b];
+      for (int b = 0; b < B; ++b) acc += lr[b];
       ex.loss_out[ex.step_ctr ? *ex.step_ctr : 0] = acc / (float)B;
     }
   }
@@ -141,11 +153,12 @@ void fc_reduce(const float* part, const float* bias, float* out, int B, int G, i
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
   const dim3 grid((unsigned)((K + 255) / 256));
-  const size_t lds = sizeof(float) * B * NO;
-  if (mask)
-    hipLaunchKernelGGL(fc_bwd_kernel<true>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex);
-  else
-    hipLaunchKernelGGL(fc_bwd_kernel<false>, grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex);
+  const bool xe = ex.part != nullptr;
+  const size_t lds = sizeof(float) * B * (NO + (xe ? 1 : 0));
+#define LB(M, XE) hipLaunchKernelGGL((fc_bwd_kernel<M, XE>), grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
+  if (xe) { if (mask) LB(true, true); else LB(false, true); }
+  else { if (mask) LB(true, false); else LB(false, false); }
+#undef LB
 }
 
 }  // namespace ddp_amd

@@ -31,4 +31,13 @@ struct BatchIdx {
   }
 };
 
+// Source of SimpleCNN's first-layer activation when a kernel recomputes it on the fly
+// (a1 = relu(conv1(x0[idx])) / bf16) instead of reading a stored a1 tensor.
+struct C1Src {
+  const unsigned char* x = nullptr;  // uint8 dataset [rows][H*W]
+  BatchIdx bi{};
+  const float* w = nullptr;          // conv1 weight [32][9]
+  const float* b = nullptr;          // conv1 bias [32]
+};
+
 }  // namespace ddp_amd

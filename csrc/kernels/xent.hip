@@ -102,33 +102,11 @@ __global__ __launch_bounds__(256) void xent_rows_kernel(const float* __restrict_
                                                         BatchIdx bi, float* __restrict__ dlogits,
                                                         float* __restrict__ loss_rows,
                                                         float gscale) {
-  const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
-  const int c = lane >> 2, j = lane & 3;
-  const bool own = c < NO;
-  float s = 0.f;
-  if (own) {
-    const float* src = part + ((long)b * NO + c) * G;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int g = j;
-    for (; g + 12 < G; g += 16) {  // 4 independent loads in flight
-      a0 += src[g]; a1 += src[g + 4]; a2 += src[g + 8]; a3 += src[g + 12];
-    }
-    for (; g < G; g += 4) a0 += src[g];
-    s = ((a0 + a1) + a2) + a3;
-  }
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  const float x = own ? s + bias[c] : -INFINITY;
-  const float mx = wave_max(x);
-  const float e = (own && j == 0) ? __expf(x - mx) : 0.f;
-  const float se = wave_sum(e);
   const int label = labels32[bi.row(b, bi.base())];
-  const float xl = wave_sum((own && j == 0 && c == label) ? x : 0.f);
-  if (own && j == 0)
-    dlogits[(long)b * NO + c] = (e / se - (c == label ? 1.f : 0.f)) * gscale;
-  if (lane == 0) loss_rows[b] = mx + __logf(se) - xl;
+  const float l = xent_row_wave(part + (long)b * NO * G, G, bias, NO, label, gscale, dlogits + (long)b * NO);
+  if ((threadIdx.x & 63) == 0) loss_rows[b] = l;
 }
 
 void xent_rows(const float* part, int G, const float* bias, int NO, int B, const int* labels32,

@@ -17,6 +17,11 @@
 //   sgd            wait both buckets; p -= lr*g over the flat buffer, bf16 shadows,
 //                  step counter += 1 (the next step's batch window)
 //
+// fuse_level 1 drops conv1_fwd and xent: conv3x3_fwd / dgrad / wgrad recompute
+// a1 = relu(conv1(x)) from the uint8 images in their LDS staging pass (C1Src) and
+// fc_bwd runs the softmax cross-entropy in its prologue -> 6 kernels per step,
+// bit-identical to level 0 (same FMA orders, same fixed-order reductions).
+//
 // Buckets follow the reference DDP's rebuilt layout:
 // bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB).
 #include "runtime/runtime.h"
@@ -79,19 +84,37 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   float* P = b_.params;
   float* G = b_.grads;
 
+  const bool f1 = cfg_.fuse_level >= 1;
+  C1Src c1;
+  c1.x = b_.images;
+  c1.bi = bi;
+  c1.w = P + b_.off_w1;
+  c1.b = P + b_.off_b1;
+  const C1Src* pc1 = f1 ? &c1 : nullptr;
+
   // ---- forward
-  conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
-  conv3x3_fwd(b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true, b_.wfc_bf16,
-              b_.fc_part, NO, cfg_.pxt_fwd, cs_);
+  if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
+  conv3x3_fwd(f1 ? nullptr : b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true,
+              b_.wfc_bf16, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1);
   // ---- loss + fc backward (bucket 0)
-  xent_rows(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits, b_.loss_rows,
-            1.f / (float)B, cs_);
+  if (!f1)
+    xent_rows(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits, b_.loss_rows,
+              1.f / (float)B, cs_);
   FcBwdExtras ex;
   ex.dbias = G + b_.off_bfc;  // fc bias grad (bucket 0), prescaled
   ex.dbias_scale = inv_ws;
   ex.loss_rows = b_.loss_rows;
   ex.loss_out = b_.loss_hist;  // per-epoch history, indexed by the step counter
   ex.step_ctr = b_.step_ctr;
+  if (f1) {
+    ex.loss_rows = nullptr;
+    ex.part = b_.fc_part;
+    ex.G = HW / 16;
+    ex.fc_bias = P + b_.off_bfc;
+    ex.labels32 = b_.labels;
+    ex.bi = bi;
+    ex.gscale = 1.f / (float)B;
+  }
   fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
          /*mask=*/true, cs_, ex);
   if (dist) {
@@ -101,9 +124,10 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
   }
   // ---- conv backward (bucket 1)
-  conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
-                b_.w1slab, cfg_.pxt_dgrad, cs_);
-  conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_);
+  conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, f1 ? nullptr : b_.a1, b_.dz1, B, H, W, C1, C2,
+                b_.images, true, bi, b_.w1slab, cfg_.pxt_dgrad, cs_, pc1);
+  conv3x3_wgrad(b_.dz2, nullptr, f1 ? nullptr : b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows,
+                cs_, pc1);
   SlabSet ss{};
   const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);

@@ -125,6 +125,10 @@ struct EngineConfig {
   float lr, momentum, dampening, weight_decay;
   int nesterov, maximize;
   int force_allreduce;  // run the bucket all-reduces even at world size 1 (tests)
+  // 0: 8 kernels (a1 materialised, separate cross-entropy kernel)
+  // 1: 6 kernels - conv1 recomputed inside conv2 fwd/dgrad/wgrad from the uint8
+  //    images (a1 never touches HBM) and cross-entropy folded into fc_bwd
+  int fuse_level = 0;
 };
 
 class SimpleCNNEngine {

@@ -39,6 +39,9 @@ class EngineOptions:
     wgrad_rows: int | None = None
     bucket_cap_mb: float = 25.0
     force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
+    # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
+    # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd)
+    fuse_level: int = 0
 
 
 class FusedSimpleCNNEngine:
@@ -91,7 +94,8 @@ class FusedSimpleCNNEngine:
                    lr=float(g["lr"]), momentum=float(g["momentum"]),
                    dampening=float(g["dampening"]), weight_decay=float(g["weight_decay"]),
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
-                   force_allreduce=bool(self.opts.force_allreduce))
+                   force_allreduce=bool(self.opts.force_allreduce),
+                   fuse_level=int(self.opts.fuse_level))
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:

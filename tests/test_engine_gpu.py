@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 dev = "cuda"
 
 
-def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentum=0.0):
+def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentum=0.0,
+           fuse_level=0):
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
     from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
     from ddp_amd.models import SimpleCNN
@@ -20,7 +21,8 @@ def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentu
     imgs, labels = synthetic_mnist(n)
     data = DeviceMNIST(imgs, labels, dev)
     eng = FusedSimpleCNNEngine(model, opt, data, B, 1, 0,
-                               opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph))
+                               opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph,
+                                                  fuse_level=fuse_level))
     eng.refresh()
     return model, opt, data, eng, imgs, labels
 
@@ -54,6 +56,35 @@ def test_graph_replay_bitwise_equals_eager():
     e1.synchronize(); e2.synchronize()
     for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         assert torch.equal(a, b), n
+
+
+@pytest.mark.parametrize("B", [32, 20])
+def test_fuse_level1_bitwise_equals_level0(B):
+    """6-kernel step (conv1 recomputed inside conv2 fwd/dgrad/wgrad, xent inside fc_bwd)
+    must reproduce the 8-kernel step bit for bit: params, momentum and loss history."""
+    m0, _, _, e0, _, _ = _setup(B=B, use_graph=False, momentum=0.9)
+    m1, _, _, e1, _, _ = _setup(B=B, use_graph=True, momentum=0.9, fuse_level=1)
+    e0.run_steps(7)
+    e1.run_steps(7)
+    e0.synchronize(); e1.synchronize()
+    for (n, a), (_, b) in zip(m0.named_parameters(), m1.named_parameters()):
+        assert torch.equal(a, b), n
+    assert torch.equal(e0.t["loss_hist"][:7], e1.t["loss_hist"][:7])
+
+
+def test_fuse_level1_one_step_matches_bf16_reference():
+    model, opt, data, eng, imgs, labels = _setup(use_graph=False, fuse_level=1)
+    before = {k: v.detach().cpu().clone() for k, v in _native(model).items()}
+    eng.run_steps(1)
+    eng.synchronize()
+    idx = eng.sampler.indices()[:32]
+    loss, g = R.simple_cnn_step_bf16(before, imgs[idx].float() / 255.0, labels[idx])
+    after = {k: v.detach().cpu() for k, v in _native(model).items()}
+    for k in g:
+        got = (before[k] - after[k]) / 0.01
+        err = (got - g[k]).norm() / g[k].norm()
+        assert err < 1e-2, f"{k}: rel err {err:.2e}"
+    assert abs(eng.t["loss_hist"][0].item() - loss.item()) < 1e-4
 
 
 def test_run_epoch_ragged_and_logging():
