@@ -46,20 +46,30 @@ class TrainOptions:
     max_steps: int | None = None      # stop each epoch early (smoke tests)
     metrics_json: str | None = None   # append per-epoch throughput records here
     fault: tuple | None = None        # (epoch, step, rank|-1): simulate a crash there (resume tests)
+    fuse_level: int | None = None     # fused engine fusion level (None: engine default)
+    grad_accum: int = 1               # micro-batches per optimizer step (module/CPU path)
+    global_loss: bool = False         # log the all-reduced mean loss (module/CPU path, bug B14)
+    pg_timeout_s: float | None = None
 
 
 def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
               opts: TrainOptions | None = None):
     opts = opts or TrainOptions()
-    backend = setup(rank=rank, world_size=world_size, backend=opts.backend)
+    backend = setup(rank=rank, world_size=world_size, backend=opts.backend,
+                    timeout_s=opts.pg_timeout_s)
     on_gpu = backend == "nccl"
     device = torch.device("cuda", local_rank(rank)) if on_gpu else torch.device("cpu")
     print(f"Rank {rank} initialized", flush=True)
+    if opts.grad_accum < 1:
+        raise ValueError("--grad_accum must be >= 1")
 
     if opts.seed is not None:
         torch.manual_seed(opts.seed)  # B15: reproducible init (rank 0's weights win anyway)
     model = SimpleCNN().to(device)
     fused = on_gpu and opts.engine == "fused"
+    if fused and (opts.grad_accum != 1 or opts.global_loss):
+        raise ValueError("--grad_accum / --global_loss need the module path (--engine module) "
+                         "or the CPU path; the fused engine runs one micro-batch per step")
     if fused:
         fs = flat_space(model)
 
@@ -96,9 +106,10 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
         from .fused_step import EngineOptions, FusedSimpleCNNEngine
 
         comm = native_comm() if world_size > 1 else None
-        engine = FusedSimpleCNNEngine(model, opt, ddata, batch_size, world_size, rank, comm,
-                                      EngineOptions(graph_steps=opts.graph_steps,
-                                                    bucket_cap_mb=opts.bucket_cap_mb))
+        eo = EngineOptions(graph_steps=opts.graph_steps, bucket_cap_mb=opts.bucket_cap_mb)
+        if opts.fuse_level is not None:
+            eo.fuse_level = opts.fuse_level
+        engine = FusedSimpleCNNEngine(model, opt, ddata, batch_size, world_size, rank, comm, eo)
         engine.refresh()
 
     for epoch in range(start_epoch, epochs):
@@ -118,7 +129,8 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
         else:
             nsteps = _run_module_epoch(ddp_model, loader, loss_fn, opt, device, log,
                                        opts.log_every,
-                                       fault_step if fault_step is not None else opts.max_steps)
+                                       fault_step if fault_step is not None else opts.max_steps,
+                                       opts.grad_accum, opts.global_loss)
         if fault_step is not None:
             _inject_fault(rank, epoch, nsteps)
         if on_gpu:
@@ -164,19 +176,45 @@ def _verify_and_broadcast(fs, model, world_size):
             dist.broadcast(b, src=0)
 
 
-def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_steps):
+def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_steps,
+                      grad_accum=1, global_loss=False):
+    """The reference's loop (train_ddp.py:195-202).  With ``grad_accum`` > 1 the
+    optimizer steps every ``grad_accum`` batches; the first ``grad_accum - 1`` backward
+    passes run under ``no_sync`` (no all-reduce) and the loss is scaled so the update
+    equals one large-batch step.  A ragged tail still flushes with a synchronised
+    backward."""
     n = 0
+    nb = len(loader) if hasattr(loader, "__len__") else None
+    if max_steps is not None:
+        nb = max_steps if nb is None else min(nb, max_steps)
+    opt.zero_grad()
     for batch_idx, batch in enumerate(loader):
         images, labels = batch if isinstance(batch, (tuple, list)) else tuple(batch)
         images = images.to(device, non_blocking=True)
         labels = labels.to(device, non_blocking=True)
-        opt.zero_grad()
+        if grad_accum == 1:
+            opt.zero_grad()
+        last = nb is not None and batch_idx + 1 >= nb
+        boundary = grad_accum == 1 or (batch_idx + 1) % grad_accum == 0 or last
         output = model(images)
         loss = loss_fn(output, labels)
-        loss.backward()
-        opt.step()
+        scaled = loss / grad_accum if grad_accum > 1 else loss
+        if boundary or not hasattr(model, "no_sync"):
+            scaled.backward()
+        else:
+            with model.no_sync():
+                scaled.backward()
+        if boundary:
+            opt.step()
+            if grad_accum > 1:
+                opt.zero_grad()
         if batch_idx % log_every == 0:
-            log(batch_idx, loss.item())
+            lv = loss.detach()
+            if global_loss and dist.is_initialized() and dist.get_world_size() > 1:
+                lv = lv.clone()
+                dist.all_reduce(lv)
+                lv = lv / dist.get_world_size()
+            log(batch_idx, lv.item())
         n += 1
         if max_steps is not None and n >= max_steps:
             break

@@ -164,3 +164,19 @@ def test_cli_under_torchrun_2proc(tmp_path):
     assert "Rank 0 initialized" in out and "Rank 1 initialized" in out and "Rank 2" not in out
     assert "Epoch 0 | Batch 10 | Loss:" in out
     assert os.path.exists(tmp_path / "checkpoints" / "epoch_0.pt")
+
+
+def test_grad_accum_matches_large_batch(tmp_path):
+    """--grad_accum 2 at batch 16 == one step at batch 32 (same samples, mean loss)."""
+    from ddp_amd.engine.trainer import TrainOptions, ddp_train
+
+    def run(bs, accum, sub):
+        o = TrainOptions(backend="gloo", data="synthetic", save=False, num_workers=0,
+                         max_steps=8 * accum, checkpoint_dir=str(tmp_path / sub), grad_accum=accum,
+                         log_every=1000)
+        return ddp_train(0, 1, 1, bs, o)
+
+    m1 = run(32, 1, "a")
+    m2 = run(16, 2, "b")
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6), n

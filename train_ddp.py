@@ -45,6 +45,14 @@ def parse_args(argv=None):
     p.add_argument("--num_workers", type=int, default=2, help="CPU DataLoader workers")
     p.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch (module/CPU path)")
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
+    p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1],
+                   help="fused engine: 0 = 8 kernels/step, 1 = 6 kernels/step (default: engine default)")
+    p.add_argument("--grad_accum", type=int, default=1,
+                   help="micro-batches per optimizer step (module/CPU path; DDP no_sync)")
+    p.add_argument("--global_loss", action="store_true",
+                   help="log the all-reduced mean loss instead of rank 0's local loss (module/CPU path)")
+    p.add_argument("--pg_timeout_min", type=float, default=30.0,
+                   help="process-group timeout in minutes (reference default 30)")
     p.add_argument("--fault_at", default=None, metavar="EPOCH:STEP[:RANK]",
                    help="simulate a crash (os._exit) at that step; re-run to auto-resume")
     return p.parse_args(argv)
@@ -58,6 +66,8 @@ def main(argv=None):
                         log_every=a.log_every, graph_steps=a.graph_steps,
                         bucket_cap_mb=a.bucket_cap_mb, num_workers=a.num_workers,
                         max_steps=a.max_steps, metrics_json=a.metrics_json,
+                        fuse_level=a.fuse_level, grad_accum=a.grad_accum,
+                        global_loss=a.global_loss, pg_timeout_s=a.pg_timeout_min * 60.0,
                         fault=tuple(int(v) for v in a.fault_at.split(":")) if a.fault_at else None)
     launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
 
