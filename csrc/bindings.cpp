@@ -513,6 +513,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1_fwd", &op_conv1_fwd);
   m.def("conv1_wgrad", &op_conv1_wgrad);
   m.def("conv1_wgrad_blocks", &conv1_wgrad_blocks);
+  m.def("plan_buckets", &plan_buckets, "torch DDP bucket size rule over gradient-ready byte sizes",
+        py::arg("nbytes"), py::arg("first_cap_bytes"), py::arg("cap_bytes"));
+  py::class_<BucketState>(m, "BucketState")
+      .def(py::init<std::vector<int>, int>())
+      .def("mark_ready", &BucketState::mark_ready)
+      .def("set_launched", &BucketState::set_launched)
+      .def("unlaunched", &BucketState::unlaunched)
+      .def("pending", &BucketState::pending)
+      .def("reset", &BucketState::reset);
   m.def("conv3x3_fwd", &op_conv3x3_fwd);
   m.def("conv3x3_dgrad", &op_conv3x3_dgrad);
   m.def("conv3x3_dgrad_fused_w1", &op_conv3x3_dgrad_fused_w1);

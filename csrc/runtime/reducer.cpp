@@ -24,13 +24,9 @@ Reducer::Reducer(std::shared_ptr<Comm> comm, float* flat_grad, std::vector<long>
       bucket_num_(std::move(bucket_numels)),
       prescale_(prescale) {
   const int nb = (int)bucket_off_.size();
-  init_pending_.assign(nb, 0);
-  for (int b : pbucket_) {
-    if (b < 0 || b >= nb) throw std::runtime_error("reducer: parameter mapped to bad bucket");
-    init_pending_[b]++;
-  }
-  pending_ = init_pending_;
-  launched_.assign(nb, 0);
+  if (poff_.size() != pnum_.size() || poff_.size() != pbucket_.size() || bucket_num_.size() != (size_t)nb)
+    throw std::runtime_error("reducer: inconsistent parameter / bucket tables");
+  state_ = BucketState(pbucket_, nb);
   ready_.resize(nb);
   done_.resize(nb);
   for (int b = 0; b < nb; ++b) {
@@ -48,10 +44,7 @@ Reducer::~Reducer() {
   for (auto e : done_) hipEventDestroy(e);
 }
 
-void Reducer::reset() {
-  pending_ = init_pending_;
-  std::fill(launched_.begin(), launched_.end(), 0);
-}
+void Reducer::reset() { state_.reset(); }
 
 void Reducer::launch_bucket(int b, hipStream_t compute) {
   DDP_HIP_CHECK(hipEventRecord(ready_[b], compute));
@@ -63,24 +56,22 @@ void Reducer::launch_bucket(int b, hipStream_t compute) {
     ++calls_;
   }
   DDP_HIP_CHECK(hipEventRecord(done_[b], comm_stream_));
-  launched_[b] = 1;
+  state_.set_launched(b);
 }
 
 void Reducer::mark_ready(int param, const float* grad_src, hipStream_t compute) {
   if (param < 0 || param >= (int)poff_.size()) throw std::runtime_error("reducer: bad param index");
-  const int b = pbucket_[param];
   float* dst = flat_ + poff_[param];
   const float scale = (prescale_ && comm_) ? 1.f / (float)comm_->world() : 1.f;
   if (grad_src != nullptr && grad_src != dst) scale_copy(dst, grad_src, pnum_[param], scale, compute);
   else if (scale != 1.f) scale_copy(dst, dst, pnum_[param], scale, compute);
-  if (--pending_[b] == 0) launch_bucket(b, compute);
+  const int b = state_.mark_ready(param);
+  if (b >= 0) launch_bucket(b, compute);
 }
 
 void Reducer::finalize(hipStream_t compute) {
-  for (int b = 0; b < (int)bucket_off_.size(); ++b) {
-    if (!launched_[b]) launch_bucket(b, compute);  // unused params: reduce what is there
-    DDP_HIP_CHECK(hipStreamWaitEvent(compute, done_[b], 0));
-  }
+  for (int b : state_.unlaunched()) launch_bucket(b, compute);  // unused params: reduce what is there
+  for (int b = 0; b < (int)bucket_off_.size(); ++b) DDP_HIP_CHECK(hipStreamWaitEvent(compute, done_[b], 0));
   reset();
 }
 

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "kernels/launchers.h"
+#include "runtime/bucket_state.h"
 
 #define DDP_HIP_CHECK(expr)                                                              \
   do {                                                                                   \
@@ -87,8 +88,7 @@ class Reducer {
   std::vector<long> poff_, pnum_;
   std::vector<int> pbucket_;
   std::vector<long> bucket_off_, bucket_num_;
-  std::vector<int> pending_, init_pending_;
-  std::vector<char> launched_;
+  BucketState state_;
   std::vector<hipEvent_t> ready_, done_;
   hipStream_t comm_stream_ = nullptr;
   bool prescale_;

@@ -87,6 +87,29 @@ def test_fuse_level1_one_step_matches_bf16_reference():
     assert abs(eng.t["loss_hist"][0].item() - loss.item()) < 1e-4
 
 
+@pytest.mark.parametrize("fuse_level", [0, 1])
+@pytest.mark.parametrize("B", [1, 12, 16, 24, 48, 64])
+def test_engine_batch_sweep_nan_poisoned(B, fuse_level):
+    """SURVEY §4.1 batch sizes; every intermediate buffer starts as NaN so a kernel that
+    reads something its producer did not write shows up as a non-finite gradient."""
+    model, opt, data, eng, imgs, labels = _setup(B=B, use_graph=False, fuse_level=fuse_level)
+    for k in ("a1", "a2", "dz2", "dz1", "fc_part", "dlogits", "loss_rows", "w2slab", "w1slab"):
+        eng.t[k].fill_(float("nan"))
+    eng.fs.grads.fill_(float("nan"))
+    before = {k: v.detach().cpu().clone() for k, v in _native(model).items()}
+    eng.run_steps(1)
+    eng.synchronize()
+    idx = eng.sampler.indices()[:B]
+    loss, g = R.simple_cnn_step_bf16(before, imgs[idx].float() / 255.0, labels[idx])
+    after = {k: v.detach().cpu() for k, v in _native(model).items()}
+    for k in g:
+        got = (before[k] - after[k]) / 0.01
+        assert torch.isfinite(got).all(), k
+        err = (got - g[k]).norm() / g[k].norm()
+        assert err < 1e-2, f"B={B} {k}: rel err {err:.2e}"
+    assert abs(eng.t["loss_hist"][0].item() - loss.item()) < 1e-4
+
+
 def test_run_epoch_ragged_and_logging():
     model, opt, data, eng, _, _ = _setup(n=1000, B=32, graph_steps=10)
     seen = []
