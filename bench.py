@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--fuse_level", type=int, default=None,
                     help="engine fusion level (0: 8 kernels/step, 1: 6 kernels/step); default = engine default")
+    ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
+    ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
+    ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
@@ -92,8 +95,9 @@ def main():
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
     k = args.graph_steps or graph_chunk(args.steps)
     eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph)
-    if args.fuse_level is not None:
-        eo.fuse_level = args.fuse_level
+    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows"):
+        if getattr(args, f) is not None:
+            setattr(eo, f, getattr(args, f))
     eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
     eng.refresh()
     if not args.no_graph:
@@ -140,7 +144,9 @@ def main():
                        "global_batch": ws * args.batch_size, "per_rank_batch": args.batch_size,
                        "seq_len": None, "image": "1x28x28", "parallelism": f"dp{ws}",
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
-                       "graph_steps": k, "fuse_level": eo.fuse_level, "params_finite": finite},
+                       "graph_steps": k, "fuse_level": eo.fuse_level,
+                       "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
+                                  "wgrad_rows": eng.wgrad_rows}, "params_finite": finite},
         }), flush=True)
     if ws > 1:
         dist.barrier(device_ids=[lrank])

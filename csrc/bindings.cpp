@@ -197,7 +197,13 @@ void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, 
   const long K = X.numel() / B;
   TORCH_CHECK(X.numel() == (long)B * K && dX.numel() == X.numel(), "fc_bwd: X/dX shape");
   TORCH_CHECK(Wf.numel() == (long)NO * K && dW.numel() == Wf.numel() && NO <= 16, "fc_bwd: W shape");
-  TORCH_CHECK((long)B * NO * 4 <= 64 * 1024, "fc_bwd: batch too large for LDS");
+  TORCH_CHECK(fc_bwd_lds(B, NO, false) <= 160 * 1024, "fc_bwd: batch too large for LDS");
+  TORCH_CHECK(K % 4 == 0, "fc_bwd: in_features must be a multiple of 4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dW.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(X.data_ptr()) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(dX.data_ptr()) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(Wf.data_ptr()) % 8 == 0,
+              "fc_bwd: misaligned buffers");
   FcBwdExtras ex;
   if (dbias) {
     check(*dbias, "dbias", at::kFloat);
@@ -248,7 +254,7 @@ void op_xent_rows(const Tensor& part, int G, const Tensor& bias, const Tensor& l
   check(part, "part", at::kFloat); check(bias, "bias", at::kFloat); check(labels32, "labels", at::kInt);
   check(dlogits, "dlogits", at::kFloat); check(loss_rows, "loss_rows", at::kFloat);
   const int B = dlogits.size(0), NO = dlogits.size(1);
-  TORCH_CHECK(NO <= 16 && bias.numel() == NO, "xent_rows: at most 16 classes");
+  TORCH_CHECK(bias.numel() == NO && (long)B * NO * 4 <= 64 * 1024, "xent_rows: bias size / batch*classes too large");
   TORCH_CHECK(part.numel() >= (long)B * NO * G && loss_rows.numel() >= B, "xent_rows: sizes");
   BatchIdx bi = make_bi(idx, std::nullopt, 0, 0, labels32.numel());
   if (!idx) TORCH_CHECK(labels32.numel() >= B, "xent_rows: labels");

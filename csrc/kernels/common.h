@@ -101,37 +101,42 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Softmax cross-entropy of one row on one wave from split-K fc partials laid out
-// [NO][G] (part_row = part + b*NO*G): 4 lanes per class, fixed summation order.
-// Writes dl_row[c] = (softmax - onehot) * gscale (lanes with j == 0) and returns
-// the row loss (valid on every lane).  Shared by xent_rows and the XENT prologue of
-// fc_bwd so both produce bit-identical values.
-__device__ __forceinline__ float xent_row_wave(const float* __restrict__ part_row, int G,
-                                               const float* __restrict__ bias, int NO, int label,
-                                               float gscale, float* dl_row) {
-  const int lane = threadIdx.x & 63;
-  const int c = lane >> 2, j = lane & 3;
-  const bool own = c < NO;
-  float s = 0.f;
-  if (own) {
-    const float* src = part_row + (long)c * G;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int g = j;
-    for (; g + 12 < G; g += 16) {  // 4 independent loads in flight
-      a0 += src[g]; a1 += src[g + 4]; a2 += src[g + 8]; a3 += src[g + 12];
+// Whole-batch softmax cross-entropy on one workgroup, fixed summation order.
+// part: split-K partial logits [B][NO][G] (G partials per logit).  Phase 1: one
+// thread per (row, class) sums its G partials with all loads of a 64-chunk in flight
+// (one memory round trip for the SimpleCNN shape, G = 49) into s_logit (LDS,
+// [B*NO]).  Phase 2: one thread per row: max, sum-exp, loss = logsumexp - x[label],
+// dl = (softmax - onehot) * gscale.  Used by xent_rows (separate kernel) and by the
+// XENT prologue of fc_bwd, so both produce bit-identical values.
+__device__ __forceinline__ void xent_batch_block(const float* __restrict__ part, int G,
+                                                 const float* __restrict__ bias, int NO, int B,
+                                                 const int* __restrict__ labels32, const BatchIdx& bi,
+                                                 float gscale, float* s_logit, float* dl, float* loss) {
+  for (int p = threadIdx.x; p < B * NO; p += blockDim.x) {
+    const float* src = part + (long)p * G;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int g0 = 0; g0 < G; g0 += 64) {
+      float v[64];
+#pragma unroll
+      for (int u = 0; u < 64; ++u) v[u] = (g0 + u < G) ? src[g0 + u] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 64; ++u) a[u & 3] += v[u];
     }
-    for (; g < G; g += 4) a0 += src[g];
-    s = ((a0 + a1) + a2) + a3;
+    s_logit[p] = bias[p % NO] + ((a[0] + a[1]) + (a[2] + a[3]));
   }
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  const float x = own ? s + bias[c] : -INFINITY;
-  const float mx = wave_max(x);
-  const float e = (own && j == 0) ? __expf(x - mx) : 0.f;
-  const float se = wave_sum(e);
-  const float xl = wave_sum((own && j == 0 && c == label) ? x : 0.f);
-  if (own && j == 0) dl_row[c] = (e / se - (c == label ? 1.f : 0.f)) * gscale;
-  return mx + __logf(se) - xl;
+  __syncthreads();
+  const int base = bi.base();
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float* x = s_logit + b * NO;
+    const int label = labels32[bi.row(b, base)];
+    float mx = x[0];
+    for (int o = 1; o < NO; ++o) mx = fmaxf(mx, x[o]);
+    float se = 0.f;
+    for (int o = 0; o < NO; ++o) se += __expf(x[o] - mx);
+    const float inv = 1.f / se;
+    for (int o = 0; o < NO; ++o) dl[b * NO + o] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
+    loss[b] = mx + __logf(se) - x[label];
+  }
 }
 
 }  // namespace ddp_amd

@@ -67,23 +67,28 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __
   out[i] = s + (bias ? bias[o] : 0.f);
 }
 
-template <bool MASK, bool XENT>
+// fc backward: a block owns 256 consecutive columns k (4 per lane, 8-byte loads)
+// and its 4 waves split the batch rows (wave w: rows w, w+4, ...), so every wave has
+// its rows' loads in flight at once; the per-wave dW partials are summed in fixed
+// wave order through LDS.  NOT = compile-time class capacity (guards o < NO).
+template <bool MASK, bool XENT, int NOT>
 __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ dL,
                                                      const bf16_t* __restrict__ X,
                                                      const bf16_t* __restrict__ Wf,
                                                      bf16_t* __restrict__ dX, float* __restrict__ dW,
                                                      float scale, int B, long K, int NO,
                                                      FcBwdExtras ex) {
-  extern __shared__ __attribute__((aligned(16))) float s_dl[];  // [B][NO] (+ [B] row losses)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_dl = smem;                 // [B][NO]
+  float* s_loss = smem + B * NO;      // [B]        (XENT)
+  float* s_logit = s_loss + B;        // [B][NO]    (XENT)
+  float* s_red = smem + (XENT ? B * (2 * NO + 1) : B * NO);  // [3][NO][256] wave partials
+  s_red = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(s_red) + 15) & ~(uintptr_t)15);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (XENT) {
-    // every block recomputes the (tiny) cross-entropy backward: B rows, one wave per row
-    const int base = ex.bi.base();
-    for (int b = threadIdx.x >> 6; b < B; b += 4) {
-      const int label = ex.labels32[ex.bi.row(b, base)];
-      const float l = xent_row_wave(ex.part + (long)b * NO * ex.G, ex.G, ex.fc_bias, NO, label,
-                                    ex.gscale, s_dl + b * NO);
-      if ((threadIdx.x & 63) == 0) s_dl[B * NO + b] = l;
-    }
+    // every block recomputes the (tiny) cross-entropy backward of the whole batch
+    xent_batch_block(ex.part, ex.G, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_logit,
+                     s_dl, s_loss);
   } else {
     for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
   }
@@ -96,45 +101,79 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ d
       ex.dbias[threadIdx.x] = acc * ex.dbias_scale;
     }
     if ((XENT || ex.loss_rows) && ex.loss_out && threadIdx.x == 64) {
-      const float* lr = XENT ? s_dl + B * NO : ex.loss_rows;
+      const float* lr = XENT ? s_loss : ex.loss_rows;
       float acc = 0.f;
       for (int b = 0; b < B; ++b) acc += lr[b];
       ex.loss_out[ex.step_ctr ? *ex.step_ctr : 0] = acc / (float)B;
     }
   }
-  const long k = (long)blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
-  float w[FC_MAXO], dw[FC_MAXO];
+  const long k0 = (long)blockIdx.x * 256 + lane * 4;
+  const bool active = k0 < K;  // host guarantees K % 4 == 0
+  float w[NOT][4], dw[NOT][4];
 #pragma unroll
-  for (int o = 0; o < FC_MAXO; ++o) {
-    w[o] = (o < NO) ? bf2f(Wf[(long)o * K + k]) : 0.f;
-    dw[o] = 0.f;
+  for (int o = 0; o < NOT; ++o) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    if (active && o < NO) unpack4(*reinterpret_cast<const uint2*>(Wf + (long)o * K + k0), t);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { w[o][c] = t[c]; dw[o][c] = 0.f; }
   }
-  // 32 rows per chunk: all activation loads of the chunk are issued before any math
-  for (int b0 = 0; b0 < B; b0 += 32) {
-    const int nb = min(32, B - b0);
-    float xa[32];
+  constexpr int RB = 8;  // rows in flight per wave
+  for (int b0 = wave; b0 < B; b0 += 4 * RB) {
+    uint2 xr[RB];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) xa[u] = (u < nb) ? bf2f(X[(long)(b0 + u) * K + k]) : 0.f;
+    for (int u = 0; u < RB; ++u) {
+      const int b = b0 + 4 * u;
+      xr[u] = (active && b < B) ? *reinterpret_cast<const uint2*>(X + (long)b * K + k0) : make_uint2(0u, 0u);
+    }
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      if (u < nb) {
-        const float* dl = s_dl + (b0 + u) * NO;
-        float dz = 0.f;
+    for (int u = 0; u < RB; ++u) {
+      const int b = b0 + 4 * u;
+      if (b < B) {
+        float xa[4];
+        unpack4(xr[u], xa);
+        const float* dl = s_dl + b * NO;
+        float dz[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int o = 0; o < FC_MAXO; ++o)
+        for (int o = 0; o < NOT; ++o)
           if (o < NO) {
-            dz = fmaf(dl[o], w[o], dz);
-            dw[o] = fmaf(dl[o], xa[u], dw[o]);
+            const float d = dl[o];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              dz[c] = fmaf(d, w[o][c], dz[c]);
+              dw[o][c] = fmaf(d, xa[c], dw[o][c]);
+            }
           }
-        if (MASK && !(xa[u] > 0.f)) dz = 0.f;
-        dX[(long)(b0 + u) * K + k] = f2bf(dz);
+        if (MASK) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) dz[c] = xa[c] > 0.f ? dz[c] : 0.f;
+        }
+        if (active) *reinterpret_cast<uint2*>(dX + (long)b * K + k0) = pack4(dz[0], dz[1], dz[2], dz[3]);
       }
     }
   }
+  // fixed-order reduction of the 4 waves' dW partials
+  if (wave > 0) {
 #pragma unroll
-  for (int o = 0; o < FC_MAXO; ++o)
-    if (o < NO) dW[(long)o * K + k] = dw[o] * scale;
+    for (int o = 0; o < NOT; ++o)
+      if (o < NO)
+        *reinterpret_cast<float4*>(s_red + ((wave - 1) * NO + o) * 256 + lane * 4) =
+            make_float4(dw[o][0], dw[o][1], dw[o][2], dw[o][3]);
+  }
+  __syncthreads();
+  if (wave == 0 && active) {
+#pragma unroll
+    for (int o = 0; o < NOT; ++o)
+      if (o < NO) {
+        float4 r = make_float4(dw[o][0], dw[o][1], dw[o][2], dw[o][3]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const float4 t = *reinterpret_cast<const float4*>(s_red + (q * NO + o) * 256 + lane * 4);
+          r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
+        }
+        r.x *= scale; r.y *= scale; r.z *= scale; r.w *= scale;
+        *reinterpret_cast<float4*>(dW + (long)o * K + k0) = r;
+      }
+  }
 }
 
 void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
@@ -150,14 +189,23 @@ void fc_reduce(const float* part, const float* bias, float* out, int B, int G, i
                      B, G, NO);
 }
 
+size_t fc_bwd_lds(int B, int NO, bool xent) {
+  return sizeof(float) * ((size_t)B * (xent ? 2 * NO + 1 : NO) + 4 + (size_t)3 * NO * 256);
+}
+
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
   const dim3 grid((unsigned)((K + 255) / 256));
   const bool xe = ex.part != nullptr;
-  const size_t lds = sizeof(float) * B * (NO + (xe ? 1 : 0));
-#define LB(M, XE) hipLaunchKernelGGL((fc_bwd_kernel<M, XE>), grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
-  if (xe) { if (mask) LB(true, true); else LB(false, true); }
-  else { if (mask) LB(true, false); else LB(false, false); }
+  const size_t lds = fc_bwd_lds(B, NO, xe);
+#define LB(M, XE, N) hipLaunchKernelGGL((fc_bwd_kernel<M, XE, N>), grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
+  if (NO == 10) {
+    if (xe) { if (mask) LB(true, true, 10); else LB(false, true, 10); }
+    else { if (mask) LB(true, false, 10); else LB(false, false, 10); }
+  } else {
+    if (xe) { if (mask) LB(true, true, FC_MAXO); else LB(false, true, FC_MAXO); }
+    else { if (mask) LB(true, false, FC_MAXO); else LB(false, false, FC_MAXO); }
+  }
 #undef LB
 }
 

@@ -102,17 +102,14 @@ __global__ __launch_bounds__(256) void xent_rows_kernel(const float* __restrict_
                                                         BatchIdx bi, float* __restrict__ dlogits,
                                                         float* __restrict__ loss_rows,
                                                         float gscale) {
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int label = labels32[bi.row(b, bi.base())];
-  const float l = xent_row_wave(part + (long)b * NO * G, G, bias, NO, label, gscale, dlogits + (long)b * NO);
-  if ((threadIdx.x & 63) == 0) loss_rows[b] = l;
+  extern __shared__ __attribute__((aligned(16))) float s_logit[];  // [B*NO]
+  xent_batch_block(part, G, bias, NO, B, labels32, bi, gscale, s_logit, dlogits, loss_rows);
 }
 
 void xent_rows(const float* part, int G, const float* bias, int NO, int B, const int* labels32,
                BatchIdx bi, float* dlogits, float* loss_rows, float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(xent_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, part, G, bias, NO, B,
-                     labels32, bi, dlogits, loss_rows, gscale);
+  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(256), sizeof(float) * B * NO, s, part, G, bias,
+                     NO, B, labels32, bi, dlogits, loss_rows, gscale);
 }
 
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,

@@ -68,7 +68,7 @@ class FusedSimpleCNNEngine:
         self.sampler = ShardedSampler(len(data), world_size, rank, shuffle=True, seed=seed)
         n_rank = len(self.sampler)
         B, HW = self.B, 28 * 28
-        R = self.opts.wgrad_rows or wgrad_rows(28, B)
+        R = self.wgrad_rows = self.opts.wgrad_rows or wgrad_rows(28, B)
         g = self.opt.param_groups[0]
         if g["momentum"] != 0 and self.opt.momentum_buffer is None:
             self.opt.momentum_buffer = torch.zeros_like(fs.params)
@@ -187,7 +187,12 @@ class FusedSimpleCNNEngine:
             self._bench_started = True
         k = self.opts.graph_steps
         n_full = len(self.sampler) // self.B
-        done = 0
+        done = init = 0
+        if nsteps > 0 and self.opt.momentum_buffer is not None and not self.opt.steps:
+            self._wrap_if_needed(1, n_full)
+            self.eng.step(self.B, self.B)  # momentum buffer initialisation step (eager)
+            done = init = 1
+            self.opt.steps = 1
         while done < nsteps:
             if self.opts.use_graph and nsteps - done >= k and k <= n_full:
                 self._ensure_graph()
@@ -199,6 +204,7 @@ class FusedSimpleCNNEngine:
                 self.eng.step(self.B, self.B)
                 done += 1
         self.steps_done += done
+        self.opt.steps += done - init
         return done
 
     _bench_started = False
