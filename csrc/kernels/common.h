@@ -116,11 +116,12 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
     const float* src = part + (long)p * G;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     for (int g0 = 0; g0 < G; g0 += 64) {
+      // unconditional loads at clamped addresses (all 64 in flight), masked afterwards
       float v[64];
 #pragma unroll
-      for (int u = 0; u < 64; ++u) v[u] = (g0 + u < G) ? src[g0 + u] : 0.f;
+      for (int u = 0; u < 64; ++u) v[u] = src[min(g0 + u, G - 1)];
 #pragma unroll
-      for (int u = 0; u < 64; ++u) a[u & 3] += v[u];
+      for (int u = 0; u < 64; ++u) a[u & 3] += (g0 + u < G) ? v[u] : 0.f;
     }
     s_logit[p] = bias[p % NO] + ((a[0] + a[1]) + (a[2] + a[3]));
   }

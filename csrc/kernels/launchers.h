@@ -90,6 +90,7 @@ struct FcBwdExtras {
   float gscale = 1.f;
 };
 size_t fc_bwd_lds(int B, int NO, bool xent);
+void noop(int blocks, int* sink, hipStream_t s);
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
 

@@ -151,6 +151,15 @@ void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, c
   hipLaunchKernelGGL(sgd_kernel, dim3(grid), dim3(256), 0, s, p, g, mbuf, n, a, sh, step_ctr);
 }
 
+// empty kernel: the per-launch floor (dispatch + drain + boundary) for kernel benches
+__global__ void noop_kernel(int* __restrict__ sink) {
+  if (sink && blockIdx.x == 0 && threadIdx.x == 0) sink[0] = 0;
+}
+
+void noop(int blocks, int* sink, hipStream_t s) {
+  hipLaunchKernelGGL(noop_kernel, dim3(blocks), dim3(256), 0, s, sink);
+}
+
 void grad_reduce(const SlabSet& ss, hipStream_t s) {
   long blocks = 0;
   for (int k = 0; k < ss.count; ++k) blocks += (ss.s[k].n + 63) / 64;
