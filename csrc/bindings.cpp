@@ -254,7 +254,7 @@ void op_xent_rows(const Tensor& part, int G, const Tensor& bias, const Tensor& l
   check(part, "part", at::kFloat); check(bias, "bias", at::kFloat); check(labels32, "labels", at::kInt);
   check(dlogits, "dlogits", at::kFloat); check(loss_rows, "loss_rows", at::kFloat);
   const int B = dlogits.size(0), NO = dlogits.size(1);
-  TORCH_CHECK(bias.numel() == NO && (long)B * NO * 4 <= 64 * 1024, "xent_rows: bias size / batch*classes too large");
+  TORCH_CHECK(bias.numel() == NO && NO <= 16, "xent_rows: at most 16 classes");
   TORCH_CHECK(part.numel() >= (long)B * NO * G && loss_rows.numel() >= B, "xent_rows: sizes");
   BatchIdx bi = make_bi(idx, std::nullopt, 0, 0, labels32.numel());
   if (!idx) TORCH_CHECK(labels32.numel() >= B, "xent_rows: labels");
@@ -439,8 +439,13 @@ ShadowSet make_shadows(const py::list& shadows) {
     check(dst, "shadow dst", at::kBFloat16);
     const long n = t[1].cast<long>();
     TORCH_CHECK(dst.numel() == n, "shadow dst size mismatch");
-    sh.r[sh.count++] = ShadowRegion{t[0].cast<long>(), n, bf(dst), t[3].cast<int>(), t[4].cast<int>(),
-                                    t[5].cast<int>(), t[6].cast<int>()};
+    const int kind = t[3].cast<int>(), a = t[4].cast<int>(), b = t[5].cast<int>(), c = t[6].cast<int>();
+    TORCH_CHECK(kind >= SHADOW_BF16 && kind <= SHADOW_BF16_FCFRAG, "unknown shadow kind");
+    if (kind == SHADOW_BF16_TAPT) TORCH_CHECK((long)a * b * c == n, "TAPT shadow: Co*T*Ci != n");
+    if (kind == SHADOW_BF16_FCFRAG)
+      TORCH_CHECK(a % 16 == 0 && b % 16 == 0 && n % ((long)a * b) == 0 && n < (1L << 31),
+                  "FCFRAG shadow: HW and C must be multiples of 16, n a multiple of HW*C");
+    sh.r[sh.count++] = ShadowRegion{t[0].cast<long>(), n, bf(dst), kind, a, b, c};
   }
   return sh;
 }
@@ -661,6 +666,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.w2_bf16 = bf(need("w2_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
              b.w2t_bf16 = bf(need("w2t_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
              b.wfc_bf16 = bf(need("wfc_bf16", at::kBFloat16, (long)c.NO * HW * c.C2));
+             b.wfc_frag = bf(need("wfc_frag", at::kBFloat16, (long)c.NO * HW * c.C2));
+             TORCH_CHECK(fc_bwd_lds(c.max_batch, c.NO, true) <= 160 * 1024, "engine: batch too large for fc_bwd LDS");
              b.a1 = bf(need("a1", at::kBFloat16, B * HW * c.C1));
              b.a2 = bf(need("a2", at::kBFloat16, B * HW * c.C2));
              b.dz2 = bf(need("dz2", at::kBFloat16, B * HW * c.C2));

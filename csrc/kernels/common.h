@@ -83,60 +83,80 @@ __device__ __forceinline__ float conv1_eval(const float* w1, const float* b1, co
   return fmaxf(acc, 0.f);
 }
 
-// fixed-order butterfly sum over all 64 lanes (every lane gets the total)
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+// ---- cross-lane reductions on DPP (VALU modifiers, no LDS round trips) --------------
+// dpp<CTRL>(v): v of the lane selected by the DPP control (quad_perm 0x00-0xFF,
+// row_half_mirror 0x141, row_mirror 0x140), all rows / banks enabled.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+// Sum / max over each 16-lane row (lanes sharing lane >> 4); every lane of the row
+// gets the result.  Pairs, quads, halves, row: a fixed association order, identical
+// on every lane (each step combines two equal-shaped partial sums commutatively).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
   return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ float lane_bcast(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+// fixed-order sum over all 64 lanes (every lane gets the total): rows, then
+// ((r0 + r1) + (r2 + r3)) from lane reads
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row16_sum(v);
+  return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
 }
 // sum over the 16 lanes that share (lane >> 4)
-__device__ __forceinline__ float sum16(float v) {
-#pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
-}
+__device__ __forceinline__ float sum16(float v) { return row16_sum(v); }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
-  return v;
+  v = row16_max(v);
+  return fmaxf(fmaxf(lane_bcast(v, 0), lane_bcast(v, 16)), fmaxf(lane_bcast(v, 32), lane_bcast(v, 48)));
 }
 
 // Whole-batch softmax cross-entropy on one workgroup, fixed summation order.
-// part: split-K partial logits [B][NO][G] (G partials per logit).  Phase 1: one
-// thread per (row, class) sums its G partials with all loads of a 64-chunk in flight
-// (one memory round trip for the SimpleCNN shape, G = 49) into s_logit (LDS,
-// [B*NO]).  Phase 2: one thread per row: max, sum-exp, loss = logsumexp - x[label],
-// dl = (softmax - onehot) * gscale.  Used by xent_rows (separate kernel) and by the
-// XENT prologue of fc_bwd, so both produce bit-identical values.
+// part: split-K partial logits [B][NO][G] (G partials per logit), NO <= 16.
+// One 16-lane row per batch row, lane o = class o: the lane sums its G partials
+// (all loads of a 64-chunk in flight, clamped addresses, masked afterwards), then
+// max / sum-exp / the label's logit are 16-lane DPP reductions.  Writes
+// dl[b*NO + o] = (softmax - onehot) * gscale and loss[b] = logsumexp - x[label].
+// Used by xent_rows (own kernel) and by the XENT prologue of fc_bwd, so both
+// produce bit-identical values.  blockDim.x must be a multiple of 64.
 __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part, int G,
                                                  const float* __restrict__ bias, int NO, int B,
                                                  const int* __restrict__ labels32, const BatchIdx& bi,
-                                                 float gscale, float* s_logit, float* dl, float* loss) {
-  for (int p = threadIdx.x; p < B * NO; p += blockDim.x) {
-    const float* src = part + (long)p * G;
+                                                 float gscale, float* dl, float* loss) {
+  const int o = threadIdx.x & 15;
+  const bool own = o < NO;
+  const int base = bi.base();
+  for (int b = threadIdx.x >> 4; b < B; b += blockDim.x >> 4) {
+    const int label = labels32[bi.row(b, base)];
+    const float* src = part + ((long)b * NO + (own ? o : 0)) * G;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     for (int g0 = 0; g0 < G; g0 += 64) {
-      // unconditional loads at clamped addresses (all 64 in flight), masked afterwards
       float v[64];
 #pragma unroll
       for (int u = 0; u < 64; ++u) v[u] = src[min(g0 + u, G - 1)];
 #pragma unroll
       for (int u = 0; u < 64; ++u) a[u & 3] += (g0 + u < G) ? v[u] : 0.f;
     }
-    s_logit[p] = bias[p % NO] + ((a[0] + a[1]) + (a[2] + a[3]));
-  }
-  __syncthreads();
-  const int base = bi.base();
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const float* x = s_logit + b * NO;
-    const int label = labels32[bi.row(b, base)];
-    float mx = x[0];
-    for (int o = 1; o < NO; ++o) mx = fmaxf(mx, x[o]);
-    float se = 0.f;
-    for (int o = 0; o < NO; ++o) se += __expf(x[o] - mx);
-    const float inv = 1.f / se;
-    for (int o = 0; o < NO; ++o) dl[b * NO + o] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
-    loss[b] = mx + __logf(se) - x[label];
+    const float x = own ? bias[o] + ((a[0] + a[1]) + (a[2] + a[3])) : -INFINITY;
+    const float mx = row16_max(x);
+    const float e = own ? __expf(x - mx) : 0.f;
+    const float se = row16_sum(e);
+    const float xl = row16_sum(own && o == label ? x : 0.f);
+    if (own) dl[b * NO + o] = (e / se - (o == label ? 1.f : 0.f)) * gscale;
+    if (o == 0) loss[b] = mx + __logf(se) - xl;
   }
 }
 

@@ -14,9 +14,11 @@
 //
 // Fusions (templates):
 //  * fwd:   bias + ReLU epilogue; FUSE_FC additionally dots the bf16 output tile
-//           with the following Linear layer's weight (SimpleCNN's fc, stored
-//           [out][H*W][C]) and writes per-16-pixel partial logits, so the fc
-//           forward never re-reads the activation (SURVEY.md §2.4 K5 note).
+//           with the following Linear layer's weight (SimpleCNN's fc, given in
+//           the MFMA-fragment order of SHADOW_BF16_FCFRAG so every lane's 8-byte
+//           slice of a wave-instruction is contiguous) and writes per-16-pixel
+//           partial logits, so the fc forward never re-reads the activation
+//           (SURVEY.md §2.4 K5 note).
 //  * dgrad: ReLU mask of the upstream gradient (MASK_DY, module path) and of the
 //           layer input (MASK_X: d(relu1)); FUSE_W1 accumulates conv1's weight
 //           and bias gradient from the just-computed dZ1 (Cin=1 conv, K11).
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
 #pragma unroll
         for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o)
           wv[pt][t][o] = *reinterpret_cast<const uint2*>(
-              wfc + ((long)o * HW + rem[pt]) * Cout + co0 + 16 * t + 4 * (lane >> 4));
+              wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
   }
   __syncthreads();
 
@@ -255,6 +257,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
   bf16_t* sDY = sWT + 32 * WS;                           // [XR][Cout]
   float* sx0 = reinterpret_cast<float*>(sDY + XR * DS);  // [XR] conv1 input (FUSE_W1)
   float* s_w1 = sx0 + XR;                                // [4][320] (FUSE_W1)
+  float* s_c1 = s_w1 + 4 * 320;                          // conv1 w/b (A1X mask recompute)
   const long P0 = (long)blockIdx.x * CH;
   const long Pbase = P0 - W - 1;
 
@@ -278,6 +281,8 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
             return v;
           },
           [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * 8; *reinterpret_cast<bf16x8*>(sDY + r * DS + c) = v; });
+  if (A1X)
+    for (int i = threadIdx.x; i < Cin * 10; i += 256) s_c1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
   if (FUSE_W1) {
     const int base = x0_u8 ? bi.base() : 0;
     for (int r = threadIdx.x; r < XR; r += 256) {
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
       float v[4] = {acc[pt][t][0], acc[pt][t][1], acc[pt][t][2], acc[pt][t][3]};
       if (MASK_X && A1X) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (bf2f(f2bf(conv1_eval(c1.w, c1.b, xv, ci + j))) > 0.f) ? v[j] : 0.f;
+        for (int j = 0; j < 4; ++j) v[j] = (bf2f(f2bf(conv1_eval(s_c1, s_c1 + Cin * 9, xv, ci + j))) > 0.f) ? v[j] : 0.f;
       } else if (MASK_X) {
         float xm[4];
         unpack4(xa[pt][t], xm);
@@ -581,7 +586,7 @@ size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x) {
 size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
   const size_t XR = 64 * pxt + 2 * W + 2;
   return sizeof(bf16_t) * ((size_t)32 * (9 * Cout + 8) + XR * (Cout + 8)) +
-         (fuse_w1 ? sizeof(float) * (XR + 4 * 320) : 0);
+         (fuse_w1 ? sizeof(float) * (XR + 5 * 320) : 0);
 }
 
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,

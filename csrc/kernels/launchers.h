@@ -107,7 +107,10 @@ struct SgdArgs {
   float lr, momentum, dampening, weight_decay;
   int nesterov, maximize, first_step, update;
 };
-enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2 };
+// SHADOW_BF16_FCFRAG: fc weight [o][hw][c] (a = HW, b = C) -> the MFMA-fragment order
+// read by the conv3x3_fwd FC epilogue, [o][hw/16][c/16][(c/4)%4][hw%16][c%4], so each
+// wave-instruction of that epilogue loads 512 contiguous bytes.
+enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2, SHADOW_BF16_FCFRAG = 3 };
 constexpr int MAX_SHADOWS = 4;
 struct ShadowRegion {
   long off, n;

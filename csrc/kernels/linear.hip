@@ -81,14 +81,12 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ d
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_dl = smem;                 // [B][NO]
   float* s_loss = smem + B * NO;      // [B]        (XENT)
-  float* s_logit = s_loss + B;        // [B][NO]    (XENT)
-  float* s_red = smem + (XENT ? B * (2 * NO + 1) : B * NO);  // [3][NO][256] wave partials
+  float* s_red = smem + (XENT ? B * (NO + 1) : B * NO);  // [3][NO][256] wave partials
   s_red = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(s_red) + 15) & ~(uintptr_t)15);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (XENT) {
     // every block recomputes the (tiny) cross-entropy backward of the whole batch
-    xent_batch_block(ex.part, ex.G, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_logit,
-                     s_dl, s_loss);
+    xent_batch_block(ex.part, ex.G, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_dl, s_loss);
   } else {
     for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
   }
@@ -190,7 +188,7 @@ void fc_reduce(const float* part, const float* bias, float* out, int B, int G, i
 }
 
 size_t fc_bwd_lds(int B, int NO, bool xent) {
-  return sizeof(float) * ((size_t)B * (xent ? 2 * NO + 1 : NO) + 4 + (size_t)3 * NO * 256);
+  return sizeof(float) * ((size_t)B * (xent ? NO + 1 : NO) + 4 + (size_t)3 * NO * 256);
 }
 
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,

@@ -15,6 +15,15 @@
 
 namespace ddp_amd {
 
+// destination index of element j (multiple of 4 for a quad) in the FCFRAG layout
+__device__ __forceinline__ int fcfrag_index(int j, int HW, int C) {
+  const int o = j / (HW * C);
+  const int rem = j - o * HW * C;
+  const int hw = rem / C, c = rem - (rem / C) * C;
+  const int G = HW >> 4, T = C >> 4;
+  return ((((o * G + (hw >> 4)) * T + (c >> 4)) * 4 + ((c >> 2) & 3)) * 16 + (hw & 15)) * 4 + (c & 3);
+}
+
 __device__ __forceinline__ float sgd_one(float v, float d, float* mb, const SgdArgs& a) {
   if (a.maximize) d = -d;
   if (a.weight_decay != 0.f) d = fmaf(a.weight_decay, v, d);
@@ -53,8 +62,13 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
         const long j = i - sh.r[r].off;
         if (j + 3 >= 0 && j < sh.r[r].n) {
           const float e[4] = {v.x, v.y, v.z, v.w};
-          if (sh.r[r].kind == SHADOW_BF16 && j >= 0 && j + 3 < sh.r[r].n && ((sh.r[r].off & 3) == 0)) {
+          const bool whole = j >= 0 && j + 3 < sh.r[r].n && ((sh.r[r].off & 3) == 0);
+          if (sh.r[r].kind == SHADOW_BF16 && whole) {
             *reinterpret_cast<uint2*>(sh.r[r].dst + j) = pack4(e[0], e[1], e[2], e[3]);
+          } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG && whole) {
+            // C % 4 == 0: the quad is 4 consecutive channels of one (o, hw) -> 8 contiguous bytes
+            *reinterpret_cast<uint2*>(sh.r[r].dst + fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)) =
+                pack4(e[0], e[1], e[2], e[3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -62,6 +76,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
               if (jj < 0 || jj >= sh.r[r].n) continue;
               if (sh.r[r].kind == SHADOW_BF16) {
                 sh.r[r].dst[jj] = f2bf(e[u]);
+              } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
+                sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(e[u]);
               } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
                 const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
                 const long co = jj / ((long)T * Ci);
@@ -89,6 +105,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
       if (j < 0 || j >= sh.r[r].n) continue;
       if (sh.r[r].kind == SHADOW_BF16) {
         sh.r[r].dst[j] = f2bf(v);
+      } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
+        sh.r[r].dst[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = f2bf(v);
       } else {
         const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
         const long co = j / ((long)T * Ci);

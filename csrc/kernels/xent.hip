@@ -96,20 +96,21 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ par
 // the G partials g = j, j+4, ... in order, then a fixed 2-step butterfly combines
 // the 4 lanes.  Writes per-row loss and dlogits; the batch mean loss and the fc
 // bias gradient are finished by fc_bwd's first block (it already holds dlogits).
-__global__ __launch_bounds__(256) void xent_rows_kernel(const float* __restrict__ part, int G,
+__global__ __launch_bounds__(1024) void xent_rows_kernel(const float* __restrict__ part, int G,
                                                         const float* __restrict__ bias, int NO,
                                                         int B, const int* __restrict__ labels32,
                                                         BatchIdx bi, float* __restrict__ dlogits,
                                                         float* __restrict__ loss_rows,
                                                         float gscale) {
-  extern __shared__ __attribute__((aligned(16))) float s_logit[];  // [B*NO]
-  xent_batch_block(part, G, bias, NO, B, labels32, bi, gscale, s_logit, dlogits, loss_rows);
+  xent_batch_block(part, G, bias, NO, B, labels32, bi, gscale, dlogits, loss_rows);
 }
 
 void xent_rows(const float* part, int G, const float* bias, int NO, int B, const int* labels32,
                BatchIdx bi, float* dlogits, float* loss_rows, float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(256), sizeof(float) * B * NO, s, part, G, bias,
-                     NO, B, labels32, bi, dlogits, loss_rows, gscale);
+  // one 16-lane row per batch row: B*16 threads in one workgroup (<= 1024)
+  const int threads = B * 16 <= 256 ? 256 : (B * 16 <= 512 ? 512 : 1024);
+  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(threads), 0, s, part, G, bias, NO, B, labels32,
+                     bi, dlogits, loss_rows, gscale);
 }
 
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,

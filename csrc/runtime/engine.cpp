@@ -68,7 +68,9 @@ void SimpleCNNEngine::refresh_shadows() {
   sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, cfg_.C2, 9, cfg_.C1};
   sh.r[2] = ShadowRegion{b_.off_wfc, (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, b_.wfc_bf16,
                          SHADOW_BF16, 0, 0, 0};
-  sh.count = 3;
+  sh.r[3] = ShadowRegion{b_.off_wfc, (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, b_.wfc_frag,
+                         SHADOW_BF16_FCFRAG, cfg_.H * cfg_.W, cfg_.C2, 0};
+  sh.count = 4;
   sgd_step(b_.params, b_.grads, nullptr, b_.n_params, a, sh, nullptr, cs_);
   DDP_HIP_CHECK(hipGetLastError());
 }
@@ -95,7 +97,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // ---- forward
   if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
   conv3x3_fwd(f1 ? nullptr : b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true,
-              b_.wfc_bf16, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1);
+              b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1);
   // ---- loss + fc backward (bucket 0)
   if (!f1)
     xent_rows(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits, b_.loss_rows,
@@ -153,7 +155,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
   sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
   sh.r[2] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
-  sh.count = 3;
+  sh.r[3] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+  sh.count = 4;
   sgd_step(P, G, b_.momentum, b_.n_params, a, sh, b_.step_ctr, cs_);
 }
 

@@ -106,7 +106,7 @@ struct EngineBuffers {
   // gradient buckets (reference rebuilt order: [fl.*], [net.2.*, net.0.*])
   long bucket0_off, bucket0_n, bucket1_off, bucket1_n;
   // bf16 shadows
-  bf16_t *w2_bf16, *w2t_bf16, *wfc_bf16;
+  bf16_t *w2_bf16, *w2t_bf16, *wfc_bf16, *wfc_frag;  // wfc_frag: FCFRAG order (conv2 fwd FC epilogue)
   // activations / scratch (sized for max batch)
   bf16_t *a1, *a2, *dz2, *dz1;
   float *fc_part, *dlogits, *loss_rows, *loss_hist, *w2slab, *w1slab;

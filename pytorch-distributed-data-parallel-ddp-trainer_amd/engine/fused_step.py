@@ -78,7 +78,7 @@ class FusedSimpleCNNEngine:
             params=fs.params, grads=fs.grads,
             momentum=self.opt.momentum_buffer if self.opt.momentum_buffer is not None else e(1),
             w2_bf16=e(64 * 9 * 32, dt=BF16), w2t_bf16=e(64 * 9 * 32, dt=BF16),
-            wfc_bf16=e(10 * HW * 64, dt=BF16),
+            wfc_bf16=e(10 * HW * 64, dt=BF16), wfc_frag=e(10 * HW * 64, dt=BF16),
             a1=e(B * HW * 32, dt=BF16), a2=e(B * HW * 64, dt=BF16),
             dz2=e(B * HW * 64, dt=BF16), dz1=e(B * HW * 32, dt=BF16),
             fc_part=e(B * (HW // 16) * 10), dlogits=e(B * 10), loss_rows=e(B),

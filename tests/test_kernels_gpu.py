@@ -76,7 +76,9 @@ def test_conv3x3_fwd_fused_fc(C, B):
     bfc = (torch.randn(10) * 0.1).to(dev)
     y = torch.empty(B, H, W, 64, dtype=BF, device=dev)
     part = torch.full((B, 10, H * W // 16), float("nan"), device=dev)
-    C.conv3x3_fwd(x, w, b, y, True, wfc, part, 10, 2)
+    from ddp_amd.ops.functional import fc_weight_frag
+
+    C.conv3x3_fwd(x, w, b, y, True, fc_weight_frag(wfc, H * W, 64), part, 10, 2)
     logits = part.sum(2) + bfc
     ref = R.fc_nhwc(y.float(), wfc.float(), bfc)  # the fc of exactly the stored bf16 activation
     close(logits, ref, rtol=1e-3, atol=1e-3)
@@ -250,6 +252,16 @@ def test_sgd_transposed_shadow(C):
     C.sgd(w, g, None, 0.0, 0.0, 0.0, 0.0, False, False, False, False, [(0, w.numel(), sh, 2, 64, 9, 32)])
     ref = w.view(64, 9, 32).permute(1, 2, 0).contiguous().view(-1).to(BF)
     assert torch.equal(sh.cpu(), ref.cpu())
+
+
+def test_sgd_fcfrag_shadow(C):
+    from ddp_amd.ops.functional import fc_weight_frag
+
+    w = torch.randn(10 * 784 * 64, device=dev)
+    sh = torch.empty(w.numel(), dtype=BF, device=dev)
+    C.sgd(w, torch.zeros_like(w), None, 0.0, 0.0, 0.0, 0.0, False, False, False, False,
+          [(0, w.numel(), sh, 3, 784, 64, 0)])
+    assert torch.equal(sh.cpu(), fc_weight_frag(w, 784, 64).view(-1).cpu())
 
 
 def _native_params(model):
