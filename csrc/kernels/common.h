@@ -125,7 +125,7 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Whole-batch softmax cross-entropy on one workgroup, fixed summation order.
-// part: split-K partial logits [B][NO][G] (G partials per logit), NO <= 16.
+// part: split-K partial logits [B][G][NO] (G partials per logit), NO <= 16.
 // One 16-lane row per batch row, lane o = class o: the lane sums its G partials
 // (all loads of a 64-chunk in flight, clamped addresses, masked afterwards), then
 // max / sum-exp / the label's logit are 16-lane DPP reductions.  Writes
@@ -141,12 +141,12 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
   const int base = bi.base();
   for (int b = threadIdx.x >> 4; b < B; b += blockDim.x >> 4) {
     const int label = labels32[bi.row(b, base)];
-    const float* src = part + ((long)b * NO + (own ? o : 0)) * G;
+    const float* src = part + (long)b * G * NO + (own ? o : 0);
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     for (int g0 = 0; g0 < G; g0 += 64) {
       float v[64];
 #pragma unroll
-      for (int u = 0; u < 64; ++u) v[u] = src[min(g0 + u, G - 1)];
+      for (int u = 0; u < 64; ++u) v[u] = src[(long)min(g0 + u, G - 1) * NO];
 #pragma unroll
       for (int u = 0; u < 64; ++u) a[u & 3] += (g0 + u < G) ? v[u] : 0.f;
     }

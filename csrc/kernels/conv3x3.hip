@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     }
   }
 
-  // epilogue: bias + ReLU + bf16 store (+ fc partial logits, layout [B][NOF][HW/16])
+  // epilogue: bias + ReLU + bf16 store (+ fc partial logits, layout [B][HW/16][NOF])
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
 #pragma unroll
       for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
         const float s = wave_sum(fcs[o]);
-        if (lane == 0 && tile0 < Ptot) fc_part[(n * NOF + o) * G + g] = s;
+        if (lane == 0 && tile0 < Ptot) fc_part[(n * G + g) * NOF + o] = s;
       }
     }
   }

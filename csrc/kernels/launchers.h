@@ -81,7 +81,7 @@ struct FcBwdExtras {
   float* loss_out = nullptr;
   const int* step_ctr = nullptr;
   // XENT: compute dL (softmax cross-entropy backward) in the prologue of every block
-  // from the fused conv+fc partials [B][NO][G] instead of reading dL; loss_rows unused.
+  // from the fused conv+fc partials [B][G][NO] instead of reading dL; loss_rows unused.
   const float* part = nullptr;
   int G = 0;
   const float* fc_bias = nullptr;

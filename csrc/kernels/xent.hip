@@ -91,11 +91,10 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ par
       dbias[c] = (((s_db[0][c] + s_db[1][c]) + s_db[2][c]) + s_db[3][c]) * dbias_scale;
 }
 
-// Engine variant: one wave per row, partial logits in [B][NO][G] layout (written by
-// the fused conv2 epilogue).  Lanes 4c..4c+3 own class c (c < NO <= 16): each sums
-// the G partials g = j, j+4, ... in order, then a fixed 2-step butterfly combines
-// the 4 lanes.  Writes per-row loss and dlogits; the batch mean loss and the fc
-// bias gradient are finished by fc_bwd's first block (it already holds dlogits).
+// Engine variant (fusion level 0): one workgroup, one 16-lane row per batch row over
+// partial logits in [B][G][NO] layout (written by the fused conv2 epilogue), see
+// xent_batch_block (common.h).  Writes per-row loss and dlogits; the batch mean loss
+// and the fc bias gradient are finished by fc_bwd's first block (it holds dlogits).
 __global__ __launch_bounds__(1024) void xent_rows_kernel(const float* __restrict__ part, int G,
                                                         const float* __restrict__ bias, int NO,
                                                         int B, const int* __restrict__ labels32,

@@ -21,7 +21,12 @@ from ddp_amd import native  # noqa: E402
 BF = torch.bfloat16
 
 
-def timed(fn, reps, iters):
+def timed(fn, reps, iters, eager=False):
+    if eager:  # plain launches (for counter collection); host-bound timing
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return float("nan")
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--eager", action="store_true", help="no graphs (rocprofv3 --pmc runs)")
     a = ap.parse_args()
     C = native.require()
     dev = "cuda"
@@ -84,7 +90,7 @@ def main():
         if a.only and a.only not in name:
             return
         try:
-            res[name] = round(timed(fn, a.reps, a.iters), 2)
+            res[name] = round(timed(fn, a.reps, a.iters, a.eager), 2)
         except Exception as e:  # report, keep going
             res[name] = f"error: {e}"
         print(f"{name:48s} {res[name]}", flush=True)
@@ -115,9 +121,10 @@ def main():
     w1slab = torch.empty(C.conv3x3_dgrad_blocks(B, H, W, 2) * 320, device=dev)
     gw = torch.empty(C2 * 9 * C1 + C2 + 320, device=dev)
     n_w2 = C2 * 9 * C1
-    segs = [(slab, n_w2 + C2, 0, n_w2, nb, gw, 1.0), (slab, n_w2 + C2, n_w2, C2, nb, gw[n_w2:], 1.0),
-            (w1slab, 320, 0, 288, w1slab.numel() // 320, gw[n_w2 + C2:], 1.0),
-            (w1slab, 320, 288, 32, w1slab.numel() // 320, gw[n_w2 + C2 + 288:], 1.0)]
+    o1, o2 = n_w2 + C2, n_w2 + C2 + 288
+    segs = [(slab, n_w2 + C2, 0, n_w2, nb, gw[:n_w2], 1.0), (slab, n_w2 + C2, n_w2, C2, nb, gw[n_w2:o1], 1.0),
+            (w1slab, 320, 0, 288, w1slab.numel() // 320, gw[o1:o2], 1.0),
+            (w1slab, 320, 288, 32, w1slab.numel() // 320, gw[o2:o2 + 32], 1.0)]
     run("grad_reduce (4 segs)", lambda: C.grad_reduce(segs))
     n = 520586
     p = r(n + 64)[:n]

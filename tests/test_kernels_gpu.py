@@ -75,11 +75,11 @@ def test_conv3x3_fwd_fused_fc(C, B):
     wfc = rnd(10, H * W, 64, scale=0.01, seed=6)
     bfc = (torch.randn(10) * 0.1).to(dev)
     y = torch.empty(B, H, W, 64, dtype=BF, device=dev)
-    part = torch.full((B, 10, H * W // 16), float("nan"), device=dev)
+    part = torch.full((B, H * W // 16, 10), float("nan"), device=dev)
     from ddp_amd.ops.functional import fc_weight_frag
 
     C.conv3x3_fwd(x, w, b, y, True, fc_weight_frag(wfc, H * W, 64), part, 10, 2)
-    logits = part.sum(2) + bfc
+    logits = part.sum(1) + bfc
     ref = R.fc_nhwc(y.float(), wfc.float(), bfc)  # the fc of exactly the stored bf16 activation
     close(logits, ref, rtol=1e-3, atol=1e-3)
     # engine cross-entropy over those [B][10][49] partials (+ fc bias grad / mean loss in fc_bwd)
