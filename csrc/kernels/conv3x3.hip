@@ -30,25 +30,42 @@
 
 namespace ddp_amd {
 
-// Cooperative global -> LDS copy of n 16-byte chunks: every thread keeps up to 8
-// loads in flight before its LDS writes (one memory round trip per 8 chunks instead
-// of one per chunk).  src(i) returns chunk i (zero-filled where out of range).
-template <typename SrcFn, typename DstFn>
-__device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
-  for (int base = threadIdx.x; base < n; base += 256 * 8) {
-    bf16x8 v[8];
+// Cooperative global -> LDS copy of 16-byte chunks from up to two index spaces
+// (n1 chunks of src1/dst1, then n2 of src2/dst2): every thread issues up to INF
+// loads before its first LDS write, so a block's whole staging is ONE memory round
+// trip when (n1 + n2) <= 256 * INF.  src(i) returns chunk i (zero-filled where out of
+// range).
+template <int INF, typename S1, typename D1, typename S2, typename D2>
+__device__ __forceinline__ void stage2(int n1, S1 src1, D1 dst1, int n2, S2 src2, D2 dst2) {
+  const int n = n1 + n2;
+  for (int base = threadIdx.x; base < n; base += 256 * INF) {
+    bf16x8 v[INF];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < INF; ++u) {
       const int i = base + u * 256;
-      v[u] = (i < n) ? src(i) : zero8();
+      v[u] = (i < n1) ? src1(i) : ((i < n) ? src2(i - n1) : zero8());
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < INF; ++u) {
       const int i = base + u * 256;
-      if (i < n) dst(i, v[u]);
+      if (i < n1) dst1(i, v[u]);
+      else if (i < n) dst2(i - n1, v[u]);
     }
   }
 }
+template <typename SrcFn, typename DstFn>
+__device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
+  stage2<8>(n, src, dst, 0, src, dst);
+}
+
+// Geometry specialisation: kernels take <GH, GW, GCI, GCO>; non-zero values replace
+// the runtime H, W, Cin, Cout so all index arithmetic (divisions by W, H*W, channel
+// counts) folds to constants.  The launchers pick <28, 28, 32, 64> - SimpleCNN's
+// conv2 - when the shape matches and the generic <0, 0, 0, 0> otherwise.
+#define DDP_GEOM_OVERRIDE()                                    \
+  if (GH) {                                                    \
+    H = GH; W = GW; Cin = GCI; Cout = GCO;                     \
+  }
 
 // LDS geometry shared by fwd / dgrad: a block covers CH = 64*PXT consecutive output
 // pixels of the flattened [B*H*W] space and stages the LINEAR pixel range
@@ -61,12 +78,13 @@ __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
 // A1X: the input X is NOT read from memory but recomputed in the staging pass as
 // relu(conv1(x)) from the uint8 dataset (x0 via the batch index list) - SimpleCNN's
 // first layer folded into the second (Cin must equal conv1's 32 output channels).
-template <int PXT, bool RELU, int NOF, bool A1X>
+template <int PXT, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO>
 __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     bf16_t* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
     const bf16_t* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
@@ -80,19 +98,19 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
   const long Pbase = P0 - W - 1;
 
   const int wc = KW / 8;
-  stage16(64 * wc,
-          [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
-          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sW + r * WS + c) = v; });
   const int xc = Cin / 8;
-  if (!A1X) {
-    stage16(XR * xc,
-            [&](int i) {
-              const int r = i / xc, c = (i - r * xc) * 8;
-              const long P = Pbase + r;
-              return (P >= 0 && P < Ptot) ? ld8(X + P * Cin + c) : zero8();
-            },
-            [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
-  } else {
+  // weights and (unless recomputed) the input rows in ONE round of loads
+  stage2<16>(64 * wc,
+             [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
+             [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sW + r * WS + c) = v; },
+             A1X ? 0 : XR * xc,
+             [&](int i) {
+               const int r = i / xc, c = (i - r * xc) * 8;
+               const long P = Pbase + r;
+               return (P >= 0 && P < Ptot) ? ld8(X + P * Cin + c) : zero8();
+             },
+             [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
+  if (A1X) {
     // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), conv1 weights, then a1
     float* sxx = reinterpret_cast<float*>(sX + XR * XS);
     float* sw1 = sxx + XR + 2 * W + 2;
@@ -240,12 +258,13 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
 // ---------------------------------------------------------------- data gradient
 // A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
 // being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
-template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X>
+template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI, int GCO>
 __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
     const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
@@ -261,15 +280,28 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
   const long P0 = (long)blockIdx.x * CH;
   const long Pbase = P0 - W - 1;
 
+  // conv1 input values for the fused w1 gradient: loads issued before the staging
+  // round so the dependent index -> image chain overlaps it
+  auto x0_at = [&](int r) {
+    const long P = Pbase + r;
+    float v = 0.f;
+    if (P >= 0 && P < Ptot) {
+      const int n = (int)(P / HW), rm = (int)(P - (long)n * HW);
+      if (x0_u8) v = (float)((const unsigned char*)x0)[(long)bi.row(n, bi.base()) * HW + rm] / 255.0f;
+      else v = ((const float*)x0)[P];
+    }
+    return v;
+  };
+  const float x0_pre = (FUSE_W1 && (int)threadIdx.x < XR) ? x0_at(threadIdx.x) : 0.f;
   const int wc = KW / 8, cpc = Cout / 8;
-  stage16(32 * wc,
+  stage2<16>(32 * wc,
           [&](int i) {
             const int r = i / wc, rest = (i - r * wc) * 8;  // rest = tap*Cout + co
             const int tap = rest / Cout, co = rest - tap * Cout;
             return ld8(WT + ((long)tap * Cin + ci_blk + r) * Cout + co);
           },
-          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sWT + r * WS + c) = v; });
-  stage16(XR * cpc,
+          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sWT + r * WS + c) = v; },
+          XR * cpc,
           [&](int i) {
             const int r = i / cpc, c = (i - r * cpc) * 8;
             const long P = Pbase + r;
@@ -284,17 +316,8 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
   if (A1X)
     for (int i = threadIdx.x; i < Cin * 10; i += 256) s_c1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
   if (FUSE_W1) {
-    const int base = x0_u8 ? bi.base() : 0;
-    for (int r = threadIdx.x; r < XR; r += 256) {
-      const long P = Pbase + r;
-      float v = 0.f;
-      if (P >= 0 && P < Ptot) {
-        const int n = (int)(P / HW), rm = (int)(P - (long)n * HW);
-        if (x0_u8) v = (float)((const unsigned char*)x0)[(long)bi.row(n, base) * HW + rm] / 255.0f;
-        else v = ((const float*)x0)[P];
-      }
-      sx0[r] = v;
-    }
+    if ((int)threadIdx.x < XR) sx0[threadIdx.x] = x0_pre;
+    for (int r = threadIdx.x + 256; r < XR; r += 256) sx0[r] = x0_at(r);
   }
 
   const int kofs = 8 * (lane >> 4);
@@ -433,11 +456,12 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // so the two 16-lane groups of a half-wave read 8 consecutive rows (conflict-free).
 // A1X: the X tile (a1 rows r0-1 .. r0+R) is recomputed from the uint8 images (rows
 // r0-2 .. r0+R+1) instead of being read from a stored a1 tensor.
-template <bool MASK_DY, bool A1X>
+template <bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
 __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
     float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  DDP_GEOM_OVERRIDE();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nRC = (H + R - 1) / R;
   const int n = blockIdx.x / nRC;
@@ -449,9 +473,9 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
   bf16_t* sX = sdY + (long)nslot * DS;
   const int XW = Wp + 2;
 
-  // ---- stage dY rows (masked) and X rows with halo (8 loads in flight per thread)
+  // ---- stage dY rows (masked) and X rows with halo: one round of loads
   const int cpy_dy = Cout / 8, cpy_x = Cin / 8;
-  stage16(nslot * cpy_dy,
+  stage2<16>(nslot * cpy_dy,
           [&](int i) {
             const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
             const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
@@ -467,21 +491,20 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
           [&](int i, bf16x8 v) {
             const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
             *reinterpret_cast<bf16x8*>(sdY + (long)slot * DS + ch) = v;
+          },
+          A1X ? 0 : (R + 2) * XW * cpy_x,
+          [&](int i) {
+            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+            const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+            const int hh = r0 - 1 + rr, ww = cc - 1;
+            return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                       ? ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
+          },
+          [&](int i, bf16x8 v) {
+            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+            *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
           });
-  if (!A1X) {
-    stage16((R + 2) * XW * cpy_x,
-            [&](int i) {
-              const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
-              const int rr = pos / XW, cc = pos - (pos / XW) * XW;
-              const int hh = r0 - 1 + rr, ww = cc - 1;
-              return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                         ? ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
-            },
-            [&](int i, bf16x8 v) {
-              const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
-              *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
-            });
-  } else {
+  if (A1X) {
     // uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, conv1 weights, then a1
     const int XW2 = Wp + 4, XR2 = R + 4;
     float* sxx = reinterpret_cast<float*>(sX + (long)(R + 2) * XW * XS);
@@ -589,6 +612,10 @@ size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
          (fuse_w1 ? sizeof(float) * (XR + 5 * 320) : 0);
 }
 
+static inline bool simplecnn_geom(int H, int W, int Cin, int Cout) {
+  return H == 28 && W == 28 && Cin == 32 && Cout == 64;
+}
+
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
                  int pxt, hipStream_t s, const C1Src* c1) {
@@ -599,7 +626,14 @@ void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y
   const size_t lds = conv3x3_fwd_lds(W, Cin, pxt, a1x);
   const bool fc = wfc != nullptr;  // host guarantees NO == 10 when fused
   const C1Src cs = a1x ? *c1 : C1Src();
-#define LF(PX, RL, NF, AX) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF, AX>), grid, dim3(256), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs)
+  const bool g = simplecnn_geom(H, W, Cin, Cout);
+#define LF(PX, RL, NF, AX)                                                                             \
+  do {                                                                                                 \
+    if (g) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF, AX, 28, 28, 32, 64>), grid, dim3(256),  \
+                              lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs);         \
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF, AX, 0, 0, 0, 0>), grid, dim3(256), lds,   \
+                            s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs);                \
+  } while (0)
   if (pxt == 2) {
     if (fc && a1x) LF(2, true, 10, true);
     else if (fc) LF(2, true, 10, false); else if (relu) LF(2, true, 0, false); else LF(2, false, 0, false);
@@ -620,7 +654,16 @@ void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const
   const bool mdy = Yact != nullptr, mx = Xact != nullptr || c1 != nullptr, w1 = w1slab != nullptr;
   const size_t lds = conv3x3_dgrad_lds(W, Cout, pxt, w1);
   const C1Src cs = c1 ? *c1 : C1Src();
-#define LD(PX, A, Bm, C, AX) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C, AX>), grid, dim3(256), lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab, cs)
+  const bool g = simplecnn_geom(H, W, Cin, Cout);
+#define LD(PX, A, Bm, C, AX)                                                                              \
+  do {                                                                                                    \
+    if (g) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C, AX, 28, 28, 32, 64>), grid, dim3(256), \
+                              lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi,   \
+                              w1slab, cs);                                                              \
+    else hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C, AX, 0, 0, 0, 0>), grid, dim3(256), lds,  \
+                            s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab,   \
+                            cs);                                                                        \
+  } while (0)
   if (pxt == 2) {
     if (w1 && c1) LD(2, false, true, true, true);
     else if (w1) LD(2, false, true, true, false);
@@ -659,7 +702,14 @@ void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float*
   const dim3 grid(conv3x3_wgrad_blocks(B, H, R), (Cout / 32) * (Cin / 16) / 4);
   const size_t lds = conv3x3_wgrad_lds(W, Cin, Cout, R, c1 != nullptr);
   const C1Src cs = c1 ? *c1 : C1Src();
-#define LW(M, AX) hipLaunchKernelGGL((conv3x3_wgrad_kernel<M, AX>), grid, dim3(256), lds, s, dY, Yact, X, slab, B, H, W, Cin, Cout, R, cs)
+  const bool g = simplecnn_geom(H, W, Cin, Cout);
+#define LW(M, AX)                                                                                   \
+  do {                                                                                              \
+    if (g) hipLaunchKernelGGL((conv3x3_wgrad_kernel<M, AX, 28, 28, 32, 64>), grid, dim3(256), lds, s, \
+                              dY, Yact, X, slab, B, H, W, Cin, Cout, R, cs);                      \
+    else hipLaunchKernelGGL((conv3x3_wgrad_kernel<M, AX, 0, 0, 0, 0>), grid, dim3(256), lds, s, dY,  \
+                            Yact, X, slab, B, H, W, Cin, Cout, R, cs);                            \
+  } while (0)
   if (c1) { if (Yact) LW(true, true); else LW(false, true); }
   else { if (Yact) LW(true, false); else LW(false, false); }
 #undef LW
