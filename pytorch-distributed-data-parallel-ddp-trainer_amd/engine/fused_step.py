@@ -41,7 +41,7 @@ class EngineOptions:
     force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
     # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd)
-    fuse_level: int = 0
+    fuse_level: int = 1
 
 
 class FusedSimpleCNNEngine:
