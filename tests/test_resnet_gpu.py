@@ -159,25 +159,37 @@ def test_pools_and_head(C):
 
 
 def test_resnet18_hip_vs_cpu_fp32():
+    """Whole-network gradients of the HIP ResNet-18 vs an fp32 CPU oracle.
+
+    A random-init ResNet-18 amplifies rounding through 20 BatchNorm backwards, so a
+    fixed tolerance is meaningless: the bar is the precision floor, i.e. the error
+    that torch's own bf16 CPU run of the same network shows against the same fp32
+    oracle (scripts/debug_resnet.py prints both columns).  The HIP path must be no
+    worse than that floor (plus a small slack) on every parameter."""
     from ddp_amd.models import resnet18
     from ddp_amd.ops import CrossEntropyLoss
 
     torch.manual_seed(0)
     cpu = resnet18(num_classes=10)
+    cpu16 = resnet18(num_classes=10)
+    cpu16.load_state_dict(cpu.state_dict())
     gpu = resnet18(num_classes=10).to(dev)
     gpu.load_state_dict(cpu.state_dict())
     x = torch.randn(4, 3, 64, 64)
     y = torch.randint(0, 10, (4,))
     lc = F.cross_entropy(cpu(x), y)
     lc.backward()
+    cpu16 = cpu16.to(torch.bfloat16)
+    F.cross_entropy(cpu16(x.to(torch.bfloat16)).float(), y).backward()
     lg = CrossEntropyLoss()(gpu(x.to(dev)), y.to(dev))
     lg.backward()
     assert abs(lg.item() - lc.item()) < 5e-2
     bad = []
-    for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
-        e = relerr(pg.grad, pc.grad)
-        if e > 0.15:  # bf16 activations through 20 layers vs fp32
-            bad.append((n, e))
+    for (n, pc), (_, p16), (_, pg) in zip(cpu.named_parameters(), cpu16.named_parameters(),
+                                          gpu.named_parameters()):
+        e, floor = relerr(pg.grad, pc.grad), relerr(p16.grad.float(), pc.grad)
+        if e > 1.25 * floor + 0.03:
+            bad.append((n, e, floor))
     assert not bad, bad
     for (n, bc), (_, bg) in zip(cpu.named_buffers(), gpu.named_buffers()):
         if bc.dtype.is_floating_point:
