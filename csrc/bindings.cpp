@@ -107,7 +107,8 @@ void op_conv3x3_fwd(const Tensor& X, const Tensor& Wt, const Tensor& bias, Tenso
     check(*fc_part, "fc_part", at::kFloat);
     TORCH_CHECK(Cout == 64 && (H * W) % 16 == 0 && NO == 10, "fused fc: Cout==64, HW%16==0, NO==10");
     TORCH_CHECK(wfc->numel() == (long)NO * H * W * Cout, "fused fc: wfc shape");
-    TORCH_CHECK(fc_part->numel() >= (long)B * (H * W / 16) * NO, "fused fc: fc_part too small");
+    TORCH_CHECK(fc_part->numel() >= 2L * conv3x3_dgrad_blocks(B, H, W, pxt) * NO,
+                "fused fc: fc_part too small ([blocks][2][NO])");
     wf = cbf(*wfc);
     part = fc_part->data_ptr<float>();
   }
@@ -198,7 +199,7 @@ void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, 
   TORCH_CHECK(X.numel() == (long)B * K && dX.numel() == X.numel(), "fc_bwd: X/dX shape");
   TORCH_CHECK(Wf.numel() == (long)NO * K && dW.numel() == Wf.numel() && NO <= 16, "fc_bwd: W shape");
   TORCH_CHECK(fc_bwd_lds(B, NO, false) <= 160 * 1024, "fc_bwd: batch too large for LDS");
-  TORCH_CHECK(K % 4 == 0, "fc_bwd: in_features must be a multiple of 4");
+  TORCH_CHECK(K % 2 == 0, "fc_bwd: in_features must be even");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(dW.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(X.data_ptr()) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(dX.data_ptr()) % 8 == 0 &&
@@ -249,17 +250,20 @@ void op_xent(const Tensor& part, int G, std::optional<Tensor> bias, const Tensor
   kcheck();
 }
 
-void op_xent_rows(const Tensor& part, int G, const Tensor& bias, const Tensor& labels32,
+void op_xent_rows(const Tensor& part, int HW, int CH, const Tensor& bias, const Tensor& labels32,
                   std::optional<Tensor> idx, Tensor& dlogits, Tensor& loss_rows, double gscale) {
   check(part, "part", at::kFloat); check(bias, "bias", at::kFloat); check(labels32, "labels", at::kInt);
   check(dlogits, "dlogits", at::kFloat); check(loss_rows, "loss_rows", at::kFloat);
   const int B = dlogits.size(0), NO = dlogits.size(1);
   TORCH_CHECK(bias.numel() == NO && NO <= 16, "xent_rows: at most 16 classes");
-  TORCH_CHECK(part.numel() >= (long)B * NO * G && loss_rows.numel() >= B, "xent_rows: sizes");
+  TORCH_CHECK(CH > 0 && CH <= HW && HW / CH + 2 <= 16, "xent_rows: block geometry");
+  const long nblk = ((long)B * HW + CH - 1) / CH;
+  TORCH_CHECK(part.numel() >= nblk * 2 * NO && loss_rows.numel() >= B, "xent_rows: sizes");
+  TORCH_CHECK((long)B * NO * 4 <= 64 * 1024, "xent_rows: batch too large");
   BatchIdx bi = make_bi(idx, std::nullopt, 0, 0, labels32.numel());
   if (!idx) TORCH_CHECK(labels32.numel() >= B, "xent_rows: labels");
-  xent_rows(part.data_ptr<float>(), G, bias.data_ptr<float>(), NO, B, labels32.data_ptr<int>(), bi,
-            dlogits.data_ptr<float>(), loss_rows.data_ptr<float>(), (float)gscale, cur_stream());
+  xent_rows(part.data_ptr<float>(), HW, CH, bias.data_ptr<float>(), NO, B, labels32.data_ptr<int>(),
+            bi, dlogits.data_ptr<float>(), loss_rows.data_ptr<float>(), (float)gscale, cur_stream());
   kcheck();
 }
 
@@ -534,6 +538,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("pending", &BucketState::pending)
       .def("reset", &BucketState::reset);
   m.def("noop", [](int blocks) { noop(blocks, nullptr, cur_stream()); kcheck(); });
+  m.def("stamps_set", [](std::optional<Tensor> buf) {
+    if (buf) TORCH_CHECK(buf->is_cuda() && buf->numel() * buf->element_size() >=
+                             (int64_t)STAMP_K_COUNT * STAMP_KSTRIDE * 8, "stamp buffer too small");
+    stamps_set(buf ? buf->data_ptr() : nullptr);
+  });
+  m.attr("STAMP_KSTRIDE") = STAMP_KSTRIDE;
+  m.attr("STAMP_K_COUNT") = (int)STAMP_K_COUNT;
   m.def("conv3x3_fwd", &op_conv3x3_fwd);
   m.def("conv3x3_dgrad", &op_conv3x3_dgrad);
   m.def("conv3x3_dgrad_fused_w1", &op_conv3x3_dgrad_fused_w1);
@@ -672,13 +683,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.a2 = bf(need("a2", at::kBFloat16, B * HW * c.C2));
              b.dz2 = bf(need("dz2", at::kBFloat16, B * HW * c.C2));
              b.dz1 = bf(need("dz1", at::kBFloat16, B * HW * c.C1));
-             b.fc_part = need("fc_part", at::kFloat, B * (HW / 16) * c.NO).data_ptr<float>();
+             b.fc_part = need("fc_part", at::kFloat, 2L * conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_fwd) * c.NO).data_ptr<float>();
              b.dlogits = need("dlogits", at::kFloat, B * c.NO).data_ptr<float>();
              b.loss_rows = need("loss_rows", at::kFloat, B).data_ptr<float>();
              b.loss_hist = need("loss_hist", at::kFloat, 1).data_ptr<float>();
              b.w2slab = need("w2slab", at::kFloat, (long)conv3x3_wgrad_blocks(B, c.H, c.wgrad_rows) * (9L * c.C1 * c.C2 + c.C2)).data_ptr<float>();
              b.w1slab = need("w1slab", at::kFloat, (long)conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_dgrad) * 320).data_ptr<float>();
              b.step_ctr = need("step_ctr", at::kInt, 1).data_ptr<int>();
+             b.xb = need("xb", at::kByte, B * HW).data_ptr<unsigned char>();
+             b.yb = need("yb", at::kInt, B).data_ptr<int>();
              Tensor images = need("images", at::kByte, HW);
              b.images = images.data_ptr<unsigned char>();
              Tensor labels = need("labels", at::kInt, 1);

@@ -27,6 +27,26 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 constexpr int WAVE = 64;
 
+// ---- diagnostic in-kernel phase stamps (scripts/stamps.py) ---------------------------
+// Each kernel TU has its own device pointer (set by stamps_set(); null in normal runs,
+// so a stamp costs one scalar load + branch).  DDP_STAMP(kid, slot) makes lane 0 of the
+// block's first wave store the 100 MHz constant-rate clock (s_memrealtime, comparable
+// across CUs) at buf[kid][block][slot]; kid = kernel id (STAMP_K_*), 8 slots per block.
+namespace {
+__constant__ unsigned long long* g_stamp_buf = nullptr;  // constant: a scalar load, no vmcnt wait
+}
+#define DDP_STAMP(kid, slot)                                                                 \
+  do {                                                                                       \
+    unsigned long long* _sb = g_stamp_buf;                                                   \
+    if (_sb && threadIdx.x == 0) {                                                           \
+      const unsigned _blk = blockIdx.x + blockIdx.y * gridDim.x;                             \
+      if (_blk < 4096)                                                                       \
+        _sb[(kid) * STAMP_KSTRIDE + _blk * STAMP_SLOTS + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                        \
+  } while (0)
+#define DDP_STAMPS_SETTER(name)                                                              \
+  void name(void* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &p, sizeof(p)); }
+
 __device__ __forceinline__ float bf2f(bf16_t b) {
   return __builtin_bit_cast(float, ((unsigned)b) << 16);
 }
@@ -83,6 +103,55 @@ __device__ __forceinline__ float conv1_eval(const float* w1, const float* b1, co
   return fmaxf(acc, 0.f);
 }
 
+// Recompute SimpleCNN's first layer a1 = relu(conv1(x)) (32 channels) into bf16 LDS
+// rows, bit-identical to conv1_fwd_kernel (conv1_eval order).  Wave w of a 256-thread
+// block owns channel group g = w (channels 8g..8g+7) for every position, so its conv1
+// weights are wave-uniform: Conv1Group loads them ONCE per wave into registers (call
+// conv1_group_load early - e.g. before the staging round - so the loads overlap it).
+// The only LDS traffic is the 9 input taps and one 16-byte store per position.
+//   valid(pos) -> position inside the image (else the row is zero-filled)
+//   tap(pos, k) -> input value of tap k (0 outside the image)
+//   dst(pos, g) -> bf16_t* of channels 8g..8g+7 of position pos
+struct Conv1Group {
+  float w[8][9];
+  float b[8];
+};
+__device__ __forceinline__ Conv1Group conv1_group_load(const float* __restrict__ w1,
+                                                       const float* __restrict__ b1, int g) {
+  Conv1Group r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.w[j][k] = w1[(8 * g + j) * 9 + k];
+    r.b[j] = b1[8 * g + j];
+  }
+  return r;
+}
+__device__ __forceinline__ float conv1_eval_g(const Conv1Group& cg, const float* v, int j) {
+  float acc = cg.b[j];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc = fmaf(cg.w[j][k], v[k], acc);  // == conv1_eval
+  return fmaxf(acc, 0.f);
+}
+template <typename ValidFn, typename TapFn, typename DstFn>
+__device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group& cg, int g,
+                                                     ValidFn valid, TapFn tap, DstFn dst) {
+  for (int pos = threadIdx.x & 63; pos < npos; pos += 64) {
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (valid(pos)) {
+      float v[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) v[k] = tap(pos, k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = conv1_eval_g(cg, v, j);
+    }
+    uint4 pk;
+    const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
+    pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
+    *reinterpret_cast<uint4*>(dst(pos, g)) = pk;
+  }
+}
+
 // ---- cross-lane reductions on DPP (VALU modifiers, no LDS round trips) --------------
 // dpp<CTRL>(v): v of the lane selected by the DPP control (quad_perm 0x00-0xFF,
 // row_half_mirror 0x141, row_mirror 0x140), all rows / banks enabled.
@@ -125,39 +194,59 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Whole-batch softmax cross-entropy on one workgroup, fixed summation order.
-// part: split-K partial logits [B][G][NO] (G partials per logit), NO <= 16.
-// One 16-lane row per batch row, lane o = class o: the lane sums its G partials
-// (all loads of a 64-chunk in flight, clamped addresses, masked afterwards), then
-// max / sum-exp / the label's logit are 16-lane DPP reductions.  Writes
-// dl[b*NO + o] = (softmax - onehot) * gscale and loss[b] = logsumexp - x[label].
-// Used by xent_rows (own kernel) and by the XENT prologue of fc_bwd, so both
-// produce bit-identical values.  blockDim.x must be a multiple of 64.
-__device__ __forceinline__ void xent_batch_block(const float* __restrict__ part, int G,
+// part: the fused conv2+fc epilogue's partial logits, one pair of [NO] rows per conv
+// block of CH consecutive pixels of the flattened [B*HW] space: part[blk][slot][o],
+// slot 0 = the image of the block's first pixel, slot 1 = the next image (CH <= HW).
+// Image b's logits are the fixed-order sum over the blocks kb0..kb1 that touch it.
+// Phase 0: thread b < B requests its row's label (a dependent step -> index -> label
+// chain) before anything else.  Phase 1: one thread per logit (b, o) loads its <= 16
+// block partials (clamped block index, masked) and adds the bias -> s_lg[b][o] (LDS
+// scratch, B*NO floats).  Phase 2: one thread per row does max / sum-exp / the label's
+// logit serially over the NO classes.  Writes dl[b*NO + o] = (softmax - onehot) * gscale
+// and loss[b] = logsumexp - x[label].  Contains a __syncthreads(): every thread of the
+// block must call it; dl / loss may be LDS or global, and the caller syncs before
+// reading them.  Used by xent_rows (own kernel) and by the XENT prologue of fc_bwd, so
+// both produce bit-identical values.
+constexpr int XENT_MAX_BLK = 16;  // conv blocks per image: HW / CH + 2 <= 16
+__device__ __forceinline__ void xent_batch_block(const float* __restrict__ part, int HW, int CH,
                                                  const float* __restrict__ bias, int NO, int B,
                                                  const int* __restrict__ labels32, const BatchIdx& bi,
-                                                 float gscale, float* dl, float* loss) {
-  const int o = threadIdx.x & 15;
-  const bool own = o < NO;
+                                                 float gscale, float* dl, float* loss, float* s_lg) {
   const int base = bi.base();
-  for (int b = threadIdx.x >> 4; b < B; b += blockDim.x >> 4) {
-    const int label = labels32[bi.row(b, base)];
-    const float* src = part + (long)b * G * NO + (own ? o : 0);
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int g0 = 0; g0 < G; g0 += 64) {
-      float v[64];
+  const int lab0 = (int)threadIdx.x < B ? labels32[bi.row(threadIdx.x, base)] : 0;
+  for (int t = threadIdx.x; t < B * NO; t += blockDim.x) {
+    const int b = t / NO, o = t - (t / NO) * NO;
+    const long p0 = (long)b * HW;
+    const int kb0 = (int)(p0 / CH), kb1 = (int)((p0 + HW - 1) / CH);
+    float v[XENT_MAX_BLK];
 #pragma unroll
-      for (int u = 0; u < 64; ++u) v[u] = src[(long)min(g0 + u, G - 1) * NO];
-#pragma unroll
-      for (int u = 0; u < 64; ++u) a[u & 3] += (g0 + u < G) ? v[u] : 0.f;
+    for (int j = 0; j < XENT_MAX_BLK; ++j) {
+      const int kb = min(kb0 + j, kb1);
+      const int slot = ((long)kb * CH) / HW == b ? 0 : 1;
+      v[j] = part[((long)kb * 2 + slot) * NO + o];
     }
-    const float x = own ? bias[o] + ((a[0] + a[1]) + (a[2] + a[3])) : -INFINITY;
-    const float mx = row16_max(x);
-    const float e = own ? __expf(x - mx) : 0.f;
-    const float se = row16_sum(e);
-    const float xl = row16_sum(own && o == label ? x : 0.f);
-    if (own) dl[b * NO + o] = (e / se - (o == label ? 1.f : 0.f)) * gscale;
-    if (o == 0) loss[b] = mx + __logf(se) - xl;
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < XENT_MAX_BLK; ++j) a += (kb0 + j <= kb1) ? v[j] : 0.f;
+    s_lg[t] = bias[o] + a;
   }
+  DDP_STAMP(STAMP_K_FC_BWD, 5);
+  __syncthreads();
+  DDP_STAMP(STAMP_K_FC_BWD, 6);
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    int label = b == (int)threadIdx.x ? lab0 : labels32[bi.row(b, base)];
+    label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
+    const float* x = s_lg + b * NO;
+    float mx = x[0];
+    for (int o = 1; o < NO; ++o) mx = fmaxf(mx, x[o]);
+    float se = 0.f;
+    for (int o = 0; o < NO; ++o) se += __expf(x[o] - mx);
+    const float inv = 1.f / se;
+    for (int o = 0; o < NO; ++o)
+      dl[b * NO + o] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
+    loss[b] = mx + __logf(se) - x[label];
+  }
+  DDP_STAMP(STAMP_K_FC_BWD, 7);
 }
 
 }  // namespace ddp_amd

@@ -150,4 +150,6 @@ void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const bf16_t* dy, con
 #undef L1W
 }
 
+DDP_STAMPS_SETTER(stamps_set_conv1)
+
 }  // namespace ddp_amd

@@ -74,6 +74,18 @@ __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
 // Weight rows are padded by 8 elements so the 16 rows of an A fragment start on
 // 16 distinct 4-bank groups (conflict-free ds_read_b128).
 
+// LDS bytes of the forward's staging area (weights, input rows, conv1 recompute
+// scratch), rounded to 16; the fused-fc epilogue's per-tile partials follow it.
+__host__ __device__ inline size_t fwd_stage_lds(int W, int Cin, int pxt, bool a1x) {
+  const size_t XR = 64 * pxt + 2 * W + 2;
+  const size_t b = sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 8) + XR * (Cin + 8)) +
+                   (a1x ? sizeof(float) * ((XR + 2 * W + 2) + Cin * 10) : 0);
+  return (b + 15) & ~(size_t)15;
+}
+constexpr int FC_MAX_NOF = 16;
+// [wave][pixel tile][channel group][class] floats
+__host__ __device__ inline size_t fc_epi_lds(int pxt, int nof) { return sizeof(float) * 4 * pxt * 4 * nof; }
+
 // ---------------------------------------------------------------- forward
 // A1X: the input X is NOT read from memory but recomputed in the staging pass as
 // relu(conv1(x)) from the uint8 dataset (x0 via the batch index list) - SimpleCNN's
@@ -84,6 +96,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     bf16_t* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
     const bf16_t* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  DDP_STAMP(STAMP_K_CONV_FWD, 0);
   DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -99,6 +112,8 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
 
   const int wc = KW / 8;
   const int xc = Cin / 8;
+  Conv1Group cg;
+  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
   stage2<16>(64 * wc,
              [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
@@ -111,9 +126,10 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
              },
              [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
   if (A1X) {
-    // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), conv1 weights, then a1
+    // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), then a1 (conv1 recompute).
+    // The block also writes its own pixels (and the labels of images starting in them)
+    // to the step's compact batch buffers, if given.
     float* sxx = reinterpret_cast<float*>(sX + XR * XS);
-    float* sw1 = sxx + XR + 2 * W + 2;
     const int NXX = XR + 2 * W + 2;
     const int base = c1.bi.base();
     for (int r = threadIdx.x; r < NXX; r += 256) {
@@ -121,34 +137,29 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
       float v = 0.f;
       if (P >= 0 && P < Ptot) {
         const int n = (int)(P / HW), rm = (int)(P - (long)n * HW);
-        v = (float)c1.x[(long)c1.bi.row(n, base) * HW + rm] / 255.0f;
+        const int row = c1.bi.row(n, base);
+        const unsigned char u = c1.x[(long)row * HW + rm];
+        v = (float)u / 255.0f;
+        if (c1.xb_out && P >= P0 && P < P0 + CH) {
+          c1.xb_out[P] = u;
+          if (rm == 0) c1.yb_out[n] = c1.labels[row];
+        }
       }
       sxx[r] = v;
     }
-    for (int i = threadIdx.x; i < Cin * 10; i += 256) sw1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
     __syncthreads();
-    for (int i = threadIdx.x; i < XR * xc; i += 256) {
-      const int r = i / xc, c0 = (i - r * xc) * 8;
-      const long P = Pbase + r;
-      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (P >= 0 && P < Ptot) {
-        const int rm = (int)(P % HW);
-        const int hh = rm / W, ww = rm - (rm / W) * W;
-        float v[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
+    DDP_STAMP(STAMP_K_CONV_FWD, 1);
+    conv1_recompute_tile(
+        XR, cg, wave, [&](int r) { const long P = Pbase + r; return P >= 0 && P < Ptot; },
+        [&](int r, int k) {
+          const long P = Pbase + r;
+          const int rm = (int)(P % HW);
+          const int hh = rm / W, ww = rm - (rm / W) * W;
           const int dh = k / 3 - 1, dw = k % 3 - 1;
           const bool ok = (unsigned)(hh + dh) < (unsigned)H && (unsigned)(ww + dw) < (unsigned)W;
-          v[k] = ok ? sxx[r + W + 1 + dh * W + dw] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = conv1_eval(sw1, sw1 + Cin * 9, v, c0 + j);
-      }
-      uint4 pk;
-      const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
-      pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-      *reinterpret_cast<uint4*>(sX + r * XS + c0) = pk;
-    }
+          return ok ? sxx[r + W + 1 + dh * W + dw] : 0.f;
+        },
+        [&](int r, int g) { return sX + r * XS + 8 * g; });
   }
 
   const int kofs = 8 * (lane >> 4);
@@ -181,6 +192,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
               wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
   }
   __syncthreads();
+  DDP_STAMP(STAMP_K_CONV_FWD, 2);
 
   f32x4 acc[PXT][4];
 #pragma unroll
@@ -211,7 +223,10 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     }
   }
 
-  // epilogue: bias + ReLU + bf16 store (+ fc partial logits, layout [B][HW/16][NOF])
+  DDP_STAMP(STAMP_K_CONV_FWD, 3);
+  // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
+  // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
+  float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, PXT, A1X));
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -241,18 +256,34 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
       }
     }
     if (NOF > 0) {
-      // the 16-pixel tile lies in one image (HW % 16 == 0, checked on host)
-      const long tile0 = P0 + (wave * PXT + pt) * 16;
-      const int G = HW / 16;
-      const long n = tile0 / HW;
-      const int g = (int)((tile0 - n * HW) / 16);
+      // sum over the tile's 16 pixels (the 16 lanes of a row share a channel group)
 #pragma unroll
       for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
-        const float s = wave_sum(fcs[o]);
-        if (lane == 0 && tile0 < Ptot) fc_part[(n * G + g) * NOF + o] = s;
+        const float s = sum16(fcs[o]);
+        if ((lane & 15) == 0) s_fc[(((wave * PXT + pt) * 4) + (lane >> 4)) * NOF + o] = s;
       }
     }
   }
+  if (NOF > 0) {
+    __syncthreads();
+    // per (image slot, class): fixed-order sum over the block's tiles of that image and
+    // the 4 channel groups.  Slot 0 = the image of the block's first pixel, slot 1 = the
+    // next one (a block of 64*PXT <= HW pixels spans at most two images).
+    if ((int)threadIdx.x < 2 * NOF) {
+      const int slot = threadIdx.x / NOF, o = threadIdx.x - (threadIdx.x / NOF) * NOF;
+      const long img = P0 / HW + slot;
+      float acc_o = 0.f;
+      for (int tile = 0; tile < 4 * PXT; ++tile) {
+        const long tp = P0 + tile * 16;
+        if (tp < Ptot && tp / HW == img) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc_o += s_fc[(tile * 4 + g) * NOF + o];
+        }
+      }
+      fc_part[((long)blockIdx.x * 2 + slot) * NOF + o] = acc_o;
+    }
+  }
+  DDP_STAMP(STAMP_K_CONV_FWD, 4);
 }
 
 // ---------------------------------------------------------------- data gradient
@@ -264,6 +295,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  DDP_STAMP(STAMP_K_DGRAD, 0);
   DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
   bf16_t* sDY = sWT + 32 * WS;                           // [XR][Cout]
   float* sx0 = reinterpret_cast<float*>(sDY + XR * DS);  // [XR] conv1 input (FUSE_W1)
   float* s_w1 = sx0 + XR;                                // [4][320] (FUSE_W1)
-  float* s_c1 = s_w1 + 4 * 320;                          // conv1 w/b (A1X mask recompute)
+  unsigned char* s_m1 = reinterpret_cast<unsigned char*>(s_w1 + 4 * 320);  // [CH][4] a1>0 bits (A1X)
   const long P0 = (long)blockIdx.x * CH;
   const long Pbase = P0 - W - 1;
 
@@ -293,6 +325,8 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     return v;
   };
   const float x0_pre = (FUSE_W1 && (int)threadIdx.x < XR) ? x0_at(threadIdx.x) : 0.f;
+  Conv1Group cg;
+  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
   const int wc = KW / 8, cpc = Cout / 8;
   stage2<16>(32 * wc,
           [&](int i) {
@@ -313,11 +347,34 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
             return v;
           },
           [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * 8; *reinterpret_cast<bf16x8*>(sDY + r * DS + c) = v; });
-  if (A1X)
-    for (int i = threadIdx.x; i < Cin * 10; i += 256) s_c1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
   if (FUSE_W1) {
     if ((int)threadIdx.x < XR) sx0[threadIdx.x] = x0_pre;
     for (int r = threadIdx.x + 256; r < XR; r += 256) sx0[r] = x0_at(r);
+  }
+  if (A1X) {
+    // ReLU-input mask of the block's own pixels: bit j of s_m1[lp*4 + g] = (a1[lp][8g+j] > 0),
+    // a1 recomputed from conv1 exactly as stored (bf16-rounded), channel group wave-uniform
+    __syncthreads();
+    const int g = wave;
+    for (int lp = lane; lp < CH; lp += 64) {
+      const long P = P0 + lp;
+      unsigned m = 0;
+      if (P < Ptot) {
+        const int rm = (int)(P % HW);
+        const int hh = rm / W, ww = rm - (rm / W) * W;
+        float v[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int dh = k / 3 - 1, dw = k % 3 - 1;
+          const bool ok = (unsigned)(hh + dh) < (unsigned)H && (unsigned)(ww + dw) < (unsigned)W;
+          v[k] = ok ? sx0[lp + W + 1 + dh * W + dw] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          m |= (bf2f(f2bf(conv1_eval_g(cg, v, j))) > 0.f ? 1u : 0u) << j;
+      }
+      s_m1[lp * 4 + g] = (unsigned char)m;
+    }
   }
 
   const int kofs = 8 * (lane >> 4);
@@ -344,6 +401,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     }
   }
   __syncthreads();
+  DDP_STAMP(STAMP_K_DGRAD, 1);
 
   f32x4 acc[PXT][2];
 #pragma unroll
@@ -371,6 +429,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     }
   }
 
+  DDP_STAMP(STAMP_K_DGRAD, 2);
   float w1a[FUSE_W1 ? 2 : 1][4][10];
   if (FUSE_W1) {
 #pragma unroll
@@ -397,8 +456,10 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
       const int ci = ci_blk + 16 * t + 4 * (lane >> 4);
       float v[4] = {acc[pt][t][0], acc[pt][t][1], acc[pt][t][2], acc[pt][t][3]};
       if (MASK_X && A1X) {
+        const int lp = (wave * PXT + pt) * 16 + col;
+        const unsigned m = s_m1[lp * 4 + (ci >> 3)] >> (ci & 7);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (bf2f(f2bf(conv1_eval(s_c1, s_c1 + Cin * 9, xv, ci + j))) > 0.f) ? v[j] : 0.f;
+        for (int j = 0; j < 4; ++j) v[j] = ((m >> j) & 1u) ? v[j] : 0.f;
       } else if (MASK_X) {
         float xm[4];
         unpack4(xa[pt][t], xm);
@@ -420,6 +481,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
       }
     }
   }
+  DDP_STAMP(STAMP_K_DGRAD, 3);
   if (FUSE_W1) {
     // reduce over the 16 pixel lanes that share a channel group, then over waves (fixed order)
 #pragma unroll
@@ -443,6 +505,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     for (int i = threadIdx.x; i < 320; i += 256)
       w1slab[(long)blockIdx.x * 320 + i] = ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i];
   }
+  DDP_STAMP(STAMP_K_DGRAD, 4);
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -461,6 +524,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
     float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  DDP_STAMP(STAMP_K_WGRAD, 0);
   DDP_GEOM_OVERRIDE();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nRC = (H + R - 1) / R;
@@ -473,6 +537,8 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
   bf16_t* sX = sdY + (long)nslot * DS;
   const int XW = Wp + 2;
 
+  Conv1Group cg;
+  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
   // ---- stage dY rows (masked) and X rows with halo: one round of loads
   const int cpy_dy = Cout / 8, cpy_x = Cin / 8;
   stage2<16>(nslot * cpy_dy,
@@ -505,10 +571,9 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
             *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
           });
   if (A1X) {
-    // uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, conv1 weights, then a1
+    // uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, then a1 (conv1 recompute)
     const int XW2 = Wp + 4, XR2 = R + 4;
     float* sxx = reinterpret_cast<float*>(sX + (long)(R + 2) * XW * XS);
-    float* sw1 = sxx + XR2 * XW2;
     const long img = (long)c1.bi.row(n, c1.bi.base()) * H * W;
     for (int i = threadIdx.x; i < XR2 * XW2; i += 256) {
       const int rr = i / XW2, cc = i - (i / XW2) * XW2;
@@ -516,27 +581,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
       sxx[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
                    ? (float)c1.x[img + hh * W + ww] / 255.0f : 0.f;
     }
-    for (int i = threadIdx.x; i < Cin * 10; i += 256) sw1[i] = (i < Cin * 9) ? c1.w[i] : c1.b[i - Cin * 9];
     __syncthreads();
-    for (int i = threadIdx.x; i < (R + 2) * XW * cpy_x; i += 256) {
-      const int pos = i / cpy_x, c0 = (i - pos * cpy_x) * 8;
-      const int rr = pos / XW, cc = pos - (pos / XW) * XW;
-      const int hh = r0 - 1 + rr, ww = cc - 1;
-      float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) {
-        float v[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) v[k] = sxx[(rr + k / 3) * XW2 + cc + k % 3];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = conv1_eval(sw1, sw1 + Cin * 9, v, c0 + j);
-      }
-      uint4 pk;
-      const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
-      pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-      *reinterpret_cast<uint4*>(sX + (long)pos * XS + c0) = pk;
-    }
+    DDP_STAMP(STAMP_K_WGRAD, 1);
+    conv1_recompute_tile(
+        (R + 2) * XW, cg, wave,
+        [&](int pos) {
+          const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+          return (unsigned)(r0 - 1 + rr) < (unsigned)H && (unsigned)(cc - 1) < (unsigned)W;
+        },
+        [&](int pos, int k) {
+          const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+          return sxx[(rr + k / 3) * XW2 + cc + k % 3];
+        },
+        [&](int pos, int g) { return sX + (long)pos * XS + 8 * g; });
   }
   __syncthreads();
+  DDP_STAMP(STAMP_K_WGRAD, 2);
 
   // ---- wave assignment: (pair of 16-wide co tiles) x (16-wide ci tile)
   const int nct = Cin / 16;
@@ -586,6 +646,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
     accb[1] = mfma16(a[1], ones, accb[1]);
   }
 
+  DDP_STAMP(STAMP_K_WGRAD, 3);
   // ---- slab row: [Cout][3][3][Cin] (OHWI, the weight's native layout) then [Cout] bias
   float* out = slab + (long)blockIdx.x * ((long)Cout * 9 * Cin + Cout);
 #pragma unroll
@@ -597,19 +658,18 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
       for (int tap = 0; tap < 9; ++tap) out[((long)co * 9 + tap) * Cin + ciT + i16] = acc[c][tap][r];
       if (ciT == 0 && i16 == 0) out[(long)Cout * 9 * Cin + co] = accb[c][r];
     }
+  DDP_STAMP(STAMP_K_WGRAD, 4);
 }
 
 // ---------------------------------------------------------------- launchers
 size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x) {
-  const size_t XR = 64 * pxt + 2 * W + 2;
-  return sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 8) + XR * (Cin + 8)) +
-         (a1x ? sizeof(float) * ((XR + 2 * W + 2) + Cin * 10) : 0);
+  return fwd_stage_lds(W, Cin, pxt, a1x) + fc_epi_lds(pxt, FC_MAX_NOF);
 }
 
 size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
   const size_t XR = 64 * pxt + 2 * W + 2;
   return sizeof(bf16_t) * ((size_t)32 * (9 * Cout + 8) + XR * (Cout + 8)) +
-         (fuse_w1 ? sizeof(float) * (XR + 5 * 320) : 0);
+         (fuse_w1 ? sizeof(float) * (XR + 4 * 320) + 4 * 64 * pxt : 0);
 }
 
 static inline bool simplecnn_geom(int H, int W, int Cin, int Cout) {
@@ -714,5 +774,7 @@ void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float*
   else { if (Yact) LW(true, false); else LW(false, false); }
 #undef LW
 }
+
+DDP_STAMPS_SETTER(stamps_set_conv3x3)
 
 }  // namespace ddp_amd

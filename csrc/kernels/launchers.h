@@ -8,6 +8,9 @@
 
 namespace ddp_amd {
 
+// ---- diagnostic phase stamps (common.h DDP_STAMP); buf = u64[STAMP_K_COUNT][4096][8] or null
+void stamps_set(void* buf);
+
 // ---- conv1 (Cin = 1) ---------------------------------------------------------------
 void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, bf16_t* y,
                int B, int H, int W, int Cout, hipStream_t s);
@@ -82,8 +85,8 @@ struct FcBwdExtras {
   const int* step_ctr = nullptr;
   // XENT: compute dL (softmax cross-entropy backward) in the prologue of every block
   // from the fused conv+fc partials [B][G][NO] instead of reading dL; loss_rows unused.
-  const float* part = nullptr;
-  int G = 0;
+  const float* part = nullptr;  // fused conv partials [blk][2][NO] (common.h xent_batch_block)
+  int HW = 0, CH = 0;           // image pixels, pixels per conv block
   const float* fc_bias = nullptr;
   const int* labels32 = nullptr;
   BatchIdx bi{};
@@ -99,8 +102,9 @@ void xent(const float* part, int G, const float* bias, int C, int B, const long 
           const int* labels32, BatchIdx bi, float* logits_out, float* dlogits, float* loss_out,
           float* dbias, float gscale, float dbias_scale, hipStream_t s);
 
-void xent_rows(const float* part, int G, const float* bias, int NO, int B, const int* labels32,
-               BatchIdx bi, float* dlogits, float* loss_rows, float gscale, hipStream_t s);
+void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int B,
+               const int* labels32, BatchIdx bi, float* dlogits, float* loss_rows, float gscale,
+               hipStream_t s);
 
 // ---- optimizer / reductions -----------------------------------------------------------
 struct SgdArgs {

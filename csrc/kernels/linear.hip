@@ -67,30 +67,56 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __
   out[i] = s + (bias ? bias[o] : 0.f);
 }
 
-// fc backward: a block owns 256 consecutive columns k (4 per lane, 8-byte loads)
-// and its 4 waves split the batch rows (wave w: rows w, w+4, ...), so every wave has
-// its rows' loads in flight at once; the per-wave dW partials are summed in fixed
-// wave order through LDS.  NOT = compile-time class capacity (guards o < NO).
-template <bool MASK, bool XENT, int NOT>
-__global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ dL,
-                                                     const bf16_t* __restrict__ X,
-                                                     const bf16_t* __restrict__ Wf,
-                                                     bf16_t* __restrict__ dX, float* __restrict__ dW,
-                                                     float scale, int B, long K, int NO,
-                                                     FcBwdExtras ex) {
+// fc backward: a block of WPB waves owns FCB_COLS = 128 consecutive columns k (2 per
+// lane, one 4-byte load per row) and its waves split the batch rows (wave w: rows
+// w, w + WPB, ...).  The W columns and the first RB rows of X are requested BEFORE the
+// prologue (cross-entropy backward / dL copy) so they land while it runs.  Every
+// branch on the row count or the class count is wave-uniform (scalar), row addresses
+// are clamped instead of guarded, so a wave keeps all its loads in flight.  dW: the
+// waves' partials are summed in fixed wave order through LDS and written as coalesced
+// rows.  NOT = compile-time class capacity (NOT == 10 fixes NO = 10).
+constexpr int FCB_COLS = 128;
+constexpr int FCB_RB = 8;  // rows in flight per wave
+
+template <bool MASK, bool XENT, int NOT, int WPB>
+__global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restrict__ dL,
+                                                          const bf16_t* __restrict__ X,
+                                                          const bf16_t* __restrict__ Wf,
+                                                          bf16_t* __restrict__ dX,
+                                                          float* __restrict__ dW, float scale,
+                                                          int B, long K, int NO_rt,
+                                                          FcBwdExtras ex) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* s_dl = smem;                 // [B][NO]
-  float* s_loss = smem + B * NO;      // [B]        (XENT)
-  float* s_red = smem + (XENT ? B * (NO + 1) : B * NO);  // [3][NO][256] wave partials
-  s_red = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(s_red) + 15) & ~(uintptr_t)15);
+  DDP_STAMP(STAMP_K_FC_BWD, 0);
+  const int NO = NOT == 10 ? 10 : NO_rt;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* s_dl = smem;            // [B][NO]
+  float* s_loss = s_dl + B * NO;  // [B]
+  float* s_lg = s_loss + B;       // [B][NO] cross-entropy scratch (XENT)
+  float* s_red = smem + (((XENT ? 2 * B * NO : B * NO) + B + 3) & ~3);  // [WPB][NOT][COLS]
+
+  const long col = (long)blockIdx.x * FCB_COLS + 2 * lane;
+  const bool active = col < K;  // host guarantees K % 2 == 0
+  const long cc = active ? col : 0;
+  // ---- this block's loads first (independent of the prologue)
+  unsigned wr[NOT];
+#pragma unroll
+  for (int o = 0; o < NOT; ++o) wr[o] = (o < NO) ? *reinterpret_cast<const unsigned*>(Wf + (long)o * K + cc) : 0u;
+  const int nr = B > wave ? (B - wave + WPB - 1) / WPB : 0;  // rows of this wave (uniform)
+  unsigned xr[FCB_RB];
+#pragma unroll
+  for (int u = 0; u < FCB_RB; ++u) {
+    const int b = min(wave + WPB * u, B - 1);
+    xr[u] = *reinterpret_cast<const unsigned*>(X + (long)b * K + cc);
+  }
+  // ---- prologue: dL of the whole batch into LDS
   if (XENT) {
-    // every block recomputes the (tiny) cross-entropy backward of the whole batch
-    xent_batch_block(ex.part, ex.G, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_dl, s_loss);
+    xent_batch_block(ex.part, ex.HW, ex.CH, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_dl, s_loss, s_lg);
   } else {
-    for (int i = threadIdx.x; i < B * NO; i += 256) s_dl[i] = dL[i];
+    for (int i = threadIdx.x; i < B * NO; i += WPB * 64) s_dl[i] = dL[i];
   }
   __syncthreads();
+  DDP_STAMP(STAMP_K_FC_BWD, 1);
   if (blockIdx.x == 0) {
     // fc bias gradient (sum over the batch, fixed order) and the batch-mean loss
     if (ex.dbias && threadIdx.x < NO) {
@@ -105,73 +131,68 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const float* __restrict__ d
       ex.loss_out[ex.step_ctr ? *ex.step_ctr : 0] = acc / (float)B;
     }
   }
-  const long k0 = (long)blockIdx.x * 256 + lane * 4;
-  const bool active = k0 < K;  // host guarantees K % 4 == 0
-  float w[NOT][4], dw[NOT][4];
+  float w0[NOT], w1[NOT], dw0[NOT], dw1[NOT];
 #pragma unroll
   for (int o = 0; o < NOT; ++o) {
-    float t[4] = {0.f, 0.f, 0.f, 0.f};
-    if (active && o < NO) unpack4(*reinterpret_cast<const uint2*>(Wf + (long)o * K + k0), t);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) { w[o][c] = t[c]; dw[o][c] = 0.f; }
+    w0[o] = __builtin_bit_cast(float, wr[o] << 16);
+    w1[o] = __builtin_bit_cast(float, wr[o] & 0xffff0000u);
+    dw0[o] = 0.f;
+    dw1[o] = 0.f;
   }
-  constexpr int RB = 8;  // rows in flight per wave
-  for (int b0 = wave; b0 < B; b0 += 4 * RB) {
-    uint2 xr[RB];
+  for (int u0 = 0; u0 < nr; u0 += FCB_RB) {
+    if (u0 > 0) {
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      const int b = b0 + 4 * u;
-      xr[u] = (active && b < B) ? *reinterpret_cast<const uint2*>(X + (long)b * K + k0) : make_uint2(0u, 0u);
+      for (int u = 0; u < FCB_RB; ++u) {
+        const int b = min(wave + WPB * (u0 + u), B - 1);
+        xr[u] = *reinterpret_cast<const unsigned*>(X + (long)b * K + cc);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      const int b = b0 + 4 * u;
-      if (b < B) {
-        float xa[4];
-        unpack4(xr[u], xa);
+    for (int u = 0; u < FCB_RB; ++u) {
+      if (u0 + u < nr) {  // wave-uniform
+        const int b = wave + WPB * (u0 + u);
+        const float x0 = __builtin_bit_cast(float, xr[u] << 16);
+        const float x1 = __builtin_bit_cast(float, xr[u] & 0xffff0000u);
         const float* dl = s_dl + b * NO;
-        float dz[4] = {0.f, 0.f, 0.f, 0.f};
+        float dz0 = 0.f, dz1 = 0.f;
 #pragma unroll
         for (int o = 0; o < NOT; ++o)
           if (o < NO) {
             const float d = dl[o];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              dz[c] = fmaf(d, w[o][c], dz[c]);
-              dw[o][c] = fmaf(d, xa[c], dw[o][c]);
-            }
+            dz0 = fmaf(d, w0[o], dz0);
+            dz1 = fmaf(d, w1[o], dz1);
+            dw0[o] = fmaf(d, x0, dw0[o]);
+            dw1[o] = fmaf(d, x1, dw1[o]);
           }
         if (MASK) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) dz[c] = xa[c] > 0.f ? dz[c] : 0.f;
+          dz0 = x0 > 0.f ? dz0 : 0.f;
+          dz1 = x1 > 0.f ? dz1 : 0.f;
         }
-        if (active) *reinterpret_cast<uint2*>(dX + (long)b * K + k0) = pack4(dz[0], dz[1], dz[2], dz[3]);
+        if (active)
+          *reinterpret_cast<unsigned*>(dX + (long)b * K + col) =
+              (unsigned)f2bf(dz0) | ((unsigned)f2bf(dz1) << 16);
       }
     }
   }
-  // fixed-order reduction of the 4 waves' dW partials
-  if (wave > 0) {
+  DDP_STAMP(STAMP_K_FC_BWD, 2);
+  // ---- fixed-order reduction of the waves' dW partials
 #pragma unroll
-    for (int o = 0; o < NOT; ++o)
-      if (o < NO)
-        *reinterpret_cast<float4*>(s_red + ((wave - 1) * NO + o) * 256 + lane * 4) =
-            make_float4(dw[o][0], dw[o][1], dw[o][2], dw[o][3]);
-  }
+  for (int o = 0; o < NOT; ++o)
+    if (o < NO)
+      *reinterpret_cast<float2*>(s_red + (wave * NOT + o) * FCB_COLS + 2 * lane) = make_float2(dw0[o], dw1[o]);
   __syncthreads();
-  if (wave == 0 && active) {
+  DDP_STAMP(STAMP_K_FC_BWD, 3);
+  for (int i = threadIdx.x; i < NO * FCB_COLS; i += WPB * 64) {
+    const int o = i / FCB_COLS, c = i - (i / FCB_COLS) * FCB_COLS;
+    const long k = (long)blockIdx.x * FCB_COLS + c;
+    if (k < K) {
+      float acc = s_red[o * FCB_COLS + c];
 #pragma unroll
-    for (int o = 0; o < NOT; ++o)
-      if (o < NO) {
-        float4 r = make_float4(dw[o][0], dw[o][1], dw[o][2], dw[o][3]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const float4 t = *reinterpret_cast<const float4*>(s_red + (q * NO + o) * 256 + lane * 4);
-          r.x += t.x; r.y += t.y; r.z += t.z; r.w += t.w;
-        }
-        r.x *= scale; r.y *= scale; r.z *= scale; r.w *= scale;
-        *reinterpret_cast<float4*>(dW + (long)o * K + k0) = r;
-      }
+      for (int w = 1; w < WPB; ++w) acc += s_red[(w * NOT + o) * FCB_COLS + c];
+      dW[(long)o * K + k] = acc * scale;
+    }
   }
+  DDP_STAMP(STAMP_K_FC_BWD, 4);
 }
 
 void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
@@ -187,16 +208,20 @@ void fc_reduce(const float* part, const float* bias, float* out, int B, int G, i
                      B, G, NO);
 }
 
+constexpr int FCB_WPB = 8;  // waves per fc_bwd block
+
 size_t fc_bwd_lds(int B, int NO, bool xent) {
-  return sizeof(float) * ((size_t)B * (xent ? NO + 1 : NO) + 4 + (size_t)3 * NO * 256);
+  const int NOT = NO == 10 ? 10 : FC_MAXO;
+  const size_t head = (((size_t)(xent ? 2 * B * NO : B * NO) + B + 3) & ~(size_t)3);
+  return sizeof(float) * (head + (size_t)FCB_WPB * NOT * FCB_COLS);
 }
 
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
-  const dim3 grid((unsigned)((K + 255) / 256));
+  const dim3 grid((unsigned)((K + FCB_COLS - 1) / FCB_COLS));
   const bool xe = ex.part != nullptr;
   const size_t lds = fc_bwd_lds(B, NO, xe);
-#define LB(M, XE, N) hipLaunchKernelGGL((fc_bwd_kernel<M, XE, N>), grid, dim3(256), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
+#define LB(M, XE, N) hipLaunchKernelGGL((fc_bwd_kernel<M, XE, N, FCB_WPB>), grid, dim3(FCB_WPB * 64), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
   if (NO == 10) {
     if (xe) { if (mask) LB(true, true, 10); else LB(false, true, 10); }
     else { if (mask) LB(true, false, 10); else LB(false, false, 10); }
@@ -206,5 +231,7 @@ void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, floa
   }
 #undef LB
 }
+
+DDP_STAMPS_SETTER(stamps_set_linear)
 
 }  // namespace ddp_amd

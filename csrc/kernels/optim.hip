@@ -40,6 +40,7 @@ __device__ __forceinline__ float sgd_one(float v, float d, float* mb, const SgdA
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ mbuf, long n, SgdArgs a,
                                                   ShadowSet sh, int* __restrict__ step_ctr) {
+  DDP_STAMP(STAMP_K_SGD, 0);
   const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
@@ -115,12 +116,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
     }
   }
   if (step_ctr && blockIdx.x == 0 && threadIdx.x == 0) step_ctr[0] += 1;
+  DDP_STAMP(STAMP_K_SGD, 1);
 }
 
 // Block = 64 consecutive outputs x 4 row groups: thread (c, g) sums rows g, g+4, ...
 // (8 loads in flight), then the 4 group sums are added in fixed order via LDS.
 __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
   __shared__ float part[4][64];
+  DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
   const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
   // segments are laid out back to back, each padded to a multiple of 64 outputs, so
   // a block (64 outputs) never straddles two segments
@@ -152,6 +155,7 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
     const SlabSeg& sg = ss.s[k];  // k is block-uniform
     sg.dst[i] = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
   }
+  DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
 }
 
 __global__ void scale_copy_kernel(float* __restrict__ dst, const float* __restrict__ src, long n,
@@ -189,6 +193,19 @@ void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s
   const long blocks = (n + 255) / 256;
   const unsigned grid = (unsigned)(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024);
   hipLaunchKernelGGL(scale_copy_kernel, dim3(grid), dim3(256), 0, s, dst, src, n, scale);
+}
+
+DDP_STAMPS_SETTER(stamps_set_optim)
+void stamps_set_conv1(void*);
+void stamps_set_conv3x3(void*);
+void stamps_set_linear(void*);
+void stamps_set_xent(void*);
+void stamps_set(void* p) {
+  stamps_set_optim(p);
+  stamps_set_conv1(p);
+  stamps_set_conv3x3(p);
+  stamps_set_linear(p);
+  stamps_set_xent(p);
 }
 
 }  // namespace ddp_amd

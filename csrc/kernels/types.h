@@ -38,6 +38,19 @@ struct C1Src {
   BatchIdx bi{};
   const float* w = nullptr;          // conv1 weight [32][9]
   const float* b = nullptr;          // conv1 bias [32]
+  // conv3x3_fwd only (optional): write the step's batch compactly - images xb[B][H*W]
+  // (uint8) and labels yb[B] (from `labels` through bi) - so that the backward kernels
+  // read it directly (identity BatchIdx) instead of repeating the step -> index -> row
+  // lookup chain (two dependent memory round trips each).
+  unsigned char* xb_out = nullptr;
+  int* yb_out = nullptr;
+  const int* labels = nullptr;
 };
+
+// diagnostic phase-stamp kernel ids / buffer geometry (common.h DDP_STAMP)
+enum { STAMP_K_CONV_FWD = 0, STAMP_K_FC_BWD = 1, STAMP_K_DGRAD = 2, STAMP_K_WGRAD = 3,
+       STAMP_K_GRAD_REDUCE = 4, STAMP_K_SGD = 5, STAMP_K_XENT = 6, STAMP_K_CONV1 = 7,
+       STAMP_K_COUNT = 8 };
+constexpr int STAMP_SLOTS = 8, STAMP_KSTRIDE = 4096 * STAMP_SLOTS;
 
 }  // namespace ddp_amd

@@ -91,25 +91,26 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ par
       dbias[c] = (((s_db[0][c] + s_db[1][c]) + s_db[2][c]) + s_db[3][c]) * dbias_scale;
 }
 
-// Engine variant (fusion level 0): one workgroup, one 16-lane row per batch row over
-// partial logits in [B][G][NO] layout (written by the fused conv2 epilogue), see
-// xent_batch_block (common.h).  Writes per-row loss and dlogits; the batch mean loss
-// and the fc bias gradient are finished by fc_bwd's first block (it holds dlogits).
-__global__ __launch_bounds__(1024) void xent_rows_kernel(const float* __restrict__ part, int G,
+// Engine variant (fusion level 0): one workgroup over the per-block partial logits
+// [blk][2][NO] written by the fused conv2 epilogue, see xent_batch_block (common.h).
+// Writes per-row loss and dlogits; the batch mean loss and the fc bias gradient are
+// finished by fc_bwd's first block (it holds dlogits).
+__global__ __launch_bounds__(1024) void xent_rows_kernel(const float* __restrict__ part, int HW, int CH,
                                                         const float* __restrict__ bias, int NO,
                                                         int B, const int* __restrict__ labels32,
                                                         BatchIdx bi, float* __restrict__ dlogits,
                                                         float* __restrict__ loss_rows,
                                                         float gscale) {
-  xent_batch_block(part, G, bias, NO, B, labels32, bi, gscale, dlogits, loss_rows);
+  extern __shared__ float s_lg[];
+  xent_batch_block(part, HW, CH, bias, NO, B, labels32, bi, gscale, dlogits, loss_rows, s_lg);
 }
 
-void xent_rows(const float* part, int G, const float* bias, int NO, int B, const int* labels32,
-               BatchIdx bi, float* dlogits, float* loss_rows, float gscale, hipStream_t s) {
-  // one 16-lane row per batch row: B*16 threads in one workgroup (<= 1024)
-  const int threads = B * 16 <= 256 ? 256 : (B * 16 <= 512 ? 512 : 1024);
-  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(threads), 0, s, part, G, bias, NO, B, labels32,
-                     bi, dlogits, loss_rows, gscale);
+void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int B,
+               const int* labels32, BatchIdx bi, float* dlogits, float* loss_rows, float gscale,
+               hipStream_t s) {
+  const int threads = B * NO <= 256 ? 256 : (B * NO <= 512 ? 512 : 1024);
+  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(threads), sizeof(float) * B * NO, s, part, HW, CH,
+                     bias, NO, B, labels32, bi, dlogits, loss_rows, gscale);
 }
 
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,
@@ -118,5 +119,7 @@ void xent(const float* part, int G, const float* bias, int C, int B, const long 
   hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(256), 0, s, part, G, bias, C, B, labels64, labels32,
                      bi, logits_out, dlogits, loss_out, dbias, gscale, dbias_scale);
 }
+
+DDP_STAMPS_SETTER(stamps_set_xent)
 
 }  // namespace ddp_amd

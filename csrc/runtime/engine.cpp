@@ -87,12 +87,26 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   float* G = b_.grads;
 
   const bool f1 = cfg_.fuse_level >= 1;
+  // level 1: the forward gathers the batch (step counter -> index list -> dataset row)
+  // and writes it compactly (xb images, yb labels); every later kernel of the step reads
+  // the compact copy with the identity index (no dependent lookup chain).
   C1Src c1;
   c1.x = b_.images;
   c1.bi = bi;
   c1.w = P + b_.off_w1;
   c1.b = P + b_.off_b1;
+  c1.xb_out = b_.xb;
+  c1.yb_out = b_.yb;
+  c1.labels = b_.labels;
   const C1Src* pc1 = f1 ? &c1 : nullptr;
+  BatchIdx bid{nullptr, nullptr, 0, 0};
+  bid.n_rows = B;
+  C1Src c1b;
+  c1b.x = b_.xb;
+  c1b.bi = bid;
+  c1b.w = c1.w;
+  c1b.b = c1.b;
+  const C1Src* pc1b = f1 ? &c1b : nullptr;
 
   // ---- forward
   if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
@@ -100,8 +114,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
               b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1);
   // ---- loss + fc backward (bucket 0)
   if (!f1)
-    xent_rows(b_.fc_part, HW / 16, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits, b_.loss_rows,
-              1.f / (float)B, cs_);
+    xent_rows(b_.fc_part, HW, 64 * cfg_.pxt_fwd, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits,
+              b_.loss_rows, 1.f / (float)B, cs_);
   FcBwdExtras ex;
   ex.dbias = G + b_.off_bfc;  // fc bias grad (bucket 0), prescaled
   ex.dbias_scale = inv_ws;
@@ -111,10 +125,11 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   if (f1) {
     ex.loss_rows = nullptr;
     ex.part = b_.fc_part;
-    ex.G = HW / 16;
+    ex.HW = HW;
+    ex.CH = 64 * cfg_.pxt_fwd;
     ex.fc_bias = P + b_.off_bfc;
-    ex.labels32 = b_.labels;
-    ex.bi = bi;
+    ex.labels32 = b_.yb;
+    ex.bi = bid;
     ex.gscale = 1.f / (float)B;
   }
   fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
@@ -127,9 +142,9 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   }
   // ---- conv backward (bucket 1)
   conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, f1 ? nullptr : b_.a1, b_.dz1, B, H, W, C1, C2,
-                b_.images, true, bi, b_.w1slab, cfg_.pxt_dgrad, cs_, pc1);
+                f1 ? b_.xb : b_.images, true, f1 ? bid : bi, b_.w1slab, cfg_.pxt_dgrad, cs_, pc1b);
   conv3x3_wgrad(b_.dz2, nullptr, f1 ? nullptr : b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows,
-                cs_, pc1);
+                cs_, pc1b);
   SlabSet ss{};
   const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);

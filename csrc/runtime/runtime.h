@@ -111,6 +111,8 @@ struct EngineBuffers {
   bf16_t *a1, *a2, *dz2, *dz1;
   float *fc_part, *dlogits, *loss_rows, *loss_hist, *w2slab, *w1slab;
   int* step_ctr;
+  unsigned char* xb;  // the step's batch, compact: u8 [max_batch][H*W] (fuse level 1)
+  int* yb;            // its labels [max_batch]
   // data
   const unsigned char* images;  // u8 [N][H*W]
   const int* labels;            // i32 [N]

@@ -81,11 +81,14 @@ class FusedSimpleCNNEngine:
             wfc_bf16=e(10 * HW * 64, dt=BF16), wfc_frag=e(10 * HW * 64, dt=BF16),
             a1=e(B * HW * 32, dt=BF16), a2=e(B * HW * 64, dt=BF16),
             dz2=e(B * HW * 64, dt=BF16), dz1=e(B * HW * 32, dt=BF16),
-            fc_part=e(B * (HW // 16) * 10), dlogits=e(B * 10), loss_rows=e(B),
+            fc_part=e(2 * self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_fwd) * 10),  # [blk][2][10]
+            dlogits=e(B * 10), loss_rows=e(B),
             loss_hist=torch.zeros(self.steps_per_epoch + 1, device=dev),
             w2slab=e(self.C.conv3x3_wgrad_blocks(B, 28, R) * (64 * 9 * 32 + 64)),
             w1slab=e(self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_dgrad) * 320),
             step_ctr=torch.zeros(1, dtype=torch.int32, device=dev),
+            xb=torch.empty(B * HW, dtype=torch.uint8, device=dev),   # the step's batch (compact)
+            yb=torch.empty(B, dtype=torch.int32, device=dev),
             images=data.images_u8.view(-1), labels=data.labels_i32,
             idx=torch.zeros(n_rank, dtype=torch.int32, device=dev),
         )

@@ -179,3 +179,19 @@ def fc_weight_frag(w: torch.Tensor, hw: int, c: int) -> torch.Tensor:
     no = w.numel() // (hw * c)
     v = w.reshape(no, hw // 16, 16, c // 16, 4, 4)
     return v.permute(0, 1, 3, 4, 2, 5).contiguous().to(torch.bfloat16)
+
+
+def fold_block_partials(part: torch.Tensor, B: int, HW: int, CH: int) -> torch.Tensor:
+    """Logits (without bias) from the fused conv2+fc epilogue's per-block partials.
+
+    ``part`` is [blocks][2][NO]: block k covers pixels [k*CH, (k+1)*CH) of the flattened
+    [B*HW] space; slot 0 belongs to the image of its first pixel, slot 1 to the next
+    image (csrc/kernels/common.h xent_batch_block).  Reference/test helper."""
+    nblk, _, NO = part.shape
+    out = torch.zeros(B, NO, dtype=part.dtype, device=part.device)
+    for k in range(nblk):
+        n0 = (k * CH) // HW
+        out[n0] += part[k, 0]
+        if n0 + 1 < B and ((k + 1) * CH - 1) // HW > n0:
+            out[n0 + 1] += part[k, 1]
+    return out

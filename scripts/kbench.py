@@ -75,7 +75,7 @@ def main():
     wfc = (r(NO, HW, C2) * 0.01).to(BF)
     a1 = torch.relu(r(B, H, W, C1)).to(BF)
     a2 = torch.empty(B, H, W, C2, dtype=BF, device=dev)
-    part = torch.empty(B * NO * (HW // 16), device=dev)
+    part = torch.empty(2 * NO * C.conv3x3_dgrad_blocks(B, H, W, 1), device=dev)
     dl = r(B, NO) * 0.01
     dz2 = torch.empty(B, H, W, C2, dtype=BF, device=dev)
     dz1 = torch.empty(B, H, W, C1, dtype=BF, device=dev)
@@ -103,7 +103,7 @@ def main():
         run(f"conv3x3_fwd pxt{pxt} relu", lambda: C.conv3x3_fwd(a1, w2, b2, a2, True, None, None, NO, pxt))
         run(f"conv3x3_fwd pxt{pxt} +fc", lambda: C.conv3x3_fwd(a1, w2, b2, a2, True, wfc, part, NO, pxt))
     C.conv3x3_fwd(a1, w2, b2, a2, True, wfc, part, NO, 2)
-    run("xent_rows", lambda: C.xent_rows(part, HW // 16, bfc, labels, idx, dl, lossr, 1.0 / B))
+    run("xent_rows", lambda: C.xent_rows(part, HW, 128, bfc, labels, idx, dl, lossr, 1.0 / B))
     run("fc_bwd mask", lambda: C.fc_bwd(dl, a2.view(B, -1), wfc.view(NO, -1), dz2.view(B, -1), dWfc, 1.0,
                                          True, dbias, lossr, losso))
     for pxt in (1, 2):

@@ -1,0 +1,88 @@
+"""In-kernel phase timeline of the fused SimpleCNN step (diagnostic).
+
+Runs the headline engine (same construction as bench.py) with the per-TU stamp buffer
+set (csrc/kernels/common.h DDP_STAMP), executes a few eager steps, and prints for each
+kernel and stamp slot the median / max (over blocks) time since that kernel's first
+block started, in microseconds (100 MHz s_memrealtime -> 10 ns resolution).
+
+    python scripts/stamps.py [--batch_size 32] [--fuse_level 1]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+NAMES = {0: "conv3x3_fwd", 1: "fc_bwd", 2: "conv3x3_dgrad", 3: "conv3x3_wgrad",
+         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "conv1"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch_size", type=int, default=32)
+    ap.add_argument("--fuse_level", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--graph", action="store_true", help="stamp the last step of a replayed graph")
+    a = ap.parse_args()
+    from ddp_amd import native
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+
+    C = native.require()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = SimpleCNN().to(dev)
+    opt = FusedSGD(model, lr=0.01)
+    imgs, labels = synthetic_mnist()
+    eo = EngineOptions(use_graph=a.graph, graph_steps=10)
+    if a.fuse_level is not None:
+        eo.fuse_level = a.fuse_level
+    eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, dev, "synthetic"),
+                               a.batch_size, 1, 0, None, eo)
+    eng.refresh()
+    eng.run_steps(10 if a.graph else 3)
+    eng.synchronize()
+    buf = torch.zeros(C.STAMP_K_COUNT * C.STAMP_KSTRIDE, dtype=torch.int64, device=dev)
+    C.stamps_set(buf)
+    for _ in range(a.steps):
+        buf.zero_()
+        torch.cuda.synchronize()
+        eng.run_steps(10 if a.graph else 1)
+        eng.synchronize()
+    C.stamps_set(None)
+    st = buf.view(C.STAMP_K_COUNT, 4096, 8).cpu().double()
+    t0 = None
+    rows = []
+    for k in range(C.STAMP_K_COUNT):
+        s = st[k]
+        live = s[:, 0] > 0
+        if not live.any():
+            continue
+        s = s[live]
+        kstart = s[:, 0].min()
+        t0 = kstart if t0 is None else min(t0, kstart)
+        rows.append((kstart, k, s))
+    rows.sort(key=lambda r: r[0])
+    print(f"batch {a.batch_size}; times in us; 'start' = kernel's first block vs the first kernel")
+    for kstart, k, s in rows:
+        nb = s.shape[0]
+        line = [f"{NAMES.get(k, k):14s} blocks {nb:4d} start {(kstart - t0) / 100:7.2f} |"]
+        for slot in range(8):
+            v = s[:, slot]
+            ok = v > 0
+            if not ok.any():
+                continue
+            d = (v[ok] - kstart) / 100.0
+            line.append(f" s{slot} med {d.median().item():6.2f} max {d.max().item():6.2f}")
+        # per-block durations (first -> last stamp)
+        last = s.max(dim=1).values
+        dur = (last - s[:, 0]) / 100.0
+        line.append(f" | blk dur med {dur.median().item():.2f} max {dur.max().item():.2f}")
+        print("".join(line))
+
+
+if __name__ == "__main__":
+    main()

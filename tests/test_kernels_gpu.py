@@ -75,18 +75,19 @@ def test_conv3x3_fwd_fused_fc(C, B):
     wfc = rnd(10, H * W, 64, scale=0.01, seed=6)
     bfc = (torch.randn(10) * 0.1).to(dev)
     y = torch.empty(B, H, W, 64, dtype=BF, device=dev)
-    part = torch.full((B, H * W // 16, 10), float("nan"), device=dev)
-    from ddp_amd.ops.functional import fc_weight_frag
+    nblk = C.conv3x3_dgrad_blocks(B, H, W, 2)  # conv blocks of 128 pixels
+    part = torch.full((nblk, 2, 10), float("nan"), device=dev)
+    from ddp_amd.ops.functional import fc_weight_frag, fold_block_partials
 
     C.conv3x3_fwd(x, w, b, y, True, fc_weight_frag(wfc, H * W, 64), part, 10, 2)
-    logits = part.sum(1) + bfc
+    logits = fold_block_partials(part, B, H * W, 128) + bfc
     ref = R.fc_nhwc(y.float(), wfc.float(), bfc)  # the fc of exactly the stored bf16 activation
     close(logits, ref, rtol=1e-3, atol=1e-3)
-    # engine cross-entropy over those [B][10][49] partials (+ fc bias grad / mean loss in fc_bwd)
+    # engine cross-entropy over those [blocks][2][10] partials (+ fc bias grad / mean loss in fc_bwd)
     labels = torch.randint(0, 10, (B,)).to(torch.int32).to(dev)
     dl = torch.empty(B, 10, device=dev)
     rows = torch.empty(B, device=dev)
-    C.xent_rows(part, 49, bfc, labels, None, dl, rows, 1.0 / B)
+    C.xent_rows(part, H * W, 128, bfc, labels, None, dl, rows, 1.0 / B)
     rl, rd = R.cross_entropy(ref, labels.long())
     close(dl, rd, rtol=1e-4, atol=1e-6)
     close(rows.mean(), rl, rtol=1e-5, atol=1e-5)
