@@ -108,6 +108,8 @@ __device__ __forceinline__ float conv1_eval(const float* w1, const float* b1, co
 // block owns channel group g = w (channels 8g..8g+7) for every position, so its conv1
 // weights are wave-uniform: Conv1Group loads them ONCE per wave into registers (call
 // conv1_group_load early - e.g. before the staging round - so the loads overlap it).
+// With more than 4 waves, waves w and w + 4 share group w % 4 and split the positions
+// (pos0 = 64 * (w / 4), pstride = 64 * waves / 4).
 // The only LDS traffic is the 9 input taps and one 16-byte store per position.
 //   valid(pos) -> position inside the image (else the row is zero-filled)
 //   tap(pos, k) -> input value of tap k (0 outside the image)
@@ -134,9 +136,9 @@ __device__ __forceinline__ float conv1_eval_g(const Conv1Group& cg, const float*
   return fmaxf(acc, 0.f);
 }
 template <typename ValidFn, typename TapFn, typename DstFn>
-__device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group& cg, int g,
-                                                     ValidFn valid, TapFn tap, DstFn dst) {
-  for (int pos = threadIdx.x & 63; pos < npos; pos += 64) {
+__device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group& cg, int g, int pos0,
+                                                     int pstride, ValidFn valid, TapFn tap, DstFn dst) {
+  for (int pos = pos0 + (threadIdx.x & 63); pos < npos; pos += pstride) {
     float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (valid(pos)) {
       float v[9];
@@ -150,6 +152,27 @@ __device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group&
     pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
     *reinterpret_cast<uint4*>(dst(pos, g)) = pk;
   }
+}
+
+// ---- optimizer element update (torch/optim/sgd.py _single_tensor_sgd semantics)
+// destination index of element j (multiple of 4 for a quad) in the FCFRAG layout
+__device__ __forceinline__ int fcfrag_index(int j, int HW, int C) {
+  const int o = j / (HW * C);
+  const int rem = j - o * HW * C;
+  const int hw = rem / C, c = rem - (rem / C) * C;
+  const int G = HW >> 4, T = C >> 4;
+  return ((((o * G + (hw >> 4)) * T + (c >> 4)) * 4 + ((c >> 2) & 3)) * 16 + (hw & 15)) * 4 + (c & 3);
+}
+
+__device__ __forceinline__ float sgd_one(float v, float d, float* mb, const SgdArgs& a) {
+  if (a.maximize) d = -d;
+  if (a.weight_decay != 0.f) d = fmaf(a.weight_decay, v, d);
+  if (a.momentum != 0.f) {
+    const float buf = a.first_step ? d : fmaf(1.f - a.dampening, d, a.momentum * (*mb));
+    *mb = buf;
+    d = a.nesterov ? fmaf(a.momentum, buf, d) : buf;
+  }
+  return fmaf(-a.lr, d, v);
 }
 
 // ---- cross-lane reductions on DPP (VALU modifiers, no LDS round trips) --------------

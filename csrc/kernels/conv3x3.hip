@@ -35,19 +35,19 @@ namespace ddp_amd {
 // loads before its first LDS write, so a block's whole staging is ONE memory round
 // trip when (n1 + n2) <= 256 * INF.  src(i) returns chunk i (zero-filled where out of
 // range).
-template <int INF, typename S1, typename D1, typename S2, typename D2>
+template <int INF, int NT = 256, typename S1, typename D1, typename S2, typename D2>
 __device__ __forceinline__ void stage2(int n1, S1 src1, D1 dst1, int n2, S2 src2, D2 dst2) {
   const int n = n1 + n2;
-  for (int base = threadIdx.x; base < n; base += 256 * INF) {
+  for (int base = threadIdx.x; base < n; base += NT * INF) {
     bf16x8 v[INF];
 #pragma unroll
     for (int u = 0; u < INF; ++u) {
-      const int i = base + u * 256;
+      const int i = base + u * NT;
       v[u] = (i < n1) ? src1(i) : ((i < n) ? src2(i - n1) : zero8());
     }
 #pragma unroll
     for (int u = 0; u < INF; ++u) {
-      const int i = base + u * 256;
+      const int i = base + u * NT;
       if (i < n1) dst1(i, v[u]);
       else if (i < n) dst2(i - n1, v[u]);
     }
@@ -71,39 +71,44 @@ __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
 // pixels of the flattened [B*H*W] space and stages the LINEAR pixel range
 // [P0 - W - 1, P0 + CH + W + 1): every 3x3 neighbour of the block's pixels is in it
 // (neighbours in another image row/image are zeroed by the (h,w) bounds test).
-// Weight rows are padded by 8 elements so the 16 rows of an A fragment start on
-// 16 distinct 4-bank groups (conflict-free ds_read_b128).
+// Weight and activation rows are padded by 16 elements: a row stride of 8 mod 16 dwords
+// is the one at which ds_read_b128's four 16-lane groups (rows l & 15, k offset
+// 4 * (l >> 4) dwords) cover all 64 banks exactly once - conflict-free fragment reads
+// (the previous 8-element pad gave 2-way conflicts).
 
 // LDS bytes of the forward's staging area (weights, input rows, conv1 recompute
 // scratch), rounded to 16; the fused-fc epilogue's per-tile partials follow it.
 __host__ __device__ inline size_t fwd_stage_lds(int W, int Cin, int pxt, bool a1x) {
-  const size_t XR = 64 * pxt + 2 * W + 2;
-  const size_t b = sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 8) + XR * (Cin + 8)) +
+  const size_t XR = 64 * pxt + 2 * W + 2;  // a block covers CH = 64 * pxt pixels
+  const size_t b = sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 16) + XR * (Cin + 16)) +
                    (a1x ? sizeof(float) * ((XR + 2 * W + 2) + Cin * 10) : 0);
   return (b + 15) & ~(size_t)15;
 }
 constexpr int FC_MAX_NOF = 16;
-// [wave][pixel tile][channel group][class] floats
+// [16-pixel tile][channel group][class] floats (CH / 16 = 4 * pxt tiles per block)
 __host__ __device__ inline size_t fc_epi_lds(int pxt, int nof) { return sizeof(float) * 4 * pxt * 4 * nof; }
 
 // ---------------------------------------------------------------- forward
 // A1X: the input X is NOT read from memory but recomputed in the staging pass as
 // relu(conv1(x)) from the uint8 dataset (x0 via the batch index list) - SimpleCNN's
 // first layer folded into the second (Cin must equal conv1's 32 output channels).
-template <int PXT, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO>
-__global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
+// NW waves per block, PXT 16-pixel tiles per wave: a block covers CH = 16 * NW * PXT
+// pixels (64 * pxt in launcher terms).  With NW = 8 two waves share each SIMD, which
+// doubles the VALU issue rate of the conv1 recompute and the fc epilogue.
+template <int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO>
+__global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
     bf16_t* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
     const bf16_t* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DDP_STAMP(STAMP_K_CONV_FWD, 0);
   DDP_GEOM_OVERRIDE();
-  constexpr int CH = 64 * PXT;
+  constexpr int CH = 16 * NW * PXT, NT = NW * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
   const int co0 = blockIdx.y * 64;
-  const int KW = 9 * Cin, WS = KW + 8, XS = Cin + 8;
+  const int KW = 9 * Cin, WS = KW + 16, XS = Cin + 16;  // row strides = 8 mod 16 dwords: conflict-free b128 fragment reads
   const int XR = CH + 2 * W + 2;
   bf16_t* sW = reinterpret_cast<bf16_t*>(smem);
   bf16_t* sX = sW + 64 * WS;
@@ -113,9 +118,9 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
   const int wc = KW / 8;
   const int xc = Cin / 8;
   Conv1Group cg;
-  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
+  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave & 3);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
-  stage2<16>(64 * wc,
+  stage2<64 / NW, NT>(64 * wc,
              [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
              [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sW + r * WS + c) = v; },
              A1X ? 0 : XR * xc,
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     float* sxx = reinterpret_cast<float*>(sX + XR * XS);
     const int NXX = XR + 2 * W + 2;
     const int base = c1.bi.base();
-    for (int r = threadIdx.x; r < NXX; r += 256) {
+    for (int r = threadIdx.x; r < NXX; r += NT) {
       const long P = Pbase - W - 1 + r;
       float v = 0.f;
       if (P >= 0 && P < Ptot) {
@@ -150,7 +155,8 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
     __syncthreads();
     DDP_STAMP(STAMP_K_CONV_FWD, 1);
     conv1_recompute_tile(
-        XR, cg, wave, [&](int r) { const long P = Pbase + r; return P >= 0 && P < Ptot; },
+        XR, cg, wave & 3, 64 * (wave >> 2), 64 * (NW / 4),
+        [&](int r) { const long P = Pbase + r; return P >= 0 && P < Ptot; },
         [&](int r, int k) {
           const long P = Pbase + r;
           const int rm = (int)(P % HW);
@@ -160,6 +166,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
           return ok ? sxx[r + W + 1 + dh * W + dw] : 0.f;
         },
         [&](int r, int g) { return sX + r * XS + 8 * g; });
+    DDP_STAMP(STAMP_K_CONV_FWD, 5);
   }
 
   const int kofs = 8 * (lane >> 4);
@@ -226,7 +233,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
   DDP_STAMP(STAMP_K_CONV_FWD, 3);
   // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
-  float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, PXT, A1X));
+  float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X));
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -264,6 +271,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
       }
     }
   }
+  DDP_STAMP(STAMP_K_CONV_FWD, 6);
   if (NOF > 0) {
     __syncthreads();
     // per (image slot, class): fixed-order sum over the block's tiles of that image and
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
       const int slot = threadIdx.x / NOF, o = threadIdx.x - (threadIdx.x / NOF) * NOF;
       const long img = P0 / HW + slot;
       float acc_o = 0.f;
-      for (int tile = 0; tile < 4 * PXT; ++tile) {
+      for (int tile = 0; tile < NW * PXT; ++tile) {
         const long tp = P0 + tile * 16;
         if (tp < Ptot && tp / HW == img) {
 #pragma unroll
@@ -290,26 +298,25 @@ __global__ __launch_bounds__(256) void conv3x3_fwd_kernel(
 // A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
 // being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
 template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI, int GCO>
-__global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
+__device__ __forceinline__ void dgrad_body(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
     const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
-    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by) {
   DDP_STAMP(STAMP_K_DGRAD, 0);
   DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
-  const int ci_blk = blockIdx.y * 32;
-  const int KW = 9 * Cout, WS = KW + 8, DS = Cout + 8;
+  const int ci_blk = by * 32;
+  const int KW = 9 * Cout, WS = KW + 16, DS = Cout + 16;  // row strides = 8 mod 16 dwords (conflict-free)
   const int XR = CH + 2 * W + 2;
   bf16_t* sWT = reinterpret_cast<bf16_t*>(smem);        // [32 ci][9*Cout]
   bf16_t* sDY = sWT + 32 * WS;                           // [XR][Cout]
   float* sx0 = reinterpret_cast<float*>(sDY + XR * DS);  // [XR] conv1 input (FUSE_W1)
   float* s_w1 = sx0 + XR;                                // [4][320] (FUSE_W1)
   unsigned char* s_m1 = reinterpret_cast<unsigned char*>(s_w1 + 4 * 320);  // [CH][4] a1>0 bits (A1X)
-  const long P0 = (long)blockIdx.x * CH;
+  const long P0 = (long)bx * CH;
   const long Pbase = P0 - W - 1;
 
   // conv1 input values for the fused w1 gradient: loads issued before the staging
@@ -467,7 +474,7 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
         for (int j = 0; j < 4; ++j) v[j] = xm[j] > 0.f ? v[j] : 0.f;
       }
       const uint2 pk = pack4(v[0], v[1], v[2], v[3]);
-      if (valid[pt]) *reinterpret_cast<uint2*>(dX + Pp[pt] * Cin + ci) = pk;
+      if (dX && valid[pt]) *reinterpret_cast<uint2*>(dX + Pp[pt] * Cin + ci) = pk;  // dX null: only the fused w1 grad needs it
       if (FUSE_W1) {
         float q[4];
         unpack4(pk, q);
@@ -503,9 +510,19 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 320; i += 256)
-      w1slab[(long)blockIdx.x * 320 + i] = ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i];
+      w1slab[(long)bx * 320 + i] = ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i];
   }
   DDP_STAMP(STAMP_K_DGRAD, 4);
+}
+
+template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI, int GCO>
+__global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
+    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
+    const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
+    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  dgrad_body<PXT, MASK_DY, MASK_X, FUSE_W1, A1X, GH, GW, GCI, GCO>(
+      dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, x0_u8, bi, w1slab, c1, smem, blockIdx.x, blockIdx.y);
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -520,16 +537,15 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // A1X: the X tile (a1 rows r0-1 .. r0+R) is recomputed from the uint8 images (rows
 // r0-2 .. r0+R+1) instead of being read from a stored a1 tensor.
 template <bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
-__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
+__device__ __forceinline__ void wgrad_body(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
-    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by) {
   DDP_STAMP(STAMP_K_WGRAD, 0);
   DDP_GEOM_OVERRIDE();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nRC = (H + R - 1) / R;
-  const int n = blockIdx.x / nRC;
-  const int r0 = (blockIdx.x - n * nRC) * R;
+  const int n = bx / nRC;
+  const int r0 = (bx - n * nRC) * R;
   const int Wp = (W + 7) & ~7;
   const int DS = Cout + 16, XS = Cin + 16;  // LDS row strides (elements)
   const int nslot = ((R * Wp + 31) / 32) * 32;
@@ -584,7 +600,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
     __syncthreads();
     DDP_STAMP(STAMP_K_WGRAD, 1);
     conv1_recompute_tile(
-        (R + 2) * XW, cg, wave,
+        (R + 2) * XW, cg, wave, 0, 64,
         [&](int pos) {
           const int rr = pos / XW, cc = pos - (pos / XW) * XW;
           return (unsigned)(r0 - 1 + rr) < (unsigned)H && (unsigned)(cc - 1) < (unsigned)W;
@@ -600,7 +616,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 
   // ---- wave assignment: (pair of 16-wide co tiles) x (16-wide ci tile)
   const int nct = Cin / 16;
-  const int asg = blockIdx.y * 4 + wave;
+  const int asg = by * 4 + wave;
   const int coT = (asg / nct) * 32;
   const int ciT = (asg - (asg / nct) * nct) * 16;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
@@ -648,7 +664,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 
   DDP_STAMP(STAMP_K_WGRAD, 3);
   // ---- slab row: [Cout][3][3][Cin] (OHWI, the weight's native layout) then [Cout] bias
-  float* out = slab + (long)blockIdx.x * ((long)Cout * 9 * Cin + Cout);
+  float* out = slab + (long)bx * ((long)Cout * 9 * Cin + Cout);
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -661,6 +677,36 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
   DDP_STAMP(STAMP_K_WGRAD, 4);
 }
 
+template <bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
+__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
+    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
+    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  wgrad_body<MASK_DY, A1X, GH, GW, GCI, GCO>(dY, Yact, X, slab, B, H, W, Cin, Cout, R, c1, smem,
+                                              blockIdx.x, blockIdx.y);
+}
+
+// ---------------------------------------------------------------- fused conv backward
+// SimpleCNN's whole conv backward in ONE launch (fusion level 1): blocks [0, nd) run the
+// data gradient (+ fused conv1 weight gradient, recomputed ReLU mask), blocks [nd, nd+nw)
+// the weight gradient.  Both only read dZ2 and the compact batch, so they are
+// independent; one launch saves a dependent kernel boundary and lets the wgrad blocks
+// fill the CUs the dgrad grid leaves idle (2 blocks per CU: <= 256 VGPR+AGPR per lane).
+// Block-uniform role branch.
+template <int PXT, int GH, int GW, int GCI, int GCO>
+__global__ __launch_bounds__(256, 2) void conv3x3_bwd_kernel(
+    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ WT, bf16_t* __restrict__ dX,
+    float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
+    int R, int nd, C1Src c1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x < nd)
+    dgrad_body<PXT, false, true, true, true, GH, GW, GCI, GCO>(
+        dY, nullptr, WT, nullptr, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, blockIdx.x, 0);
+  else
+    wgrad_body<false, true, GH, GW, GCI, GCO>(dY, nullptr, nullptr, slab, B, H, W, Cin, Cout, R, c1,
+                                             smem, blockIdx.x - nd, 0);
+}
+
 // ---------------------------------------------------------------- launchers
 size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x) {
   return fwd_stage_lds(W, Cin, pxt, a1x) + fc_epi_lds(pxt, FC_MAX_NOF);
@@ -668,7 +714,7 @@ size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x) {
 
 size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
   const size_t XR = 64 * pxt + 2 * W + 2;
-  return sizeof(bf16_t) * ((size_t)32 * (9 * Cout + 8) + XR * (Cout + 8)) +
+  return sizeof(bf16_t) * ((size_t)32 * (9 * Cout + 16) + XR * (Cout + 16)) +
          (fuse_w1 ? sizeof(float) * (XR + 4 * 320) + 4 * 64 * pxt : 0);
 }
 
@@ -687,12 +733,15 @@ void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y
   const bool fc = wfc != nullptr;  // host guarantees NO == 10 when fused
   const C1Src cs = a1x ? *c1 : C1Src();
   const bool g = simplecnn_geom(H, W, Cin, Cout);
+  // one 16-pixel tile per wave: pxt 2 -> 8 waves (2 per SIMD), pxt 1 -> 4 waves
 #define LF(PX, RL, NF, AX)                                                                             \
   do {                                                                                                 \
-    if (g) hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF, AX, 28, 28, 32, 64>), grid, dim3(256),  \
-                              lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs);         \
-    else hipLaunchKernelGGL((conv3x3_fwd_kernel<PX, RL, NF, AX, 0, 0, 0, 0>), grid, dim3(256), lds,   \
-                            s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs);                \
+    if (g) hipLaunchKernelGGL((conv3x3_fwd_kernel<1, 4 * PX, RL, NF, AX, 28, 28, 32, 64>), grid,     \
+                              dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,      \
+                              fc_part, cs);                                                         \
+    else hipLaunchKernelGGL((conv3x3_fwd_kernel<1, 4 * PX, RL, NF, AX, 0, 0, 0, 0>), grid,           \
+                            dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, \
+                            cs);                                                                    \
   } while (0)
   if (pxt == 2) {
     if (fc && a1x) LF(2, true, 10, true);
@@ -773,6 +822,28 @@ void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float*
   if (c1) { if (Yact) LW(true, true); else LW(false, true); }
   else { if (Yact) LW(true, false); else LW(false, false); }
 #undef LW
+}
+
+size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R) {
+  const size_t a = conv3x3_dgrad_lds(W, Cout, pxt, true), b = conv3x3_wgrad_lds(W, Cin, Cout, R, true);
+  return a > b ? a : b;
+}
+
+void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, hipStream_t s) {
+  const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = conv3x3_wgrad_blocks(B, H, R);
+  const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R);
+  const bool g = simplecnn_geom(H, W, Cin, Cout);
+  // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
+#define LBW(PX)                                                                                     \
+  do {                                                                                              \
+    if (g) hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, 28, 28, 32, 64>), dim3(nd + nw), dim3(256), lds, \
+                              s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1);          \
+    else hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, 0, 0, 0, 0>), dim3(nd + nw), dim3(256), lds, s, \
+                            dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1);               \
+  } while (0)
+  if (pxt == 2) LBW(2); else LBW(1);
+#undef LBW
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv3x3)

@@ -26,6 +26,11 @@ void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const
                    bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
                    BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1 = nullptr);
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
+// fused level-1 conv backward (dgrad + conv1 wgrad slabs, and conv2 wgrad slabs) in one
+// launch; Cin == 32 (conv1's channels), (Cout / 32) * (Cin / 16) == 4
+void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, hipStream_t s);
+size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false);
 size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x = false);
@@ -91,6 +96,16 @@ struct FcBwdExtras {
   const int* labels32 = nullptr;
   BatchIdx bi{};
   float gscale = 1.f;
+  // Fused optimizer for the fc WEIGHT (single-process steps, where dW is final when this
+  // kernel writes it): sgd.update != 0 -> p_w -= SGD(dW) in the dW epilogue, plus the
+  // bf16 shadows.  Each block updates only the columns it alone reads, so it is race
+  // free; the fc bias (read by every block's prologue) is updated by grad_reduce.
+  SgdArgs sgd{};
+  float* p_w = nullptr;       // fp32 master [NO][K]
+  float* m_w = nullptr;       // momentum buffer [NO][K] (momentum != 0)
+  bf16_t* sh_plain = nullptr;  // bf16 shadow [NO][K]
+  bf16_t* sh_frag = nullptr;   // FCFRAG shadow (conv3x3_fwd epilogue order)
+  int frag_HW = 0, frag_C = 0;
 };
 size_t fc_bwd_lds(int B, int NO, bool xent);
 void noop(int blocks, int* sink, hipStream_t s);
@@ -107,10 +122,6 @@ void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int
                hipStream_t s);
 
 // ---- optimizer / reductions -----------------------------------------------------------
-struct SgdArgs {
-  float lr, momentum, dampening, weight_decay;
-  int nesterov, maximize, first_step, update;
-};
 // SHADOW_BF16_FCFRAG: fc weight [o][hw][c] (a = HW, b = C) -> the MFMA-fragment order
 // read by the conv3x3_fwd FC epilogue, [o][hw/16][c/16][(c/4)%4][hw%16][c%4], so each
 // wave-instruction of that epilogue loads 512 contiguous bytes.
@@ -131,10 +142,20 @@ struct SlabSeg {
   int rows;
   float* dst;
   float scale;
+  // fused optimizer (SlabSet::sgd.update): master / momentum at the gradient's index,
+  // bf16 shadow (plain) and / or the [tap][ci][co] transposed shadow (t_co/t_taps/t_ci)
+  float* p = nullptr;
+  float* m = nullptr;
+  bf16_t* sh = nullptr;
+  bf16_t* sh_t = nullptr;
+  int t_co = 0, t_taps = 0, t_ci = 0;
 };
+constexpr int MAX_SLAB_SEGS = 6;
 struct SlabSet {
-  SlabSeg s[4];
+  SlabSeg s[MAX_SLAB_SEGS];
   int count;
+  SgdArgs sgd{};              // update != 0 -> apply SGD to segments with p set
+  int* step_ctr = nullptr;    // += 1 at the end (the step's last kernel)
 };
 void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, const ShadowSet& sh,
               int* step_ctr, hipStream_t s);

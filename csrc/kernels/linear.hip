@@ -189,7 +189,18 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
       float acc = s_red[o * FCB_COLS + c];
 #pragma unroll
       for (int w = 1; w < WPB; ++w) acc += s_red[(w * NOT + o) * FCB_COLS + c];
-      dW[(long)o * K + k] = acc * scale;
+      const float g = acc * scale;
+      const long idx = (long)o * K + k;
+      if (dW) dW[idx] = g;  // null: fused optimizer consumes it in registers
+      if (ex.sgd.update) {  // single-process step: dW is final -> fused SGD + shadows
+        float m = ex.m_w ? ex.m_w[idx] : 0.f;
+        const float pn = sgd_one(ex.p_w[idx], g, &m, ex.sgd);
+        ex.p_w[idx] = pn;
+        if (ex.m_w) ex.m_w[idx] = m;
+        const bf16_t pb = f2bf(pn);
+        if (ex.sh_plain) ex.sh_plain[idx] = pb;
+        if (ex.sh_frag) ex.sh_frag[fcfrag_index((int)idx, ex.frag_HW, ex.frag_C)] = pb;
+      }
     }
   }
   DDP_STAMP(STAMP_K_FC_BWD, 4);

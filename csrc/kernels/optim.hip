@@ -15,26 +15,6 @@
 
 namespace ddp_amd {
 
-// destination index of element j (multiple of 4 for a quad) in the FCFRAG layout
-__device__ __forceinline__ int fcfrag_index(int j, int HW, int C) {
-  const int o = j / (HW * C);
-  const int rem = j - o * HW * C;
-  const int hw = rem / C, c = rem - (rem / C) * C;
-  const int G = HW >> 4, T = C >> 4;
-  return ((((o * G + (hw >> 4)) * T + (c >> 4)) * 4 + ((c >> 2) & 3)) * 16 + (hw & 15)) * 4 + (c & 3);
-}
-
-__device__ __forceinline__ float sgd_one(float v, float d, float* mb, const SgdArgs& a) {
-  if (a.maximize) d = -d;
-  if (a.weight_decay != 0.f) d = fmaf(a.weight_decay, v, d);
-  if (a.momentum != 0.f) {
-    const float buf = a.first_step ? d : fmaf(1.f - a.dampening, d, a.momentum * (*mb));
-    *mb = buf;
-    d = a.nesterov ? fmaf(a.momentum, buf, d) : buf;
-  }
-  return fmaf(-a.lr, d, v);
-}
-
 // 4 consecutive elements per thread (16-byte loads/stores); n4 = n / 4 quads, the
 // (n % 4) tail is handled by the first threads of block 0.
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -153,8 +133,22 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
   __syncthreads();
   if (grp == 0 && live) {
     const SlabSeg& sg = ss.s[k];  // k is block-uniform
-    sg.dst[i] = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
+    const float g = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
+    sg.dst[i] = g;
+    if (ss.sgd.update && sg.p) {  // single-process step: the gradient is final -> fused SGD
+      float m = sg.m ? sg.m[i] : 0.f;
+      const float pn = sgd_one(sg.p[i], g, &m, ss.sgd);
+      sg.p[i] = pn;
+      if (sg.m) sg.m[i] = m;
+      if (sg.sh) sg.sh[i] = f2bf(pn);
+      if (sg.sh_t) {  // OHWI [co][tap][ci] -> [tap][ci][co]
+        const long per = (long)sg.t_taps * sg.t_ci;
+        const long co = i / per;
+        sg.sh_t[(i - co * per) * sg.t_co + co] = f2bf(pn);
+      }
+    }
   }
+  if (ss.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) ss.step_ctr[0] += 1;
   DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
 }
 

@@ -47,6 +47,13 @@ struct C1Src {
   const int* labels = nullptr;
 };
 
+// torch.optim.SGD hyper-parameters of one step (first_step: momentum buffer init;
+// update == 0: shadows only)
+struct SgdArgs {
+  float lr, momentum, dampening, weight_decay;
+  int nesterov, maximize, first_step, update;
+};
+
 // diagnostic phase-stamp kernel ids / buffer geometry (common.h DDP_STAMP)
 enum { STAMP_K_CONV_FWD = 0, STAMP_K_FC_BWD = 1, STAMP_K_DGRAD = 2, STAMP_K_WGRAD = 3,
        STAMP_K_GRAD_REDUCE = 4, STAMP_K_SGD = 5, STAMP_K_XENT = 6, STAMP_K_CONV1 = 7,

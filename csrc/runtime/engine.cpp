@@ -106,7 +106,6 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   c1b.bi = bid;
   c1b.w = c1.w;
   c1b.b = c1.b;
-  const C1Src* pc1b = f1 ? &c1b : nullptr;
 
   // ---- forward
   if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
@@ -132,8 +131,26 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ex.bi = bid;
     ex.gscale = 1.f / (float)B;
   }
-  fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
-         /*mask=*/true, cs_, ex);
+  // single-process steps: no all-reduce separates a gradient from its update, so the
+  // optimizer runs in the epilogues of the kernels that finish each gradient (fc weight:
+  // fc_bwd; convs + fc bias: grad_reduce) and the separate SGD pass disappears
+  const bool fopt = !dist && cfg_.fuse_opt;
+  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2, n_fc = (long)NO * HW * C2;
+  const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
+                   cfg_.maximize, first_momentum_step ? 1 : 0, 1};
+  float* M = b_.momentum;  // null when momentum == 0
+  if (fopt) {
+    ex.sgd = sa;
+    ex.p_w = P + b_.off_wfc;
+    ex.m_w = M ? M + b_.off_wfc : nullptr;
+    ex.sh_plain = b_.wfc_bf16;
+    ex.sh_frag = b_.wfc_frag;
+    ex.frag_HW = HW;
+    ex.frag_C = C2;
+  }
+  // (fused optimizer: the fc weight gradient is consumed in registers and not stored)
+  fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
+         (long)HW * C2, NO, /*mask=*/true, cs_, ex);
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
@@ -141,12 +158,16 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
   }
   // ---- conv backward (bucket 1)
-  conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, f1 ? nullptr : b_.a1, b_.dz1, B, H, W, C1, C2,
-                f1 ? b_.xb : b_.images, true, f1 ? bid : bi, b_.w1slab, cfg_.pxt_dgrad, cs_, pc1b);
-  conv3x3_wgrad(b_.dz2, nullptr, f1 ? nullptr : b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows,
-                cs_, pc1b);
+  if (f1) {
+    // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
+    conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
+                cfg_.wgrad_rows, c1b, cs_);
+  } else {
+    conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
+                  b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
+    conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
+  }
   SlabSet ss{};
-  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
   ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, n_w2, wblk, G + b_.off_w2, inv_ws};
   ss.s[1] = SlabSeg{b_.w2slab, w2row, n_w2, (long)C2, wblk, G + b_.off_b2, inv_ws};
@@ -154,7 +175,27 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   ss.s[2] = SlabSeg{b_.w1slab, 320, 0, (long)C1 * 9, dblk, G + b_.off_w1, inv_ws};
   ss.s[3] = SlabSeg{b_.w1slab, 320, (long)C1 * 9, (long)C1, dblk, G + b_.off_b1, inv_ws};
   ss.count = 4;
+  if (fopt) {
+    auto opt = [&](SlabSeg& sg, long off) {
+      sg.p = P + off;
+      sg.m = M ? M + off : nullptr;
+    };
+    opt(ss.s[0], b_.off_w2);
+    ss.s[0].sh = b_.w2_bf16;
+    ss.s[0].sh_t = b_.w2t_bf16;
+    ss.s[0].t_co = C2; ss.s[0].t_taps = 9; ss.s[0].t_ci = C1;
+    opt(ss.s[1], b_.off_b2);
+    opt(ss.s[2], b_.off_w1);
+    opt(ss.s[3], b_.off_b1);
+    // fc bias: its gradient (fc_bwd block 0) is already final; a 1-row "slab" in place
+    ss.s[4] = SlabSeg{G + b_.off_bfc, (long)NO, 0, (long)NO, 1, G + b_.off_bfc, 1.f};
+    opt(ss.s[4], b_.off_bfc);
+    ss.count = 5;
+    ss.sgd = sa;
+    ss.step_ctr = b_.step_ctr;  // the step's last kernel advances the batch window
+  }
   grad_reduce(ss, cs_);
+  if (fopt) return;
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
@@ -164,15 +205,13 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
   }
   // ---- optimizer + bf16 shadows + next batch window
-  SgdArgs a{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
-            cfg_.maximize, first_momentum_step ? 1 : 0, 1};
   ShadowSet sh{};
   sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
   sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
-  sh.r[2] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
-  sh.r[3] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+  sh.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
+  sh.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
   sh.count = 4;
-  sgd_step(P, G, b_.momentum, b_.n_params, a, sh, b_.step_ctr, cs_);
+  sgd_step(P, G, M, b_.n_params, sa, sh, b_.step_ctr, cs_);
 }
 
 void SimpleCNNEngine::step(int batch, int batch_stride) {

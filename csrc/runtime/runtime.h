@@ -131,6 +131,9 @@ struct EngineConfig {
   // 1: 6 kernels - conv1 recomputed inside conv2 fwd/dgrad/wgrad from the uint8
   //    images (a1 never touches HBM) and cross-entropy folded into fc_bwd
   int fuse_level = 0;
+  // 1: single-process steps apply SGD in the epilogues of fc_bwd / grad_reduce (no
+  //    separate optimizer kernel); 0: always the flat SGD kernel (equivalence tests)
+  int fuse_opt = 1;
 };
 
 class SimpleCNNEngine {

@@ -42,6 +42,8 @@ class EngineOptions:
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
     # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd)
     fuse_level: int = 1
+    # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
+    fuse_opt: bool = True
 
 
 class FusedSimpleCNNEngine:
@@ -98,7 +100,7 @@ class FusedSimpleCNNEngine:
                    dampening=float(g["dampening"]), weight_decay=float(g["weight_decay"]),
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
-                   fuse_level=int(self.opts.fuse_level))
+                   fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt))
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:

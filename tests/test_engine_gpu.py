@@ -9,7 +9,7 @@ dev = "cuda"
 
 
 def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentum=0.0,
-           fuse_level=0):
+           fuse_level=0, fuse_opt=True, weight_decay=0.0):
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
     from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
     from ddp_amd.models import SimpleCNN
@@ -17,12 +17,12 @@ def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentu
 
     torch.manual_seed(seed)
     model = SimpleCNN().to(dev)
-    opt = FusedSGD(model, lr=lr, momentum=momentum)
+    opt = FusedSGD(model, lr=lr, momentum=momentum, weight_decay=weight_decay)
     imgs, labels = synthetic_mnist(n)
     data = DeviceMNIST(imgs, labels, dev)
     eng = FusedSimpleCNNEngine(model, opt, data, B, 1, 0,
                                opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph,
-                                                  fuse_level=fuse_level))
+                                                  fuse_level=fuse_level, fuse_opt=fuse_opt))
     eng.refresh()
     return model, opt, data, eng, imgs, labels
 
@@ -70,6 +70,26 @@ def test_fuse_level1_bitwise_equals_level0(B):
     for (n, a), (_, b) in zip(m0.named_parameters(), m1.named_parameters()):
         assert torch.equal(a, b), n
     assert torch.equal(e0.t["loss_hist"][:7], e1.t["loss_hist"][:7])
+
+
+@pytest.mark.parametrize("momentum,wd", [(0.0, 0.0), (0.9, 1e-4)])
+def test_fused_optimizer_bitwise_equals_sgd_kernel(momentum, wd):
+    """Single-process steps apply SGD in the fc_bwd / grad_reduce epilogues; the result
+    must equal the separate flat SGD kernel bit for bit (same sgd_one, same values)."""
+    m1, o1, _, e1, _, _ = _setup(use_graph=True, momentum=momentum, weight_decay=wd, fuse_level=1,
+                                 fuse_opt=False)
+    m2, o2, _, e2, _, _ = _setup(use_graph=True, momentum=momentum, weight_decay=wd, fuse_level=1,
+                                 fuse_opt=True)
+    e1.run_steps(11)
+    e2.run_steps(11)
+    e1.synchronize(); e2.synchronize()
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
+    if momentum:
+        assert torch.equal(o1.momentum_buffer, o2.momentum_buffer)
+    for k in ("w2_bf16", "w2t_bf16", "wfc_bf16", "wfc_frag"):
+        assert torch.equal(e1.t[k], e2.t[k]), k
+    assert torch.equal(e1.t["step_ctr"], e2.t["step_ctr"])
 
 
 def test_fuse_level1_one_step_matches_bf16_reference():
