@@ -11,7 +11,8 @@ random-init weights (no network for the real dataset), bf16 compute with fp32
 master weights / gradients / optimizer.  A timed step is the complete training
 step of the reference's loop: batch gather + forward + loss + backward + DDP
 bucket all-reduce (RCCL, N>1) + SGD update - executed by the native fused
-engine (8 HIP kernels + 2 RCCL all-reduces, replayed from a hipGraph).
+engine (4-5 HIP kernels + 2 bucket all-reduces - the direct xGMI kernel, RCCL as the
+fallback - replayed from a hipGraph).
 
 W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
 ``torch.cuda.synchronize()`` on both sides; the step time is the MAX over ranks;
@@ -56,6 +57,8 @@ def main():
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
+                    help="bucket all-reduce at N>1: direct xGMI kernel (RCCL fallback) or RCCL")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
@@ -95,6 +98,7 @@ def main():
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
     k = args.graph_steps or graph_chunk(args.steps)
     eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph)
+    eo.comm = args.comm
     for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows"):
         if getattr(args, f) is not None:
             setattr(eo, f, getattr(args, f))
@@ -125,6 +129,13 @@ def main():
     ms = dt * 1000.0 / args.steps
     img_s = ws * args.batch_size * args.steps / dt
     finite = bool(torch.isfinite(fs.params).all().item())
+    same = True
+    if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
+        ref = fs.params.detach().clone()
+        dist.broadcast(ref, src=0)
+        diff = torch.tensor([0 if torch.equal(ref, fs.params) else 1], device=dev)
+        dist.all_reduce(diff)
+        same = int(diff.item()) == 0
     if rank == 0:
         base = BASELINE_IMG_S.get(ws)
         print(json.dumps({
@@ -146,7 +157,8 @@ def main():
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
                        "graph_steps": k, "fuse_level": eo.fuse_level,
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
-                                  "wgrad_rows": eng.wgrad_rows}, "params_finite": finite},
+                                  "wgrad_rows": eng.wgrad_rows}, "params_finite": finite,
+                       "bucket_allreduce": eng.comm_kind, "params_identical_across_ranks": same},
         }), flush=True)
     if ws > 1:
         dist.barrier(device_ids=[lrank])

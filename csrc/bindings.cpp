@@ -610,6 +610,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                               stream_or_current(stream));
            }, py::arg("send"), py::arg("recv"), py::arg("op") = 0, py::arg("stream") = 0);
 
+  py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
+      .def(py::init<int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def("add_channel", &XgmiComm::add_channel, py::arg("off"), py::arg("n"))
+      .def("set_data", [](XgmiComm& x, Tensor& t) {
+        check(t, "data", at::kFloat);
+        x.set_data(t.data_ptr<float>(), t.numel());
+      })
+      .def("export_handles", [](const XgmiComm& x) { return py::bytes(x.export_handles()); })
+      .def("import_handles", [](XgmiComm& x, const std::vector<py::bytes>& all) {
+        std::vector<std::string> v;
+        for (const auto& b : all) v.emplace_back(b);
+        x.import_handles(v);
+      })
+      .def("all_reduce", [](XgmiComm& x, int ch, double scale) {
+        x.all_reduce(ch, cur_stream(), (float)scale);
+      }, py::arg("channel"), py::arg("scale") = 1.0)
+      .def("error_flags", &XgmiComm::error_flags)
+      .def("set_timeout", &XgmiComm::set_timeout)
+      .def_property_readonly("rank", &XgmiComm::rank)
+      .def_property_readonly("world", &XgmiComm::world);
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init([](std::shared_ptr<Comm> comm, Tensor& flat, std::vector<long> poff,
                        std::vector<long> pnum, std::vector<int> pb, std::vector<long> boff,
@@ -713,6 +733,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("destroy_graph", &SimpleCNNEngine::destroy_graph)
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
+      .def("set_xgmi", &SimpleCNNEngine::set_xgmi)
       .def_property_readonly("graph_steps", &SimpleCNNEngine::graph_steps)
       .def_property_readonly("stream", [](SimpleCNNEngine& e) { return (uint64_t)e.stream(); });
 }

@@ -1,0 +1,125 @@
+// Direct (all-to-all) two-shot SUM all-reduce over xGMI for the DDP gradient buckets.
+//
+// Why not only RCCL: an 8x MI355X node is a full mesh of point-to-point xGMI links
+// (7 per GPU).  A ring all-reduce moves 2(N-1)/N of the bucket over ONE link per step;
+// the direct algorithm below moves each byte over its own link, all 7 links at once,
+// in two hops, and runs as ONE kernel inside the step's hipGraph (no proxy thread, no
+// protocol selection).  SimpleCNN's buckets are 2.0 MB and 75 KB (SURVEY.md §2.6
+// I6/I7), i.e. latency-bound: two cross-GPU barriers + 2 x (bucket / N) per link.
+//
+//   B0  entry barrier: every rank's gradient bucket is final
+//   RS  rank r pulls its slice r from all peers (system-scope loads over xGMI), sums in
+//       FIXED rank order 0..N-1 (bitwise identical on every rank), writes the reduced
+//       slice to its stage buffer (parity = call number & 1)
+//   B1  every rank finished RS (so nobody reads any rank's gradient buffer any more)
+//   AG  rank r pulls every peer's reduced slice from its stage buffer into its own
+//       gradient buffer (local stores)
+//
+// Pull-only: no GPU ever writes another GPU's memory, so each GPU's own L2 stays
+// coherent for its own buffers.  Everything a peer reads is produced with system-scope
+// (write-through) stores and read with system-scope loads, and every storing wave
+// drains its stores (s_waitcnt vmcnt(0)) before the block's flag store.  The stage
+// buffer is double-buffered by call parity, which removes the exit barrier: call k+2
+// reuses call k's stage only after every rank passed call k+1's B0.
+//
+// Barriers are per block: block b of every rank handles the same element range of every
+// slice, and only ever waits for block b of its peers.  Flags are monotonic per-block counters in
+// uncached memory; every spin is bounded (XgmiArgs::timeout_ticks of the 100 MHz clock):
+// on timeout the block sets the error word and stops waiting, so a broken peer makes
+// the result wrong (detected by the host) instead of hanging the GPU.
+#include "kernels/common.h"
+#include "kernels/launchers.h"
+
+namespace ddp_amd {
+
+
+
+// Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
+// has signalled `target` to us.  Caller guarantees every wave drained its stores.
+__device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target, unsigned* s_fail) {
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < a.world && !*s_fail) {
+    unsigned* dst = a.sig[t] + XGMI_FLAG_OFF + blockIdx.x * XGMI_MAX_RANKS + a.rank;
+    __hip_atomic_store(dst, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned* src = a.sig[a.rank] + XGMI_FLAG_OFF + blockIdx.x * XGMI_MAX_RANKS + t;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        __hip_atomic_store(a.sig[a.rank] + XGMI_ERR_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *s_fail = 1u;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// One element of the slice per thread and rank: all N loads of a thread are in flight
+// at once (RS: the N contributions; AG: the N reduced slices), so each phase is one
+// xGMI round trip.  Grid = ceil(slice / XGMI_THREADS) blocks (<= XGMI_MAX_BLOCKS).
+__global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
+  __shared__ unsigned s_epoch, s_fail;
+  const int N = a.world, r = a.rank;
+  unsigned* my = a.sig[r];
+  // sticky failure: after any timeout every later call skips its barriers at once
+  // (the host raises on the error word; a broken run must not cost timeouts per step)
+  const bool failed_before = __hip_atomic_load(my + XGMI_ERR_OFF, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+  if (threadIdx.x == 0) {
+    // per-block call counter (only this block of this rank touches it); every call of a
+    // channel uses the same grid, so the counters of all blocks stay equal
+    const unsigned e = my[XGMI_SEQ_OFF + blockIdx.x] + 1u;
+    my[XGMI_SEQ_OFF + blockIdx.x] = e;
+    s_epoch = e;
+    s_fail = failed_before ? 1u : 0u;
+  }
+  __syncthreads();
+  const unsigned e = s_epoch;
+  const long slice = a.slice;  // elements per rank slice (the last rank's may be shorter)
+  const long i = (long)blockIdx.x * XGMI_THREADS + threadIdx.x;
+  const bool live = i < slice;
+  const long par = (long)(e & 1u) * slice;
+
+  xgmi_barrier(a, 2u * e, &s_fail);  // B0
+  if (!s_fail && live) {
+    // ---- RS: element i of my slice, fixed-order sum over ranks 0..N-1
+    const long g = (long)r * slice + i;
+    if (g < a.n) {
+      float v[XGMI_MAX_RANKS];
+#pragma unroll
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld_sys(a.data[p] + a.off + g) : 0.f;
+      float sum = v[0];
+#pragma unroll
+      for (int p = 1; p < XGMI_MAX_RANKS; ++p)
+        if (p < N) sum += v[p];
+      st_sys(a.stage[r] + par + i, sum);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  xgmi_barrier(a, 2u * e + 1u, &s_fail);  // B1
+  if (!s_fail && live) {
+    // ---- AG: element i of every rank's reduced slice into my gradient buffer
+    float v[XGMI_MAX_RANKS];
+#pragma unroll
+    for (int p = 0; p < XGMI_MAX_RANKS; ++p)
+      v[p] = (p < N && (long)p * slice + i < a.n) ? ld_sys(a.stage[p] + par + i) : 0.f;
+    float* out = a.data[r] + a.off;
+#pragma unroll
+    for (int p = 0; p < XGMI_MAX_RANKS; ++p)
+      if (p < N && (long)p * slice + i < a.n) out[(long)p * slice + i] = v[p] * a.scale;
+  }
+}
+
+int xgmi_blocks(long n, int world) {
+  const long slice = (n + world - 1) / world;
+  const long b = (slice + XGMI_THREADS - 1) / XGMI_THREADS;
+  return (int)(b < 1 ? 1 : b);
+}
+
+void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(blocks), dim3(XGMI_THREADS), 0, s, a);
+}
+
+}  // namespace ddp_amd

@@ -154,6 +154,16 @@ __device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group&
   }
 }
 
+// ---- system-scope (cross-GPU coherent) element access: sc0 sc1 global loads / stores
+// (write-through; loads bypass the non-coherent caches).  Used for every byte another
+// GPU reads over xGMI (kernels/allreduce.hip).
+__device__ __forceinline__ float ld_sys(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- optimizer element update (torch/optim/sgd.py _single_tensor_sgd semantics)
 // destination index of element j (multiple of 4 for a quad) in the FCFRAG layout
 __device__ __forceinline__ int fcfrag_index(int j, int HW, int C) {

@@ -220,8 +220,10 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       for (int pt = 0; pt < PXT; ++pt) {
         const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        b[pt] = ok ? *reinterpret_cast<const bf16x8*>(sX + (rowc[pt] + dh * W + dw) * XS + ci0 + kofs)
-                   : zero8();
+        // unconditional read (the row is always inside the staged range), then a select:
+        // no exec-masked LDS read, so the reads of a tap pipeline ahead of the MFMAs
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sX + (rowc[pt] + dh * W + dw) * XS + ci0 + kofs);
+        b[pt] = ok ? v : zero8();
       }
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt)
@@ -425,8 +427,8 @@ __device__ __forceinline__ void dgrad_body(
       for (int pt = 0; pt < PXT; ++pt) {
         const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        b[pt] = ok ? *reinterpret_cast<const bf16x8*>(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs)
-                   : zero8();
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs);
+        b[pt] = ok ? v : zero8();  // unconditional read + select (see the forward)
       }
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {

@@ -106,6 +106,7 @@ struct FcBwdExtras {
   bf16_t* sh_plain = nullptr;  // bf16 shadow [NO][K]
   bf16_t* sh_frag = nullptr;   // FCFRAG shadow (conv3x3_fwd epilogue order)
   int frag_HW = 0, frag_C = 0;
+  int sys_store = 0;  // dW / dbias with system-scope stores (read by peers over xGMI)
 };
 size_t fc_bwd_lds(int B, int NO, bool xent);
 void noop(int blocks, int* sink, hipStream_t s);
@@ -120,6 +121,25 @@ void xent(const float* part, int G, const float* bias, int C, int B, const long 
 void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int B,
                const int* labels32, BatchIdx bi, float* dlogits, float* loss_rows, float gscale,
                hipStream_t s);
+
+// ---- direct two-shot xGMI all-reduce (allreduce.hip) ----------------------------------
+constexpr int XGMI_MAX_RANKS = 8, XGMI_THREADS = 256, XGMI_MAX_BLOCKS = 1024;
+// signal words of one channel: [block][src rank] flags, [block] call counters, error word
+constexpr int XGMI_FLAG_OFF = 0;
+constexpr int XGMI_SEQ_OFF = XGMI_MAX_BLOCKS * XGMI_MAX_RANKS;
+constexpr int XGMI_ERR_OFF = XGMI_SEQ_OFF + XGMI_MAX_BLOCKS;
+constexpr int XGMI_SIG_WORDS = XGMI_ERR_OFF + 64;
+struct XgmiArgs {
+  float* data[XGMI_MAX_RANKS];    // every rank's gradient buffer (peer-mapped; [rank] = own)
+  float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats
+  unsigned* sig[XGMI_MAX_RANKS];  // every rank's signal words (uncached)
+  long off, n, slice;             // bucket offset / length in the gradient buffer; n / world rounded up
+  float scale;                    // applied to the result (1: producers prescaled by 1/world)
+  int rank, world;
+  unsigned long long timeout_ticks;  // per barrier spin, 100 MHz ticks
+};
+int xgmi_blocks(long n, int world);
+void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s);
 
 // ---- optimizer / reductions -----------------------------------------------------------
 // SHADOW_BF16_FCFRAG: fc weight [o][hw][c] (a = HW, b = C) -> the MFMA-fragment order
@@ -156,6 +176,7 @@ struct SlabSet {
   int count;
   SgdArgs sgd{};              // update != 0 -> apply SGD to segments with p set
   int* step_ctr = nullptr;    // += 1 at the end (the step's last kernel)
+  int sys_store = 0;          // dst with system-scope stores (read by peers over xGMI)
 };
 void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, const ShadowSet& sh,
               int* step_ctr, hipStream_t s);

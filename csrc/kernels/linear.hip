@@ -122,7 +122,8 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
     if (ex.dbias && threadIdx.x < NO) {
       float acc = 0.f;
       for (int b = 0; b < B; ++b) acc += s_dl[b * NO + threadIdx.x];
-      ex.dbias[threadIdx.x] = acc * ex.dbias_scale;
+      if (ex.sys_store) st_sys(ex.dbias + threadIdx.x, acc * ex.dbias_scale);
+      else ex.dbias[threadIdx.x] = acc * ex.dbias_scale;
     }
     if ((XENT || ex.loss_rows) && ex.loss_out && threadIdx.x == 64) {
       const float* lr = XENT ? s_loss : ex.loss_rows;
@@ -191,7 +192,10 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
       for (int w = 1; w < WPB; ++w) acc += s_red[(w * NOT + o) * FCB_COLS + c];
       const float g = acc * scale;
       const long idx = (long)o * K + k;
-      if (dW) dW[idx] = g;  // null: fused optimizer consumes it in registers
+      if (dW) {  // null: fused optimizer consumes it in registers
+        if (ex.sys_store) st_sys(dW + idx, g);
+        else dW[idx] = g;
+      }
       if (ex.sgd.update) {  // single-process step: dW is final -> fused SGD + shadows
         float m = ex.m_w ? ex.m_w[idx] : 0.f;
         const float pn = sgd_one(ex.p_w[idx], g, &m, ex.sgd);

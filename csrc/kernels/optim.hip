@@ -134,7 +134,8 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
   if (grp == 0 && live) {
     const SlabSeg& sg = ss.s[k];  // k is block-uniform
     const float g = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
-    sg.dst[i] = g;
+    if (ss.sys_store) st_sys(sg.dst + i, g);
+    else sg.dst[i] = g;
     if (ss.sgd.update && sg.p) {  // single-process step: the gradient is final -> fused SGD
       float m = sg.m ? sg.m[i] : 0.f;
       const float pn = sgd_one(sg.p[i], g, &m, ss.sgd);

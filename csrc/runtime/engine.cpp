@@ -78,7 +78,8 @@ void SimpleCNNEngine::refresh_shadows() {
 void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   const int H = cfg_.H, W = cfg_.W, HW = H * W, C1 = cfg_.C1, C2 = cfg_.C2, NO = cfg_.NO;
   if (B <= 0 || B > cfg_.max_batch) throw std::runtime_error("engine: bad batch size");
-  const bool dist = comm_ && (comm_->world() > 1 || cfg_.force_allreduce);
+  const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
+  const bool dist = use_x || (comm_ && (comm_->world() > 1 || cfg_.force_allreduce));
   const float inv_ws = 1.f / (float)cfg_.world;
   BatchIdx bi{b_.idx, b_.step_ctr, stride, 0};
   bi.n_idx = b_.n_idx;
@@ -139,6 +140,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
                    cfg_.maximize, first_momentum_step ? 1 : 0, 1};
   float* M = b_.momentum;  // null when momentum == 0
+  ex.sys_store = use_x ? 1 : 0;  // bucket 0 is read by the peers over xGMI
   if (fopt) {
     ex.sgd = sa;
     ex.p_w = P + b_.off_wfc;
@@ -154,7 +156,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
-    comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
+    if (use_x) xgmi_->all_reduce(0, ms_);
+    else comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
     DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
   }
   // ---- conv backward (bucket 1)
@@ -194,12 +197,14 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ss.sgd = sa;
     ss.step_ctr = b_.step_ctr;  // the step's last kernel advances the batch window
   }
+  ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
   grad_reduce(ss, cs_);
   if (fopt) return;
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
-    comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
+    if (use_x) xgmi_->all_reduce(1, ms_);
+    else comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
     DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
     DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
     DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
@@ -212,6 +217,15 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   sh.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
   sh.count = 4;
   sgd_step(P, G, M, b_.n_params, sa, sh, b_.step_ctr, cs_);
+}
+
+void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x) {
+  if (x) {
+    if (x->channels() != 2) throw std::runtime_error("engine: xgmi needs one channel per bucket (2)");
+    if (x->world() != cfg_.world) throw std::runtime_error("engine: xgmi world size mismatch");
+  }
+  destroy_graph();
+  xgmi_ = std::move(x);
 }
 
 void SimpleCNNEngine::step(int batch, int batch_stride) {

@@ -60,6 +60,47 @@ class Comm {
   int rank_ = 0, world_ = 1;
 };
 
+// ---------------------------------------------------------------- direct xGMI all-reduce
+// One channel per gradient bucket (a fixed [off, off + n) range of the gradient buffer);
+// see xgmi.cpp / kernels/allreduce.hip.  Producers of a bucket must write it with
+// system-scope stores (peers read it over xGMI right after the kernel boundary).
+class XgmiComm {
+ public:
+  XgmiComm(int rank, int world, int device);
+  ~XgmiComm();
+  XgmiComm(const XgmiComm&) = delete;
+  XgmiComm& operator=(const XgmiComm&) = delete;
+  int add_channel(long off, long n);
+  void set_data(float* data, long numel);
+  std::string export_handles() const;
+  void import_handles(const std::vector<std::string>& all);
+  void all_reduce(int channel, hipStream_t s, float scale = 1.f);
+  unsigned error_flags() const;  // != 0: a barrier timed out (result invalid)
+  void set_timeout(double seconds) { timeout_s_ = seconds; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int channels() const { return (int)ch_.size(); }
+
+ private:
+  struct Channel {
+    long off = 0, n = 0, slice = 0;
+    int blocks = 1;
+    float* stage_local = nullptr;
+    unsigned* sig_local = nullptr;
+    float* stage[XGMI_MAX_RANKS] = {};
+    unsigned* sig[XGMI_MAX_RANKS] = {};
+  };
+  int rank_, world_, device_;
+  float* data_ = nullptr;
+  char* data_base_ = nullptr;
+  long data_off_ = 0;
+  float* data_peer_[XGMI_MAX_RANKS] = {};
+  std::vector<Channel> ch_;
+  std::vector<void*> opened_;
+  bool imported_ = false;
+  double timeout_s_ = 2.0;
+};
+
 // ---------------------------------------------------------------- gradient reducer
 // DDP gradient synchronisation for an arbitrary list of parameters (the module
 // path).  Gradients live in one flat fp32 buffer cut into buckets; when the last
@@ -153,12 +194,16 @@ class SimpleCNNEngine {
   hipStream_t stream() const { return cs_; }
   void synchronize();
   void set_momentum_started(bool v) { momentum_started_ = v; }
+  // bucket all-reduces over the direct xGMI kernel (channel 0 = bucket 0, 1 = bucket 1)
+  // instead of RCCL; set before capturing a graph
+  void set_xgmi(std::shared_ptr<XgmiComm> x);
 
  private:
   void launch_step(int batch, int batch_stride, bool first_momentum_step);
   EngineConfig cfg_;
   EngineBuffers b_;
   std::shared_ptr<Comm> comm_;
+  std::shared_ptr<XgmiComm> xgmi_;
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_;
   hipGraph_t graph_ = nullptr;

@@ -1,0 +1,157 @@
+// Host side of the direct xGMI all-reduce (kernels/allreduce.hip).
+//
+// Every rank registers its gradient buffer (any pointer into a hipMalloc allocation:
+// the IPC handle names the allocation, the offset is exchanged next to it) and, per
+// channel (= gradient bucket), allocates a stage buffer (2 x slice floats, call-parity
+// double buffering) and uncached signal words.  The Python layer exchanges the opaque
+// handle blobs through the c10d TCPStore; import_handles() maps every peer's buffers
+// (hipIpcOpenMemHandle: xGMI peer mappings on a multi-GPU node, a second mapping of the
+// same memory when several ranks share one GPU in tests).  all_reduce() is one kernel
+// launch on the caller's stream, capturable in a hipGraph.
+#include <cstring>
+
+#include "runtime/runtime.h"
+
+namespace ddp_amd {
+
+namespace {
+constexpr size_t kHandle = sizeof(hipIpcMemHandle_t);
+
+void put_handle(std::string& out, void* base) {
+  hipIpcMemHandle_t h;
+  DDP_HIP_CHECK(hipIpcGetMemHandle(&h, base));
+  out.append(reinterpret_cast<const char*>(&h), kHandle);
+}
+void put_i64(std::string& out, long long v) { out.append(reinterpret_cast<const char*>(&v), 8); }
+}  // namespace
+
+XgmiComm::XgmiComm(int rank, int world, int device) : rank_(rank), world_(world), device_(device) {
+  if (world < 1 || world > XGMI_MAX_RANKS)
+    throw std::runtime_error("xgmi: world size must be 1.." + std::to_string(XGMI_MAX_RANKS));
+  if (rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad rank");
+  DDP_HIP_CHECK(hipSetDevice(device));
+}
+
+XgmiComm::~XgmiComm() {
+  if (process_exiting()) return;
+  for (void* p : opened_) hipIpcCloseMemHandle(p);
+  for (auto& c : ch_) {
+    if (c.stage_local) hipFree(c.stage_local);
+    if (c.sig_local) hipFree(c.sig_local);
+  }
+}
+
+int XgmiComm::add_channel(long off, long n) {
+  if (imported_) throw std::runtime_error("xgmi: add channels before import_handles");
+  Channel c;
+  c.off = off;
+  c.n = n;
+  c.slice = (n + world_ - 1) / world_;
+  c.blocks = xgmi_blocks(n, world_);
+  if (c.blocks > XGMI_MAX_BLOCKS) throw std::runtime_error("xgmi: bucket too large for one channel");
+  DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c.stage_local), sizeof(float) * 2 * c.slice));
+  DDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c.sig_local),
+                                      sizeof(unsigned) * XGMI_SIG_WORDS, hipDeviceMallocUncached));
+  DDP_HIP_CHECK(hipMemset(c.sig_local, 0, sizeof(unsigned) * XGMI_SIG_WORDS));
+  DDP_HIP_CHECK(hipMemset(c.stage_local, 0, sizeof(float) * 2 * c.slice));
+  DDP_HIP_CHECK(hipDeviceSynchronize());
+  ch_.push_back(c);
+  return (int)ch_.size() - 1;
+}
+
+void XgmiComm::set_data(float* data, long numel) {
+  if (imported_) throw std::runtime_error("xgmi: set_data before import_handles");
+  for (auto& c : ch_)
+    if (c.off < 0 || c.off + c.n > numel) throw std::runtime_error("xgmi: channel outside the data buffer");
+  data_ = data;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  DDP_HIP_CHECK(hipMemGetAddressRange(&base, &size, data));
+  data_base_ = reinterpret_cast<char*>(base);
+  data_off_ = reinterpret_cast<char*>(data) - data_base_;
+}
+
+std::string XgmiComm::export_handles() const {
+  if (!data_) throw std::runtime_error("xgmi: set_data first");
+  std::string out;
+  put_i64(out, (long long)ch_.size());
+  put_handle(out, data_base_);
+  put_i64(out, data_off_);
+  for (const auto& c : ch_) {
+    put_handle(out, c.stage_local);
+    put_handle(out, c.sig_local);
+  }
+  return out;
+}
+
+void XgmiComm::import_handles(const std::vector<std::string>& all) {
+  if ((int)all.size() != world_) throw std::runtime_error("xgmi: need one handle blob per rank");
+  const size_t want = 8 + kHandle + 8 + ch_.size() * 2 * kHandle;
+  auto open = [&](const char* p) {
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, p, kHandle);
+    void* dev = nullptr;
+    DDP_HIP_CHECK(hipIpcOpenMemHandle(&dev, h, hipIpcMemLazyEnablePeerAccess));
+    opened_.push_back(dev);
+    return reinterpret_cast<char*>(dev);
+  };
+  for (int r = 0; r < world_; ++r) {
+    const std::string& b = all[r];
+    if (b.size() != want) throw std::runtime_error("xgmi: handle blob size mismatch (channel layout differs)");
+    long long nch = 0, off = 0;
+    std::memcpy(&nch, b.data(), 8);
+    if (nch != (long long)ch_.size()) throw std::runtime_error("xgmi: channel count differs across ranks");
+    const char* p = b.data() + 8;
+    std::memcpy(&off, p + kHandle, 8);
+    if (r == rank_) {
+      data_peer_[r] = data_;
+    } else {
+      data_peer_[r] = reinterpret_cast<float*>(open(p) + off);
+    }
+    p += kHandle + 8;
+    for (auto& c : ch_) {
+      if (r == rank_) {
+        c.stage[r] = c.stage_local;
+        c.sig[r] = c.sig_local;
+      } else {
+        c.stage[r] = reinterpret_cast<float*>(open(p));
+        c.sig[r] = reinterpret_cast<unsigned*>(open(p + kHandle));
+      }
+      p += 2 * kHandle;
+    }
+  }
+  imported_ = true;
+}
+
+void XgmiComm::all_reduce(int channel, hipStream_t s, float scale) {
+  if (!imported_) throw std::runtime_error("xgmi: import_handles first");
+  if (channel < 0 || channel >= (int)ch_.size()) throw std::runtime_error("xgmi: bad channel");
+  const Channel& c = ch_[channel];
+  XgmiArgs a{};
+  for (int r = 0; r < world_; ++r) {
+    a.data[r] = data_peer_[r];
+    a.stage[r] = c.stage[r];
+    a.sig[r] = c.sig[r];
+  }
+  a.off = c.off;
+  a.n = c.n;
+  a.slice = c.slice;
+  a.scale = scale;
+  a.rank = rank_;
+  a.world = world_;
+  a.timeout_ticks = (unsigned long long)(timeout_s_ * 1e8);
+  xgmi_allreduce(a, c.blocks, s);
+  DDP_HIP_CHECK(hipGetLastError());
+}
+
+unsigned XgmiComm::error_flags() const {
+  unsigned e = 0;
+  for (const auto& c : ch_) {
+    unsigned v = 0;
+    DDP_HIP_CHECK(hipMemcpy(&v, c.sig_local + XGMI_ERR_OFF, sizeof(v), hipMemcpyDeviceToHost));
+    e |= v;
+  }
+  return e;
+}
+
+}  // namespace ddp_amd

@@ -44,6 +44,9 @@ class EngineOptions:
     fuse_level: int = 1
     # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
     fuse_opt: bool = True
+    # bucket all-reduce data plane at world size > 1: "xgmi" = the direct two-shot kernel
+    # (falls back to RCCL when its self-test fails), "rccl" = RCCL, "auto" = xgmi
+    comm: str = "auto"
 
 
 class FusedSimpleCNNEngine:
@@ -102,7 +105,17 @@ class FusedSimpleCNNEngine:
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt))
         use_comm = world_size > 1 or self.opts.force_allreduce
+        self.xgmi = None
+        if use_comm and self.opts.comm in ("auto", "xgmi"):
+            from ..parallel.xgmi import create_xgmi
+
+            self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size)
+        if use_comm and self.xgmi is None and comm is None:
+            raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
+        self.comm_kind = "xgmi" if self.xgmi is not None else ("rccl" if use_comm else "none")
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
+        if self.xgmi is not None:
+            self.eng.set_xgmi(self.xgmi)
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:
             self.eng.set_momentum_started(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)
@@ -123,6 +136,8 @@ class FusedSimpleCNNEngine:
 
     def synchronize(self):
         self.eng.synchronize()
+        if self.xgmi is not None and self.xgmi.error_flags():
+            raise RuntimeError("xGMI all-reduce: a cross-GPU barrier timed out (results invalid)")
 
     def _ensure_graph(self):
         k = self.opts.graph_steps
