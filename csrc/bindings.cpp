@@ -257,6 +257,7 @@ void op_xent_rows(const Tensor& part, int HW, int CH, const Tensor& bias, const 
   const int B = dlogits.size(0), NO = dlogits.size(1);
   TORCH_CHECK(bias.numel() == NO && NO <= 16, "xent_rows: at most 16 classes");
   TORCH_CHECK(CH > 0 && CH <= HW && HW / CH + 2 <= 16, "xent_rows: block geometry");
+  TORCH_CHECK((long)B * HW < (1L << 31), "xent_rows: B * HW must fit in int32");
   const long nblk = ((long)B * HW + CH - 1) / CH;
   TORCH_CHECK(part.numel() >= nblk * 2 * NO && loss_rows.numel() >= B, "xent_rows: sizes");
   TORCH_CHECK((long)B * NO * 4 <= 64 * 1024, "xent_rows: batch too large");

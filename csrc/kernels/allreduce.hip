@@ -34,6 +34,26 @@ namespace ddp_amd {
 
 
 
+// bf16 shadows of one updated parameter (flat index j), same layouts as sgd_kernel
+__device__ __forceinline__ void shadow_one(const ShadowSet& sh, long j, float v) {
+#pragma unroll
+  for (int r = 0; r < MAX_SHADOWS; ++r) {
+    if (r >= sh.count) break;
+    const long k = j - sh.r[r].off;
+    if (k < 0 || k >= sh.r[r].n) continue;
+    const bf16_t b = f2bf(v);
+    if (sh.r[r].kind == SHADOW_BF16) {
+      sh.r[r].dst[k] = b;
+    } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
+      sh.r[r].dst[fcfrag_index((int)k, sh.r[r].a, sh.r[r].b)] = b;
+    } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
+      const long per = (long)sh.r[r].b * sh.r[r].c;
+      const long co = k / per;
+      sh.r[r].dst[(k - co * per) * sh.r[r].a + co] = b;
+    }
+  }
+}
+
 // Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
 // has signalled `target` to us.  Caller guarantees every wave drained its stores.
 __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target, unsigned* s_fail) {
@@ -107,9 +127,23 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
       v[p] = (p < N && (long)p * slice + i < a.n) ? ld_sys(a.stage[p] + par + i) : 0.f;
     float* out = a.data[r] + a.off;
 #pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p)
-      if (p < N && (long)p * slice + i < a.n) out[(long)p * slice + i] = v[p] * a.scale;
+    for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
+      const long k = (long)p * slice + i;
+      if (p < N && k < a.n) {
+        const float g = v[p] * a.scale;
+        out[k] = g;
+        if (a.sgd.update) {  // fused optimizer: same update on every rank
+          const long j = a.off + k;
+          float m = a.mbuf ? a.mbuf[j] : 0.f;
+          const float pn = sgd_one(a.params[j], g, &m, a.sgd);
+          a.params[j] = pn;
+          if (a.mbuf) a.mbuf[j] = m;
+          shadow_one(a.sh, j, pn);
+        }
+      }
+    }
   }
+  if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
 }
 
 int xgmi_blocks(long n, int world) {

@@ -247,20 +247,26 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
                                                  float gscale, float* dl, float* loss, float* s_lg) {
   const int base = bi.base();
   const int lab0 = (int)threadIdx.x < B ? labels32[bi.row(threadIdx.x, base)] : 0;
+  DDP_STAMP(STAMP_K_XENT, 1);  // label load issued
   for (int t = threadIdx.x; t < B * NO; t += blockDim.x) {
+    // 32-bit index math only (B * HW < 2^31, checked on the host): 64-bit divisions
+    // by runtime values are long software sequences.  Block kb0 is the only one that can
+    // start in the previous image (slot 1); every later block starts inside image b.
     const int b = t / NO, o = t - (t / NO) * NO;
-    const long p0 = (long)b * HW;
-    const int kb0 = (int)(p0 / CH), kb1 = (int)((p0 + HW - 1) / CH);
+    const int p0 = b * HW;
+    const int kb0 = p0 / CH, kb1 = (p0 + HW - 1) / CH;
+    const int slot0 = kb0 * CH == p0 ? 0 : 1;
     float v[XENT_MAX_BLK];
 #pragma unroll
     for (int j = 0; j < XENT_MAX_BLK; ++j) {
       const int kb = min(kb0 + j, kb1);
-      const int slot = ((long)kb * CH) / HW == b ? 0 : 1;
-      v[j] = part[((long)kb * 2 + slot) * NO + o];
+      v[j] = part[(kb * 2 + (j == 0 ? slot0 : 0)) * NO + o];
     }
+    DDP_STAMP(STAMP_K_XENT, 2);  // partial loads issued
     float a = 0.f;
 #pragma unroll
     for (int j = 0; j < XENT_MAX_BLK; ++j) a += (kb0 + j <= kb1) ? v[j] : 0.f;
+    DDP_STAMP(STAMP_K_XENT, 3);  // partials arrived and summed
     s_lg[t] = bias[o] + a;
   }
   DDP_STAMP(STAMP_K_FC_BWD, 5);

@@ -122,25 +122,6 @@ void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int
                const int* labels32, BatchIdx bi, float* dlogits, float* loss_rows, float gscale,
                hipStream_t s);
 
-// ---- direct two-shot xGMI all-reduce (allreduce.hip) ----------------------------------
-constexpr int XGMI_MAX_RANKS = 8, XGMI_THREADS = 256, XGMI_MAX_BLOCKS = 1024;
-// signal words of one channel: [block][src rank] flags, [block] call counters, error word
-constexpr int XGMI_FLAG_OFF = 0;
-constexpr int XGMI_SEQ_OFF = XGMI_MAX_BLOCKS * XGMI_MAX_RANKS;
-constexpr int XGMI_ERR_OFF = XGMI_SEQ_OFF + XGMI_MAX_BLOCKS;
-constexpr int XGMI_SIG_WORDS = XGMI_ERR_OFF + 64;
-struct XgmiArgs {
-  float* data[XGMI_MAX_RANKS];    // every rank's gradient buffer (peer-mapped; [rank] = own)
-  float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats
-  unsigned* sig[XGMI_MAX_RANKS];  // every rank's signal words (uncached)
-  long off, n, slice;             // bucket offset / length in the gradient buffer; n / world rounded up
-  float scale;                    // applied to the result (1: producers prescaled by 1/world)
-  int rank, world;
-  unsigned long long timeout_ticks;  // per barrier spin, 100 MHz ticks
-};
-int xgmi_blocks(long n, int world);
-void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s);
-
 // ---- optimizer / reductions -----------------------------------------------------------
 // SHADOW_BF16_FCFRAG: fc weight [o][hw][c] (a = HW, b = C) -> the MFMA-fragment order
 // read by the conv3x3_fwd FC epilogue, [o][hw/16][c/16][(c/4)%4][hw%16][c%4], so each
@@ -182,5 +163,33 @@ void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, c
               int* step_ctr, hipStream_t s);
 void grad_reduce(const SlabSet& ss, hipStream_t s);
 void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s);
+
+// ---- direct two-shot xGMI all-reduce (allreduce.hip) ----------------------------------
+constexpr int XGMI_MAX_RANKS = 8, XGMI_THREADS = 256, XGMI_MAX_BLOCKS = 1024;
+// signal words of one channel: [block][src rank] flags, [block] call counters, error word
+constexpr int XGMI_FLAG_OFF = 0;
+constexpr int XGMI_SEQ_OFF = XGMI_MAX_BLOCKS * XGMI_MAX_RANKS;
+constexpr int XGMI_ERR_OFF = XGMI_SEQ_OFF + XGMI_MAX_BLOCKS;
+constexpr int XGMI_SIG_WORDS = XGMI_ERR_OFF + 64;
+struct XgmiArgs {
+  float* data[XGMI_MAX_RANKS];    // every rank's gradient buffer (peer-mapped; [rank] = own)
+  float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats
+  unsigned* sig[XGMI_MAX_RANKS];  // every rank's signal words (uncached)
+  long off, n, slice;             // bucket offset / length in the gradient buffer; n / world rounded up
+  float scale;                    // applied to the result (1: producers prescaled by 1/world)
+  int rank, world;
+  unsigned long long timeout_ticks;  // per barrier spin, 100 MHz ticks
+  // Optional optimizer fused into the all-gather (sgd.update != 0): every rank applies
+  // the same SGD to the same reduced gradient, so parameters stay bitwise identical:
+  // param / momentum at the element's flat index (params + off + k), bf16 shadows of
+  // the regions in `sh` (indices relative to the flat parameter buffer).
+  SgdArgs sgd;
+  float* params;
+  float* mbuf;
+  ShadowSet sh;
+  int* step_ctr;  // += 1 by block 0 at the end (the step's last kernel), may be null
+};
+int xgmi_blocks(long n, int world);
+void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s);
 
 }  // namespace ddp_amd

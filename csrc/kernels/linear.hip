@@ -109,6 +109,7 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
     const int b = min(wave + WPB * u, B - 1);
     xr[u] = *reinterpret_cast<const unsigned*>(X + (long)b * K + cc);
   }
+  DDP_STAMP(STAMP_K_XENT, 0);  // loads of W / X issued
   // ---- prologue: dL of the whole batch into LDS
   if (XENT) {
     xent_batch_block(ex.part, ex.HW, ex.CH, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_dl, s_loss, s_lg);

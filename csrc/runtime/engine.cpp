@@ -156,8 +156,16 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
-    if (use_x) xgmi_->all_reduce(0, ms_);
-    else comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
+    if (use_x) {
+      // SGD of bucket 0 (fc weight + bias) fused into the all-gather: no optimizer kernel
+      ShadowSet sh0{};
+      sh0.r[0] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
+      sh0.r[1] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+      sh0.count = 2;
+      xgmi_->all_reduce_sgd(0, ms_, sa, P, M, sh0, nullptr);
+    } else {
+      comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
+    }
     DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
   }
   // ---- conv backward (bucket 1)
@@ -203,11 +211,19 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   if (dist) {
     DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
     DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
-    if (use_x) xgmi_->all_reduce(1, ms_);
-    else comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
+    if (use_x) {
+      ShadowSet sh1{};
+      sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
+      sh1.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
+      sh1.count = 2;
+      xgmi_->all_reduce_sgd(1, ms_, sa, P, M, sh1, b_.step_ctr);  // the step's last kernel
+    } else {
+      comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
+    }
     DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
     DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
     DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
+    if (use_x) return;  // the optimizer ran inside the all-reduces
   }
   // ---- optimizer + bf16 shadows + next batch window
   ShadowSet sh{};

@@ -75,6 +75,9 @@ class XgmiComm {
   std::string export_handles() const;
   void import_handles(const std::vector<std::string>& all);
   void all_reduce(int channel, hipStream_t s, float scale = 1.f);
+  // the same, with SGD fused into the all-gather (see XgmiArgs)
+  void all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
+                      const ShadowSet& sh, int* step_ctr, float scale = 1.f);
   unsigned error_flags() const;  // != 0: a barrier timed out (result invalid)
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   int rank() const { return rank_; }

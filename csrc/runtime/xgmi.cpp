@@ -124,6 +124,11 @@ void XgmiComm::import_handles(const std::vector<std::string>& all) {
 }
 
 void XgmiComm::all_reduce(int channel, hipStream_t s, float scale) {
+  all_reduce_sgd(channel, s, SgdArgs{}, nullptr, nullptr, ShadowSet{}, nullptr, scale);
+}
+
+void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params,
+                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale) {
   if (!imported_) throw std::runtime_error("xgmi: import_handles first");
   if (channel < 0 || channel >= (int)ch_.size()) throw std::runtime_error("xgmi: bad channel");
   const Channel& c = ch_[channel];
@@ -140,6 +145,12 @@ void XgmiComm::all_reduce(int channel, hipStream_t s, float scale) {
   a.rank = rank_;
   a.world = world_;
   a.timeout_ticks = (unsigned long long)(timeout_s_ * 1e8);
+  a.sgd = sgd;
+  a.params = params;
+  a.mbuf = mbuf;
+  a.sh = sh;
+  a.step_ctr = step_ctr;
+  if (sgd.update && !params) throw std::runtime_error("xgmi: fused SGD needs the parameter buffer");
   xgmi_allreduce(a, c.blocks, s);
   DDP_HIP_CHECK(hipGetLastError());
 }

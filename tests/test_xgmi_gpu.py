@@ -81,7 +81,11 @@ def _engine_worker(rank, world, port, q):
                                    16, world, rank, None, EngineOptions(graph_steps=5, comm="xgmi"))
         assert eng.comm_kind == "xgmi"
         eng.refresh()
-        eng.run_steps(16)
+        p0 = fs.params.detach().cpu().clone()
+        eng.run_steps(1)
+        eng.synchronize()
+        p_one = fs.params.detach().cpu().clone()
+        eng.run_steps(15)
         eng.synchronize()
         p = fs.params.detach().cpu()
         allp = [None] * world
@@ -89,6 +93,24 @@ def _engine_worker(rank, world, port, q):
         for r in range(world):
             assert torch.equal(allp[r], allp[0]), f"rank {r} params differ from rank 0"
         assert torch.isfinite(p).all()
+        if rank == 0:
+            # DDP semantics: 2 ranks x 16 (DistributedSampler shards of the same 32-image
+            # window) == 1 rank x 32, up to summation order
+            # (one step: longer runs drift apart through bf16 weight-shadow roundings)
+            torch.manual_seed(0)
+            m1 = SimpleCNN().cuda()
+            f1 = flat_space(m1)
+            assert torch.equal(f1.params.detach().cpu(), p0)
+            o1 = FusedSGD(m1, lr=0.05, momentum=0.9)
+            e1 = FusedSimpleCNNEngine(m1, o1, DeviceMNIST(imgs, labels, torch.device("cuda", 0)),
+                                      32, 1, 0, None, EngineOptions(graph_steps=5))
+            e1.refresh()
+            e1.run_steps(1)
+            e1.synchronize()
+            d1 = f1.params.detach().cpu() - p0
+            d2 = p_one - p0
+            err = ((d2 - d1).norm() / d1.norm()).item()
+            assert err < 1e-4, f"2-rank xGMI step vs 1-rank step: rel err of the update {err:.2e}"
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok", float(p.double().sum())))  # plain float: no shared-memory tensor
