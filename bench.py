@@ -59,6 +59,9 @@ def main():
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="bucket all-reduce at N>1: direct xGMI kernel (RCCL fallback) or RCCL")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="control-plane process group (nccl = RCCL); gloo + --comm xgmi rehearses "
+                         "N ranks on ONE GPU (RCCL refuses duplicate GPUs)")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
@@ -81,18 +84,28 @@ def main():
     if ws != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
     lrank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":  # rehearsal: several ranks may share the visible GPUs
+        lrank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(lrank)
     dev = torch.device("cuda", lrank)
     comm = None
     if ws > 1:
-        setup(rank, ws, backend="nccl", verbose=False)
-        comm = native_comm()
+        setup(rank, ws, backend=args.backend, verbose=False)
+        if args.backend == "nccl":
+            comm = native_comm()
+        elif args.comm == "rccl":
+            raise SystemExit("--backend gloo has no RCCL data plane: use --comm xgmi")
 
     torch.manual_seed(0)
     model = SimpleCNN().to(dev)
     fs = flat_space(model)
     if ws > 1:
-        dist.broadcast(fs.params, src=0)  # DDP construction semantics (rank-0 init)
+        if args.backend == "nccl":
+            dist.broadcast(fs.params, src=0)  # DDP construction semantics (rank-0 init)
+        else:
+            t = fs.params.detach().cpu()
+            dist.broadcast(t, src=0)
+            fs.params.data.copy_(t)
     opt = FusedSGD(model, lr=args.lr)
     imgs, labels = synthetic_mnist()
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
@@ -113,7 +126,10 @@ def main():
 
     def barrier():
         if ws > 1:
-            dist.barrier(device_ids=[lrank])
+            if args.backend == "nccl":
+                dist.barrier(device_ids=[lrank])
+            else:
+                dist.barrier()
         torch.cuda.synchronize()
 
     barrier()
@@ -123,7 +139,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = dt * 1000.0 / args.steps
@@ -131,9 +147,11 @@ def main():
     finite = bool(torch.isfinite(fs.params).all().item())
     same = True
     if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
-        ref = fs.params.detach().clone()
+        pd = dev if args.backend == "nccl" else "cpu"
+        mine = fs.params.detach().to(pd)
+        ref = mine.clone()
         dist.broadcast(ref, src=0)
-        diff = torch.tensor([0 if torch.equal(ref, fs.params) else 1], device=dev)
+        diff = torch.tensor([0 if torch.equal(ref, mine) else 1], device=pd)
         dist.all_reduce(diff)
         same = int(diff.item()) == 0
     if rank == 0:
@@ -161,7 +179,7 @@ def main():
                        "bucket_allreduce": eng.comm_kind, "params_identical_across_ranks": same},
         }), flush=True)
     if ws > 1:
-        dist.barrier(device_ids=[lrank])
+        barrier()
         dist.destroy_process_group()
 
 
