@@ -164,6 +164,24 @@ __device__ __forceinline__ void st_sys(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---- write-through stores for large once-read kernel outputs (split-K slabs, dZ2):
+// agent-scope (sc1) stores leave L2 at store time instead of sitting dirty until the
+// kernel-end write-back, which otherwise lengthens the next dependent launch boundary
+// by ~bytes / 6 TB/s (MI355X_MICROARCH.md, price row 'boundary').
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(uint2* p, uint2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     ((unsigned long long)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(bf16_t* p, bf16_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- optimizer element update (torch/optim/sgd.py _single_tensor_sgd semantics)
 // destination index of element j (multiple of 4 for a quad) in the FCFRAG layout
 __device__ __forceinline__ int fcfrag_index(int j, int HW, int C) {

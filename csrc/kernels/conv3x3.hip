@@ -249,7 +249,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       float v2 = acc[pt][t][2] + bv.z, v3 = acc[pt][t][3] + bv.w;
       if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
       const uint2 pk = pack4(v0, v1, v2, v3);
-      if (valid[pt]) *reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co) = pk;
+      if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
       if (NOF > 0) {
         float q[4];
         unpack4(pk, q);  // the bf16 values actually stored (what backward re-reads)
@@ -512,7 +512,7 @@ __device__ __forceinline__ void dgrad_body(
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 320; i += 256)
-      w1slab[(long)bx * 320 + i] = ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i];
+      st_wt(w1slab + (long)bx * 320 + i, ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i]);
   }
   DDP_STAMP(STAMP_K_DGRAD, 4);
 }
@@ -673,8 +673,8 @@ __device__ __forceinline__ void wgrad_body(
     for (int r = 0; r < 4; ++r) {
       const int co = coT + 16 * c + 4 * g + r;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) out[((long)co * 9 + tap) * Cin + ciT + i16] = acc[c][tap][r];
-      if (ciT == 0 && i16 == 0) out[(long)Cout * 9 * Cin + co] = accb[c][r];
+      for (int tap = 0; tap < 9; ++tap) st_wt(out + ((long)co * 9 + tap) * Cin + ciT + i16, acc[c][tap][r]);
+      if (ciT == 0 && i16 == 0) st_wt(out + (long)Cout * 9 * Cin + co, accb[c][r]);
     }
   DDP_STAMP(STAMP_K_WGRAD, 4);
 }

@@ -171,8 +171,8 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
           dz1 = x1 > 0.f ? dz1 : 0.f;
         }
         if (active)
-          *reinterpret_cast<unsigned*>(dX + (long)b * K + col) =
-              (unsigned)f2bf(dz0) | ((unsigned)f2bf(dz1) << 16);
+          st_wt(reinterpret_cast<unsigned*>(dX + (long)b * K + col),
+                (unsigned)f2bf(dz0) | ((unsigned)f2bf(dz1) << 16));  // dZ2: write-through
       }
     }
   }
@@ -200,11 +200,11 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
       if (ex.sgd.update) {  // single-process step: dW is final -> fused SGD + shadows
         float m = ex.m_w ? ex.m_w[idx] : 0.f;
         const float pn = sgd_one(ex.p_w[idx], g, &m, ex.sgd);
-        ex.p_w[idx] = pn;
+        st_wt(ex.p_w + idx, pn);  // write-through: no dirty L2 at the kernel boundary
         if (ex.m_w) ex.m_w[idx] = m;
         const bf16_t pb = f2bf(pn);
-        if (ex.sh_plain) ex.sh_plain[idx] = pb;
-        if (ex.sh_frag) ex.sh_frag[fcfrag_index((int)idx, ex.frag_HW, ex.frag_C)] = pb;
+        if (ex.sh_plain) st_wt(ex.sh_plain + idx, pb);
+        if (ex.sh_frag) st_wt(ex.sh_frag + fcfrag_index((int)idx, ex.frag_HW, ex.frag_C), pb);
       }
     }
   }
