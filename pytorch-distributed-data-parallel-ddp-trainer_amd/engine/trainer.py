@@ -47,6 +47,7 @@ class TrainOptions:
     metrics_json: str | None = None   # append per-epoch throughput records here
     fault: tuple | None = None        # (epoch, step, rank|-1): simulate a crash there (resume tests)
     fuse_level: int | None = None     # fused engine fusion level (None: engine default)
+    comm: str = "auto"                # fused engine bucket all-reduce: auto/xgmi (direct kernel) | rccl
     grad_accum: int = 1               # micro-batches per optimizer step (module/CPU path)
     global_loss: bool = False         # log the all-reduced mean loss (module/CPU path, bug B14)
     pg_timeout_s: float | None = None
@@ -105,8 +106,9 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
     if fused:
         from .fused_step import EngineOptions, FusedSimpleCNNEngine
 
-        comm = native_comm() if world_size > 1 else None
-        eo = EngineOptions(graph_steps=opts.graph_steps, bucket_cap_mb=opts.bucket_cap_mb)
+        comm = native_comm() if world_size > 1 and dist.get_backend() == "nccl" else None
+        eo = EngineOptions(graph_steps=opts.graph_steps, bucket_cap_mb=opts.bucket_cap_mb,
+                           comm=opts.comm)
         if opts.fuse_level is not None:
             eo.fuse_level = opts.fuse_level
         engine = FusedSimpleCNNEngine(model, opt, ddata, batch_size, world_size, rank, comm, eo)

@@ -46,7 +46,11 @@ def parse_args(argv=None):
     p.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch (module/CPU path)")
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
     p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1],
-                   help="fused engine: 0 = 8 kernels/step, 1 = 6 kernels/step (default: engine default)")
+                   help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
+                        "1 = 4 kernels/step (default)")
+    p.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
+                   help="fused engine bucket all-reduce at world size > 1: direct xGMI kernel "
+                        "(RCCL fallback) or RCCL")
     p.add_argument("--grad_accum", type=int, default=1,
                    help="micro-batches per optimizer step (module/CPU path; DDP no_sync)")
     p.add_argument("--global_loss", action="store_true",
@@ -68,6 +72,7 @@ def main(argv=None):
                         max_steps=a.max_steps, metrics_json=a.metrics_json,
                         fuse_level=a.fuse_level, grad_accum=a.grad_accum,
                         global_loss=a.global_loss, pg_timeout_s=a.pg_timeout_min * 60.0,
+                        comm=a.comm,
                         fault=tuple(int(v) for v in a.fault_at.split(":")) if a.fault_at else None)
     launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
 
