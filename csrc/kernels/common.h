@@ -252,9 +252,10 @@ __device__ __forceinline__ float wave_max(float v) {
 // Phase 0: thread b < B requests its row's label (a dependent step -> index -> label
 // chain) before anything else.  Phase 1: one thread per logit (b, o) loads its <= 16
 // block partials (clamped block index, masked) and adds the bias -> s_lg[b][o] (LDS
-// scratch, B*NO floats).  Phase 2: one thread per row does max / sum-exp / the label's
-// logit serially over the NO classes.  Writes dl[b*NO + o] = (softmax - onehot) * gscale
-// and loss[b] = logsumexp - x[label].  Contains a __syncthreads(): every thread of the
+// scratch, B*NO floats; the prefetched labels go to s_lab, B ints).  Phase 2: one thread
+// per logit again; each evaluates its row's max / sum-exp serially over the NO classes
+// (same order in every thread of the row, so bit-identical) and then its own class.
+// Writes dl[b*NO + o] = (softmax - onehot) * gscale and loss[b] = logsumexp - x[label].  Contains a __syncthreads(): every thread of the
 // block must call it; dl / loss may be LDS or global, and the caller syncs before
 // reading them.  Used by xent_rows (own kernel) and by the XENT prologue of fc_bwd, so
 // both produce bit-identical values.
@@ -262,7 +263,8 @@ constexpr int XENT_MAX_BLK = 16;  // conv blocks per image: HW / CH + 2 <= 16
 __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part, int HW, int CH,
                                                  const float* __restrict__ bias, int NO, int B,
                                                  const int* __restrict__ labels32, const BatchIdx& bi,
-                                                 float gscale, float* dl, float* loss, float* s_lg) {
+                                                 float gscale, float* dl, float* loss, float* s_lg,
+                                                 int* s_lab) {
   const int base = bi.base();
   const int lab0 = (int)threadIdx.x < B ? labels32[bi.row(threadIdx.x, base)] : 0;
   DDP_STAMP(STAMP_K_XENT, 1);  // label load issued
@@ -288,20 +290,23 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
     s_lg[t] = bias[o] + a;
   }
   DDP_STAMP(STAMP_K_FC_BWD, 5);
+  if ((int)threadIdx.x < B) s_lab[threadIdx.x] = lab0;
   __syncthreads();
   DDP_STAMP(STAMP_K_FC_BWD, 6);
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    int label = b == (int)threadIdx.x ? lab0 : labels32[bi.row(b, base)];
+  // Phase 2, one thread per logit again: every thread of row b evaluates the row's max
+  // and sum-exp in the same serial order (bit-identical values), then its own class.
+  for (int t = threadIdx.x; t < B * NO; t += blockDim.x) {
+    const int b = t / NO, o = t - (t / NO) * NO;
+    int label = (int)threadIdx.x < B && b < (int)blockDim.x ? s_lab[b] : labels32[bi.row(b, base)];
     label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
     const float* x = s_lg + b * NO;
     float mx = x[0];
-    for (int o = 1; o < NO; ++o) mx = fmaxf(mx, x[o]);
+    for (int k = 1; k < NO; ++k) mx = fmaxf(mx, x[k]);
     float se = 0.f;
-    for (int o = 0; o < NO; ++o) se += __expf(x[o] - mx);
+    for (int k = 0; k < NO; ++k) se += __expf(x[k] - mx);
     const float inv = 1.f / se;
-    for (int o = 0; o < NO; ++o)
-      dl[b * NO + o] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
-    loss[b] = mx + __logf(se) - x[label];
+    dl[t] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
+    if (o == 0) loss[b] = mx + __logf(se) - x[label];
   }
   DDP_STAMP(STAMP_K_FC_BWD, 7);
 }

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
   float* s_dl = smem;            // [B][NO]
   float* s_loss = s_dl + B * NO;  // [B]
   float* s_lg = s_loss + B;       // [B][NO] cross-entropy scratch (XENT)
-  float* s_red = smem + (((XENT ? 2 * B * NO : B * NO) + B + 3) & ~3);  // [WPB][NOT][COLS]
+  int* s_lab = reinterpret_cast<int*>(s_lg + B * NO);  // [B] labels (XENT)
+  float* s_red = smem + (((XENT ? 2 * B * NO + B : B * NO) + B + 3) & ~3);  // [WPB][NOT][COLS]
 
   const long col = (long)blockIdx.x * FCB_COLS + 2 * lane;
   const bool active = col < K;  // host guarantees K % 2 == 0
@@ -109,10 +110,27 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
     const int b = min(wave + WPB * u, B - 1);
     xr[u] = *reinterpret_cast<const unsigned*>(X + (long)b * K + cc);
   }
+  // fused-SGD operands of this thread's dW outputs (final loop below): requested now so
+  // the optimizer tail has no dependent global round trip
+  constexpr int PRE = (NOT * FCB_COLS + WPB * 64 - 1) / (WPB * 64);
+  float pre_p[PRE], pre_m[PRE];
+  if (ex.sgd.update) {
+#pragma unroll
+    for (int j = 0; j < PRE; ++j) {
+      const int i = threadIdx.x + j * WPB * 64;
+      const int o = i / FCB_COLS, c = i - (i / FCB_COLS) * FCB_COLS;
+      const long k = (long)blockIdx.x * FCB_COLS + c;
+      const bool ok = i < NO * FCB_COLS && k < K;
+      const long idx = ok ? (long)o * K + k : 0;
+      pre_p[j] = ex.p_w[idx];
+      pre_m[j] = ex.m_w ? ex.m_w[idx] : 0.f;
+    }
+  }
   DDP_STAMP(STAMP_K_XENT, 0);  // loads of W / X issued
   // ---- prologue: dL of the whole batch into LDS
   if (XENT) {
-    xent_batch_block(ex.part, ex.HW, ex.CH, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_dl, s_loss, s_lg);
+    xent_batch_block(ex.part, ex.HW, ex.CH, ex.fc_bias, NO, B, ex.labels32, ex.bi, ex.gscale, s_dl,
+                     s_loss, s_lg, s_lab);
   } else {
     for (int i = threadIdx.x; i < B * NO; i += WPB * 64) s_dl[i] = dL[i];
   }
@@ -184,7 +202,10 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
       *reinterpret_cast<float2*>(s_red + (wave * NOT + o) * FCB_COLS + 2 * lane) = make_float2(dw0[o], dw1[o]);
   __syncthreads();
   DDP_STAMP(STAMP_K_FC_BWD, 3);
-  for (int i = threadIdx.x; i < NO * FCB_COLS; i += WPB * 64) {
+#pragma unroll
+  for (int jj = 0; jj < PRE; ++jj) {
+    const int i = threadIdx.x + jj * WPB * 64;
+    if (i >= NO * FCB_COLS) break;
     const int o = i / FCB_COLS, c = i - (i / FCB_COLS) * FCB_COLS;
     const long k = (long)blockIdx.x * FCB_COLS + c;
     if (k < K) {
@@ -198,8 +219,8 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
         else dW[idx] = g;
       }
       if (ex.sgd.update) {  // single-process step: dW is final -> fused SGD + shadows
-        float m = ex.m_w ? ex.m_w[idx] : 0.f;
-        const float pn = sgd_one(ex.p_w[idx], g, &m, ex.sgd);
+        float m = pre_m[jj];
+        const float pn = sgd_one(pre_p[jj], g, &m, ex.sgd);
         st_wt(ex.p_w + idx, pn);  // write-through: no dirty L2 at the kernel boundary
         if (ex.m_w) ex.m_w[idx] = m;
         const bf16_t pb = f2bf(pn);
@@ -228,7 +249,7 @@ constexpr int FCB_WPB = 8;  // waves per fc_bwd block
 
 size_t fc_bwd_lds(int B, int NO, bool xent) {
   const int NOT = NO == 10 ? 10 : FC_MAXO;
-  const size_t head = (((size_t)(xent ? 2 * B * NO : B * NO) + B + 3) & ~(size_t)3);
+  const size_t head = (((size_t)(xent ? 2 * B * NO + B : B * NO) + B + 3) & ~(size_t)3);
   return sizeof(float) * (head + (size_t)FCB_WPB * NOT * FCB_COLS);
 }
 

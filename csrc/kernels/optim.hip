@@ -115,6 +115,12 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
     i -= padded;
   }
   const bool live = k < ss.count && i < ss.s[k].n;
+  // fused-SGD operands first (same round trip as the slab loads)
+  float p0 = 0.f, m0 = 0.f;
+  if (ss.sgd.update && live && grp == 0 && ss.s[k].p) {
+    p0 = ss.s[k].p[i];
+    m0 = ss.s[k].m ? ss.s[k].m[i] : 0.f;
+  }
   float acc = 0.f;
   if (live) {
     const SlabSeg& sg = ss.s[k];
@@ -137,8 +143,8 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
     if (ss.sys_store) st_sys(sg.dst + i, g);
     else sg.dst[i] = g;
     if (ss.sgd.update && sg.p) {  // single-process step: the gradient is final -> fused SGD
-      float m = sg.m ? sg.m[i] : 0.f;
-      const float pn = sgd_one(sg.p[i], g, &m, ss.sgd);
+      float m = m0;
+      const float pn = sgd_one(p0, g, &m, ss.sgd);
       sg.p[i] = pn;
       if (sg.m) sg.m[i] = m;
       if (sg.sh) sg.sh[i] = f2bf(pn);

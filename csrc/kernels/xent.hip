@@ -101,15 +101,16 @@ __global__ __launch_bounds__(1024) void xent_rows_kernel(const float* __restrict
                                                         BatchIdx bi, float* __restrict__ dlogits,
                                                         float* __restrict__ loss_rows,
                                                         float gscale) {
-  extern __shared__ float s_lg[];
-  xent_batch_block(part, HW, CH, bias, NO, B, labels32, bi, gscale, dlogits, loss_rows, s_lg);
+  extern __shared__ float s_lg[];  // [B][NO] logits, then [B] labels
+  xent_batch_block(part, HW, CH, bias, NO, B, labels32, bi, gscale, dlogits, loss_rows, s_lg,
+                   reinterpret_cast<int*>(s_lg + B * NO));
 }
 
 void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int B,
                const int* labels32, BatchIdx bi, float* dlogits, float* loss_rows, float gscale,
                hipStream_t s) {
   const int threads = B * NO <= 256 ? 256 : (B * NO <= 512 ? 512 : 1024);
-  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(threads), sizeof(float) * B * NO, s, part, HW, CH,
+  hipLaunchKernelGGL(xent_rows_kernel, dim3(1), dim3(threads), sizeof(float) * B * (NO + 1), s, part, HW, CH,
                      bias, NO, B, labels32, bi, dlogits, loss_rows, gscale);
 }
 
