@@ -356,10 +356,12 @@ __device__ __forceinline__ void dgrad_body(
             return v;
           },
           [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * 8; *reinterpret_cast<bf16x8*>(sDY + r * DS + c) = v; });
+  DDP_STAMP(STAMP_K_CONV1, 0);  // stage2 done (weights + dY in LDS, own waves)
   if (FUSE_W1) {
     if ((int)threadIdx.x < XR) sx0[threadIdx.x] = x0_pre;
     for (int r = threadIdx.x + 256; r < XR; r += 256) sx0[r] = x0_at(r);
   }
+  DDP_STAMP(STAMP_K_CONV1, 1);  // x0 staged
   if (A1X) {
     // ReLU-input mask of the block's own pixels: bit j of s_m1[lp*4 + g] = (a1[lp][8g+j] > 0),
     // a1 recomputed from conv1 exactly as stored (bf16-rounded), channel group wave-uniform
@@ -384,6 +386,7 @@ __device__ __forceinline__ void dgrad_body(
       }
       s_m1[lp * 4 + g] = (unsigned char)m;
     }
+    DDP_STAMP(STAMP_K_CONV1, 2);  // mask computed
   }
 
   const int kofs = 8 * (lane >> 4);

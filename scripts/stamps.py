@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 NAMES = {0: "conv3x3_fwd", 1: "fc_bwd", 2: "conv3x3_dgrad", 3: "conv3x3_wgrad",
-         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "conv1"}
+         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging"}
 
 
 def main():
