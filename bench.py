@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
+    ap.add_argument("--store_a1", type=int, default=None, choices=[0, 1, 2],
+                    help="fused engine: conv1 output for the backward recomputed (0) / stored for dgrad (1) / for both (2)")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="bucket all-reduce at N>1: direct xGMI kernel (RCCL fallback) or RCCL")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -112,7 +114,7 @@ def main():
     k = args.graph_steps or graph_chunk(args.steps)
     eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph)
     eo.comm = args.comm
-    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows"):
+    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1"):
         if getattr(args, f) is not None:
             setattr(eo, f, getattr(args, f))
     eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
@@ -175,7 +177,8 @@ def main():
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
                        "graph_steps": k, "fuse_level": eo.fuse_level,
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
-                                  "wgrad_rows": eng.wgrad_rows}, "params_finite": finite,
+                                  "wgrad_rows": eng.wgrad_rows, "store_a1": eo.store_a1},
+                       "params_finite": finite,
                        "bucket_allreduce": eng.comm_kind, "params_identical_across_ranks": same},
         }), flush=True)
     if ws > 1:

@@ -669,6 +669,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.force_allreduce = cfgd.contains("force_allreduce") ? cfgd["force_allreduce"].cast<bool>() : false;
              c.fuse_level = cfgd.contains("fuse_level") ? cfgd["fuse_level"].cast<int>() : 0;
              c.fuse_opt = cfgd.contains("fuse_opt") ? (int)cfgd["fuse_opt"].cast<bool>() : 1;
+             c.store_a1 = cfgd.contains("store_a1") ? cfgd["store_a1"].cast<int>() : 0;
+             TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");
              TORCH_CHECK(c.fuse_level == 0 || c.fuse_level == 1, "engine: fuse_level must be 0 or 1");
              TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0) <= 160 * 1024 &&
                              conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0) <= 160 * 1024 &&

@@ -200,6 +200,17 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   }
   __syncthreads();
   DDP_STAMP(STAMP_K_CONV_FWD, 2);
+  if (A1X && c1.a1_out) {
+    // the block's own a1 rows (LDS rows W+1 .. W+CH) -> a1_out, 16 bytes per thread-step
+    const int xc8 = Cin / 8;
+    for (int i = threadIdx.x; i < CH * xc8; i += NT) {
+      const int lp = i / xc8, c = (i - lp * xc8) * 8;
+      const long P = P0 + lp;
+      if (P < Ptot)
+        *reinterpret_cast<bf16x8*>(c1.a1_out + P * Cin + c) =
+            *reinterpret_cast<const bf16x8*>(sX + (lp + W + 1) * XS + c);
+    }
+  }
 
   f32x4 acc[PXT][4];
 #pragma unroll
@@ -698,18 +709,23 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // independent; one launch saves a dependent kernel boundary and lets the wgrad blocks
 // fill the CUs the dgrad grid leaves idle (2 blocks per CU: <= 256 VGPR+AGPR per lane).
 // Block-uniform role branch.
-template <int PXT, int GH, int GW, int GCI, int GCO>
+// DA1X / WA1X: the dgrad / wgrad role recomputes a1 = relu(conv1(x)) from the compact
+// uint8 batch; otherwise it reads the a1 the forward stored (Xact).  Measured: the dgrad
+// role only needs a1's ReLU mask of its own pixels and gets ~2 us faster reading it; the
+// wgrad role needs full a1 tiles with halo and is as fast recomputing as loading.
+template <int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO>
 __global__ __launch_bounds__(256, 2) void conv3x3_bwd_kernel(
     const bf16_t* __restrict__ dY, const bf16_t* __restrict__ WT, bf16_t* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
-    int R, int nd, C1Src c1) {
+    int R, int nd, C1Src c1, const bf16_t* __restrict__ Xact) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < nd)
-    dgrad_body<PXT, false, true, true, true, GH, GW, GCI, GCO>(
-        dY, nullptr, WT, nullptr, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, blockIdx.x, 0);
+    dgrad_body<PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
+        dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem,
+        blockIdx.x, 0);
   else
-    wgrad_body<false, true, GH, GW, GCI, GCO>(dY, nullptr, nullptr, slab, B, H, W, Cin, Cout, R, c1,
-                                             smem, blockIdx.x - nd, 0);
+    wgrad_body<false, WA1X, GH, GW, GCI, GCO>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H, W, Cin,
+                                              Cout, R, c1, smem, blockIdx.x - nd, 0);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -835,19 +851,23 @@ size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R) {
 }
 
 void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
-                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, hipStream_t s) {
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
+                 bool wgrad_load_a1, hipStream_t s) {
   const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = conv3x3_wgrad_blocks(B, H, R);
   const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R);
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
-#define LBW(PX)                                                                                     \
-  do {                                                                                              \
-    if (g) hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, 28, 28, 32, 64>), dim3(nd + nw), dim3(256), lds, \
-                              s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1);          \
-    else hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, 0, 0, 0, 0>), dim3(nd + nw), dim3(256), lds, s, \
-                            dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1);               \
+#define LBW(PX, DA, WA)                                                                                     \
+  do {                                                                                                      \
+    if (g) hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, DA, WA, 28, 28, 32, 64>), dim3(nd + nw), dim3(256),   \
+                              lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1, Xact);       \
+    else hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, DA, WA, 0, 0, 0, 0>), dim3(nd + nw), dim3(256), lds, s, \
+                            dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1, Xact);                 \
   } while (0)
-  if (pxt == 2) LBW(2); else LBW(1);
+  // Xact given: the dgrad role reads it; the wgrad role reads it only if wgrad_load_a1
+  if (!Xact) { if (pxt == 2) LBW(2, true, true); else LBW(1, true, true); }
+  else if (wgrad_load_a1) { if (pxt == 2) LBW(2, false, false); else LBW(1, false, false); }
+  else { if (pxt == 2) LBW(2, false, true); else LBW(1, false, true); }
 #undef LBW
 }
 

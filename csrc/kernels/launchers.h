@@ -28,8 +28,11 @@ void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // fused level-1 conv backward (dgrad + conv1 wgrad slabs, and conv2 wgrad slabs) in one
 // launch; Cin == 32 (conv1's channels), (Cout / 32) * (Cin / 16) == 4
+// Xact != null: the dgrad role reads the forward's stored a1 (C1Src::a1_out) for its ReLU
+// mask instead of recomputing conv1; the wgrad role too when wgrad_load_a1
 void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
-                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, hipStream_t s);
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
+                 bool wgrad_load_a1, hipStream_t s);
 size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false);

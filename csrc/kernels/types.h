@@ -45,6 +45,9 @@ struct C1Src {
   unsigned char* xb_out = nullptr;
   int* yb_out = nullptr;
   const int* labels = nullptr;
+  // conv3x3_fwd only (optional): also store the recomputed a1 of the block's own pixels
+  // (NHWC bf16, [B*H*W][Cin]) so the backward reads it instead of recomputing conv1
+  bf16_t* a1_out = nullptr;
 };
 
 // torch.optim.SGD hyper-parameters of one step (first_step: momentum buffer init;

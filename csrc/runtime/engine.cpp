@@ -99,6 +99,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   c1.xb_out = b_.xb;
   c1.yb_out = b_.yb;
   c1.labels = b_.labels;
+  if (cfg_.store_a1) c1.a1_out = b_.a1;
   const C1Src* pc1 = f1 ? &c1 : nullptr;
   BatchIdx bid{nullptr, nullptr, 0, 0};
   bid.n_rows = B;
@@ -172,7 +173,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   if (f1) {
     // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
     conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
-                cfg_.wgrad_rows, c1b, cs_);
+                cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_);
   } else {
     conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
                   b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);

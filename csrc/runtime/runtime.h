@@ -178,6 +178,10 @@ struct EngineConfig {
   // 1: single-process steps apply SGD in the epilogues of fc_bwd / grad_reduce (no
   //    separate optimizer kernel); 0: always the flat SGD kernel (equivalence tests)
   int fuse_opt = 1;
+  // level 1: 0 = the conv backward recomputes conv1 from the compact batch; 1 = the
+  // forward also stores a1 (own pixels) and the dgrad role reads its ReLU mask from it;
+  // 2 = the wgrad role reads a1 tiles too
+  int store_a1 = 0;
 };
 
 class SimpleCNNEngine {

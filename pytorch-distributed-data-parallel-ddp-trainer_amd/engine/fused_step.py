@@ -44,6 +44,10 @@ class EngineOptions:
     fuse_level: int = 1
     # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
     fuse_opt: bool = True
+    # level 1: 0 = the conv backward recomputes conv1 from the compact uint8 batch;
+    # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
+    # wgrad role reads a1 tiles too
+    store_a1: int = 0
     # bucket all-reduce data plane at world size > 1: "xgmi" = the direct two-shot kernel
     # (falls back to RCCL when its self-test fails), "rccl" = RCCL, "auto" = xgmi
     comm: str = "auto"
@@ -103,7 +107,8 @@ class FusedSimpleCNNEngine:
                    dampening=float(g["dampening"]), weight_decay=float(g["weight_decay"]),
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
-                   fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt))
+                   fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
+                   store_a1=int(self.opts.store_a1))
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
         if use_comm and self.opts.comm in ("auto", "xgmi"):

@@ -9,7 +9,7 @@ dev = "cuda"
 
 
 def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentum=0.0,
-           fuse_level=0, fuse_opt=True, weight_decay=0.0):
+           fuse_level=0, fuse_opt=True, weight_decay=0.0, store_a1=True):
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
     from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
     from ddp_amd.models import SimpleCNN
@@ -22,7 +22,8 @@ def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentu
     data = DeviceMNIST(imgs, labels, dev)
     eng = FusedSimpleCNNEngine(model, opt, data, B, 1, 0,
                                opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph,
-                                                  fuse_level=fuse_level, fuse_opt=fuse_opt))
+                                                  fuse_level=fuse_level, fuse_opt=fuse_opt,
+                                                  store_a1=store_a1))
     eng.refresh()
     return model, opt, data, eng, imgs, labels
 
@@ -90,6 +91,19 @@ def test_fused_optimizer_bitwise_equals_sgd_kernel(momentum, wd):
     for k in ("w2_bf16", "w2t_bf16", "wfc_bf16", "wfc_frag"):
         assert torch.equal(e1.t[k], e2.t[k]), k
     assert torch.equal(e1.t["step_ctr"], e2.t["step_ctr"])
+
+
+@pytest.mark.parametrize("store_a1", [1, 2])
+def test_stored_a1_bitwise_equals_recomputed_a1(store_a1):
+    """Level 1 either stores a1 in the forward for the conv backward or recomputes conv1
+    there from the compact batch; both must give the same parameters bit for bit."""
+    m1, _, _, e1, _, _ = _setup(use_graph=True, fuse_level=1, store_a1=store_a1, momentum=0.9)
+    m2, _, _, e2, _, _ = _setup(use_graph=True, fuse_level=1, store_a1=0, momentum=0.9)
+    e1.run_steps(11)
+    e2.run_steps(11)
+    e1.synchronize(); e2.synchronize()
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
 
 
 def test_fuse_level1_one_step_matches_bf16_reference():
