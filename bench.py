@@ -179,7 +179,8 @@ def main():
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
                                   "wgrad_rows": eng.wgrad_rows, "store_a1": eo.store_a1},
                        "params_finite": finite,
-                       "bucket_allreduce": eng.comm_kind, "params_identical_across_ranks": same},
+                       "bucket_allreduce": eng.comm_kind, "params_identical_across_ranks": same,
+                       "allreduce_pair_us": eng.allreduce_us},
         }), flush=True)
     if ws > 1:
         barrier()

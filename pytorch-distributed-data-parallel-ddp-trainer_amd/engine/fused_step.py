@@ -111,10 +111,17 @@ class FusedSimpleCNNEngine:
                    store_a1=int(self.opts.store_a1))
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
+        self.allreduce_us = None
         if use_comm and self.opts.comm in ("auto", "xgmi"):
-            from ..parallel.xgmi import create_xgmi
+            from ..parallel.xgmi import create_xgmi, pick_data_plane
 
             self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size)
+            if self.xgmi is not None and comm is not None and self.opts.comm == "auto":
+                # both data planes work here: measure one step's bucket all-reduces with
+                # each on this node and keep the faster (rank 0 decides for everyone)
+                use_x, self.allreduce_us = pick_data_plane(self.xgmi, comm, fs.grads, ranges, rank)
+                if not use_x:
+                    self.xgmi = None
         if use_comm and self.xgmi is None and comm is None:
             raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
         self.comm_kind = "xgmi" if self.xgmi is not None else ("rccl" if use_comm else "none")

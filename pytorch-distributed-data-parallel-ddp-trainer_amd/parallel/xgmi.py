@@ -85,3 +85,43 @@ def _self_test(x, grads, buckets, rank, world) -> bool:
     finally:
         grads.copy_(saved)
         torch.cuda.current_stream().synchronize()
+
+
+def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int = 30, store=None):
+    """Time the engine's two bucket all-reduces over the xGMI kernel and over RCCL on
+    this node (``iters`` back-to-back pairs each, after a warm-up); returns
+    ``(use_xgmi, {"xgmi": us, "rccl": us})`` with rank 0's measurement and decision
+    broadcast through the store, so every rank picks the same data plane.  The
+    gradient buffer's contents are clobbered (the engine rewrites every bucket each step)."""
+    store = store or dist.distributed_c10d._get_default_store()
+    gen = next(_gen)
+    views = [grads[off:off + n] for off, n in buckets]
+
+    def t_xgmi():
+        for ch in range(len(buckets)):
+            x.all_reduce(ch)
+
+    def t_rccl():
+        for v in views:
+            comm.all_reduce(v)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1000.0 / iters
+
+    tx = timed(t_xgmi)
+    tr = timed(t_rccl)
+    ok = x.error_flags() == 0
+    key = f"ddp_amd/xgmi/pick/{gen}"
+    if rank == 0:
+        store.set(key, f"{int(ok and tx <= tr)} {tx:.2f} {tr:.2f}".encode())
+    use, a, b = store.get(key).decode().split()
+    return use == "1", {"xgmi": float(a), "rccl": float(b)}
