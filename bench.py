@@ -214,12 +214,26 @@ def bench_resnet(args):
     xs = [to_nhwc4(torch.randn(B, 3, S, S, device=dev, generator=g)) for _ in range(pool)]
     ys = [torch.randint(0, 1000, (B,), device=dev, generator=g) for _ in range(pool)]
 
-    def step(i):
+    def train_step(x, y):
         opt.zero_grad()
-        loss = lossf(ddp(xs[i % pool]), ys[i % pool])
+        loss = lossf(ddp(x), y)
         loss.backward()
         opt.step()
         return loss
+
+    if not args.no_graph:
+        # whole-step hipGraph (engine/graph_step.py); its capture warm-up steps are
+        # part of the untimed warm-up
+        from ddp_amd.engine import GraphedStep
+
+        nwarm = max(1, min(3, args.warmup))
+        graphed = GraphedStep(train_step, (xs[0], ys[0]), warmup=nwarm)
+
+        def step(i):
+            return graphed(xs[i % pool], ys[i % pool])
+    else:
+        def step(i):
+            return train_step(xs[i % pool], ys[i % pool])
 
     for i in range(args.warmup):
         step(i)
@@ -249,7 +263,8 @@ def bench_resnet(args):
             "data": f"synthetic (3x{S}x{S} gaussian images, random labels, random-init weights)",
             "config": {"model": f"ResNet-18 ({param_count(model):,} params)", "global_batch": ws * B,
                        "per_rank_batch": B, "seq_len": None, "parallelism": f"dp{ws}",
-                       "engine": "module path (HIP autograd + native reducer)",
+                       "engine": "module path (HIP autograd + native reducer)"
+                                 + (", eager" if args.no_graph else ", whole step in one hipGraph"),
                        "loss": round(float(loss.item()), 4)},
         }), flush=True)
     dist.destroy_process_group()

@@ -279,33 +279,67 @@ ConvGeom geom_of(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, i
   return g;
 }
 
+ConvPlan plan_of(const ConvGeom& g, bool dgrad, int bp, int bc, int splits) {
+  TORCH_CHECK(bp == 0 || bp == 64 || bp == 128, "conv_gemm: pixel tile 64 or 128");
+  TORCH_CHECK(bc == 0 || bc == 64 || bc == 128, "conv_gemm: channel tile 64 or 128");
+  const int C = dgrad ? g.Cin : g.Cout;
+  TORCH_CHECK(bc == 0 || C % bc == 0, "conv_gemm: channel tile must divide the channels");
+  return conv_gemm_plan(g, dgrad, bp, bc, splits);
+}
+
+// (bp, bc, splits, stat_rows) of the plan; for dgrad X = dX-shaped layer input, Y = dY
+py::tuple op_conv_gemm_plan(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, int pad,
+                            bool dgrad, int bp, int bc, int splits) {
+  const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
+  const ConvPlan pl = plan_of(g, dgrad, bp, bc, splits);
+  return py::make_tuple(pl.bp, pl.bc, pl.splits, dgrad ? 0 : conv_gemm_stat_rows(g, pl));
+}
+
 void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> bias, Tensor& Y,
-                      int KH, int KW, int stride, int pad, bool relu, std::optional<Tensor> stats) {
+                      int KH, int KW, int stride, int pad, bool relu, std::optional<Tensor> stats,
+                      std::optional<Tensor> part, int bp, int bc, int splits) {
   check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(Y, "Y", at::kBFloat16);
   const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
-  TORCH_CHECK(g.Cin % 32 == 0 || (g.Cin == 4 && g.Cout == 64), "conv_gemm: Cin % 32 (or stem Cin=4, Cout=64)");
+  TORCH_CHECK(g.Cin % 32 == 0 || (g.Cin == 4 && g.Cout % 64 == 0), "conv_gemm: Cin % 32 (or stem Cin=4)");
   TORCH_CHECK(g.Cout % 64 == 0, "conv_gemm: Cout % 64");
   TORCH_CHECK(Wt.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm: weight shape");
-  const float* bp = nullptr;
-  if (bias) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == g.Cout, "bias"); bp = bias->data_ptr<float>(); }
+  const float* bp_ = nullptr;
+  if (bias) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == g.Cout, "bias"); bp_ = bias->data_ptr<float>(); }
+  ConvPlan pl = plan_of(g, false, bp, bc, (bias || relu) ? 1 : splits);
   float* st = nullptr;
   if (stats) {
     check(*stats, "stats", at::kFloat);
-    TORCH_CHECK(stats->numel() >= (long)conv_gemm_fwd_blocks(g) * 2 * g.Cout, "stats slab too small");
+    TORCH_CHECK(stats->numel() >= (long)conv_gemm_stat_rows(g, pl) * 2 * g.Cout, "stats slab too small");
     st = stats->data_ptr<float>();
   }
-  conv_gemm_fwd(g, cbf(X), cbf(Wt), bp, bf(Y), relu, st, cur_stream());
+  float* pt = nullptr;
+  if (pl.splits > 1) {
+    TORCH_CHECK(part.has_value(), "conv_gemm_fwd: split plan needs the fp32 `part` workspace");
+    check(*part, "part", at::kFloat);
+    TORCH_CHECK(part->numel() >= (long)pl.splits * g.N * g.OH * g.OW * g.Cout, "part workspace too small");
+    pt = part->data_ptr<float>();
+  }
+  conv_gemm_fwd(g, pl, cbf(X), cbf(Wt), bp_, bf(Y), relu, st, pt, cur_stream());
   kcheck();
 }
 
-void op_conv_gemm_dgrad(const Tensor& dY, const Tensor& WT, std::optional<Tensor> Xact, Tensor& dX,
-                        int KH, int KW, int stride, int pad) {
-  check(dY, "dY", at::kBFloat16); check(WT, "WT", at::kBFloat16); check(dX, "dX", at::kBFloat16);
+void op_conv_gemm_dgrad(const Tensor& dY, const Tensor& W, std::optional<Tensor> Xact, Tensor& dX,
+                        int KH, int KW, int stride, int pad, std::optional<Tensor> part, int bp, int bc,
+                        int splits) {
+  check(dY, "dY", at::kBFloat16); check(W, "W", at::kBFloat16); check(dX, "dX", at::kBFloat16);
   const ConvGeom g = geom_of(dX, dY, KH, KW, stride, pad);
   TORCH_CHECK(g.Cin % 64 == 0 && g.Cout % 32 == 0, "conv_gemm_dgrad: Cin % 64, Cout % 32");
-  TORCH_CHECK(WT.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm_dgrad: WT shape");
+  TORCH_CHECK(W.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm_dgrad: OHWI weight shape");
   if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
-  conv_gemm_dgrad(g, cbf(dY), cbf(WT), obf(Xact, "Xact"), bf(dX), cur_stream());
+  const ConvPlan pl = plan_of(g, true, bp, bc, splits);
+  float* pt = nullptr;
+  if (pl.splits > 1) {
+    TORCH_CHECK(part.has_value(), "conv_gemm_dgrad: split plan needs the fp32 `part` workspace");
+    check(*part, "part", at::kFloat);
+    TORCH_CHECK(part->numel() >= (long)pl.splits * g.N * g.H * g.W * g.Cin, "part workspace too small");
+    pt = part->data_ptr<float>();
+  }
+  conv_gemm_dgrad(g, pl, cbf(dY), cbf(W), obf(Xact, "Xact"), bf(dX), pt, cur_stream());
   kcheck();
 }
 
@@ -314,25 +348,31 @@ int op_conv_gemm_wgrad_chunks(const Tensor& X, const Tensor& dY, int KH, int KW,
   return conv_gemm_wgrad_chunks(geom_of(X, dY, KH, KW, stride, pad), ppc);
 }
 
-void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& slab, int KH, int KW, int stride,
-                        int pad, int ppc) {
-  check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(slab, "slab", at::kFloat);
+void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& out, int KH, int KW, int stride,
+                        int pad, int ppc, bool accum) {
+  check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(out, "out", at::kFloat);
   const ConvGeom g = geom_of(X, dY, KH, KW, stride, pad);
   TORCH_CHECK((g.Cin % 64 == 0 || g.Cin == 4) && g.Cout % 64 == 0, "conv_gemm_wgrad: Cin % 64 (or 4), Cout % 64");
   TORCH_CHECK(ppc % 32 == 0 && ppc > 0, "pixels per chunk must be a multiple of 32");
-  TORCH_CHECK(slab.numel() >= (long)conv_gemm_wgrad_chunks(g, ppc) * g.Cout * KH * KW * g.Cin, "slab too small");
-  conv_gemm_wgrad(g, cbf(dY), cbf(X), slab.data_ptr<float>(), ppc, cur_stream());
+  const long row = (long)g.Cout * KH * KW * (g.Cin == 4 ? 3 : g.Cin);
+  TORCH_CHECK(out.numel() >= (long)conv_gemm_wgrad_chunks(g, ppc) * row, "wgrad output too small");
+  conv_gemm_wgrad(g, cbf(dY), cbf(X), out.data_ptr<float>(), ppc, accum, cur_stream());
   kcheck();
 }
 
-void op_bn_finalize(const Tensor& slab, int nblk, int C, double count, double eps, double momentum,
-                    std::optional<Tensor> rmean, std::optional<Tensor> rvar, Tensor& mean, Tensor& invstd) {
+void op_bn_finalize(const Tensor& slab, int rows, int C, double count, double eps, double momentum,
+                    std::optional<Tensor> rmean, std::optional<Tensor> rvar, Tensor& mean, Tensor& invstd,
+                    std::optional<Tensor> nbt, Tensor& ws) {
   check(slab, "slab", at::kFloat); check(mean, "mean", at::kFloat); check(invstd, "invstd", at::kFloat);
-  TORCH_CHECK(slab.numel() >= (long)nblk * 2 * C && mean.numel() == C && invstd.numel() == C, "bn_finalize sizes");
+  check(ws, "ws", at::kFloat);
+  TORCH_CHECK(slab.numel() >= (long)rows * 2 * C && mean.numel() == C && invstd.numel() == C, "bn_finalize sizes");
+  TORCH_CHECK(ws.numel() >= (long)bn_finalize_groups(rows) * 2 * C, "bn_finalize: ws too small");
   float *rm = nullptr, *rv = nullptr;
   if (rmean) { check(*rmean, "running_mean", at::kFloat); check(*rvar, "running_var", at::kFloat); rm = rmean->data_ptr<float>(); rv = rvar->data_ptr<float>(); }
-  bn_finalize(slab.data_ptr<float>(), nblk, C, (float)count, (float)eps, (float)momentum, rm, rv,
-              mean.data_ptr<float>(), invstd.data_ptr<float>(), cur_stream());
+  long long* nb = nullptr;
+  if (nbt) { TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked"); nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()); }
+  bn_finalize(slab.data_ptr<float>(), rows, C, (float)count, (float)eps, (float)momentum, rm, rv,
+              mean.data_ptr<float>(), invstd.data_ptr<float>(), nb, ws.data_ptr<float>(), cur_stream());
   kcheck();
 }
 
@@ -340,7 +380,8 @@ void op_bn_apply(const Tensor& x, const Tensor& mean, const Tensor& invstd, cons
                  const Tensor& beta, std::optional<Tensor> res, bool relu, Tensor& y) {
   check(x, "x", at::kBFloat16); check(y, "y", at::kBFloat16);
   const int C = x.size(-1);
-  TORCH_CHECK(C % 8 == 0 && y.sizes() == x.sizes(), "bn_apply: C % 8, y shape");
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0 && y.sizes() == x.sizes(),
+              "bn_apply: C/8 must divide 256 (fixed channel group per thread), y shape");
   for (auto* t : {&mean, &invstd, &gamma, &beta}) { check(*t, "bn param", at::kFloat); TORCH_CHECK(t->numel() == C, "bn param size"); }
   if (res) TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
   bn_apply(cbf(x), x.numel() / C, C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
@@ -348,33 +389,29 @@ void op_bn_apply(const Tensor& x, const Tensor& mean, const Tensor& invstd, cons
   kcheck();
 }
 
-int op_bn_bwd_blocks(long P, int rows) { return bn_bwd_blocks(P, rows); }
-
-void op_bn_bwd_reduce(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
-                      const Tensor& invstd, Tensor& slab, int rows) {
-  check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(slab, "slab", at::kFloat);
+void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
+               const Tensor& invstd, const Tensor& gamma, double count, Tensor& ws, Tensor& sums,
+               std::optional<Tensor> dgamma, std::optional<Tensor> dbeta, bool accum, Tensor& dx,
+               std::optional<Tensor> dres) {
+  check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(dx, "dx", at::kBFloat16);
+  check(sums, "sums", at::kFloat); check(ws, "ws", at::kFloat);
   const int C = x.size(-1);
   const long P = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0 && C <= 2048, "bn_bwd_reduce: C");
-  TORCH_CHECK(slab.numel() >= (long)bn_bwd_blocks(P, rows) * 2 * C, "slab too small");
+  TORCH_CHECK(C % 64 == 0 && 256 % (C / 8) == 0 && dout.sizes() == x.sizes() && dx.sizes() == x.sizes(),
+              "bn_bwd: C % 64 with C/8 dividing 256, shapes");
+  TORCH_CHECK(P < (1L << 31), "bn_bwd: too many pixels");
+  TORCH_CHECK(sums.numel() == 2 * C, "bn_bwd: sums [2C]");
+  TORCH_CHECK(ws.numel() >= (long)bn_bwd_rows(P, C, nullptr) * 2 * C, "bn_bwd: ws too small");
+  for (auto* t : {&mean, &invstd, &gamma}) { check(*t, "bn param", at::kFloat); TORCH_CHECK(t->numel() == C, "bn param size"); }
   if (out) TORCH_CHECK(out->sizes() == x.sizes(), "out shape");
-  bn_bwd_reduce(cbf(dout), obf(out, "out"), cbf(x), P, C, mean.data_ptr<float>(),
-                invstd.data_ptr<float>(), slab.data_ptr<float>(), rows, cur_stream());
-  kcheck();
-}
-
-void op_bn_bwd_apply(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
-                     const Tensor& invstd, const Tensor& gamma, const Tensor& sums, double count,
-                     Tensor& dx, std::optional<Tensor> dres) {
-  check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(dx, "dx", at::kBFloat16);
-  check(sums, "sums", at::kFloat);
-  const int C = x.size(-1);
-  TORCH_CHECK(sums.numel() == 2 * C && dx.sizes() == x.sizes(), "bn_bwd_apply sizes");
+  float *dg = nullptr, *db = nullptr;
+  if (dgamma) { check(*dgamma, "dgamma", at::kFloat); TORCH_CHECK(dgamma->numel() == C, "dgamma"); dg = dgamma->data_ptr<float>(); }
+  if (dbeta) { check(*dbeta, "dbeta", at::kFloat); TORCH_CHECK(dbeta->numel() == C, "dbeta"); db = dbeta->data_ptr<float>(); }
   bf16_t* dr = nullptr;
   if (dres) { check(*dres, "dres", at::kBFloat16); TORCH_CHECK(dres->sizes() == x.sizes(), "dres"); dr = bf(*dres); }
-  bn_bwd_apply(cbf(dout), obf(out, "out"), cbf(x), x.numel() / C, C, mean.data_ptr<float>(),
-               invstd.data_ptr<float>(), gamma.data_ptr<float>(), sums.data_ptr<float>(),
-               (float)count, bf(dx), dr, cur_stream());
+  bn_bwd(cbf(dout), obf(out, "out"), cbf(x), P, C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+         gamma.data_ptr<float>(), (float)count, ws.data_ptr<float>(), sums.data_ptr<float>(), dg, db,
+         accum, bf(dx), dr, cur_stream());
   kcheck();
 }
 
@@ -383,6 +420,7 @@ void op_maxpool_fwd(const Tensor& x, Tensor& y, Tensor& amax) {
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), OH = y.size(1), OW = y.size(2);
   TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && y.size(3) == C, "maxpool 3x3/s2/p1 shape");
   TORCH_CHECK(amax.numel() == y.numel(), "amax size");
+  TORCH_CHECK(C % 8 == 0 && x.numel() / 8 < (1L << 31), "maxpool: C % 8 (8 channels per thread)");
   maxpool_fwd(cbf(x), N, H, W, C, OH, OW, bf(y), amax.data_ptr<unsigned char>(), cur_stream());
   kcheck();
 }
@@ -391,6 +429,7 @@ void op_maxpool_bwd(const Tensor& dy, const Tensor& amax, Tensor& dx) {
   check(dy, "dy", at::kBFloat16); check(dx, "dx", at::kBFloat16); check(amax, "amax", at::kByte);
   const int N = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3), OH = dy.size(1), OW = dy.size(2);
   TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && amax.numel() == dy.numel(), "maxpool bwd shape");
+  TORCH_CHECK(C % 8 == 0 && dy.size(3) == C && dx.numel() / 8 < (1L << 31), "maxpool bwd: C % 8");
   maxpool_bwd(cbf(dy), amax.data_ptr<unsigned char>(), N, H, W, C, OH, OW, bf(dx), cur_stream());
   kcheck();
 }
@@ -483,7 +522,7 @@ void op_grad_reduce(const py::list& segs) {
   SlabSet ss{};
   TORCH_CHECK(segs.size() <= 4, "at most 4 slab segments");
   for (auto item : segs) {
-    auto t = item.cast<py::tuple>();  // (slab, row_stride, src_off, n, rows, dst, scale)
+    auto t = item.cast<py::tuple>();  // (slab, row_stride, src_off, n, rows, dst, scale[, accum])
     Tensor slab = t[0].cast<Tensor>(), dst = t[5].cast<Tensor>();
     check(slab, "slab", at::kFloat);
     TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst");
@@ -492,8 +531,10 @@ void op_grad_reduce(const py::list& segs) {
     TORCH_CHECK(dst.numel() == n, "grad_reduce: dst size");
     TORCH_CHECK(rows >= 1 && so + n <= rs && (long)(rows - 1) * rs + so + n <= slab.numel(),
                 "grad_reduce: slab bounds");
-    ss.s[ss.count++] = SlabSeg{slab.data_ptr<float>(), rs, so, n, rows, dst.data_ptr<float>(),
-                               (float)t[6].cast<double>()};
+    ss.s[ss.count] = SlabSeg{slab.data_ptr<float>(), rs, so, n, rows, dst.data_ptr<float>(),
+                             (float)t[6].cast<double>()};
+    if (t.size() > 7) ss.s[ss.count].accum = t[7].cast<bool>() ? 1 : 0;
+    ++ss.count;
   }
   grad_reduce(ss, cur_stream());
   kcheck();
@@ -563,18 +604,30 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_reduce", &op_grad_reduce);
   m.def("scale_copy", &op_scale_copy);
   m.def("_mark_exiting", &ddp_amd::mark_exiting);
-  m.def("conv_gemm_fwd", &op_conv_gemm_fwd);
-  m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad);
+  m.def("conv_gemm_fwd", &op_conv_gemm_fwd, py::arg("X"), py::arg("W"), py::arg("bias"), py::arg("Y"),
+        py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("relu") = false,
+        py::arg("stats") = py::none(), py::arg("part") = py::none(), py::arg("bp") = 0, py::arg("bc") = 0,
+        py::arg("splits") = 0);
+  m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad, py::arg("dY"), py::arg("W"), py::arg("Xact"), py::arg("dX"),
+        py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(),
+        py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
-  m.def("conv_gemm_wgrad", &op_conv_gemm_wgrad);
-  m.def("conv_gemm_fwd_blocks", [](const Tensor& X, const Tensor& Y, int KH, int KW, int s, int p) {
-    return conv_gemm_fwd_blocks(geom_of(X, Y, KH, KW, s, p));
+  m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
+    return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));
   });
+  m.def("conv_gemm_wgrad_ppc", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
+    return conv_gemm_wgrad_ppc(geom_of(X, dY, KH, KW, st, pd));
+  });
+  m.def("conv_gemm_wgrad", &op_conv_gemm_wgrad, py::arg("dY"), py::arg("X"), py::arg("out"), py::arg("KH"),
+        py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("ppc"), py::arg("accum") = false);
+  m.def("conv_gemm_plan", &op_conv_gemm_plan, py::arg("X"), py::arg("Y"), py::arg("KH"), py::arg("KW"),
+        py::arg("stride"), py::arg("pad"), py::arg("dgrad") = false, py::arg("bp") = 0, py::arg("bc") = 0,
+        py::arg("splits") = 0);
   m.def("bn_finalize", &op_bn_finalize);
   m.def("bn_apply", &op_bn_apply);
-  m.def("bn_bwd_blocks", &op_bn_bwd_blocks);
-  m.def("bn_bwd_reduce", &op_bn_bwd_reduce);
-  m.def("bn_bwd_apply", &op_bn_bwd_apply);
+  m.def("bn_finalize_groups", &bn_finalize_groups);
+  m.def("bn_bwd_rows", [](long P, int C) { return bn_bwd_rows(P, C, nullptr); });
+  m.def("bn_bwd", &op_bn_bwd);
   m.def("maxpool_fwd", &op_maxpool_fwd);
   m.def("maxpool_bwd", &op_maxpool_bwd);
   m.def("avgpool_fwd", &op_avgpool_fwd);

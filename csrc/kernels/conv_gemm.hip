@@ -1,57 +1,78 @@
 // General NHWC convolution as an LDS-tiled MFMA implicit GEMM (ResNet-18 layers:
-// 3x3 s1/s2, 1x1 s2 downsample; SURVEY.md §2.4 "north-star" kernels).
+// 7x7/s2 stem, 3x3 s1/s2, 1x1 s2 downsample; SURVEY.md §2.4 "north-star" kernels).
 //
 // Forward, output channels on the MFMA rows, output pixels on the columns:
 //   D[co][p] = sum_{tap, ci} W[co][tap][ci] * X[n][oh*s - pad + kh][ow*s - pad + kw][ci]
-// K-step = one tap x 32 input channels (Cin % 32 == 0).  Block tile = BCO output
-// channels x 128 output pixels, 4 waves arranged 2 (co) x 2 (px); each wave owns
-// (BCO/2) x 64 = (BCO/32) x 4 tiles of 16x16.  Per K-step the block stages the
-// weight tile [BCO][32] and the gathered input tile [128][32] into LDS (double
-// buffered: the next K-step's global loads are issued before this step's MFMAs),
-// rows padded to 40 elements (80 B) so the 16 rows of a fragment read hit distinct
-// bank groups.
+// K-step = one tap x 32 input channels (Cin % 32 == 0).  Block tile = BC output channels
+// x BP output pixels (BP, BC in {64, 128}), 4 waves arranged 2 (co) x 2 (px).  Per K-step
+// the block stages the weight tile [BC][32] and the gathered input tile [BP][32] into
+// LDS (double buffered: the next K-step's global loads are issued before this step's
+// MFMAs), rows padded to 40 elements (80 B).
 //
-// Epilogue: bf16 NHWC store (+ optional bias / ReLU) and, when requested, per-block
-// partial per-channel sum and sum-of-squares of the stored values (the training
-// BatchNorm that follows needs exactly these; fixed-order reduction in bn_stats).
+// Filling 256 CUs: ResNet-18's deep layers have few output pixels (layer4 at batch 32:
+// 1568) and long K (4608), so a plain tiling launches ~50 blocks.  The launch plan
+// (conv_gemm_plan) picks the pixel tile and splits K over grid.z; split partials go to an
+// fp32 workspace [splits][P][C] and splitk_reduce sums them in fixed split order, then
+// does what the epilogue would have done (bf16 store, ReLU mask, BatchNorm statistics).
+//
+// Epilogue (unsplit): bf16 NHWC store (+ optional bias / ReLU) and, when requested,
+// per-block partial per-channel sum and sum-of-squares of the stored values (the
+// training BatchNorm that follows needs exactly these; fixed-order reduction in
+// bn_finalize).
+//
+// The data gradient reads the OHWI weight itself: its A operand (rows ci, K = co) is the
+// transpose of the stored layout, so the [32 co][BC ci] weight tile is staged as stored
+// and the MFMA fragments are read with ds_read_b64_tr_b16 (no transposed weight copy).
 #include "kernels/common.h"
 #include "kernels/launchers.h"
 
 namespace ddp_amd {
 
-constexpr int CG_BP = 128;  // output pixels per block
-constexpr int CG_KS = 32;   // K-step (channels of one tap)
-constexpr int CG_RS = 40;   // LDS row stride (elements)
+constexpr int CG_KS = 32;  // K-step (channels of one tap)
+constexpr int CG_RS = 40;  // LDS row stride (elements) of K-contiguous tiles
+
+// K-slot permutation of the transposed (ds_read_b64_tr_b16) fragment read: fragment
+// element j of lane group g holds k = 4g + j (j < 4) or 16 + 4g + (j - 4).  The matching
+// non-transposed operand is stored to LDS in that order, so it stays one b128 read.
+__device__ __forceinline__ int trk_pos(int k4) {  // LDS position of the 4-group starting at k = 4*k4
+  return k4 < 4 ? 8 * k4 : 8 * (k4 - 4) + 4;
+}
 
 // STEM: Cin == 4 (3 real channels + 1 zero pad); a K-step covers 8 taps x 4 channels,
 // k = tap*4 + c, so the weight row [KH*KW*4] is still contiguous per K-step.
-template <int BCO, bool RELU, bool STATS, bool STEM>
+template <int BP, int BC, bool RELU, bool STATS, bool STEM, bool PART>
 __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
                                                             const bf16_t* __restrict__ Wt,
                                                             const float* __restrict__ bias,
                                                             bf16_t* __restrict__ Y,
-                                                            float* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) bf16_t sA[2][BCO * CG_RS];
-  __shared__ __attribute__((aligned(16))) bf16_t sB[2][CG_BP * CG_RS];
+                                                            float* __restrict__ stats,
+                                                            float* __restrict__ part, int ks_per) {
+  static_assert(!STEM || (BP == 128 && !PART), "stem: 128-pixel tile, unsplit");
+  __shared__ __attribute__((aligned(16))) bf16_t sA[2][BC * CG_RS];
+  __shared__ __attribute__((aligned(16))) bf16_t sB[2][BP * CG_RS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wco = wave >> 1, wpx = wave & 1;
-  constexpr int TCO = BCO / 32;  // 16-row tiles per wave (co)
-  const long OHW = (long)g.OH * g.OW;
-  const long Ptot = (long)g.N * OHW;
-  const long p0 = (long)blockIdx.x * CG_BP;
-  const int co0 = blockIdx.y * BCO;
+  constexpr int TCO = BC / 32;  // 16-row tiles per wave (co)
+  constexpr int TPX = BP / 32;  // 16-col tiles per wave (px)
+  constexpr int TPR = 256 / BP;          // staging threads per pixel row
+  constexpr int EPT = CG_KS / TPR;       // elements per thread (16 or 8)
+  const int OHW = g.OH * g.OW;
+  const int Ptot = g.N * OHW;
+  const int p0 = blockIdx.x * BP;
+  const int co0 = blockIdx.y * BC;
   const int KWC = g.KH * g.KW * g.Cin;
   const int T = g.KH * g.KW;
   const int nk = STEM ? (T + 7) / 8 : T * (g.Cin / CG_KS);
+  const int kb = blockIdx.z * ks_per;
+  const int ke = min(nk, kb + ks_per);
 
-  // this thread's staging slots: B: 2 chunks (pixel r = tid>>1 .. , 16 B each), A: BCO*4/256 chunks
-  const int bp = tid >> 1, bh = (tid & 1) * 16;  // pixel row, element offset (two 16-B chunks)
-  const long P = p0 + bp;
+  const int bp = tid / TPR, bh = (tid % TPR) * EPT;  // pixel row, element offset
+  const int P = p0 + bp;
   const bool pv = P < Ptot;
   int n_ = 0, oh = 0, ow = 0;
   if (pv) {
-    n_ = (int)(P / OHW);
-    const int r = (int)(P - (long)n_ * OHW);
+    n_ = P / OHW;
+    const int r = P - n_ * OHW;
     oh = r / g.OW;
     ow = r - oh * g.OW;
   }
@@ -74,7 +95,7 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
         rb[h2] = __builtin_bit_cast(bf16x8, q4);
       }
 #pragma unroll
-      for (int u = 0; u < BCO * 4 / 256; ++u) {
+      for (int u = 0; u < BC * 4 / 256; ++u) {
         const int c = tid + u * 256;
         const int row = c >> 2, off = (c & 3) * 8;
         const int k = ks * CG_KS + off;
@@ -89,69 +110,86 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
     const int ih = oh * g.stride - g.pad + kh, iw = ow * g.stride - g.pad + kw;
     const bool ok = pv && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
     const bf16_t* src = X + (((long)n_ * g.H + ih) * g.W + iw) * g.Cin + ci0 + bh;
-    rb[0] = ok ? ld8(src) : zero8();
-    rb[1] = ok ? ld8(src + 8) : zero8();
+#pragma unroll
+    for (int h = 0; h < EPT / 8; ++h) rb[h] = ok ? ld8(src + 8 * h) : zero8();
     // A: weight rows
 #pragma unroll
-    for (int u = 0; u < BCO * 4 / 256; ++u) {
+    for (int u = 0; u < BC * 4 / 256; ++u) {
       const int c = tid + u * 256;
       const int row = c >> 2, off = (c & 3) * 8;
       ra[u] = ld8(Wt + (long)(co0 + row) * KWC + tap * g.Cin + ci0 + off);
     }
   };
   auto store_k = [&](int buf, const bf16x8* ra, const bf16x8* rb) {
-    *reinterpret_cast<bf16x8*>(&sB[buf][bp * CG_RS + bh]) = rb[0];
-    *reinterpret_cast<bf16x8*>(&sB[buf][bp * CG_RS + bh + 8]) = rb[1];
 #pragma unroll
-    for (int u = 0; u < BCO * 4 / 256; ++u) {
+    for (int h = 0; h < EPT / 8; ++h) *reinterpret_cast<bf16x8*>(&sB[buf][bp * CG_RS + bh + 8 * h]) = rb[h];
+#pragma unroll
+    for (int u = 0; u < BC * 4 / 256; ++u) {
       const int c = tid + u * 256;
       *reinterpret_cast<bf16x8*>(&sA[buf][(c >> 2) * CG_RS + (c & 3) * 8]) = ra[u];
     }
   };
 
-  f32x4 acc[TCO][4];
+  f32x4 acc[TCO][TPX];
 #pragma unroll
   for (int i = 0; i < TCO; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 ra[BCO * 4 / 256 > 0 ? BCO * 4 / 256 : 1], rb[2];
-  load_k(0, ra, rb);
-  store_k(0, ra, rb);
+  bf16x8 ra[BC * 4 / 256 > 0 ? BC * 4 / 256 : 1], rb[2];
+  if (kb < ke) {
+    load_k(kb, ra, rb);
+    store_k(0, ra, rb);
+  }
   __syncthreads();
   const int kofs = 8 * (lane >> 4), col = lane & 15;
-  for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    const bool more = ks + 1 < nk;
+  for (int ks = kb; ks < ke; ++ks) {
+    const int cur = (ks - kb) & 1;
+    const bool more = ks + 1 < ke;
     if (more) load_k(ks + 1, ra, rb);  // in flight during this step's MFMAs
-    bf16x8 a[TCO], b[4];
+    bf16x8 a[TCO], b[TPX];
 #pragma unroll
     for (int i = 0; i < TCO; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(wco * (BCO / 2) + 16 * i + col) * CG_RS + kofs]);
+      a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(wco * (BC / 2) + 16 * i + col) * CG_RS + kofs]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * 64 + 16 * j + col) * CG_RS + kofs]);
+    for (int j = 0; j < TPX; ++j)
+      b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * (BP / 2) + 16 * j + col) * CG_RS + kofs]);
 #pragma unroll
     for (int i = 0; i < TCO; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     if (more) store_k(cur ^ 1, ra, rb);
     __syncthreads();
   }
 
   // ---- epilogue
+  if (PART) {  // fp32 split partial [z][P][Cout]: 4 consecutive channels per lane = 16 B
+    float* dst = part + (long)blockIdx.z * Ptot * g.Cout;
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) {
+      const int Pj = p0 + wpx * (BP / 2) + 16 * j + col;
+      if (Pj >= Ptot) continue;
+#pragma unroll
+      for (int i = 0; i < TCO; ++i) {
+        const int co = co0 + wco * (BC / 2) + 16 * i + 4 * (lane >> 4);
+        *reinterpret_cast<float4*>(dst + (long)Pj * g.Cout + co) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
+  }
   float csum[TCO][4], csq[TCO][4];
 #pragma unroll
   for (int i = 0; i < TCO; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) csum[i][r] = csq[i][r] = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const long Pj = p0 + wpx * 64 + 16 * j + col;
+  for (int j = 0; j < TPX; ++j) {
+    const int Pj = p0 + wpx * (BP / 2) + 16 * j + col;
     const bool ok = Pj < Ptot;
 #pragma unroll
     for (int i = 0; i < TCO; ++i) {
-      const int co = co0 + wco * (BCO / 2) + 16 * i + 4 * (lane >> 4);
+      const int co = co0 + wco * (BC / 2) + 16 * i + 4 * (lane >> 4);
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -159,7 +197,7 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
         if (RELU) v[r] = fmaxf(v[r], 0.f);
       }
       const uint2 pk = pack4(v[0], v[1], v[2], v[3]);
-      if (ok) *reinterpret_cast<uint2*>(Y + Pj * g.Cout + co) = pk;
+      if (ok) *reinterpret_cast<uint2*>(Y + (long)Pj * g.Cout + co) = pk;
       if (STATS) {
         float q[4];
         unpack4(pk, q);
@@ -174,21 +212,21 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
   }
   if (STATS) {
     // per-block partials: reduce the 16 pixel lanes, then the two pixel-waves via LDS
-    __shared__ float s_st[2][2][BCO];
+    __shared__ float s_st[2][2][BC];
 #pragma unroll
     for (int i = 0; i < TCO; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float a = sum16(csum[i][r]), b = sum16(csq[i][r]);
         if (col == 0) {
-          const int cl = wco * (BCO / 2) + 16 * i + 4 * (lane >> 4) + r;
+          const int cl = wco * (BC / 2) + 16 * i + 4 * (lane >> 4) + r;
           s_st[wpx][0][cl] = a;
           s_st[wpx][1][cl] = b;
         }
       }
     __syncthreads();
     // stats slab: [blocks_x][2][Cout]
-    for (int c = tid; c < BCO; c += 256) {
+    for (int c = tid; c < BC; c += 256) {
       float* dst = stats + (long)blockIdx.x * 2 * g.Cout;
       dst[co0 + c] = s_st[0][0][c] + s_st[1][0][c];
       dst[g.Cout + co0 + c] = s_st[0][1][c] + s_st[1][1][c];
@@ -197,34 +235,43 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
 }
 
 // ---------------------------------------------------------------- data gradient
-// D[ci][p_in] = sum_{tap, co} WT[ci][tap][co] * dY[n][(ih + pad - kh)/s][(iw + pad - kw)/s][co]
+// D[ci][p_in] = sum_{tap, co} W[co][tap][ci] * dY[n][(ih + pad - kh)/s][(iw + pad - kw)/s][co]
 // (taps whose offset is not divisible by the stride, or fall outside dY, contribute 0).
-// WT is the [Cin][KH*KW][Cout] transpose of the OHWI weight.  Optional ReLU mask by
-// the layer input's activation (MASK_X) in the epilogue.  Block = BCI input channels x
-// 128 input pixels; K-step = one tap x 32 output channels.
-template <int BCI, bool MASK_X>
+// Optional ReLU mask by the layer input's activation (MASK_X) in the epilogue.  Block =
+// BC input channels x BP input pixels; K-step = one tap x 32 output channels.  The weight
+// tile is [32 co][BC ci] as stored (row stride BC + 16 = an odd multiple of 8 dwords:
+// conflict-free transposed reads); dY is stored in the transposed read's K order.
+template <int BP, int BC, bool MASK_X, bool PART>
 __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
-                                                              const bf16_t* __restrict__ WT,
+                                                              const bf16_t* __restrict__ W,
                                                               const bf16_t* __restrict__ Xact,
-                                                              bf16_t* __restrict__ dX) {
-  __shared__ __attribute__((aligned(16))) bf16_t sA[2][BCI * CG_RS];
-  __shared__ __attribute__((aligned(16))) bf16_t sB[2][CG_BP * CG_RS];
+                                                              bf16_t* __restrict__ dX,
+                                                              float* __restrict__ part, int ks_per) {
+  constexpr int AS = BC + 16;
+  __shared__ __attribute__((aligned(16))) bf16_t sA[2][CG_KS * AS];
+  __shared__ __attribute__((aligned(16))) bf16_t sB[2][BP * CG_RS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wci = wave >> 1, wpx = wave & 1;
-  constexpr int TCI = BCI / 32;
-  const long HW = (long)g.H * g.W;
-  const long Ptot = (long)g.N * HW;
-  const long p0 = (long)blockIdx.x * CG_BP;
-  const int ci0b = blockIdx.y * BCI;
+  constexpr int TCI = BC / 32;
+  constexpr int TPX = BP / 32;
+  constexpr int TPR = 256 / BP;
+  constexpr int EPT = CG_KS / TPR;
+  constexpr int ACH = CG_KS * BC / 8 / 256;  // 16-B weight chunks per thread
+  const int HW = g.H * g.W;
+  const int Ptot = g.N * HW;
+  const int p0 = blockIdx.x * BP;
+  const int ci0b = blockIdx.y * BC;
   const int T = g.KH * g.KW;
   const int nk = T * (g.Cout / CG_KS);
-  const int bp = tid >> 1, bh = (tid & 1) * 16;
-  const long P = p0 + bp;
+  const int kb = blockIdx.z * ks_per;
+  const int ke = min(nk, kb + ks_per);
+  const int bp = tid / TPR, bh = (tid % TPR) * EPT;
+  const int P = p0 + bp;
   const bool pv = P < Ptot;
   int n_ = 0, ih = 0, iw = 0;
   if (pv) {
-    n_ = (int)(P / HW);
-    const int r = (int)(P - (long)n_ * HW);
+    n_ = P / HW;
+    const int r = P - n_ * HW;
     ih = r / g.W;
     iw = r - ih * g.W;
   }
@@ -237,227 +284,411 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
     const bool ok = pv && th >= 0 && tw >= 0 && th - oh * g.stride == 0 && tw - ow * g.stride == 0 &&
                     oh < g.OH && ow < g.OW;
     const bf16_t* src = dY + (((long)n_ * g.OH + oh) * g.OW + ow) * g.Cout + co0 + bh;
-    rb[0] = ok ? ld8(src) : zero8();
-    rb[1] = ok ? ld8(src + 8) : zero8();
 #pragma unroll
-    for (int u = 0; u < BCI * 4 / 256; ++u) {
+    for (int h = 0; h < EPT / 8; ++h) rb[h] = ok ? ld8(src + 8 * h) : zero8();
+#pragma unroll
+    for (int u = 0; u < ACH; ++u) {
       const int c = tid + u * 256;
-      const int row = c >> 2, off = (c & 3) * 8;
-      ra[u] = ld8(WT + ((long)(ci0b + row) * T + tap) * g.Cout + co0 + off);
+      const int row = c / (BC / 8), off = (c % (BC / 8)) * 8;
+      ra[u] = ld8(W + ((long)(co0 + row) * T + tap) * g.Cin + ci0b + off);
     }
   };
   auto store_k = [&](int buf, const bf16x8* ra, const bf16x8* rb) {
-    *reinterpret_cast<bf16x8*>(&sB[buf][bp * CG_RS + bh]) = rb[0];
-    *reinterpret_cast<bf16x8*>(&sB[buf][bp * CG_RS + bh + 8]) = rb[1];
+    // dY run k = bh .. bh+EPT-1 -> 4-groups at their transposed-read positions
 #pragma unroll
-    for (int u = 0; u < BCI * 4 / 256; ++u) {
+    for (int h = 0; h < EPT / 8; ++h) {
+      const uint4 q = __builtin_bit_cast(uint4, rb[h]);
+      const int k4 = (bh + 8 * h) / 4;
+      *reinterpret_cast<uint2*>(&sB[buf][bp * CG_RS + trk_pos(k4)]) = make_uint2(q.x, q.y);
+      *reinterpret_cast<uint2*>(&sB[buf][bp * CG_RS + trk_pos(k4 + 1)]) = make_uint2(q.z, q.w);
+    }
+#pragma unroll
+    for (int u = 0; u < ACH; ++u) {
       const int c = tid + u * 256;
-      *reinterpret_cast<bf16x8*>(&sA[buf][(c >> 2) * CG_RS + (c & 3) * 8]) = ra[u];
+      const int row = c / (BC / 8), off = (c % (BC / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&sA[buf][row * AS + off]) = ra[u];
     }
   };
-  f32x4 acc[TCI][4];
+  f32x4 acc[TCI][TPX];
 #pragma unroll
   for (int i = 0; i < TCI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 ra[BCI * 4 / 256 > 0 ? BCI * 4 / 256 : 1], rb[2];
-  load_k(0, ra, rb);
-  store_k(0, ra, rb);
+    for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 ra[ACH], rb[2];
+  if (kb < ke) {
+    load_k(kb, ra, rb);
+    store_k(0, ra, rb);
+  }
   __syncthreads();
   const int kofs = 8 * (lane >> 4), col = lane & 15;
-  for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    const bool more = ks + 1 < nk;
+  const int gq = lane >> 4, q = col >> 2, pq = col & 3;
+  const int rlo = (4 * gq + q) * AS, rhi = (16 + 4 * gq + q) * AS;
+  for (int ks = kb; ks < ke; ++ks) {
+    const int cur = (ks - kb) & 1;
+    const bool more = ks + 1 < ke;
     if (more) load_k(ks + 1, ra, rb);
-    bf16x8 a[TCI], b[4];
+    bf16x8 a[TCI], b[TPX];
+#pragma unroll
+    for (int i = 0; i < TCI; ++i) {
+      const int m = wci * (BC / 2) + 16 * i + 4 * pq;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sA[cur][rlo + m]);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sA[cur][rhi + m]);
+      a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < TPX; ++j)
+      b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * (BP / 2) + 16 * j + col) * CG_RS + kofs]);
 #pragma unroll
     for (int i = 0; i < TCI; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(wci * (BCI / 2) + 16 * i + col) * CG_RS + kofs]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * 64 + 16 * j + col) * CG_RS + kofs]);
-#pragma unroll
-    for (int i = 0; i < TCI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     if (more) store_k(cur ^ 1, ra, rb);
     __syncthreads();
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const long Pj = p0 + wpx * 64 + 16 * j + col;
+  for (int j = 0; j < TPX; ++j) {
+    const int Pj = p0 + wpx * (BP / 2) + 16 * j + col;
     if (Pj >= Ptot) continue;
 #pragma unroll
     for (int i = 0; i < TCI; ++i) {
-      const int ci = ci0b + wci * (BCI / 2) + 16 * i + 4 * (lane >> 4);
+      const int ci = ci0b + wci * (BC / 2) + 16 * i + 4 * (lane >> 4);
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (PART) {
+        *reinterpret_cast<float4*>(part + ((long)blockIdx.z * Ptot + Pj) * g.Cin + ci) =
+            make_float4(v[0], v[1], v[2], v[3]);
+        continue;
+      }
       if (MASK_X) {
         float xm[4];
-        unpack4(*reinterpret_cast<const uint2*>(Xact + Pj * g.Cin + ci), xm);
+        unpack4(*reinterpret_cast<const uint2*>(Xact + (long)Pj * g.Cin + ci), xm);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = xm[r] > 0.f ? v[r] : 0.f;
       }
-      *reinterpret_cast<uint2*>(dX + Pj * g.Cin + ci) = pack4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<uint2*>(dX + (long)Pj * g.Cin + ci) = pack4(v[0], v[1], v[2], v[3]);
     }
+  }
+}
+
+// ---------------------------------------------------------------- split-K reduction
+// part [S][P][C] fp32 -> out bf16 [P][C], summed in split order 0..S-1; optional ReLU mask
+// by Xact (> 0) and optional per-block BatchNorm partials [gridDim.x][2][C] (sum, sum of
+// squares of the stored bf16 values).  Thread = 8 channels of one pixel; block = C/8
+// channel groups x 256/(C/8) pixel lanes over `rpb` pixels.
+template <bool MASK, bool STATS>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int P,
+                                                            int C, int rpb,
+                                                            const bf16_t* __restrict__ Xact,
+                                                            bf16_t* __restrict__ out,
+                                                            float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) float sred[];  // [pl][2][C]
+  const int cg = C / 8, pl = 256 / cg;
+  const int tg = threadIdx.x % cg, tp = threadIdx.x / cg;
+  const long PC = (long)P * C;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  const int p0 = blockIdx.x * rpb, p1 = min(P, p0 + rpb);
+  for (int p = p0 + tp; p < p1; p += pl) {
+    const long off = (long)p * C + tg * 8;
+    float v[8];
+    {
+      const float4 a = *reinterpret_cast<const float4*>(part + off);
+      const float4 b = *reinterpret_cast<const float4*>(part + off + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    for (int z = 1; z < S; ++z) {
+      const float4 a = *reinterpret_cast<const float4*>(part + z * PC + off);
+      const float4 b = *reinterpret_cast<const float4*>(part + z * PC + off + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    if (MASK) {
+      const uint4 xm = *reinterpret_cast<const uint4*>(Xact + off);
+      float x[8];
+      unpack4(make_uint2(xm.x, xm.y), x);
+      unpack4(make_uint2(xm.z, xm.w), x + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = x[j] > 0.f ? v[j] : 0.f;
+    }
+    const uint2 lo = pack4(v[0], v[1], v[2], v[3]), hi = pack4(v[4], v[5], v[6], v[7]);
+    *reinterpret_cast<uint4*>(out + off) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    if (STATS) {
+      float r[8];
+      unpack4(lo, r);
+      unpack4(hi, r + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += r[j];
+        q[j] = fmaf(r[j], r[j], q[j]);
+      }
+    }
+  }
+  if (!STATS) return;
+  if (tp < pl) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sred[(tp * 2) * C + tg * 8 + j] = s[j];
+      sred[(tp * 2 + 1) * C + tg * 8 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int t = 0; t < pl; ++t) {
+      a += sred[(t * 2) * C + c];
+      b += sred[(t * 2 + 1) * C + c];
+    }
+    stats[(long)blockIdx.x * 2 * C + c] = a;
+    stats[(long)blockIdx.x * 2 * C + C + c] = b;
   }
 }
 
 // ---------------------------------------------------------------- weight gradient
 // D[co][(tap, ci)] = sum_p dY[p][co] * X[p @ tap][ci]; K = output pixels, split over
-// blocks (grid.z = pixel chunks) into an fp32 slab [chunks][Cout][KH*KW][Cin] that
-// grad_reduce sums in fixed order.  Block tile: 64 co x (one tap, 64 ci); per K-step
-// 32 pixels of dY [32][64] and the gathered X [32][64] go to LDS (row stride 80
-// elements = 40 dwords, an odd multiple of 8, so 8 consecutive rows of
-// ds_read_b64_tr_b16 are conflict-free), and the K-along-lane MFMA fragments are read
-// with the hardware transpose.  K index map: slot = 4g + j (j < 4), 16 + 4g + (j-4).
-constexpr int WG_RS = 80;
-// STEM (Cin == 4): the block's 64 columns are 16 taps x 4 channels (tap group
-// blockIdx.y), so the slab row layout [Cout][T][4] is unchanged.
-template <bool STEM>
+// blocks (grid.z = pixel chunks).  One chunk: the block writes the gradient itself
+// (out = [+ out] + D, `accum` for gradient accumulation); several: an fp32 slab
+// [chunks][Cout][KH*KW][Cin] that grad_reduce sums in fixed order.  Block tile: BM co x
+// (one tap, BN ci), 4 waves of (BM/2) x (BN/2); per K-step 32 pixels of dY [32][BM] and
+// the gathered X [32][BN] go to LDS (row stride BM+16 / BN+16 = an odd multiple of 8
+// dwords, so 8 consecutive rows of ds_read_b64_tr_b16 are conflict-free), and the
+// K-along-lane MFMA fragments are read with the hardware transpose.
+// STEM (Cin == 4 in X, BN = 64): the block's 64 columns are 16 taps x 4 channels (tap
+// group blockIdx.y); the output keeps only the 3 real channels: [Cout][T][3].
+template <int BM, int BN, bool STEM>
 __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                               const bf16_t* __restrict__ X,
-                                                              float* __restrict__ slab, int px_per_chunk) {
-  __shared__ __attribute__((aligned(16))) bf16_t sD[2][32 * WG_RS];
-  __shared__ __attribute__((aligned(16))) bf16_t sX[2][32 * WG_RS];
+                                                              float* __restrict__ out, int px_per_chunk,
+                                                              int accum) {
+  static_assert(!STEM || BN == 64, "stem: 16 taps x 4 channels per block");
+  constexpr int RD = BM + 16, RX = BN + 16;
+  constexpr int DPT = BM / 64, XPT = BN / 64;  // 16-B staging chunks per thread
+  constexpr int TA = BM / 32, TB = BN / 32;    // 16x16 tiles per wave
+  __shared__ __attribute__((aligned(16))) bf16_t sD[2][32 * RD];
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][32 * RX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int co0 = blockIdx.x * 64;
+  const int co0 = blockIdx.x * BM;
   const int T = g.KH * g.KW;
-  const int tap = STEM ? 0 : blockIdx.y / (g.Cin / 64);
-  const int ci0 = STEM ? 0 : (blockIdx.y - tap * (g.Cin / 64)) * 64;
+  const int tap = STEM ? 0 : blockIdx.y / (g.Cin / BN);
+  const int ci0 = STEM ? 0 : (blockIdx.y - tap * (g.Cin / BN)) * BN;
   const int kh = tap / g.KW, kw = tap - kh * g.KW;
   const int tg0 = STEM ? blockIdx.y * 16 : 0;  // first tap of this block (STEM)
-  const long OHW = (long)g.OH * g.OW;
-  const long Ptot = (long)g.N * OHW;
-  const long pbeg = (long)blockIdx.z * px_per_chunk;
-  const long pend = min(Ptot, pbeg + px_per_chunk);
-  // staging: 32 pixels x 64 ch for both tiles = 256 chunks of 16 B each -> one per thread each
-  const int sp = tid >> 3, sc = (tid & 7) * 8;
-  auto load = [&](long pk, bf16x8& vd, bf16x8& vx) {
-    const long P = pk + sp;
-    vd = zero8();
-    vx = zero8();
-    if (P < pend) {
-      const int n_ = (int)(P / OHW);
-      const int r = (int)(P - (long)n_ * OHW);
-      const int oh = r / g.OW, ow = r - (r / g.OW) * g.OW;
-      vd = ld8(dY + P * g.Cout + co0 + sc);
-      if (STEM) {
-        uint2 two[2];
+  const int OHW = g.OH * g.OW;
+  const int Ptot = g.N * OHW;
+  const int pbeg = blockIdx.z * px_per_chunk;
+  const int pend = min(Ptot, pbeg + px_per_chunk);
+  auto load = [&](int pk, bf16x8* vd, bf16x8* vx) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int t = tg0 + sc / 4 + u;
-          const int th = t / g.KW, tw = t - th * g.KW;
-          const int ih = oh * g.stride - g.pad + th, iw = ow * g.stride - g.pad + tw;
-          two[u] = (t < T && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-                       ? *reinterpret_cast<const uint2*>(X + (((long)n_ * g.H + ih) * g.W + iw) * 4)
-                       : make_uint2(0u, 0u);
+    for (int u = 0; u < DPT; ++u) {
+      const int c = tid + 256 * u;
+      const int sp = c / (BM / 8), sc = (c % (BM / 8)) * 8;
+      const int P = pk + sp;
+      vd[u] = P < pend ? ld8(dY + (long)P * g.Cout + co0 + sc) : zero8();
+    }
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) {
+      const int c = tid + 256 * u;
+      const int sp = c / (BN / 8), sc = (c % (BN / 8)) * 8;
+      const int P = pk + sp;
+      vx[u] = zero8();
+      if (P < pend) {
+        const int n_ = P / OHW;
+        const int r = P - n_ * OHW;
+        const int oh = r / g.OW, ow = r - oh * g.OW;
+        if (STEM) {
+          uint2 two[2];
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const int t = tg0 + sc / 4 + v;
+            const int th = t / g.KW, tw = t - th * g.KW;
+            const int ih = oh * g.stride - g.pad + th, iw = ow * g.stride - g.pad + tw;
+            two[v] = (t < T && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+                         ? *reinterpret_cast<const uint2*>(X + (((long)n_ * g.H + ih) * g.W + iw) * 4)
+                         : make_uint2(0u, 0u);
+          }
+          vx[u] = __builtin_bit_cast(bf16x8, make_uint4(two[0].x, two[0].y, two[1].x, two[1].y));
+        } else {
+          const int ih = oh * g.stride - g.pad + kh, iw = ow * g.stride - g.pad + kw;
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            vx[u] = ld8(X + (((long)n_ * g.H + ih) * g.W + iw) * g.Cin + ci0 + sc);
         }
-        vx = __builtin_bit_cast(bf16x8, make_uint4(two[0].x, two[0].y, two[1].x, two[1].y));
-      } else {
-        const int ih = oh * g.stride - g.pad + kh, iw = ow * g.stride - g.pad + kw;
-        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-          vx = ld8(X + (((long)n_ * g.H + ih) * g.W + iw) * g.Cin + ci0 + sc);
       }
     }
   };
-  // wave w: co tiles (2 of 4) x ci tiles (2 of 4)
-  const int wco = (wave >> 1) * 32, wci = (wave & 1) * 32;
+  auto store = [&](int buf, const bf16x8* vd, const bf16x8* vx) {
+#pragma unroll
+    for (int u = 0; u < DPT; ++u) {
+      const int c = tid + 256 * u;
+      *reinterpret_cast<bf16x8*>(&sD[buf][(c / (BM / 8)) * RD + (c % (BM / 8)) * 8]) = vd[u];
+    }
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) {
+      const int c = tid + 256 * u;
+      *reinterpret_cast<bf16x8*>(&sX[buf][(c / (BN / 8)) * RX + (c % (BN / 8)) * 8]) = vx[u];
+    }
+  };
+  // wave w: co half (wave >> 1) x column half (wave & 1)
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
   const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
-  f32x4 acc[2][2];
+  f32x4 acc[TA][TB];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 vd, vx;
+    for (int b = 0; b < TB; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 vd[DPT], vx[XPT];
   load(pbeg, vd, vx);
-  *reinterpret_cast<bf16x8*>(&sD[0][sp * WG_RS + sc]) = vd;
-  *reinterpret_cast<bf16x8*>(&sX[0][sp * WG_RS + sc]) = vx;
+  store(0, vd, vx);
   __syncthreads();
   int cur = 0;
-  for (long pk = pbeg; pk < pend; pk += 32) {
+  const int kA = 4 * gq + q, kB = 16 + 4 * gq + q;
+  for (int pk = pbeg; pk < pend; pk += 32) {
     const bool more = pk + 32 < pend;
     if (more) load(pk + 32, vd, vx);
-    const int sA = 4 * gq + q, sB = 16 + 4 * gq + q;
-    bf16x8 fa[2], fb[2];
+    bf16x8 fa[TA], fb[TB];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][sA * WG_RS + wco + 16 * a + 4 * pq]);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][sB * WG_RS + wco + 16 * a + 4 * pq]);
+    for (int a = 0; a < TA; ++a) {
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][kA * RD + wm + 16 * a + 4 * pq]);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][kB * RD + wm + 16 * a + 4 * pq]);
       fa[a] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][sA * WG_RS + wci + 16 * b + 4 * pq]);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][sB * WG_RS + wci + 16 * b + 4 * pq]);
+    for (int b = 0; b < TB; ++b) {
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][kA * RX + wn + 16 * b + 4 * pq]);
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][kB * RX + wn + 16 * b + 4 * pq]);
       fb[b] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TA; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = mfma16(fa[a], fb[b], acc[a][b]);
-    if (more) {
-      *reinterpret_cast<bf16x8*>(&sD[cur ^ 1][sp * WG_RS + sc]) = vd;
-      *reinterpret_cast<bf16x8*>(&sX[cur ^ 1][sp * WG_RS + sc]) = vx;
-    }
+      for (int b = 0; b < TB; ++b) acc[a][b] = mfma16(fa[a], fb[b], acc[a][b]);
+    if (more) store(cur ^ 1, vd, vx);
     __syncthreads();
     cur ^= 1;
   }
-  float* out = slab + (long)blockIdx.z * g.Cout * T * g.Cin;
+  const int ocin = STEM ? 3 : g.Cin;
+  float* o = out + (long)blockIdx.z * g.Cout * T * ocin;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < TA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < TB; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco + 16 * a + 4 * gq + r;
+        const int co = co0 + wm + 16 * a + 4 * gq + r;
+        long idx;
         if (STEM) {
-          const int j = wci + 16 * b + i16;  // column = tap offset * 4 + channel
+          const int j = wn + 16 * b + i16;  // column = tap offset * 4 + channel
           const int t = tg0 + j / 4;
-          if (t < T) out[((long)co * T + t) * 4 + (j & 3)] = acc[a][b][r];
+          if (t >= T || (j & 3) == 3) continue;
+          idx = ((long)co * T + t) * 3 + (j & 3);
         } else {
-          const int ci = ci0 + wci + 16 * b + i16;
-          out[((long)co * T + tap) * g.Cin + ci] = acc[a][b][r];
+          idx = ((long)co * T + tap) * g.Cin + ci0 + wn + 16 * b + i16;
         }
+        o[idx] = accum ? o[idx] + acc[a][b][r] : acc[a][b][r];
       }
 }
 
-int conv_gemm_fwd_blocks(const ConvGeom& g) {
-  const long P = (long)g.N * g.OH * g.OW;
-  return (int)((P + CG_BP - 1) / CG_BP);
+// ---------------------------------------------------------------- host side
+// Launch plan: pixel tile, channel tile and K splits.  Tuned on MI355X with
+// scripts/resnet_conv_sweep.py over ResNet-18 at batch 32 (profiles/r1_resnet):
+//  * K splits pay only for long K (>= 72 K-steps: 3x3 over >= 256 channels), where the
+//    grid is small and every split still runs >= 18 K-steps; below that the fp32
+//    partial round trip costs more than the idle CUs;
+//  * the forward takes 64-pixel tiles when 128-pixel ones give < 512 blocks, and
+//    64x64 tiles for 1x1 convolutions (2-8 K-steps: more blocks beat reuse);
+//  * the data gradient keeps 128-pixel tiles (its gather is the costlier operand).
+ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits) {
+  ConvPlan pl{};
+  const long P = dgrad ? (long)g.N * g.H * g.W : (long)g.N * g.OH * g.OW;
+  const int C = dgrad ? g.Cin : g.Cout;     // GEMM rows
+  const int T = g.KH * g.KW;
+  const bool stem = !dgrad && g.Cin == 4;
+  const int nk = stem ? (T + 7) / 8 : T * ((dgrad ? g.Cout : g.Cin) / CG_KS);
+  const bool pointwise = T == 1;
+  int c = bc ? bc : (C % 128 == 0 ? 128 : 64);
+  if (!bc && !dgrad && pointwise) c = 64;
+  if (stem) c = 64;
+  pl.bc = c;
+  auto blocks = [&](int bpx) { return ((P + bpx - 1) / bpx) * (long)(C / pl.bc); };
+  if (bp) pl.bp = bp;
+  else if (dgrad || stem) pl.bp = 128;
+  else pl.bp = (!pointwise && blocks(128) >= 512) ? 128 : 64;
+  if (stem) pl.bp = 128;
+  int s = splits;
+  if (s <= 0) s = nk >= 72 ? nk / 18 : 1;
+  if (s > 8) s = 8;
+  if (stem || s < 1) s = 1;
+  if (s > nk) s = nk;
+  pl.ks_per = (nk + s - 1) / s;
+  pl.splits = (nk + pl.ks_per - 1) / pl.ks_per;  // no empty split
+  pl.grid_x = (int)((P + pl.bp - 1) / pl.bp);
+  pl.grid_y = C / pl.bc;
+  return pl;
 }
 
-void conv_gemm_fwd(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias,
-                   bf16_t* Y, bool relu, float* stats, hipStream_t s) {
-  const int bco = (g.Cout % 128 == 0) ? 128 : 64;
-  const dim3 grid(conv_gemm_fwd_blocks(g), g.Cout / bco);
-  if (g.Cin == 4) {  // stem: 8 taps x 4 channels per K-step
-    if (bco != 64) return;  // host enforces Cout == 64 for the stem
-    if (stats) hipLaunchKernelGGL((conv_gemm_fwd_kernel<64, false, true, true>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats);
-    else if (relu) hipLaunchKernelGGL((conv_gemm_fwd_kernel<64, true, false, true>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats);
-    else hipLaunchKernelGGL((conv_gemm_fwd_kernel<64, false, false, true>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats);
+static int splitk_rows(long P, int C, int* rpb) {
+  const int pl = 256 / (C / 8);
+  long nb = (P + pl - 1) / pl;
+  if (nb > 512) nb = 512;
+  long r = (P + nb - 1) / nb;
+  r = (r + pl - 1) / pl * pl;
+  *rpb = (int)r;
+  return (int)((P + r - 1) / r);
+}
+
+int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl) {
+  if (pl.splits <= 1) return pl.grid_x;
+  int rpb;
+  return splitk_rows((long)g.N * g.OH * g.OW, g.Cout, &rpb);
+}
+
+static void splitk_reduce(const float* part, int S, long P, int C, const bf16_t* Xact, bf16_t* out,
+                          float* stats, hipStream_t s) {
+  int rpb;
+  const int nb = splitk_rows(P, C, &rpb);
+  const size_t lds = stats ? sizeof(float) * (256 / (C / 8)) * 2 * C : 0;
+#define SKR(M, ST) hipLaunchKernelGGL((splitk_reduce_kernel<M, ST>), dim3(nb), dim3(256), lds, s, part, S, (int)P, C, rpb, Xact, out, stats)
+  if (Xact) { if (stats) SKR(true, true); else SKR(true, false); }
+  else { if (stats) SKR(false, true); else SKR(false, false); }
+#undef SKR
+}
+
+void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,
+                   const float* bias, bf16_t* Y, bool relu, float* stats, float* part, hipStream_t s) {
+  const dim3 grid(pl.grid_x, pl.grid_y, pl.splits);
+  const int kp = pl.ks_per;
+  if (g.Cin == 4) {  // stem: 8 taps x 4 channels per K-step (host enforces Cout % 64)
+    if (stats) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, false, true, true, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp);
+    else if (relu) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, true, false, true, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp);
+    else hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, false, false, true, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp);
     return;
   }
-#define CGF(BC, RL, ST) hipLaunchKernelGGL((conv_gemm_fwd_kernel<BC, RL, ST, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats)
-  if (bco == 128) {
-    if (stats) { if (relu) CGF(128, true, true); else CGF(128, false, true); }
-    else { if (relu) CGF(128, true, false); else CGF(128, false, false); }
-  } else {
-    if (stats) { if (relu) CGF(64, true, true); else CGF(64, false, true); }
-    else { if (relu) CGF(64, true, false); else CGF(64, false, false); }
-  }
+#define CGF(BP, BC, RL, ST, PT) hipLaunchKernelGGL((conv_gemm_fwd_kernel<BP, BC, RL, ST, false, PT>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp)
+#define CGF_BP(BP, BC)                                                           \
+  if (pl.splits > 1) CGF(BP, BC, false, false, true);                            \
+  else if (stats) { if (relu) CGF(BP, BC, true, true, false); else CGF(BP, BC, false, true, false); } \
+  else { if (relu) CGF(BP, BC, true, false, false); else CGF(BP, BC, false, false, false); }
+  if (pl.bp == 128) { if (pl.bc == 128) { CGF_BP(128, 128) } else { CGF_BP(128, 64) } }
+  else { if (pl.bc == 128) { CGF_BP(64, 128) } else { CGF_BP(64, 64) } }
+#undef CGF_BP
 #undef CGF
+  if (pl.splits > 1) {
+    // bias / ReLU of the split path: only the BatchNorm use (no bias, no ReLU) is split
+    splitk_reduce(part, pl.splits, (long)g.N * g.OH * g.OW, g.Cout, nullptr, Y, stats, s);
+  }
 }
 
-
-void conv_gemm_dgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* WT, const bf16_t* Xact,
-                     bf16_t* dX, hipStream_t s) {
-  const long P = (long)g.N * g.H * g.W;
-  const int bci = (g.Cin % 128 == 0) ? 128 : 64;
-  const dim3 grid((unsigned)((P + CG_BP - 1) / CG_BP), g.Cin / bci);
-#define CGD(BC, MX) hipLaunchKernelGGL((conv_gemm_dgrad_kernel<BC, MX>), grid, dim3(256), 0, s, g, dY, WT, Xact, dX)
-  if (bci == 128) { if (Xact) CGD(128, true); else CGD(128, false); }
-  else { if (Xact) CGD(64, true); else CGD(64, false); }
+void conv_gemm_dgrad(const ConvGeom& g, const ConvPlan& pl, const bf16_t* dY, const bf16_t* W,
+                     const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s) {
+  const dim3 grid(pl.grid_x, pl.grid_y, pl.splits);
+  const int kp = pl.ks_per;
+#define CGD(BP, BC, MX, PT) hipLaunchKernelGGL((conv_gemm_dgrad_kernel<BP, BC, MX, PT>), grid, dim3(256), 0, s, g, dY, W, Xact, dX, part, kp)
+#define CGD_BP(BP, BC)                     \
+  if (pl.splits > 1) CGD(BP, BC, false, true); \
+  else if (Xact) CGD(BP, BC, true, false); \
+  else CGD(BP, BC, false, false);
+  if (pl.bp == 128) { if (pl.bc == 128) { CGD_BP(128, 128) } else { CGD_BP(128, 64) } }
+  else { if (pl.bc == 128) { CGD_BP(64, 128) } else { CGD_BP(64, 64) } }
+#undef CGD_BP
 #undef CGD
+  if (pl.splits > 1) splitk_reduce(part, pl.splits, (long)g.N * g.H * g.W, g.Cin, Xact, dX, nullptr, s);
 }
 
 int conv_gemm_wgrad_chunks(const ConvGeom& g, int px_per_chunk) {
@@ -465,15 +696,62 @@ int conv_gemm_wgrad_chunks(const ConvGeom& g, int px_per_chunk) {
   return (int)((P + px_per_chunk - 1) / px_per_chunk);
 }
 
-void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* slab,
-                     int px_per_chunk, hipStream_t s) {
+// Block tile of the weight gradient (scripts/resnet_conv_sweep.py, profiles/r1_resnet):
+// 128-wide tiles only while the 128-tile grid is small (< 64 tiles: those layers are
+// chunked over pixels anyway and the wider tile halves the slab traffic); otherwise
+// 64 x 64, whose 4x larger grid fills the CUs without chunking.
+static void wgrad_tile(const ConvGeom& g, int* bm, int* bn) {
+  const int T = g.KH * g.KW;
+  *bm = 64;
+  *bn = 64;
+  if (g.Cin == 4 || T == 1) return;
+  const int bm2 = g.Cout % 128 == 0 ? 128 : 64, bn2 = g.Cin % 128 == 0 ? 128 : 64;
+  if ((long)(g.Cout / bm2) * T * (g.Cin / bn2) < 64) {
+    *bm = bm2;
+    *bn = bn2;
+  }
+}
+
+int conv_gemm_wgrad_tiles(const ConvGeom& g) {
+  int bm, bn;
+  wgrad_tile(g, &bm, &bn);
+  const int gy = g.Cin == 4 ? (g.KH * g.KW + 15) / 16 : g.KH * g.KW * (g.Cin / bn);
+  return (g.Cout / bm) * gy;
+}
+
+// pixels per chunk: split K until the grid has ~target blocks (1x1: 256 - a tiny GEMM
+// whose slab reduction dominates; 128-wide tiles: 512; 64 x 64: 1024)
+int conv_gemm_wgrad_ppc(const ConvGeom& g) {
+  int bm, bn;
+  wgrad_tile(g, &bm, &bn);
+  const int T = g.KH * g.KW;
+  const long target = T == 1 ? 256 : ((bm == 128 || bn == 128) ? 512 : 1024);
+  const long tiles = conv_gemm_wgrad_tiles(g);
+  long chunks = target / tiles;
+  if (chunks < 1) chunks = 1;
+  const long P = (long)g.N * g.OH * g.OW;
+  long ppc = (P + chunks - 1) / chunks;
+  ppc = (ppc + 31) / 32 * 32;
+  return (int)(ppc < 32 ? 32 : ppc);
+}
+
+void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out,
+                     int px_per_chunk, bool accum, hipStream_t s) {
+  const int ch = conv_gemm_wgrad_chunks(g, px_per_chunk);
+  const int acc = (accum && ch == 1) ? 1 : 0;
+  int bm, bn;
+  wgrad_tile(g, &bm, &bn);
   if (g.Cin == 4) {
-    const dim3 grid(g.Cout / 64, (g.KH * g.KW + 15) / 16, conv_gemm_wgrad_chunks(g, px_per_chunk));
-    hipLaunchKernelGGL(conv_gemm_wgrad_kernel<true>, grid, dim3(256), 0, s, g, dY, X, slab, px_per_chunk);
+    const dim3 grid(g.Cout / bm, (g.KH * g.KW + 15) / 16, ch);
+    if (bm == 128) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<128, 64, true>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc);
+    else hipLaunchKernelGGL((conv_gemm_wgrad_kernel<64, 64, true>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc);
     return;
   }
-  const dim3 grid(g.Cout / 64, g.KH * g.KW * (g.Cin / 64), conv_gemm_wgrad_chunks(g, px_per_chunk));
-  hipLaunchKernelGGL(conv_gemm_wgrad_kernel<false>, grid, dim3(256), 0, s, g, dY, X, slab, px_per_chunk);
+  const dim3 grid(g.Cout / bm, g.KH * g.KW * (g.Cin / bn), ch);
+#define CGW(M, N) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, N, false>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc)
+  if (bm == 128) { if (bn == 128) CGW(128, 128); else CGW(128, 64); }
+  else { if (bn == 128) CGW(64, 128); else CGW(64, 64); }
+#undef CGW
 }
 
 }  // namespace ddp_amd

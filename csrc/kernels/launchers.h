@@ -45,28 +45,39 @@ void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float*
 struct ConvGeom {
   int N, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad;
 };
-int conv_gemm_fwd_blocks(const ConvGeom& g);
-void conv_gemm_fwd(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias,
-                   bf16_t* Y, bool relu, float* stats, hipStream_t s);
-void conv_gemm_dgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* WT, const bf16_t* Xact,
-                     bf16_t* dX, hipStream_t s);
+// launch plan: pixel tile bp (64/128), channel tile bc (64/128), K splits (grid.z)
+struct ConvPlan {
+  int bp, bc, splits, ks_per, grid_x, grid_y;
+};
+// bp / bc / splits = 0: chosen for >= ~2 blocks per CU
+ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits);
+int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl);  // BN stats slab rows (fwd)
+// splits > 1: `part` = fp32 workspace [splits][P][C]; no bias / ReLU on the split path
+void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,
+                   const float* bias, bf16_t* Y, bool relu, float* stats, float* part, hipStream_t s);
+// W: the OHWI forward weight itself (read transposed through LDS)
+void conv_gemm_dgrad(const ConvGeom& g, const ConvPlan& pl, const bf16_t* dY, const bf16_t* W,
+                     const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s);
 int conv_gemm_wgrad_chunks(const ConvGeom& g, int px_per_chunk);
-void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* slab,
-                     int px_per_chunk, hipStream_t s);
+int conv_gemm_wgrad_tiles(const ConvGeom& g);  // blocks per pixel chunk
+int conv_gemm_wgrad_ppc(const ConvGeom& g);    // tuned pixels per chunk
+// one chunk: out = the gradient ([Cout][T][Cin], stem: [Cout][T][3]), `accum` adds to it;
+// several: out = slab [chunks][...] for grad_reduce
+void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out,
+                     int px_per_chunk, bool accum, hipStream_t s);
 
 // ---- ResNet ops (resnet_ops.hip) -----------------------------------------------------
-void bn_finalize(const float* slab, int nblk, int C, float count, float eps, float momentum,
+int bn_finalize_groups(int rows);  // ws of bn_finalize: [groups][2][C]
+void bn_finalize(const float* slab, int rows, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* save_mean, float* save_invstd,
-                 hipStream_t s);
+                 long long* nbt, float* ws, hipStream_t s);
 void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* invstd,
               const float* gamma, const float* beta, const bf16_t* res, bool relu, bf16_t* y,
               hipStream_t s);
-int bn_bwd_blocks(long P, int rows);
-void bn_bwd_reduce(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C,
-                   const float* mean, const float* invstd, float* slab, int rows, hipStream_t s);
-void bn_bwd_apply(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C,
-                  const float* mean, const float* invstd, const float* gamma, const float* sums,
-                  float count, bf16_t* dx, bf16_t* dres, hipStream_t s);
+int bn_bwd_rows(long P, int C, int* rpb);  // ws of bn_bwd: [rows][2][C]
+void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
+            const float* invstd, const float* gamma, float count, float* ws, float* sums,
+            float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s);
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
                  unsigned char* amax, hipStream_t s);
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
@@ -153,6 +164,7 @@ struct SlabSeg {
   bf16_t* sh = nullptr;
   bf16_t* sh_t = nullptr;
   int t_co = 0, t_taps = 0, t_ci = 0;
+  int accum = 0;  // dst += reduced * scale (gradient accumulation) instead of dst =
 };
 constexpr int MAX_SLAB_SEGS = 6;
 struct SlabSet {

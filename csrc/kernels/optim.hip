@@ -139,7 +139,8 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
   __syncthreads();
   if (grp == 0 && live) {
     const SlabSeg& sg = ss.s[k];  // k is block-uniform
-    const float g = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
+    float g = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
+    if (sg.accum) g += sg.dst[i];
     if (ss.sys_store) st_sys(sg.dst + i, g);
     else sg.dst[i] = g;
     if (ss.sgd.update && sg.p) {  // single-process step: the gradient is final -> fused SGD

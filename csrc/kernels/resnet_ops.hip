@@ -5,36 +5,107 @@
 // BatchNorm statistics come from the producing convolution's epilogue (per-block
 // per-channel sum / sum-of-squares slabs, conv_gemm.hip); bn_finalize reduces them
 // in fixed order and updates the running buffers with torch's semantics (momentum
-// 0.1, unbiased running variance).  bn_apply fuses normalise + affine + residual
-// add + ReLU.  The backward is two passes: per-block partial sums of dy and
-// dy*xhat (with the ReLU mask from the saved output), then the per-element
-// input gradient.  All reductions are fixed-order (no atomics).
+// 0.1, unbiased running variance, num_batches_tracked).  bn_apply fuses normalise +
+// affine + residual add + ReLU.  The backward is two kernels: strip-parallel sums of
+// dy and dy*xhat (with the ReLU mask from the saved output) finished by the strip's
+// last block, which also writes dgamma / dbeta straight into the parameter
+// gradients; then the per-element input gradient.  All float reductions are
+// fixed-order (the only atomics are integer tickets).
+#include <stdexcept>
+#include <string>
+
 #include "kernels/common.h"
 #include "kernels/launchers.h"
 
+#define RN_CHECK(expr)                                                                   \
+  do {                                                                                   \
+    const hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_)); \
+  } while (0)
+
 namespace ddp_amd {
 
+// ---------------------------------------------------------------- last-arrival reductions
+// A strip of blocks reduces into per-block partials; the block that takes the strip's
+// last ticket sums the partials in FIXED order (deterministic, no float atomics) and
+// resets the ticket for the next launch.  Cross-XCD visibility without fences: an
+// agent-scope release fence writes back the XCD's whole L2 (measured: ~30 us per
+// reduction at 400 blocks), so the partials are stored write-through (agent-scope
+// atomic stores, st_wt) and drained (vmcnt(0)) before the relaxed ticket increment,
+// and the last block reads them with agent-scope atomic loads.
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool last_arrival(int* ticket, int expected, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's st_wt partials are out
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == expected - 1;
+    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // ---------------------------------------------------------------- BatchNorm
-// stats slab [nblk][2][C] -> mean/invstd (+ running stats).  Block = 64 channels x 4 groups.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ slab, int nblk,
+// stats slab [rows][2][C] -> mean / invstd (+ running stats with torch's semantics:
+// momentum, unbiased running variance; + num_batches_tracked).  grid (ceil(C/64), G):
+// block (strip, y) sums rows y, y+G, ... of its 64 channels (4 row groups, fixed
+// combine order) into ws[y]; the last block of the strip sums ws[0..G) and finalises.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ slab, int rows,
                                                           int C, float count, float eps, float momentum,
                                                           float* __restrict__ running_mean,
                                                           float* __restrict__ running_var,
                                                           float* __restrict__ save_mean,
-                                                          float* __restrict__ save_invstd) {
+                                                          float* __restrict__ save_invstd,
+                                                          long long* __restrict__ nbt,
+                                                          float* __restrict__ ws, int* __restrict__ tickets) {
   __shared__ float ps[4][64], pq[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;
+  __shared__ int s_last;
+  const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l;
+  const int G = gridDim.y, y = blockIdx.y;
+  const long C2 = 2L * C;
   float s = 0.f, q = 0.f;
-  if (c < C)
-    for (int b = grp; b < nblk; b += 4) {
-      s += slab[(long)b * 2 * C + c];
-      q += slab[(long)b * 2 * C + C + c];
+  if (c < C) {
+    int r = y + G * grp;
+    for (; r + 12 * G < rows; r += 16 * G) {  // 4 rows in flight
+      float a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = slab[(long)(r + 4 * u * G) * C2 + c];
+        b[u] = slab[(long)(r + 4 * u * G) * C2 + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s += a[u]; q += b[u]; }
     }
-  ps[grp][threadIdx.x & 63] = s;
-  pq[grp][threadIdx.x & 63] = q;
+    for (; r < rows; r += 4 * G) {
+      s += slab[(long)r * C2 + c];
+      q += slab[(long)r * C2 + C + c];
+    }
+  }
+  ps[grp][l] = s;
+  pq[grp][l] = q;
   __syncthreads();
   if (grp == 0 && c < C) {
-    const int l = threadIdx.x;
+    st_wt(ws + (long)y * C2 + c, ((ps[0][l] + ps[1][l]) + ps[2][l]) + ps[3][l]);
+    st_wt(ws + (long)y * C2 + C + c, ((pq[0][l] + pq[1][l]) + pq[2][l]) + pq[3][l]);
+  }
+  if (!last_arrival(&tickets[blockIdx.x], G, &s_last)) return;
+  s = q = 0.f;
+  if (c < C)
+    for (int yy = grp; yy < G; yy += 4) {
+      s += ld_agent(ws + (long)yy * C2 + c);
+      q += ld_agent(ws + (long)yy * C2 + C + c);
+    }
+  __syncthreads();
+  ps[grp][l] = s;
+  pq[grp][l] = q;
+  __syncthreads();
+  if (grp == 0 && c < C) {
     const float S = ((ps[0][l] + ps[1][l]) + ps[2][l]) + ps[3][l];
     const float Q = ((pq[0][l] + pq[1][l]) + pq[2][l]) + pq[3][l];
     const float mean = S / count;
@@ -47,198 +118,259 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
       running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
     }
   }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
 }
 
-// y = act((x - mean) * invstd * gamma + beta [+ res]); 8 channels per thread.
+__device__ __forceinline__ void ld8f(const float* p, float* o) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void unpack8(bf16x8 v, float* o) {
+  const uint4 u = __builtin_bit_cast(uint4, v);
+  unpack4(make_uint2(u.x, u.y), o);
+  unpack4(make_uint2(u.z, u.w), o + 4);
+}
+__device__ __forceinline__ uint4 pack8(const float* v) {
+  const uint2 lo = pack4(v[0], v[1], v[2], v[3]), hi = pack4(v[4], v[5], v[6], v[7]);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// y = act(x * sc + sh [+ res]), sc = invstd * gamma, sh = beta - mean * sc; 8 channels per
+// thread.  The grid stride is a multiple of C/8 (which divides 256), so a thread's
+// channel group - and its 16 per-channel constants - never change.
 template <bool RES, bool RELU>
-__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, long P, int C,
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, long n8, int C,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta,
                                                        const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y) {
-  const long n8 = P * C / 8;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    const int c0 = (int)((i * 8) % C);
-    const bf16x8 xv = ld8(x + i * 8);
-    bf16x8 rv = zero8();
-    if (RES) rv = ld8(res + i * 8);
-    float o[8];
+  const int c0 = (int)(t0 % (C / 8)) * 8;
+  float sc[8], sh[8], mu[8], be[8];
+  ld8f(invstd + c0, sc);
+  ld8f(gamma + c0, sh);
+  ld8f(mean + c0, mu);
+  ld8f(beta + c0, be);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] *= sh[j];
+    sh[j] = be[j] - mu[j] * sc[j];
+  }
+  for (long i = t0; i < n8; i += stride) {
+    float v[8], r[8];
+    unpack8(ld8(x + i * 8), v);
+    if (RES) unpack8(ld8(res + i * 8), r);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      float v = (bf2f((bf16_t)xv[j]) - mean[c]) * invstd[c] * gamma[c] + beta[c];
-      if (RES) v += bf2f((bf16_t)rv[j]);
-      if (RELU) v = fmaxf(v, 0.f);
-      o[j] = v;
+      v[j] = fmaf(v[j], sc[j], sh[j]);
+      if (RES) v[j] += r[j];
+      if (RELU) v[j] = fmaxf(v[j], 0.f);
     }
-    uint4 pk;
-    const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
-    pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-    *reinterpret_cast<uint4*>(y + i * 8) = pk;
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(v);
   }
 }
 
-// Backward pass 1: per-block partials of sum(dy) and sum(dy * xhat), where dy is the
-// gradient w.r.t. the BN output masked by the ReLU (out > 0) when RELU.  Block = 256
-// threads = (256 / (C/8)) pixel lanes x (C/8) channel groups over `rows` pixels.
+// Backward pass 1: sums of dy and dy * xhat per channel, dy = the gradient w.r.t. the BN
+// output masked by the ReLU (out > 0) when RELU.  grid (C/64, R): block = 8 channel
+// groups (64 channels) x 32 pixel lanes over `rpb` pixels -> ws[y]; the strip's last
+// block sums ws[0..R) in fixed order into sums[2C] = [sum dy | sum dy*xhat] and the
+// affine gradients (dbeta = sum dy, dgamma = sum dy*xhat; `accum` adds to them).
 template <bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
                                                             const bf16_t* __restrict__ out,
-                                                            const bf16_t* __restrict__ x, long P,
-                                                            int C, const float* __restrict__ mean,
-                                                            const float* __restrict__ invstd,
-                                                            float* __restrict__ slab, int rows) {
-  extern __shared__ __attribute__((aligned(16))) float sred[];  // [pl][2][C]
-  const int cg = C / 8;
-  const int pl = 256 / cg;  // pixel lanes
-  const int tg = threadIdx.x % cg, tp = threadIdx.x / cg;
-  float s[8], q[8], mu[8], is[8];
+                                                            const bf16_t* __restrict__ x, int P, int C,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, int rpb,
+                                                            float* __restrict__ ws, int* __restrict__ tickets,
+                                                            float* __restrict__ sums,
+                                                            float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta, int accum) {
+  __shared__ float sred[32][2][64];
+  __shared__ float shalf[2][128];
+  __shared__ int s_last;
+  const int tg = threadIdx.x & 7, tp = threadIdx.x >> 3;
+  const int cb = blockIdx.x * 64;
+  const int c0 = cb + tg * 8;
+  float mu[8], is[8], s[8], q[8];
+  ld8f(mean + c0, mu);
+  ld8f(invstd + c0, is);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    s[j] = q[j] = 0.f;
-    mu[j] = mean[tg * 8 + j];
-    is[j] = invstd[tg * 8 + j];
-  }
-  const long p0 = (long)blockIdx.x * rows;
-  const long p1 = min(P, p0 + rows);
-  if (tp < pl)
-    for (long p = p0 + tp; p < p1; p += pl) {
-      const long off = p * C + tg * 8;
-      const bf16x8 g = ld8(dout + off), xv = ld8(x + off);
-      bf16x8 ov = zero8();
-      if (RELU) ov = ld8(out + off);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float d = bf2f((bf16_t)g[j]);
-        if (RELU && !(bf2f((bf16_t)ov[j]) > 0.f)) d = 0.f;
-        const float xh = (bf2f((bf16_t)xv[j]) - mu[j]) * is[j];
-        s[j] += d;
-        q[j] = fmaf(d, xh, q[j]);
-      }
-    }
-  if (tp < pl) {
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  const int p0 = blockIdx.y * rpb, p1 = min(P, p0 + rpb);
+  for (int p = p0 + tp; p < p1; p += 32) {
+    const long off = (long)p * C + c0;
+    float d[8], xv[8], ov[8];
+    unpack8(ld8(dout + off), d);
+    unpack8(ld8(x + off), xv);
+    if (RELU) unpack8(ld8(out + off), ov);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      sred[(tp * 2) * C + tg * 8 + j] = s[j];
-      sred[(tp * 2 + 1) * C + tg * 8 + j] = q[j];
+      if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
+      s[j] += d[j];
+      q[j] = fmaf(d[j], (xv[j] - mu[j]) * is[j], q[j]);
     }
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sred[tp][0][tg * 8 + j] = s[j];
+    sred[tp][1][tg * 8 + j] = q[j];
+  }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float S = 0.f, Q = 0.f;
-    for (int t = 0; t < pl; ++t) {
-      S += sred[(t * 2) * C + c];
-      Q += sred[(t * 2 + 1) * C + c];
+  const int R = gridDim.y;
+  const int v = threadIdx.x & 127, which = v >> 6, cc = v & 63;
+  if (threadIdx.x < 128) {
+    float a = 0.f;
+    for (int t = 0; t < 32; ++t) a += sred[t][which][cc];
+    st_wt(ws + ((long)blockIdx.y * 2 + which) * C + cb + cc, a);
+  }
+  if (!last_arrival(&tickets[blockIdx.x], R, &s_last)) return;
+  const int h = threadIdx.x >> 7;
+  float a = 0.f;
+  {
+    int yy = h;
+    for (; yy + 14 < R; yy += 16) {
+      float t8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t8[u] = ld_agent(ws + ((long)(yy + 2 * u) * 2 + which) * C + cb + cc);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += t8[u];
     }
-    slab[(long)blockIdx.x * 2 * C + c] = S;
-    slab[(long)blockIdx.x * 2 * C + C + c] = Q;
+    for (; yy < R; yy += 2) a += ld_agent(ws + ((long)yy * 2 + which) * C + cb + cc);
+  }
+  shalf[h][v] = a;
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const float tot = shalf[0][v] + shalf[1][v];
+    const int c = cb + cc;
+    sums[which * C + c] = tot;
+    float* dst = which ? dgamma : dbeta;
+    if (dst) dst[c] = accum ? dst[c] + tot : tot;
   }
 }
 
 // Backward pass 2: dx = gamma*invstd/count * (count*dy - sum_dy - xhat*sum_dyxh); also
-// writes the residual-branch gradient (= dy masked) when dres != null.
+// writes the residual-branch gradient (= dy masked) when dres != null.  Same
+// fixed-channel-group grid stride as bn_apply.
 template <bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ out,
-                                                           const bf16_t* __restrict__ x, long P,
+                                                           const bf16_t* __restrict__ x, long n8,
                                                            int C, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ sums,
                                                            float count, bf16_t* __restrict__ dx,
                                                            bf16_t* __restrict__ dres) {
-  const long n8 = P * C / 8;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    const int c0 = (int)((i * 8) % C);
-    const bf16x8 g = ld8(dout + i * 8), xv = ld8(x + i * 8);
-    bf16x8 ov = zero8();
-    if (RELU) ov = ld8(out + i * 8);
-    float o[8], dm[8];
+  const int c0 = (int)(t0 % (C / 8)) * 8;
+  float mu[8], is[8], k[8], sd[8], sq[8];
+  ld8f(mean + c0, mu);
+  ld8f(invstd + c0, is);
+  ld8f(gamma + c0, k);
+  ld8f(sums + c0, sd);
+  ld8f(sums + C + c0, sq);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = k[j] * is[j] / count;
+  for (long i = t0; i < n8; i += stride) {
+    float d[8], xv[8], ov[8], o[8];
+    unpack8(ld8(dout + i * 8), d);
+    unpack8(ld8(x + i * 8), xv);
+    if (RELU) unpack8(ld8(out + i * 8), ov);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      float d = bf2f((bf16_t)g[j]);
-      if (RELU && !(bf2f((bf16_t)ov[j]) > 0.f)) d = 0.f;
-      dm[j] = d;
-      const float xh = (bf2f((bf16_t)xv[j]) - mean[c]) * invstd[c];
-      const float k = gamma[c] * invstd[c] / count;
-      o[j] = k * (count * d - sums[c] - xh * sums[C + c]);
+      if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
+      const float xh = (xv[j] - mu[j]) * is[j];
+      o[j] = k[j] * (count * d[j] - sd[j] - xh * sq[j]);
     }
-    uint4 pk;
-    uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
-    pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-    *reinterpret_cast<uint4*>(dx + i * 8) = pk;
-    if (dres) {
-      lo = pack4(dm[0], dm[1], dm[2], dm[3]);
-      hi = pack4(dm[4], dm[5], dm[6], dm[7]);
-      pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-      *reinterpret_cast<uint4*>(dres + i * 8) = pk;
-    }
+    *reinterpret_cast<uint4*>(dx + i * 8) = pack8(o);
+    if (dres) *reinterpret_cast<uint4*>(dres + i * 8) = pack8(d);
   }
 }
 
 // ---------------------------------------------------------------- pooling
-// 3x3 / stride 2 / pad 1 max pool; argmax (window index 0..8, first max in row-major
-// window order = torch's tie rule) saved as uint8 for the backward.
+// 3x3 / stride 2 / pad 1 max pool, 8 channels per thread (16-B loads); argmax (window
+// index 0..8, first max in row-major window order = torch's tie rule) saved as uint8.
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int H,
                                                           int W, int C, int OH, int OW,
                                                           bf16_t* __restrict__ y,
                                                           unsigned char* __restrict__ amax) {
-  const long total = (long)N * OH * OW * C;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = C / 8;
+  const int total = N * OH * OW * cg;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int c = (int)(i % C);
-  const long p = i / C;
-  const int n = (int)(p / ((long)OH * OW));
-  const int r = (int)(p - (long)n * OH * OW);
-  const int oh = r / OW, ow = r - (r / OW) * OW;
-  float best = -INFINITY;
-  int bi = 0;
+  const int g8 = (i % cg) * 8;
+  const int p = i / cg;
+  const int n = p / (OH * OW);
+  const int r = p - n * OH * OW;
+  const int oh = r / OW, ow = r - oh * OW;
+  float best[8];
+  unsigned bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0u; }
+#pragma unroll
   for (int k = 0; k < 9; ++k) {
     const int ih = oh * 2 - 1 + k / 3, iw = ow * 2 - 1 + k % 3;
     if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
-      const float v = bf2f(x[(((long)n * H + ih) * W + iw) * C + c]);
-      if (v > best || (v != v && best == best)) { best = v; bi = k; }  // NaN propagates like torch
+      float v[8];
+      unpack8(ld8(x + (((long)n * H + ih) * W + iw) * C + g8), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) { best[j] = v[j]; bi[j] = k; }
     }
   }
-  y[i] = f2bf(best);
-  amax[i] = (unsigned char)bi;
+  const long o = (long)p * C + g8;
+  *reinterpret_cast<uint4*>(y + o) = pack8(best);
+  *reinterpret_cast<uint2*>(amax + o) =
+      make_uint2(bi[0] | bi[1] << 8 | bi[2] << 16 | bi[3] << 24, bi[4] | bi[5] << 8 | bi[6] << 16 | bi[7] << 24);
 }
 
 // Gather form of the backward (deterministic): each input element sums dy over the
-// (at most 4) windows that selected it.
+// (at most 4) windows that selected it, in window order.  8 channels per thread.
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const unsigned char* __restrict__ amax,
                                                           int N, int H, int W, int C, int OH, int OW,
                                                           bf16_t* __restrict__ dx) {
-  const long total = (long)N * H * W * C;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cg = C / 8;
+  const int total = N * H * W * cg;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const int c = (int)(i % C);
-  const long p = i / C;
-  const int n = (int)(p / ((long)H * W));
-  const int r = (int)(p - (long)n * H * W);
-  const int ih = r / W, iw = r - (r / W) * W;
-  float acc = 0.f;
+  const int g8 = (i % cg) * 8;
+  const int p = i / cg;
+  const int n = p / (H * W);
+  const int r = p - n * H * W;
+  const int ih = r / W, iw = r - ih * W;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int th = ih + 1 - kh;
     if (th < 0 || (th & 1)) continue;
     const int oh = th >> 1;
     if (oh >= OH) continue;
+#pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int tw = iw + 1 - kw;
       if (tw < 0 || (tw & 1)) continue;
       const int ow = tw >> 1;
       if (ow >= OW) continue;
-      const long o = (((long)n * OH + oh) * OW + ow) * C + c;
-      if (amax[o] == kh * 3 + kw) acc += bf2f(dy[o]);
+      const long o = (((long)n * OH + oh) * OW + ow) * C + g8;
+      const uint2 am = *reinterpret_cast<const uint2*>(amax + o);
+      float d[8];
+      unpack8(ld8(dy + o), d);
+      const unsigned kk = kh * 3 + kw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned b = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
+        if (b == kk) acc[j] += d[j];
+      }
     }
   }
-  dx[i] = f2bf(acc);
+  *reinterpret_cast<uint4*>(dx + (long)p * C + g8) = pack8(acc);
 }
 
 // global average pool: [N][HW][C] bf16 -> [N][C] fp32 (thread per (n, c), fixed order)
@@ -309,56 +441,90 @@ static unsigned grid_for(long n, int per_thread = 1) {
   return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
 }
 
-void bn_finalize(const float* slab, int nblk, int C, float count, float eps, float momentum,
+// Ticket words for last_arrival: one zeroed pool per device, handed out round-robin
+// (every kernel resets the tickets it used, so a slot is clean when it comes round).
+static int* ticket_slots(int n) {
+  constexpr int kSlots = 1 << 16;
+  static int* pool[64] = {};
+  static int next[64] = {};
+  int dev = 0;
+  RN_CHECK(hipGetDevice(&dev));
+  dev &= 63;
+  if (!pool[dev]) {
+    RN_CHECK(hipMalloc(reinterpret_cast<void**>(&pool[dev]), sizeof(int) * kSlots));
+    RN_CHECK(hipMemset(pool[dev], 0, sizeof(int) * kSlots));
+    RN_CHECK(hipDeviceSynchronize());
+  }
+  if (next[dev] + n > kSlots) next[dev] = 0;
+  int* p = pool[dev] + next[dev];
+  next[dev] += n;
+  return p;
+}
+
+int bn_finalize_groups(int rows) {
+  const int g = rows / 32;
+  return g < 1 ? 1 : (g > 64 ? 64 : g);
+}
+
+void bn_finalize(const float* slab, int rows, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* save_mean, float* save_invstd,
-                 hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, slab, nblk, C, count,
-                     eps, momentum, running_mean, running_var, save_mean, save_invstd);
+                 long long* nbt, float* ws, hipStream_t s) {
+  const int strips = (C + 63) / 64, G = bn_finalize_groups(rows);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(strips, G), dim3(256), 0, s, slab, rows, C, count, eps,
+                     momentum, running_mean, running_var, save_mean, save_invstd, nbt, ws,
+                     ticket_slots(strips));
 }
 
 void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* invstd,
               const float* gamma, const float* beta, const bf16_t* res, bool relu, bf16_t* y,
               hipStream_t s) {
   const unsigned g = grid_for(P * C, 8);
-#define BA(R, L) hipLaunchKernelGGL((bn_apply_kernel<R, L>), dim3(g), dim3(256), 0, s, x, P, C, mean, invstd, gamma, beta, res, y)
+#define BA(R, L) hipLaunchKernelGGL((bn_apply_kernel<R, L>), dim3(g), dim3(256), 0, s, x, P * C / 8, C, mean, invstd, gamma, beta, res, y)
   if (res) { if (relu) BA(true, true); else BA(true, false); }
   else { if (relu) BA(false, true); else BA(false, false); }
 #undef BA
 }
 
-int bn_bwd_blocks(long P, int rows) { return (int)((P + rows - 1) / rows); }
-
-void bn_bwd_reduce(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C,
-                   const float* mean, const float* invstd, float* slab, int rows, hipStream_t s) {
-  const int pl = 256 / (C / 8);
-  const size_t lds = sizeof(float) * pl * 2 * C;
-  const dim3 grid(bn_bwd_blocks(P, rows));
-  if (out)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), lds, s, dout, out, x, P, C, mean, invstd, slab, rows);
-  else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), lds, s, dout, out, x, P, C, mean, invstd, slab, rows);
+int bn_bwd_rows(long P, int C, int* rpb) {
+  const int strips = C / 64;
+  long R = 512 / strips;
+  if (R > 256) R = 256;
+  const long maxr = (P + 31) / 32;
+  if (R > maxr) R = maxr;
+  if (R < 1) R = 1;
+  const long r = (P + R - 1) / R;
+  if (rpb) *rpb = (int)r;
+  return (int)((P + r - 1) / r);
 }
 
-void bn_bwd_apply(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C,
-                  const float* mean, const float* invstd, const float* gamma, const float* sums,
-                  float count, bf16_t* dx, bf16_t* dres, hipStream_t s) {
+void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
+            const float* invstd, const float* gamma, float count, float* ws, float* sums,
+            float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s) {
+  int rpb = 0;
+  const int R = bn_bwd_rows(P, C, &rpb);
+  const dim3 grid(C / 64, R);
+  int* tk = ticket_slots(C / 64);
+  if (out)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), 0, s, dout, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), 0, s, dout, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
   const unsigned g = grid_for(P * C, 8);
   if (out)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(256), 0, s, dout, out, x, P, C, mean, invstd, gamma, sums, count, dx, dres);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(256), 0, s, dout, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(256), 0, s, dout, out, x, P, C, mean, invstd, gamma, sums, count, dx, dres);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(256), 0, s, dout, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
 }
 
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
                  unsigned char* amax, hipStream_t s) {
-  const long total = (long)N * OH * OW * C;
+  const long total = (long)N * OH * OW * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, N,
                      H, W, C, OH, OW, y, amax);
 }
 
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
                  int OW, bf16_t* dx, hipStream_t s) {
-  const long total = (long)N * H * W * C;
+  const long total = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, dy,
                      amax, N, H, W, C, OH, OW, dx);
 }

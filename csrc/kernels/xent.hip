@@ -18,7 +18,7 @@ namespace ddp_amd {
 
 constexpr int XE_MAXM = 16;  // up to 1024 classes
 
-__global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ part, int G,
+__global__ __launch_bounds__(1024) void xent_kernel(const float* __restrict__ part, int G,
                                                    const float* __restrict__ bias, int C, int B,
                                                    const long long* __restrict__ labels64,
                                                    const int* __restrict__ labels32, BatchIdx bi,
@@ -27,16 +27,16 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ par
                                                    float* __restrict__ loss_out,
                                                    float* __restrict__ dbias, float gscale,
                                                    float dbias_scale) {
-  __shared__ float s_loss[4];
-  __shared__ float s_db[4][XE_MAXM * 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float s_loss[16];
+  __shared__ float s_db[4][XE_MAXM * 64];  // dbias: 4 waves only (see xent())
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int M = (C + 63) / 64;
   float db[XE_MAXM];
 #pragma unroll
   for (int m = 0; m < XE_MAXM; ++m) db[m] = 0.f;
   float lsum = 0.f;
   const int base = labels32 ? bi.base() : 0;
-  for (int b = wave; b < B; b += 4) {
+  for (int b = wave; b < B; b += nw) {
     const int label = labels64 ? (int)labels64[b] : labels32[bi.row(b, base)];
     float x[XE_MAXM];
     float mx = -INFINITY;
@@ -78,14 +78,18 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ par
     }
   }
   if (lane == 0) s_loss[wave] = lsum;
+  if (dbias) {
 #pragma unroll
-  for (int m = 0; m < XE_MAXM; ++m)
-    if (m < M) s_db[wave][lane + 64 * m] = db[m];
+    for (int m = 0; m < XE_MAXM; ++m)
+      if (m < M) s_db[wave][lane + 64 * m] = db[m];
+  }
   __syncthreads();
   // graph-replayed steps log their loss into a per-epoch history indexed by the step counter
-  if (threadIdx.x == 0 && loss_out)
-    loss_out[bi.step_ctr ? *bi.step_ctr : 0] =
-        (((s_loss[0] + s_loss[1]) + s_loss[2]) + s_loss[3]) / (float)B;
+  if (threadIdx.x == 0 && loss_out) {
+    float t = s_loss[0];
+    for (int w = 1; w < nw; ++w) t += s_loss[w];
+    loss_out[bi.step_ctr ? *bi.step_ctr : 0] = t / (float)B;
+  }
   if (dbias)
     for (int c = threadIdx.x; c < C; c += 256)
       dbias[c] = (((s_db[0][c] + s_db[1][c]) + s_db[2][c]) + s_db[3][c]) * dbias_scale;
@@ -117,7 +121,9 @@ void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,
           const int* labels32, BatchIdx bi, float* logits_out, float* dlogits, float* loss_out,
           float* dbias, float gscale, float dbias_scale, hipStream_t s) {
-  hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(256), 0, s, part, G, bias, C, B, labels64, labels32,
+  // one wave per row when there is no bias gradient to fold (it is reduced over 4 waves)
+  const int waves = dbias ? 4 : (B < 16 ? (B < 4 ? 4 : B) : 16);
+  hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(64 * waves), 0, s, part, G, bias, C, B, labels64, labels32,
                      bi, logits_out, dlogits, loss_out, dbias, gscale, dbias_scale);
 }
 

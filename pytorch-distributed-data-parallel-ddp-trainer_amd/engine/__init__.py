@@ -1,3 +1,4 @@
 from .fused_step import FusedSimpleCNNEngine, EngineOptions
+from .graph_step import GraphedStep
 
-__all__ = ["FusedSimpleCNNEngine", "EngineOptions"]
+__all__ = ["FusedSimpleCNNEngine", "EngineOptions", "GraphedStep"]

@@ -229,8 +229,36 @@ class FlatSpace:
                 with torch.no_grad():
                     gview.copy_(old.grad)
             newp.grad = gview
+            newp._ddp_amd_fs = self  # kernels find the bf16 weight copy through this
             mod._parameters[attr] = newp
         module._ddp_amd_flat = self
+        self._bf16 = None
+        self._bf16_version = -1
+
+    def bf16_params(self) -> torch.Tensor:
+        """bf16 copy of the flat parameters (the MFMA kernels' weight operand).
+
+        FusedSGD rewrites it inside its update kernel (a SHADOW_BF16 region over the whole
+        buffer), so a training step never converts weights; any other write to the fp32
+        parameters goes through torch ops, which bump the flat buffer's version counter
+        (shared by every parameter view), and the copy is rebuilt on the next call."""
+        if self._bf16 is None:
+            self._bf16 = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+        if self._bf16_version != self.params._version:
+            with torch.no_grad():
+                self._bf16.copy_(self.params)
+            self._bf16_version = self.params._version
+        return self._bf16
+
+    def bf16_view(self, p: torch.Tensor) -> torch.Tensor:
+        """The bf16 copy of parameter ``p`` (a view of this flat space), same shape."""
+        off = (p.data_ptr() - self.params.data_ptr()) // self.params.element_size()
+        return self.bf16_params()[off:off + p.numel()].view(p.shape)
+
+    def mark_bf16_fresh(self):
+        """Called by the optimizer after a step that rewrote the bf16 copy."""
+        if self._bf16 is not None:
+            self._bf16_version = self.params._version
 
     def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
         o, n = self.offsets[name], self.numels[name]
@@ -242,9 +270,10 @@ class FlatSpace:
 
     def reattach_grads(self):
         """Point every ``.grad`` back at its flat view (after a set_to_none zero_grad)."""
-        for n in self.names:
-            p = self.param(n)
-            g = self.view(self.grads, n)
+        pairs = getattr(self, "_pairs", None)  # cached; rebuilt if the first parameter was replaced
+        if pairs is None or self.param(self.names[0]) is not pairs[0][0]:
+            pairs = self._pairs = [(self.param(n), self.view(self.grads, n)) for n in self.names]
+        for p, g in pairs:
             if p.grad is None:
                 p.grad = g
             elif p.grad.data_ptr() != g.data_ptr():

@@ -3,34 +3,35 @@
 ==================  ================================================  ===========================================
 Function            forward kernels                                   backward kernels
 ==================  ================================================  ===========================================
-conv_bn_act         conv_gemm_fwd (+ fused BN sum/sumsq epilogue),    bn_bwd_reduce -> grad_reduce -> bn_bwd_apply,
-                    bn_finalize (running stats), bn_apply             conv_gemm_dgrad (transposed weight),
-                    (+ residual add + ReLU)                           conv_gemm_wgrad -> grad_reduce
+conv_bn_act         conv_gemm_fwd (+ BN sum/sumsq epilogue, or        bn_bwd (strip reduce -> dgamma/dbeta,
+                    split-K partials -> splitk_reduce + stats),       apply), conv_gemm_dgrad (OHWI weight read
+                    bn_finalize (running stats, batches tracked),     transposed in LDS), conv_gemm_wgrad (->
+                    bn_apply (+ residual add + ReLU)                  grad, or slabs -> grad_reduce)
 maxpool3x3s2        maxpool_fwd (argmax saved)                        maxpool_bwd (deterministic gather)
 global_avgpool      avgpool_fwd                                       avgpool_bwd
-linear_head         sgemm (+bias)                                     sgemm x2 (dX, dW), bias = sum
+linear_head         library GEMM (hipBLASLt) + bias                   library GEMMs
 ==================  ================================================  ===========================================
 
-Weights are fp32 OHWI masters converted to bf16 per call (the stem's 3 input
-channels are zero-padded to 4 so its K-steps pack 8 taps x 4 channels).
+Weights: the MFMA operand is the model's flat bf16 parameter copy (``FlatSpace.bf16_params``,
+refreshed by FusedSGD inside its update kernel) when the model is flattened (DDP /
+FusedSGD), else a per-call conversion.  The stem's 3 input channels are zero-padded to 4
+so its K-steps pack 8 taps x 4 channels.
+
+Gradients: weight / BN-affine / fc gradients are accumulated straight into ``param.grad``
+by the reducing kernel when allowed (:mod:`.direct_grad`), otherwise returned.
 """
 from __future__ import annotations
 
 import torch
 
 from .. import native
+from . import direct_grad
 
 BF16 = torch.bfloat16
 
 
 def _C():
     return native.require()
-
-
-def _wgrad_ppc(P: int, gx: int, gy: int, target_blocks: int = 1024) -> int:
-    chunks = max(1, target_blocks // max(1, gx * gy))
-    ppc = -(-P // chunks)
-    return max(32, -(-ppc // 32) * 32)
 
 
 def to_nhwc4(x: torch.Tensor) -> torch.Tensor:
@@ -41,77 +42,91 @@ def to_nhwc4(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def _weight_bf16(w: torch.Tensor) -> torch.Tensor:
+    fs = getattr(w, "_ddp_amd_fs", None)
+    if fs is not None:
+        return fs.bf16_view(w)
+    return w.detach().to(BF16)
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, running_mean, running_var, res, stride, pad, relu,
+    def forward(ctx, x, w, gamma, beta, running_mean, running_var, nbt, res, stride, pad, relu,
                 training, momentum, eps):
         N, H, W_, Cin = x.shape
         Cout, KH, KW, wcin = w.shape
         stem = Cin == 4 and wcin == 3
         OH, OW = (H + 2 * pad - KH) // stride + 1, (W_ + 2 * pad - KW) // stride + 1
-        wb = w.to(BF16)
-        if stem:
-            wb = torch.nn.functional.pad(wb, (0, 1))
-        wb = wb.contiguous()
+        wb = _weight_bf16(w)
+        wk = torch.nn.functional.pad(wb, (0, 1)) if stem else wb
         y = torch.empty(N, OH, OW, Cout, dtype=BF16, device=x.device)
         C = _C()
-        nblk = C.conv_gemm_fwd_blocks(x, y, KH, KW, stride, pad)
-        stats = torch.empty(nblk, 2, Cout, device=x.device) if training else None
-        C.conv_gemm_fwd(x, wb, None, y, KH, KW, stride, pad, False, stats)
         P = N * OH * OW
+        _, _, splits, rows = C.conv_gemm_plan(x, y, KH, KW, stride, pad)
+        part = torch.empty(splits * P * Cout, device=x.device) if splits > 1 else None
+        stats = torch.empty(rows, 2, Cout, device=x.device) if training else None
+        C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part)
         if training:
             mean = torch.empty(Cout, device=x.device)
             invstd = torch.empty(Cout, device=x.device)
-            C.bn_finalize(stats, nblk, Cout, float(P), eps, momentum, running_mean, running_var,
-                          mean, invstd)
+            ws = torch.empty(C.bn_finalize_groups(rows), 2, Cout, device=x.device)
+            C.bn_finalize(stats, rows, Cout, float(P), eps, momentum, running_mean, running_var,
+                          mean, invstd, nbt, ws)
         else:
             mean = running_mean.float().contiguous()
             invstd = torch.rsqrt(running_var.float() + eps).contiguous()
         out = torch.empty_like(y)
-        C.bn_apply(y, mean, invstd, gamma.contiguous(), beta.contiguous(),
+        C.bn_apply(y, mean, invstd, gamma.detach(), beta.detach(),
                    res.contiguous() if res is not None else None, bool(relu), out)
-        ctx.save_for_backward(x, w, y, out, mean, invstd, gamma)
+        ctx.save_for_backward(x, wb, y, out, mean, invstd)
+        ctx.params = (w, gamma, beta)
         ctx.cfg = (stride, pad, bool(relu), res is not None, stem, P)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, w, y, out, mean, invstd, gamma = ctx.saved_tensors
+        x, wb, y, out, mean, invstd = ctx.saved_tensors
+        w, gamma, beta = ctx.params
         stride, pad, relu, has_res, stem, P = ctx.cfg
         C = _C()
         dout = dout.to(BF16).contiguous()
         Cout, KH, KW, wcin = w.shape
-        rows = 256
-        nb = C.bn_bwd_blocks(P, rows)
-        slab = torch.empty(nb, 2 * Cout, device=dout.device)
-        C.bn_bwd_reduce(dout, out if relu else None, y, mean, invstd, slab, rows)
-        sums = torch.empty(2 * Cout, device=dout.device)
-        C.grad_reduce([(slab, 2 * Cout, 0, 2 * Cout, nb, sums, 1.0)])
+        dev = dout.device
+        # BatchNorm backward; dgamma / dbeta straight into the parameter gradients if allowed
+        gg, gb = direct_grad.grad_dst(gamma), direct_grad.grad_dst(beta)
+        direct_bn = gg is not None and gb is not None
+        if direct_bn:
+            dgamma, dbeta = gg, gb
+        else:
+            dgamma, dbeta = torch.empty(Cout, device=dev), torch.empty(Cout, device=dev)
+        ws = torch.empty(C.bn_bwd_rows(P, Cout), 2, Cout, device=dev)
+        sums = torch.empty(2 * Cout, device=dev)
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if has_res else None
-        C.bn_bwd_apply(dout, out if relu else None, y, mean, invstd, gamma.contiguous(), sums,
-                       float(P), dy, dres)
-        dgamma, dbeta = sums[Cout:].clone(), sums[:Cout].clone()
+        C.bn_bwd(dout, out if relu else None, y, mean, invstd, gamma.detach(), float(P), ws, sums,
+                 dgamma, dbeta, direct_bn, dy, dres)
+        # data gradient (the stem's input is the image: none)
         dx = None
         if ctx.needs_input_grad[0] and not stem:
-            wt = torch.empty(w.numel(), dtype=BF16, device=w.device)
-            C.transpose_w(w.contiguous(), wt)
             dx = torch.empty_like(x)
-            C.conv_gemm_dgrad(dy, wt, None, dx, KH, KW, stride, pad)
-        gx = Cout // 64
-        gy = (KH * KW + 15) // 16 if stem else KH * KW * (x.shape[3] // 64)
-        ppc = _wgrad_ppc(P, gx, gy)
+            _, _, splits, _ = C.conv_gemm_plan(x, dout, KH, KW, stride, pad, True)
+            part = torch.empty(splits * x.numel(), device=dev) if splits > 1 else None
+            C.conv_gemm_dgrad(dy, wb, None, dx, KH, KW, stride, pad, part)
+        # weight gradient
+        gw = direct_grad.grad_dst(w)
+        ppc = C.conv_gemm_wgrad_ppc(x, dy, KH, KW, stride, pad)
         chunks = C.conv_gemm_wgrad_chunks(x, dy, KH, KW, stride, pad, ppc)
-        cin = x.shape[3]
-        row = Cout * KH * KW * cin
-        wslab = torch.empty(chunks, row, device=dout.device)
-        C.conv_gemm_wgrad(dy, x, wslab, KH, KW, stride, pad, ppc)
-        dw = torch.empty(row, device=dout.device)
-        C.grad_reduce([(wslab, row, 0, row, chunks, dw, 1.0)])
-        dw = dw.view(Cout, KH, KW, cin)
-        if stem:
-            dw = dw[..., :wcin].contiguous()
-        return dx, dw, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
+        row = w.numel()
+        dw = gw if gw is not None else torch.empty(w.shape, device=dev)
+        if chunks == 1:
+            C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, gw is not None)
+        else:
+            slab = torch.empty(chunks, row, device=dev)
+            C.conv_gemm_wgrad(dy, x, slab, KH, KW, stride, pad, ppc, False)
+            C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, gw is not None)])
+        rw = None if gw is not None else dw
+        rg, rb = (None, None) if direct_bn else (dgamma, dbeta)
+        return dx, rw, rg, rb, None, None, None, dres, None, None, None, None, None, None
 
 
 class _MaxPool(torch.autograd.Function):
@@ -151,39 +166,44 @@ class _AvgPool(torch.autograd.Function):
 
 
 class _LinearHead(torch.autograd.Function):
+    """fp32 classifier head on library GEMMs (a plain [B,512]x[512,1000] GEMM)."""
+
     @staticmethod
     def forward(ctx, x, w, b):
-        B, K = x.shape
-        N = w.shape[0]
-        out = torch.empty(B, N, device=x.device)
         x = x.float().contiguous()
-        w = w.contiguous()
-        _C().sgemm(B, N, K, x, K, 1, w, 1, K, out, b.contiguous() if b is not None else None, 1.0)
-        ctx.save_for_backward(x, w)
-        ctx.has_bias = b is not None
+        out = torch.addmm(b.detach(), x, w.detach().t()) if b is not None else x @ w.detach().t()
+        ctx.save_for_backward(x)
+        ctx.params = (w, b)
         return out
 
     @staticmethod
     def backward(ctx, dl):
-        x, w = ctx.saved_tensors
-        B, K = x.shape
-        N = w.shape[0]
+        (x,) = ctx.saved_tensors
+        w, b = ctx.params
         dl = dl.float().contiguous()
-        dx = torch.empty(B, K, device=dl.device)
-        _C().sgemm(B, K, N, dl, N, 1, w, K, 1, dx, None, 1.0)
-        dw = torch.empty(N, K, device=dl.device)
-        _C().sgemm(N, K, B, dl, 1, N, x, K, 1, dw, None, 1.0)
-        db = dl.sum(0) if ctx.has_bias else None
-        return dx, dw, db
+        dx = dl @ w.detach()
+        gw = direct_grad.grad_dst(w)
+        if gw is not None:
+            gw.addmm_(dl.t(), x)
+            rw = None
+        else:
+            rw = dl.t() @ x
+        rb = None
+        if b is not None:
+            gb = direct_grad.grad_dst(b)
+            if gb is not None:
+                gb.add_(dl.sum(0))
+            else:
+                rb = dl.sum(0)
+        return dx, rw, rb
 
 
 def conv_bn_act(x, conv, bn, res=None, relu=True):
     training = bn.training
-    if training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
+    nbt = bn.num_batches_tracked if (training and bn.track_running_stats) else None
     momentum = bn.momentum if bn.momentum is not None else 0.1
     return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                            res, conv.stride, conv.padding, relu, training, momentum, bn.eps)
+                            nbt, res, conv.stride, conv.padding, relu, training, momentum, bn.eps)
 
 
 def maxpool3x3s2(x):

@@ -60,9 +60,13 @@ class FusedSGD:
         if fs.params.is_cuda:
             from .. import native
 
+            shadows = self.shadows
+            if fs._bf16 is not None:  # the model's bf16 weight copy, refreshed in the same pass
+                shadows = shadows + [(0, fs.numel, fs._bf16, 1, 0, 0, 0)]
             native.require().sgd(fs.params, fs.grads, self.momentum_buffer, g["lr"], g["momentum"],
                                  g["dampening"], g["weight_decay"], g["nesterov"], g["maximize"],
-                                 first, True, self.shadows)
+                                 first, True, shadows)
+            fs.mark_bf16_fresh()
         else:
             self._step_torch(first)
         self.steps += 1

@@ -129,6 +129,7 @@ class DistributedDataParallel(nn.Module):
         for n in self.fs.names:
             p = self.fs.param(n)
             if p.requires_grad:
+                # also fires for gradients the HIP Functions wrote in place (ops/direct_grad.py)
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(n)))
         self.allreduce_buckets_launched = 0
 

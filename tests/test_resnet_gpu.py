@@ -26,44 +26,76 @@ CASES = [  # N, H, Cin, Cout, K, stride, pad
     (2, 8, 256, 512, 3, 2, 1),
     (2, 7, 512, 512, 3, 1, 1),
 ]
+PLANS = [(0, 0, 0), (64, 64, 1), (128, 128, 1), (64, 128, 3), (128, 64, 2)]  # (bp, bc, splits); 0 = auto
+
+
+def _plan_ok(bp, bc, C):
+    return bc == 0 or C % bc == 0
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,K,s,p", CASES)
-def test_conv_gemm_fwd_dgrad_wgrad(C, N, H, Cin, Cout, K, s, p):
+@pytest.mark.parametrize("bp,bc,splits", PLANS)
+def test_conv_gemm_fwd_dgrad(C, N, H, Cin, Cout, K, s, p, bp, bc, splits):
+    """Forward (+ BN statistics) and data gradient (+ ReLU mask) of every launch plan:
+    pixel tile, channel tile, split-K (fp32 partials + fixed-order splitk_reduce)."""
     OH = (H + 2 * p - K) // s + 1
     x = rnd(N, H, H, Cin, relu=True, seed=1)
     w = rnd(Cout, K, K, Cin, scale=0.05, seed=2)
-    y = torch.empty(N, OH, OH, Cout, dtype=BF, device=dev)
-    nblk = C.conv_gemm_fwd_blocks(x, y, K, K, s, p)
-    stats = torch.empty(nblk, 2, Cout, device=dev)
-    C.conv_gemm_fwd(x, w, None, y, K, K, s, p, False, stats)
     xr = x.float().permute(0, 3, 1, 2)
     wr = w.float().permute(0, 3, 1, 2)
-    ref = F.conv2d(xr, wr, stride=s, padding=p).permute(0, 2, 3, 1)
-    assert relerr(y, ref) < 1e-2
-    yb = y.float()
-    st = stats.sum(0)
-    assert relerr(st[0], yb.sum((0, 1, 2))) < 1e-4
-    assert relerr(st[1], (yb * yb).sum((0, 1, 2))) < 1e-4
-    # data gradient
+    if _plan_ok(bp, bc, Cout):
+        y = torch.empty(N, OH, OH, Cout, dtype=BF, device=dev)
+        _, _, sp, rows = C.conv_gemm_plan(x, y, K, K, s, p, False, bp, bc, splits)
+        stats = torch.empty(rows, 2, Cout, device=dev)
+        part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
+        C.conv_gemm_fwd(x, w, None, y, K, K, s, p, False, stats, part, bp, bc, splits)
+        ref = F.conv2d(xr, wr, stride=s, padding=p).permute(0, 2, 3, 1)
+        assert relerr(y, ref) < 1e-2
+        yb = y.float()
+        st = stats.sum(0)
+        assert relerr(st[0], yb.sum((0, 1, 2))) < 1e-4
+        assert relerr(st[1], (yb * yb).sum((0, 1, 2))) < 1e-4
+    if _plan_ok(bp, bc, Cin):
+        dy = rnd(N, OH, OH, Cout, scale=0.5, seed=3)
+        rdx = torch.nn.grad.conv2d_input(xr.shape, wr, dy.float().permute(0, 3, 1, 2), stride=s,
+                                         padding=p).permute(0, 2, 3, 1)
+        for mask in (None, x):
+            dx = torch.empty_like(x)
+            _, _, sp, _ = C.conv_gemm_plan(x, dy, K, K, s, p, True, bp, bc, splits)
+            part = torch.empty(sp * x.numel(), device=dev) if sp > 1 else None
+            C.conv_gemm_dgrad(dy, w, mask, dx, K, K, s, p, part, bp, bc, splits)
+            want = rdx if mask is None else torch.where(x.float() > 0, rdx, torch.zeros_like(rdx))
+            assert relerr(dx, want) < 1e-2, (mask is not None)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,K,s,p", CASES)
+def test_conv_gemm_wgrad(C, N, H, Cin, Cout, K, s, p):
+    """Weight gradient: split over pixel chunks (slabs + fixed-order reduce, accumulate
+    mode) and one chunk written straight into the gradient (overwrite / accumulate)."""
+    OH = (H + 2 * p - K) // s + 1
+    x = rnd(N, H, H, Cin, relu=True, seed=1)
     dy = rnd(N, OH, OH, Cout, scale=0.5, seed=3)
-    wt = torch.empty(w.numel(), dtype=BF, device=dev)
-    C.transpose_w(w.float().contiguous(), wt)
-    dx = torch.empty_like(x)
-    C.conv_gemm_dgrad(dy, wt, None, dx, K, K, s, p)
-    rdx = torch.nn.grad.conv2d_input(xr.shape, wr, dy.float().permute(0, 3, 1, 2), stride=s, padding=p)
-    assert relerr(dx, rdx.permute(0, 2, 3, 1)) < 1e-2
-    # weight gradient (split-K slabs + fixed-order reduce), bitwise reproducible
+    rdw = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Cout, Cin, K, K),
+                                      dy.float().permute(0, 3, 1, 2), stride=s,
+                                      padding=p).permute(0, 2, 3, 1)
     P = N * OH * OH
+    row = Cout * K * K * Cin
     ppc = 64
     ch = C.conv_gemm_wgrad_chunks(x, dy, K, K, s, p, ppc)
-    row = Cout * K * K * Cin
     slab = torch.empty(ch, row, device=dev)
-    C.conv_gemm_wgrad(dy, x, slab, K, K, s, p, ppc)
-    dw = torch.empty(row, device=dev)
-    C.grad_reduce([(slab, row, 0, row, ch, dw, 1.0)])
-    rdw = torch.nn.grad.conv2d_weight(xr, wr.shape, dy.float().permute(0, 3, 1, 2), stride=s, padding=p)
-    assert relerr(dw.view(Cout, K, K, Cin), rdw.permute(0, 2, 3, 1)) < 2e-3
+    C.conv_gemm_wgrad(dy, x, slab, K, K, s, p, ppc, False)
+    prior = torch.randn(row, device=dev)
+    dw = prior.clone()
+    C.grad_reduce([(slab, row, 0, row, ch, dw, 1.0, True)])
+    assert relerr((dw - prior).view(Cout, K, K, Cin), rdw) < 2e-3
+    one = -(-P // 32) * 32
+    assert C.conv_gemm_wgrad_chunks(x, dy, K, K, s, p, one) == 1
+    d1 = torch.full((row,), 7.0, device=dev)
+    C.conv_gemm_wgrad(dy, x, d1, K, K, s, p, one, False)
+    assert relerr(d1.view(Cout, K, K, Cin), rdw) < 2e-3
+    d2 = prior.clone()
+    C.conv_gemm_wgrad(dy, x, d2, K, K, s, p, one, True)
+    assert relerr((d2 - prior).view(Cout, K, K, Cin), rdw) < 2e-3
 
 
 def test_stem_conv_7x7_s2():
@@ -83,29 +115,38 @@ def test_stem_conv_7x7_s2():
                    stride=2, padding=3).permute(0, 2, 3, 1)
     assert relerr(y, ref) < 1e-2
     dy = rnd(N, OH, OH, 64, seed=5)
-    ppc = 64
-    ch = C.conv_gemm_wgrad_chunks(x4, dy, 7, 7, 2, 3, ppc)
-    slab = torch.empty(ch, 64 * 49 * 4, device=dev)
-    C.conv_gemm_wgrad(dy, x4, slab, 7, 7, 2, 3, ppc)
-    dw = torch.empty(64 * 49 * 4, device=dev)
-    C.grad_reduce([(slab, 64 * 49 * 4, 0, 64 * 49 * 4, ch, dw, 1.0)])
     rdw = torch.nn.grad.conv2d_weight(x4[..., :3].float().permute(0, 3, 1, 2), (64, 3, 7, 7),
                                       dy.float().permute(0, 3, 1, 2), stride=2, padding=3)
-    assert relerr(dw.view(64, 7, 7, 4)[..., :3], rdw.permute(0, 2, 3, 1)) < 2e-3
+    ppc = 64
+    ch = C.conv_gemm_wgrad_chunks(x4, dy, 7, 7, 2, 3, ppc)
+    slab = torch.empty(ch, 64 * 49 * 3, device=dev)
+    C.conv_gemm_wgrad(dy, x4, slab, 7, 7, 2, 3, ppc, False)  # [Cout][T][3]: pad channel dropped
+    dw = torch.empty(64 * 49 * 3, device=dev)
+    C.grad_reduce([(slab, 64 * 49 * 3, 0, 64 * 49 * 3, ch, dw, 1.0)])
+    assert relerr(dw.view(64, 7, 7, 3), rdw.permute(0, 2, 3, 1)) < 2e-3
 
 
-def test_batchnorm_fwd_bwd_matches_torch(C):
-    N, H, Cc = 4, 8, 64
+@pytest.mark.parametrize("P_img,Cc", [(8, 64), (56, 64), (7, 512), (14, 256)])
+def test_batchnorm_fwd_bwd_matches_torch(C, P_img, Cc):
+    N, H = 4, P_img
     x = rnd(N, H, H, Cc, seed=6)
     res = rnd(N, H, H, Cc, seed=7)
     gamma = (torch.rand(Cc) + 0.5).to(dev)
     beta = (torch.randn(Cc) * 0.1).to(dev)
     P = N * H * H
     xf = x.float()
-    slab = torch.stack([xf.sum((0, 1, 2)), (xf * xf).sum((0, 1, 2))]).view(1, 2, Cc).contiguous()
+    # stats slab of 37 per-block partials (uneven split of the pixels)
+    cuts = torch.linspace(0, P, 38).long().tolist()
+    xs = xf.view(P, Cc)
+    slab = torch.stack([torch.stack([xs[a:b].sum(0), (xs[a:b] * xs[a:b]).sum(0)])
+                        for a, b in zip(cuts[:-1], cuts[1:])]).contiguous()
+    rows = slab.shape[0]
     rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    nbt = torch.zeros((), dtype=torch.long, device=dev)
     mean, invstd = torch.empty(Cc, device=dev), torch.empty(Cc, device=dev)
-    C.bn_finalize(slab, 1, Cc, float(P), 1e-5, 0.1, rm, rv, mean, invstd)
+    ws = torch.empty(C.bn_finalize_groups(rows), 2, Cc, device=dev)
+    C.bn_finalize(slab, rows, Cc, float(P), 1e-5, 0.1, rm, rv, mean, invstd, nbt, ws)
+    assert nbt.item() == 1
     out = torch.empty_like(x)
     C.bn_apply(x, mean, invstd, gamma, beta, res, True, out)
     # torch reference (fp32, NCHW)
@@ -120,17 +161,21 @@ def test_batchnorm_fwd_bwd_matches_torch(C):
     assert relerr(rm, bn.running_mean) < 1e-5 and relerr(rv, bn.running_var) < 1e-5
     dout = rnd(N, H, H, Cc, seed=8)
     ref.backward(dout.float().permute(0, 3, 1, 2))
-    nb = C.bn_bwd_blocks(P, 64)
-    s2 = torch.empty(nb, 2 * Cc, device=dev)
-    C.bn_bwd_reduce(dout, out, x, mean, invstd, s2, 64)
+    ws2 = torch.empty(C.bn_bwd_rows(P, Cc), 2, Cc, device=dev)
     sums = torch.empty(2 * Cc, device=dev)
-    C.grad_reduce([(s2, 2 * Cc, 0, 2 * Cc, nb, sums, 1.0)])
     dx = torch.empty_like(x)
     dres = torch.empty_like(x)
-    C.bn_bwd_apply(dout, out, x, mean, invstd, gamma, sums, float(P), dx, dres)
+    dg0, db0 = torch.randn(Cc, device=dev), torch.randn(Cc, device=dev)
+    dg, db = dg0.clone(), db0.clone()
+    C.bn_bwd(dout, out, x, mean, invstd, gamma, float(P), ws2, sums, dg, db, True, dx, dres)
     assert relerr(dx, xr.grad.permute(0, 2, 3, 1)) < 2e-2
     assert relerr(dres, rr.grad.permute(0, 2, 3, 1)) < 1e-2
     assert relerr(sums[Cc:], bn.weight.grad) < 1e-3 and relerr(sums[:Cc], bn.bias.grad) < 1e-3
+    assert relerr(dg - dg0, bn.weight.grad) < 1e-3 and relerr(db - db0, bn.bias.grad) < 1e-3
+    # fixed-order reductions: a second run is bitwise identical
+    sums2 = torch.empty_like(sums)
+    C.bn_bwd(dout, out, x, mean, invstd, gamma, float(P), ws2, sums2, None, None, False, dx, None)
+    assert torch.equal(sums, sums2)
 
 
 def test_pools_and_head(C):
@@ -196,3 +241,83 @@ def test_resnet18_hip_vs_cpu_fp32():
             assert relerr(bg, bc) < 2e-2, n
         else:
             assert torch.equal(bg.cpu(), bc), n
+
+
+def test_resnet18_direct_grads_and_bf16_weight_copy():
+    """Flattened model (FusedSGD/DDP): the HIP Functions accumulate weight / BN / fc
+    gradients straight into the flat .grad views and read the flat bf16 weight copy; the
+    gradients equal the unflattened model's returned ones (bitwise, except the fc GEMM
+    whose library kernel differs between addmm_ and mm), and the optimizer step leaves the
+    bf16 copy fresh (rewritten in the update kernel, no rebuild)."""
+    from ddp_amd.models import resnet18
+    from ddp_amd.ops import CrossEntropyLoss, FusedSGD
+
+    torch.manual_seed(0)
+    a = resnet18(num_classes=10).to(dev)
+    b = resnet18(num_classes=10).to(dev)
+    b.load_state_dict(a.state_dict())
+    opt = FusedSGD(b, lr=0.1, momentum=0.9)
+    fs = opt.flat
+    x = torch.randn(4, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (4,), device=dev)
+    CrossEntropyLoss()(a(x), y).backward()
+    for it in range(2):
+        opt.zero_grad()
+        CrossEntropyLoss()(b(x), y).backward()
+        if it == 0:
+            for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+                assert pb.grad.data_ptr() == fs.view(fs.grads, n).data_ptr(), n
+                if n.startswith("fc."):
+                    assert torch.allclose(pa.grad, pb.grad, rtol=1e-4, atol=1e-6), n
+                else:
+                    assert torch.equal(pa.grad, pb.grad), n
+        opt.step()
+        assert fs._bf16_version == fs.params._version
+        assert torch.equal(fs._bf16, fs.params.to(torch.bfloat16))
+    # a torch-side write to the parameters invalidates the copy; the next use rebuilds it
+    with torch.no_grad():
+        b.conv1.weight.mul_(0.5)
+    assert fs._bf16_version != fs.params._version
+    assert torch.equal(fs.bf16_view(b.conv1.weight), b.conv1.weight.to(torch.bfloat16))
+
+
+def test_graphed_step_equals_eager():
+    """GraphedStep (whole training step in one hipGraph: forward, backward with direct
+    gradients, FusedSGD with the bf16 weight copy, BN running stats) replays exactly the
+    eager step: bitwise-equal parameters and buffers after the same number of steps."""
+    from ddp_amd.engine import GraphedStep
+    from ddp_amd.models import resnet18
+    from ddp_amd.ops import CrossEntropyLoss, FusedSGD
+
+    xs = [torch.randn(4, 3, 64, 64, device=dev) for _ in range(2)]
+    ys = [torch.randint(0, 10, (4,), device=dev) for _ in range(2)]
+
+    def make_step(model):
+        opt = FusedSGD(model, lr=0.05, momentum=0.9, weight_decay=1e-4)
+        lossf = CrossEntropyLoss()
+
+        def step(x, y):
+            opt.zero_grad()
+            loss = lossf(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+        return step
+
+    torch.manual_seed(0)
+    e = resnet18(num_classes=10).to(dev)
+    f = resnet18(num_classes=10).to(dev)
+    f.load_state_dict(e.state_dict())
+    se, sf = make_step(e), make_step(f)
+    order = [0, 0, 1, 0, 1]  # graphed: 2 warm-up steps on its static input (xs[0]), then replays
+    for i in order:
+        le = se(xs[i], ys[i])
+    gf = GraphedStep(sf, (xs[0], ys[0]), warmup=2)
+    for i in order[2:]:
+        lf = gf(xs[i], ys[i])
+    torch.cuda.synchronize()
+    assert torch.equal(le, lf)
+    for (n, pe), (_, pf) in zip(e.named_parameters(), f.named_parameters()):
+        assert torch.equal(pe, pf), n
+    for (n, be), (_, bf) in zip(e.named_buffers(), f.named_buffers()):
+        assert torch.equal(be, bf), n
