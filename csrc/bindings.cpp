@@ -279,20 +279,20 @@ ConvGeom geom_of(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, i
   return g;
 }
 
-ConvPlan plan_of(const ConvGeom& g, bool dgrad, int bp, int bc, int splits) {
+ConvPlan plan_of(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity = -1) {
   TORCH_CHECK(bp == 0 || bp == 64 || bp == 128, "conv_gemm: pixel tile 64 or 128");
   TORCH_CHECK(bc == 0 || bc == 64 || bc == 128, "conv_gemm: channel tile 64 or 128");
   const int C = dgrad ? g.Cin : g.Cout;
   TORCH_CHECK(bc == 0 || C % bc == 0, "conv_gemm: channel tile must divide the channels");
-  return conv_gemm_plan(g, dgrad, bp, bc, splits);
+  return conv_gemm_plan(g, dgrad, bp, bc, splits, parity);
 }
 
 // (bp, bc, splits, stat_rows) of the plan; for dgrad X = dX-shaped layer input, Y = dY
 py::tuple op_conv_gemm_plan(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, int pad,
-                            bool dgrad, int bp, int bc, int splits) {
+                            bool dgrad, int bp, int bc, int splits, int parity) {
   const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
-  const ConvPlan pl = plan_of(g, dgrad, bp, bc, splits);
-  return py::make_tuple(pl.bp, pl.bc, pl.splits, dgrad ? 0 : conv_gemm_stat_rows(g, pl));
+  const ConvPlan pl = plan_of(g, dgrad, bp, bc, splits, parity);
+  return py::make_tuple(pl.bp, pl.bc, pl.splits, dgrad ? 0 : conv_gemm_stat_rows(g, pl), pl.parity);
 }
 
 void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> bias, Tensor& Y,
@@ -325,13 +325,13 @@ void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> b
 
 void op_conv_gemm_dgrad(const Tensor& dY, const Tensor& W, std::optional<Tensor> Xact, Tensor& dX,
                         int KH, int KW, int stride, int pad, std::optional<Tensor> part, int bp, int bc,
-                        int splits) {
+                        int splits, int parity) {
   check(dY, "dY", at::kBFloat16); check(W, "W", at::kBFloat16); check(dX, "dX", at::kBFloat16);
   const ConvGeom g = geom_of(dX, dY, KH, KW, stride, pad);
   TORCH_CHECK(g.Cin % 64 == 0 && g.Cout % 32 == 0, "conv_gemm_dgrad: Cin % 64, Cout % 32");
   TORCH_CHECK(W.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm_dgrad: OHWI weight shape");
   if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
-  const ConvPlan pl = plan_of(g, true, bp, bc, splits);
+  const ConvPlan pl = plan_of(g, true, bp, bc, splits, parity);
   float* pt = nullptr;
   if (pl.splits > 1) {
     TORCH_CHECK(part.has_value(), "conv_gemm_dgrad: split plan needs the fp32 `part` workspace");
@@ -610,7 +610,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 0);
   m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad, py::arg("dY"), py::arg("W"), py::arg("Xact"), py::arg("dX"),
         py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(),
-        py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0);
+        py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
   m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
     return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));
@@ -622,7 +622,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("ppc"), py::arg("accum") = false);
   m.def("conv_gemm_plan", &op_conv_gemm_plan, py::arg("X"), py::arg("Y"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("dgrad") = false, py::arg("bp") = 0, py::arg("bc") = 0,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("parity") = -1);
   m.def("bn_finalize", &op_bn_finalize);
   m.def("bn_apply", &op_bn_apply);
   m.def("bn_finalize_groups", &bn_finalize_groups);

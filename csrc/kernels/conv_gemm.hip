@@ -246,7 +246,8 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
                                                               const bf16_t* __restrict__ W,
                                                               const bf16_t* __restrict__ Xact,
                                                               bf16_t* __restrict__ dX,
-                                                              float* __restrict__ part, int ks_per) {
+                                                              float* __restrict__ part, int ks_per,
+                                                              int nsplit, int parity) {
   constexpr int AS = BC + 16;
   __shared__ __attribute__((aligned(16))) bf16_t sA[2][CG_KS * AS];
   __shared__ __attribute__((aligned(16))) bf16_t sB[2][BP * CG_RS];
@@ -257,28 +258,45 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
   constexpr int TPR = 256 / BP;
   constexpr int EPT = CG_KS / TPR;
   constexpr int ACH = CG_KS * BC / 8 / 256;  // 16-B weight chunks per thread
-  const int HW = g.H * g.W;
-  const int Ptot = g.N * HW;
+  // Stride-2 parity classes: input pixel (ih, iw) only meets taps with kh = ih + pad
+  // (mod 2), kw likewise, so each class (ih % 2, iw % 2) is a dense GEMM over its own
+  // 1..4 taps (3x3) instead of all 9 with 3/4 structural zeros.  grid.z = class x split.
+  int cls = 0, zs = blockIdx.z;
+  if (parity) {
+    cls = blockIdx.z / nsplit;
+    zs = blockIdx.z - cls * nsplit;
+  }
+  const int ph = cls >> 1, pw = cls & 1, ts = parity ? 2 : 1;
+  const int Hc = (g.H - ph + ts - 1) / ts, Wc = (g.W - pw + ts - 1) / ts;
+  const int HWc = Hc * Wc;
+  const int Pc = g.N * HWc;  // pixels of this class
   const int p0 = blockIdx.x * BP;
+  if (p0 >= Pc) return;  // block-uniform (a smaller class), before any barrier
   const int ci0b = blockIdx.y * BC;
-  const int T = g.KH * g.KW;
-  const int nk = T * (g.Cout / CG_KS);
-  const int kb = blockIdx.z * ks_per;
-  const int ke = min(nk, kb + ks_per);
+  const int kh0 = parity ? (ph + g.pad) & 1 : 0, kw0 = parity ? (pw + g.pad) & 1 : 0;
+  const int nth = (g.KH - kh0 + ts - 1) / ts, ntw = (g.KW - kw0 + ts - 1) / ts;
+  const int CK = g.Cout / CG_KS;
+  const int nk = nth * ntw * CK;
+  const int kper = parity ? (nk + nsplit - 1) / nsplit : ks_per;
+  const int kb = zs * kper;
+  const int ke = min(nk, kb + kper);
   const int bp = tid / TPR, bh = (tid % TPR) * EPT;
   const int P = p0 + bp;
-  const bool pv = P < Ptot;
+  const bool pv = P < Pc;
   int n_ = 0, ih = 0, iw = 0;
   if (pv) {
-    n_ = P / HW;
-    const int r = P - n_ * HW;
-    ih = r / g.W;
-    iw = r - ih * g.W;
+    n_ = P / HWc;
+    const int r = P - n_ * HWc;
+    const int i = r / Wc;
+    ih = ts * i + ph;
+    iw = ts * (r - i * Wc) + pw;
   }
   auto load_k = [&](int ks, bf16x8* ra, bf16x8* rb) {
-    const int tap = ks / (g.Cout / CG_KS);
-    const int co0 = (ks - tap * (g.Cout / CG_KS)) * CG_KS;
-    const int kh = tap / g.KW, kw = tap - kh * g.KW;
+    const int ti = ks / CK;
+    const int co0 = (ks - ti * CK) * CG_KS;
+    const int thi = ti / ntw;
+    const int kh = kh0 + ts * thi, kw = kw0 + ts * (ti - thi * ntw);
+    const int tap = kh * g.KW + kw;
     const int th = ih + g.pad - kh, tw = iw + g.pad - kw;
     const int oh = th / g.stride, ow = tw / g.stride;
     const bool ok = pv && th >= 0 && tw >= 0 && th - oh * g.stride == 0 && tw - ow * g.stride == 0 &&
@@ -290,7 +308,7 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
     for (int u = 0; u < ACH; ++u) {
       const int c = tid + u * 256;
       const int row = c / (BC / 8), off = (c % (BC / 8)) * 8;
-      ra[u] = ld8(W + ((long)(co0 + row) * T + tap) * g.Cin + ci0b + off);
+      ra[u] = ld8(W + ((long)(co0 + row) * (g.KH * g.KW) + tap) * g.Cin + ci0b + off);
     }
   };
   auto store_k = [&](int buf, const bf16x8* ra, const bf16x8* rb) {
@@ -345,26 +363,34 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
     if (more) store_k(cur ^ 1, ra, rb);
     __syncthreads();
   }
+  const long Ptot = (long)g.N * g.H * g.W;
 #pragma unroll
   for (int j = 0; j < TPX; ++j) {
     const int Pj = p0 + wpx * (BP / 2) + 16 * j + col;
-    if (Pj >= Ptot) continue;
+    if (Pj >= Pc) continue;
+    long gp = Pj;  // class pixel -> NHWC pixel index
+    if (parity) {
+      const int n = Pj / HWc;
+      const int r = Pj - n * HWc;
+      const int i = r / Wc;
+      gp = ((long)n * g.H + ts * i + ph) * g.W + ts * (r - i * Wc) + pw;
+    }
 #pragma unroll
     for (int i = 0; i < TCI; ++i) {
       const int ci = ci0b + wci * (BC / 2) + 16 * i + 4 * (lane >> 4);
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (PART) {
-        *reinterpret_cast<float4*>(part + ((long)blockIdx.z * Ptot + Pj) * g.Cin + ci) =
+        *reinterpret_cast<float4*>(part + ((long)zs * Ptot + gp) * g.Cin + ci) =
             make_float4(v[0], v[1], v[2], v[3]);
         continue;
       }
       if (MASK_X) {
         float xm[4];
-        unpack4(*reinterpret_cast<const uint2*>(Xact + (long)Pj * g.Cin + ci), xm);
+        unpack4(*reinterpret_cast<const uint2*>(Xact + gp * g.Cin + ci), xm);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = xm[r] > 0.f ? v[r] : 0.f;
       }
-      *reinterpret_cast<uint2*>(dX + (long)Pj * g.Cin + ci) = pack4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<uint2*>(dX + gp * g.Cin + ci) = pack4(v[0], v[1], v[2], v[3]);
     }
   }
 }
@@ -594,32 +620,51 @@ __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const 
 //  * the forward takes 64-pixel tiles when 128-pixel ones give < 512 blocks, and
 //    64x64 tiles for 1x1 convolutions (2-8 K-steps: more blocks beat reuse);
 //  * the data gradient keeps 128-pixel tiles (its gather is the costlier operand).
-ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits) {
+ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity) {
   ConvPlan pl{};
-  const long P = dgrad ? (long)g.N * g.H * g.W : (long)g.N * g.OH * g.OW;
   const int C = dgrad ? g.Cin : g.Cout;     // GEMM rows
   const int T = g.KH * g.KW;
   const bool stem = !dgrad && g.Cin == 4;
-  const int nk = stem ? (T + 7) / 8 : T * ((dgrad ? g.Cout : g.Cin) / CG_KS);
+  pl.parity = (dgrad && g.stride == 2 && parity != 0) ? 1 : 0;
+  // pixels per GEMM (the largest parity class) and K-steps (the class with most taps)
+  const long P = !dgrad ? (long)g.N * g.OH * g.OW
+                        : pl.parity ? (long)g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2) : (long)g.N * g.H * g.W;
+  const int taps = pl.parity ? ((g.KH + 1) / 2) * ((g.KW + 1) / 2) : T;
+  const int nk = stem ? (T + 7) / 8 : taps * ((dgrad ? g.Cout : g.Cin) / CG_KS);
+  const int classes = pl.parity ? 4 : 1;
   const bool pointwise = T == 1;
   int c = bc ? bc : (C % 128 == 0 ? 128 : 64);
   if (!bc && !dgrad && pointwise) c = 64;
   if (stem) c = 64;
   pl.bc = c;
-  auto blocks = [&](int bpx) { return ((P + bpx - 1) / bpx) * (long)(C / pl.bc); };
+  auto blocks = [&](int bpx) { return classes * ((P + bpx - 1) / bpx) * (long)(C / pl.bc); };
+  // parity classes: the 1x1 downsample has one live class (64 x 64 tiles), a 3x3 takes
+  // the narrower channel tile when the grid is small (more blocks beat K splits)
+  if (pl.parity && !bc && (pointwise || blocks(128) < 256)) pl.bc = c = 64;
   if (bp) pl.bp = bp;
+  else if (pl.parity && pointwise) pl.bp = 64;
   else if (dgrad || stem) pl.bp = 128;
   else pl.bp = (!pointwise && blocks(128) >= 512) ? 128 : 64;
   if (stem) pl.bp = 128;
   int s = splits;
-  if (s <= 0) s = nk >= 72 ? nk / 18 : 1;
+  if (s <= 0) {
+    if (pl.parity) {  // short per-class K: split only a small grid, >= 8 K-steps per split
+      const long base = blocks(pl.bp);
+      s = (pointwise || base >= 256) ? 1 : (int)((768 + base - 1) / base);
+      if (s > 4) s = 4;
+      if (s > nk / 8) s = nk / 8;
+    } else {
+      s = nk >= 72 ? nk / 18 : 1;
+    }
+  }
   if (s > 8) s = 8;
   if (stem || s < 1) s = 1;
   if (s > nk) s = nk;
   pl.ks_per = (nk + s - 1) / s;
-  pl.splits = (nk + pl.ks_per - 1) / pl.ks_per;  // no empty split
+  pl.splits = pl.parity ? s : (nk + pl.ks_per - 1) / pl.ks_per;  // parity: every class splits its own K
   pl.grid_x = (int)((P + pl.bp - 1) / pl.bp);
   pl.grid_y = C / pl.bc;
+  pl.grid_z = classes * pl.splits;
   return pl;
 }
 
@@ -677,9 +722,9 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
 
 void conv_gemm_dgrad(const ConvGeom& g, const ConvPlan& pl, const bf16_t* dY, const bf16_t* W,
                      const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s) {
-  const dim3 grid(pl.grid_x, pl.grid_y, pl.splits);
-  const int kp = pl.ks_per;
-#define CGD(BP, BC, MX, PT) hipLaunchKernelGGL((conv_gemm_dgrad_kernel<BP, BC, MX, PT>), grid, dim3(256), 0, s, g, dY, W, Xact, dX, part, kp)
+  const dim3 grid(pl.grid_x, pl.grid_y, pl.grid_z);
+  const int kp = pl.ks_per, ns = pl.splits, par = pl.parity;
+#define CGD(BP, BC, MX, PT) hipLaunchKernelGGL((conv_gemm_dgrad_kernel<BP, BC, MX, PT>), grid, dim3(256), 0, s, g, dY, W, Xact, dX, part, kp, ns, par)
 #define CGD_BP(BP, BC)                     \
   if (pl.splits > 1) CGD(BP, BC, false, true); \
   else if (Xact) CGD(BP, BC, true, false); \

@@ -47,10 +47,11 @@ struct ConvGeom {
 };
 // launch plan: pixel tile bp (64/128), channel tile bc (64/128), K splits (grid.z)
 struct ConvPlan {
-  int bp, bc, splits, ks_per, grid_x, grid_y;
+  int bp, bc, splits, ks_per, grid_x, grid_y, grid_z;
+  int parity;  // dgrad, stride 2: one dense GEMM per input-pixel parity class
 };
-// bp / bc / splits = 0: chosen for >= ~2 blocks per CU
-ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits);
+// bp / bc / splits = 0, parity = -1: chosen (tuned on ResNet-18, see conv_gemm.hip)
+ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity = -1);
 int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl);  // BN stats slab rows (fwd)
 // splits > 1: `part` = fp32 workspace [splits][P][C]; no bias / ReLU on the split path
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,

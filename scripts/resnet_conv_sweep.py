@@ -63,29 +63,34 @@ def main():
                 continue
             res = {}
             C_rows = Cout if kind == "fwd" else Cin
-            for bp, bc, s in [(0, 0, 0)] + plans:
+            pars = (-1, 0) if (kind == "dgrad" and st == 2) else (-1,)
+            for (bp, bc, s), par in itertools.product([(0, 0, 0)] + plans, pars):
                 if bc and C_rows % bc:
                     continue
                 if Cin == 4 and (bp, bc, s) != (0, 0, 0):
                     continue
+                if bp == 0 and par != -1:
+                    continue
                 if kind == "fwd":
-                    pbp, pbc, sp, nrows = C.conv_gemm_plan(x, y, K, K, st, pd, False, bp, bc, s)
+                    pbp, pbc, sp, nrows, used = C.conv_gemm_plan(x, y, K, K, st, pd, False, bp, bc, s)
                     stats = torch.empty(nrows, 2, Cout, device=dev)
                     part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
                     fn = lambda: C.conv_gemm_fwd(x, w, None, y, K, K, st, pd, False, stats, part, bp, bc, s)  # noqa: E731
                 else:
-                    pbp, pbc, sp, _ = C.conv_gemm_plan(x, dy, K, K, st, pd, True, bp, bc, s)
+                    pbp, pbc, sp, _, used = C.conv_gemm_plan(x, dy, K, K, st, pd, True, bp, bc, s, par)
                     part = torch.empty(sp * x.numel(), device=dev) if sp > 1 else None
-                    fn = lambda: C.conv_gemm_dgrad(dy, w, None, dx, K, K, st, pd, part, bp, bc, s)  # noqa: E731
-                key = "auto" if bp == 0 else f"{pbp}x{pbc}/s{sp}"
+                    fn = lambda: C.conv_gemm_dgrad(dy, w, None, dx, K, K, st, pd, part, bp, bc, s, par)  # noqa: E731
+                tag = f"{pbp}x{pbc}/s{sp}" + ("/par" if kind == "dgrad" and used else "")
+                key = "auto" if bp == 0 else tag
                 if bp and key in res:
                     continue
-                res[key] = (round(timeit(fn, a.iters), 2), f"{pbp}x{pbc}/s{sp}")
+                res[key] = (round(timeit(fn, a.iters), 2), tag)
             best = min(((v[0], v[1]) for k, v in res.items() if k != "auto"), default=res["auto"])
             flops = 2.0 * N * OH * OH * Cout * K * K * (3 if Cin == 4 else Cin)
             r = {"layer": name, "kind": kind, "auto_us": res["auto"][0], "auto_plan": res["auto"][1],
                  "best_us": best[0], "best_plan": best[1],
-                 "auto_tflops": round(flops / res["auto"][0] / 1e6, 1)}
+                 "auto_tflops": round(flops / res["auto"][0] / 1e6, 1),
+                 "all": {k: v[0] for k, v in res.items()}}
             rows.append(r)
             print(json.dumps(r), flush=True)
         # weight gradient at the auto chunking of resnet_fn

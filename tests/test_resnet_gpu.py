@@ -45,7 +45,7 @@ def test_conv_gemm_fwd_dgrad(C, N, H, Cin, Cout, K, s, p, bp, bc, splits):
     wr = w.float().permute(0, 3, 1, 2)
     if _plan_ok(bp, bc, Cout):
         y = torch.empty(N, OH, OH, Cout, dtype=BF, device=dev)
-        _, _, sp, rows = C.conv_gemm_plan(x, y, K, K, s, p, False, bp, bc, splits)
+        _, _, sp, rows, _ = C.conv_gemm_plan(x, y, K, K, s, p, False, bp, bc, splits)
         stats = torch.empty(rows, 2, Cout, device=dev)
         part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
         C.conv_gemm_fwd(x, w, None, y, K, K, s, p, False, stats, part, bp, bc, splits)
@@ -59,13 +59,16 @@ def test_conv_gemm_fwd_dgrad(C, N, H, Cin, Cout, K, s, p, bp, bc, splits):
         dy = rnd(N, OH, OH, Cout, scale=0.5, seed=3)
         rdx = torch.nn.grad.conv2d_input(xr.shape, wr, dy.float().permute(0, 3, 1, 2), stride=s,
                                          padding=p).permute(0, 2, 3, 1)
-        for mask in (None, x):
-            dx = torch.empty_like(x)
-            _, _, sp, _ = C.conv_gemm_plan(x, dy, K, K, s, p, True, bp, bc, splits)
-            part = torch.empty(sp * x.numel(), device=dev) if sp > 1 else None
-            C.conv_gemm_dgrad(dy, w, mask, dx, K, K, s, p, part, bp, bc, splits)
-            want = rdx if mask is None else torch.where(x.float() > 0, rdx, torch.zeros_like(rdx))
-            assert relerr(dx, want) < 1e-2, (mask is not None)
+        # stride 2: the parity-class decomposition (auto) and the plain 9-tap GEMM
+        for par in ((-1, 0) if s == 2 else (-1,)):
+            for mask in (None, x):
+                dx = torch.full_like(x, 3.0)  # every element must be written (zeros included)
+                _, _, sp, _, used = C.conv_gemm_plan(x, dy, K, K, s, p, True, bp, bc, splits, par)
+                assert used == (1 if (s == 2 and par != 0) else 0)
+                part = torch.empty(sp * x.numel(), device=dev) if sp > 1 else None
+                C.conv_gemm_dgrad(dy, w, mask, dx, K, K, s, p, part, bp, bc, splits, par)
+                want = rdx if mask is None else torch.where(x.float() > 0, rdx, torch.zeros_like(rdx))
+                assert relerr(dx, want) < 1e-2, (par, mask is not None)
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,K,s,p", CASES)
