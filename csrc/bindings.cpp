@@ -434,6 +434,19 @@ void op_maxpool_bwd(const Tensor& dy, const Tensor& amax, Tensor& dx) {
   kcheck();
 }
 
+void op_image_gather_nhwc4(const Tensor& imgs, const Tensor& idx, Tensor& out) {
+  TORCH_CHECK(imgs.is_cuda() && imgs.scalar_type() == at::kByte && imgs.is_contiguous() && imgs.dim() == 4 &&
+              imgs.size(3) == 3, "images: contiguous uint8 [N,H,W,3] on the GPU");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.dim() == 1, "idx: int64 [B]");
+  check(out, "out", at::kBFloat16);
+  TORCH_CHECK(out.dim() == 4 && out.size(0) == idx.size(0) && out.size(1) == imgs.size(1) &&
+              out.size(2) == imgs.size(2) && out.size(3) == 4, "out: bf16 [B,H,W,4]");
+  if (idx.numel() == 0) return;
+  image_gather_nhwc4(imgs.data_ptr<unsigned char>(), reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()),
+                     (int)idx.size(0), (int)(imgs.size(1) * imgs.size(2)), imgs.size(0), bf(out), cur_stream());
+  kcheck();
+}
+
 void op_avgpool_fwd(const Tensor& x, Tensor& y) {
   check(x, "x", at::kBFloat16); check(y, "y", at::kFloat);
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
@@ -631,6 +644,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &op_maxpool_fwd);
   m.def("maxpool_bwd", &op_maxpool_bwd);
   m.def("avgpool_fwd", &op_avgpool_fwd);
+  m.def("image_gather_nhwc4", &op_image_gather_nhwc4);
   m.def("avgpool_bwd", &op_avgpool_bwd);
   m.def("sgemm", &op_sgemm);
   m.def("transpose_w", &op_transpose_w);

@@ -83,6 +83,8 @@ void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf
                  unsigned char* amax, hipStream_t s);
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
                  int OW, bf16_t* dx, hipStream_t s);
+void image_gather_nhwc4(const unsigned char* imgs, const long long* idx, int B, int HW, long N,
+                        bf16_t* out, hipStream_t s);
 void avgpool_fwd(const bf16_t* x, int N, int HW, int C, float* y, hipStream_t s);
 void avgpool_bwd(const float* dy, int N, int HW, int C, bf16_t* dx, hipStream_t s);
 void sgemm(int M, int N, int K, const void* A, bool a_bf16, long sam, long sak, const void* B,

@@ -393,6 +393,25 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int HW, 
   dx[i] = f2bf(dy[(long)n * C + c] / (float)HW);
 }
 
+// ---------------------------------------------------------------- input pipeline
+// Device-resident uint8 RGB images [N][HW][3] + batch indices -> the stem's input:
+// NHWC bf16 [B][HW][4] = u8 / 255 with the 4th channel zero (one pixel per thread,
+// 3-byte read, 8-byte write).
+__global__ __launch_bounds__(256) void image_gather_nhwc4_kernel(const unsigned char* __restrict__ imgs,
+                                                                 const long long* __restrict__ idx,
+                                                                 int B, int HW, long N,
+                                                                 bf16_t* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * HW) return;
+  const int b = (int)(i / HW);
+  const int p = (int)(i - (long)b * HW);
+  long n = idx[b];
+  n = n < 0 ? 0 : (n >= N ? N - 1 : n);  // host validates; never read out of bounds
+  const unsigned char* src = imgs + (n * HW + p) * 3;
+  const float k = 1.f / 255.f;
+  *reinterpret_cast<uint2*>(out + i * 4) = pack4(src[0] * k, src[1] * k, src[2] * k, 0.f);
+}
+
 // ---------------------------------------------------------------- small fp32 GEMM
 // C[m][n] = alpha * sum_k A(m,k) B(k,n) + (bias ? bias[n] : 0), A(m,k) = A[m*sam + k*sak],
 // B(k,n) = B[k*sbk + n*sbn]; A/B element type float or bf16 (template).  16x16 LDS
@@ -527,6 +546,13 @@ void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int 
   const long total = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, dy,
                      amax, N, H, W, C, OH, OW, dx);
+}
+
+void image_gather_nhwc4(const unsigned char* imgs, const long long* idx, int B, int HW, long N,
+                        bf16_t* out, hipStream_t s) {
+  const long total = (long)B * HW;
+  hipLaunchKernelGGL(image_gather_nhwc4_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     imgs, idx, B, HW, N, out);
 }
 
 void avgpool_fwd(const bf16_t* x, int N, int HW, int C, float* y, hipStream_t s) {

@@ -31,7 +31,7 @@ class GraphedStep:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(max(1, warmup)):
-                step_fn(*self.static)
+                self.warmup_out = step_fn(*self.static)  # the last warm-up step's result
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):

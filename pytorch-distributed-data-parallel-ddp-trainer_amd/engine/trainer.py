@@ -8,6 +8,11 @@ with the reference's bugs fixed and the hot loop replaced:
 * GPU ``--engine module``: the module path (HIP autograd Functions + our DDP with
   the native C++ reducer) - the reference's loop shape, kernel-for-kernel on HIP;
 * CPU: gloo + the reference's loop over a DataLoader (BASELINE config 1).
+
+``model="resnet18"`` (BASELINE config 5) trains torchvision-layout ResNet-18 on
+synthetic ImageNet-shaped data through the module path (GPU: the HIP ResNet Functions,
+our DDP and the native reducer, optionally the whole step in one hipGraph; CPU: the
+PyTorch oracle), with the same launcher, logging, checkpoint and resume contract.
 """
 from __future__ import annotations
 
@@ -18,8 +23,9 @@ import time
 import torch
 import torch.distributed as dist
 
-from ..data import DeviceMNIST, DeviceMNISTLoader, get_dataloader, load_mnist
-from ..models import SimpleCNN
+from ..data import (DeviceImageLoader, DeviceImages, DeviceMNIST, DeviceMNISTLoader, get_dataloader,
+                    load_mnist, synthetic_imagenet)
+from ..models import SimpleCNN, resnet18
 from ..models.layers import flat_space
 from ..ops import CrossEntropyLoss, FusedSGD
 from ..parallel import DistributedDataParallel as DDP
@@ -51,6 +57,11 @@ class TrainOptions:
     grad_accum: int = 1               # micro-batches per optimizer step (module/CPU path)
     global_loss: bool = False         # log the all-reduced mean loss (module/CPU path, bug B14)
     pg_timeout_s: float | None = None
+    model: str = "simplecnn"          # simplecnn | resnet18 (BASELINE config 5)
+    image_size: int = 224             # resnet18: synthetic image side
+    num_classes: int = 1000           # resnet18
+    dataset_size: int = 2048          # resnet18: synthetic images resident per rank
+    graph_module: bool = False        # module path on GPU: capture each step in a hipGraph
 
 
 def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
@@ -66,8 +77,15 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
 
     if opts.seed is not None:
         torch.manual_seed(opts.seed)  # B15: reproducible init (rank 0's weights win anyway)
-    model = SimpleCNN().to(device)
-    fused = on_gpu and opts.engine == "fused"
+    if opts.model == "resnet18":
+        model = resnet18(num_classes=opts.num_classes).to(device)
+        if on_gpu and opts.engine == "fused" and rank == 0:
+            print("Rank 0: resnet18 runs on the module path (the fused engine is SimpleCNN's)", flush=True)
+    elif opts.model == "simplecnn":
+        model = SimpleCNN().to(device)
+    else:
+        raise ValueError(f"unknown model {opts.model!r}")
+    fused = on_gpu and opts.engine == "fused" and opts.model == "simplecnn"
     if fused and (opts.grad_accum != 1 or opts.global_loss):
         raise ValueError("--grad_accum / --global_loss need the module path (--engine module) "
                          "or the CPU path; the fused engine runs one micro-batch per step")
@@ -81,7 +99,11 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
         fs = ddp_model.fs
     print(f"Rank {rank} model wrapped in DDP", flush=True)
 
-    if on_gpu:
+    if opts.model == "resnet18":
+        imgs, labels = synthetic_imagenet(opts.dataset_size, opts.image_size, opts.num_classes)
+        loader = DeviceImageLoader(DeviceImages(imgs, labels, device), batch_size, world_size, rank)
+        sampler = loader.sampler
+    elif on_gpu:
         imgs, labels, src = load_mnist(opts.data_root, opts.data)
         ddata = DeviceMNIST(imgs, labels, device, src)
         loader = DeviceMNISTLoader(ddata, batch_size, world_size, rank)
@@ -132,7 +154,8 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
             nsteps = _run_module_epoch(ddp_model, loader, loss_fn, opt, device, log,
                                        opts.log_every,
                                        fault_step if fault_step is not None else opts.max_steps,
-                                       opts.grad_accum, opts.global_loss)
+                                       opts.grad_accum, opts.global_loss,
+                                       graph=on_gpu and opts.graph_module)
         if fault_step is not None:
             _inject_fault(rank, epoch, nsteps)
         if on_gpu:
@@ -179,12 +202,18 @@ def _verify_and_broadcast(fs, model, world_size):
 
 
 def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_steps,
-                      grad_accum=1, global_loss=False):
+                      grad_accum=1, global_loss=False, graph=False):
     """The reference's loop (train_ddp.py:195-202).  With ``grad_accum`` > 1 the
     optimizer steps every ``grad_accum`` batches; the first ``grad_accum - 1`` backward
     passes run under ``no_sync`` (no all-reduce) and the loss is scaled so the update
     equals one large-batch step.  A ragged tail still flushes with a synchronised
-    backward."""
+    backward.  ``graph``: full-batch steps replay one captured hipGraph (GraphedStep;
+    its capture warm-up steps are real steps on the first batch); a ragged last batch
+    runs eagerly."""
+    if graph:
+        if grad_accum != 1 or global_loss:
+            raise ValueError("--graph_module runs one micro-batch per step without loss all-reduce")
+        return _run_graphed_epoch(model, loader, loss_fn, opt, log, log_every, max_steps)
     n = 0
     nb = len(loader) if hasattr(loader, "__len__") else None
     if max_steps is not None:
@@ -217,6 +246,38 @@ def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_s
                 dist.all_reduce(lv)
                 lv = lv / dist.get_world_size()
             log(batch_idx, lv.item())
+        n += 1
+        if max_steps is not None and n >= max_steps:
+            break
+    return n
+
+
+_graphed = {}
+
+
+def _run_graphed_epoch(model, loader, loss_fn, opt, log, log_every, max_steps):
+    from .graph_step import GraphedStep
+
+    def step(x, y):
+        opt.zero_grad()
+        loss = loss_fn(model(x), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    n = 0
+    for batch_idx, (images, labels) in enumerate(loader):
+        key = (id(model), tuple(images.shape))
+        if key not in _graphed:
+            if _graphed and images.shape[0] < next(iter(_graphed))[1][0]:
+                loss = step(images, labels)  # ragged tail: eager, no new capture
+            else:
+                _graphed[key] = GraphedStep(step, (images, labels), warmup=1)  # = this batch's step
+                loss = _graphed[key].warmup_out
+        else:
+            loss = _graphed[key](images, labels)
+        if batch_idx % log_every == 0:
+            log(batch_idx, loss.item())
         n += 1
         if max_steps is not None and n >= max_steps:
             break

@@ -324,3 +324,57 @@ def test_graphed_step_equals_eager():
         assert torch.equal(pe, pf), n
     for (n, be), (_, bf) in zip(e.named_buffers(), f.named_buffers()):
         assert torch.equal(be, bf), n
+
+
+def test_image_gather_nhwc4_matches_cpu_pipeline():
+    from ddp_amd.data import DeviceImages, synthetic_imagenet
+
+    imgs, labels = synthetic_imagenet(12, 20, 7, seed=3)
+    g, c = DeviceImages(imgs, labels, dev), DeviceImages(imgs, labels, "cpu")
+    idx = torch.tensor([5, 0, 11, 5])
+    xg, yg = g.gather(idx.to(dev))
+    xc, yc = c.gather(idx)
+    assert xg.dtype == BF and tuple(xg.shape) == (4, 20, 20, 4)
+    assert torch.equal(xg[..., 3].float().cpu(), torch.zeros(4, 20, 20))
+    assert torch.equal(xg[..., :3].float().cpu(), xc.permute(0, 2, 3, 1).to(BF).float())
+    assert torch.equal(yg.cpu(), yc)
+
+
+def _resnet_trainer_worker(rank, port, ckdir, graph, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        from ddp_amd.engine.trainer import TrainOptions, ddp_train
+
+        opts = TrainOptions(checkpoint_dir=ckdir, log_every=1, model="resnet18", image_size=64,
+                            num_classes=10, dataset_size=40, momentum=0.9, graph_module=graph)
+        model = ddp_train(rank, 1, 1, 8, opts)
+        q.put(("ok", float(sum(p.double().sum() for p in model.parameters()))))
+    except Exception as e:  # noqa: BLE001
+        q.put((repr(e), None))
+
+
+def test_resnet18_trainer_gpu_graph_equals_eager(tmp_path, capfd):
+    """`train_ddp.py --model resnet18` on the GPU module path (RCCL PG of size 1): the
+    graphed loop (--graph_module: warm-up step on batch 0, then replays, eager ragged
+    tail) trains exactly like the eager loop, and writes the torchvision-layout checkpoint."""
+    import torch.multiprocessing as mp
+
+    from ddp_amd.parallel import free_port
+
+    ctx = mp.get_context("spawn")
+    res = {}
+    for graph in (False, True):
+        q = ctx.Queue()
+        p = ctx.Process(target=_resnet_trainer_worker,
+                        args=(0, free_port(), str(tmp_path / f"ck{int(graph)}"), graph, q))
+        p.start()
+        res[graph] = q.get(timeout=240)
+        p.join(timeout=60)
+        assert res[graph][0] == "ok", res[graph]
+    assert res[True][1] == res[False][1]
+    out = capfd.readouterr().out
+    assert "Epoch 0 | Batch 4 | Loss:" in out  # 40 images / batch 8: 5 steps, logged each step
+    ck = torch.load(str(tmp_path / "ck1" / "epoch_0.pt"), weights_only=True)
+    assert tuple(ck["model"]["conv1.weight"].shape) == (64, 3, 7, 7)

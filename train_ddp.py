@@ -57,6 +57,13 @@ def parse_args(argv=None):
                    help="log the all-reduced mean loss instead of rank 0's local loss (module/CPU path)")
     p.add_argument("--pg_timeout_min", type=float, default=30.0,
                    help="process-group timeout in minutes (reference default 30)")
+    p.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
+                   help="resnet18 = BASELINE config 5 on synthetic ImageNet-shaped data (module path)")
+    p.add_argument("--image_size", type=int, default=224, help="resnet18: synthetic image side")
+    p.add_argument("--num_classes", type=int, default=1000, help="resnet18: classes")
+    p.add_argument("--dataset_size", type=int, default=2048, help="resnet18: synthetic images")
+    p.add_argument("--graph_module", action="store_true",
+                   help="module path on GPU: replay each training step as one captured hipGraph")
     p.add_argument("--fault_at", default=None, metavar="EPOCH:STEP[:RANK]",
                    help="simulate a crash (os._exit) at that step; re-run to auto-resume")
     return p.parse_args(argv)
@@ -72,7 +79,9 @@ def main(argv=None):
                         max_steps=a.max_steps, metrics_json=a.metrics_json,
                         fuse_level=a.fuse_level, grad_accum=a.grad_accum,
                         global_loss=a.global_loss, pg_timeout_s=a.pg_timeout_min * 60.0,
-                        comm=a.comm,
+                        comm=a.comm, model=a.model, image_size=a.image_size,
+                        num_classes=a.num_classes, dataset_size=a.dataset_size,
+                        graph_module=a.graph_module,
                         fault=tuple(int(v) for v in a.fault_at.split(":")) if a.fault_at else None)
     launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
 
