@@ -59,8 +59,9 @@ def main():
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
     ap.add_argument("--store_a1", type=int, default=None, choices=[0, 1, 2],
                     help="fused engine: conv1 output for the backward recomputed (0) / stored for dgrad (1) / for both (2)")
-    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
-                    help="bucket all-reduce at N>1: direct xGMI kernel (RCCL fallback) or RCCL")
+    ap.add_argument("--comm", choices=["auto", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
+                    help="bucket all-reduce at N>1: auto = fastest of xGMI two-shot (xgmi2), xGMI with the "
+                         "one-shot kernel for the small bucket (xgmi1) and RCCL, timed on the node")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="control-plane process group (nccl = RCCL); gloo + --comm xgmi rehearses "
                          "N ranks on ONE GPU (RCCL refuses duplicate GPUs)")

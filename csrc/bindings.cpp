@@ -680,7 +680,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
       .def(py::init<int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("device"))
-      .def("add_channel", &XgmiComm::add_channel, py::arg("off"), py::arg("n"))
+      .def("add_channel", &XgmiComm::add_channel, py::arg("off"), py::arg("n"), py::arg("oneshot") = false)
+      .def("oneshot", &XgmiComm::oneshot)
+      .def_property_readonly("channels", &XgmiComm::channels)
       .def("set_data", [](XgmiComm& x, Tensor& t) {
         check(t, "data", at::kFloat);
         x.set_data(t.data_ptr<float>(), t.numel());
@@ -803,7 +805,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("destroy_graph", &SimpleCNNEngine::destroy_graph)
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
-      .def("set_xgmi", &SimpleCNNEngine::set_xgmi)
+      .def("set_xgmi", &SimpleCNNEngine::set_xgmi, py::arg("xgmi"), py::arg("ch0") = 0, py::arg("ch1") = 1)
       .def_property_readonly("graph_steps", &SimpleCNNEngine::graph_steps)
       .def_property_readonly("stream", [](SimpleCNNEngine& e) { return (uint64_t)e.stream(); });
 }

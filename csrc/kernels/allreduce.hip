@@ -22,6 +22,14 @@
 // buffer is double-buffered by call parity, which removes the exit barrier: call k+2
 // reuses call k's stage only after every rank passed call k+1's B0.
 //
+// One-shot variant (XgmiArgs::oneshot, small buckets): every rank publishes its whole
+// bucket to its stage buffer (parity-double-buffered), ONE barrier, then every rank pulls
+// all N published buckets and sums them in fixed rank order - each rank computes the
+// full result itself (bitwise identical everywhere), trading N x the bytes for one fewer
+// cross-GPU barrier, which wins when the bucket is a few tens of KB (SimpleCNN's
+// 75 KB conv bucket).  Stage reuse: call k+2 rewrites parity k's stage only after every
+// rank passed call k+1's barrier, i.e. finished reading call k.
+//
 // Barriers are per block: block b of every rank handles the same element range of every
 // slice, and only ever waits for block b of its peers.  Flags are monotonic per-block counters in
 // uncached memory; every spin is bounded (XgmiArgs::timeout_ticks of the 100 MHz clock):
@@ -102,6 +110,35 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
   const bool live = i < slice;
   const long par = (long)(e & 1u) * slice;
 
+  if (a.oneshot) {
+    // ---- publish my bucket element i, one barrier, sum every rank's copy in rank order
+    const long par1 = (long)(e & 1u) * a.n;
+    const bool in = i < a.n;
+    if (in) st_sys(a.stage[r] + par1 + i, a.data[r][a.off + i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    xgmi_barrier(a, 2u * e, &s_fail);
+    if (!s_fail && in) {
+      float v[XGMI_MAX_RANKS];
+#pragma unroll
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld_sys(a.stage[p] + par1 + i) : 0.f;
+      float sum = v[0];
+#pragma unroll
+      for (int p = 1; p < XGMI_MAX_RANKS; ++p)
+        if (p < N) sum += v[p];
+      const float g = sum * a.scale;
+      a.data[r][a.off + i] = g;
+      if (a.sgd.update) {
+        const long j = a.off + i;
+        float m = a.mbuf ? a.mbuf[j] : 0.f;
+        const float pn = sgd_one(a.params[j], g, &m, a.sgd);
+        a.params[j] = pn;
+        if (a.mbuf) a.mbuf[j] = m;
+        shadow_one(a.sh, j, pn);
+      }
+    }
+    if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
+    return;
+  }
   xgmi_barrier(a, 2u * e, &s_fail);  // B0
   if (!s_fail && live) {
     // ---- RS: element i of my slice, fixed-order sum over ranks 0..N-1
@@ -146,8 +183,8 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
   if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
 }
 
-int xgmi_blocks(long n, int world) {
-  const long slice = (n + world - 1) / world;
+int xgmi_blocks(long n, int world, bool oneshot) {
+  const long slice = oneshot ? n : (n + world - 1) / world;
   const long b = (slice + XGMI_THREADS - 1) / XGMI_THREADS;
   return (int)(b < 1 ? 1 : b);
 }

@@ -191,9 +191,10 @@ constexpr int XGMI_ERR_OFF = XGMI_SEQ_OFF + XGMI_MAX_BLOCKS;
 constexpr int XGMI_SIG_WORDS = XGMI_ERR_OFF + 64;
 struct XgmiArgs {
   float* data[XGMI_MAX_RANKS];    // every rank's gradient buffer (peer-mapped; [rank] = own)
-  float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats
+  float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats (one-shot: 2 x n)
   unsigned* sig[XGMI_MAX_RANKS];  // every rank's signal words (uncached)
   long off, n, slice;             // bucket offset / length in the gradient buffer; n / world rounded up
+  int oneshot;                    // 1: publish whole bucket, one barrier, every rank sums all (small buckets)
   float scale;                    // applied to the result (1: producers prescaled by 1/world)
   int rank, world;
   unsigned long long timeout_ticks;  // per barrier spin, 100 MHz ticks
@@ -207,7 +208,7 @@ struct XgmiArgs {
   ShadowSet sh;
   int* step_ctr;  // += 1 by block 0 at the end (the step's last kernel), may be null
 };
-int xgmi_blocks(long n, int world);
+int xgmi_blocks(long n, int world, bool oneshot = false);
 void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s);
 
 }  // namespace ddp_amd

@@ -163,7 +163,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       sh0.r[0] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
       sh0.r[1] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
       sh0.count = 2;
-      xgmi_->all_reduce_sgd(0, ms_, sa, P, M, sh0, nullptr);
+      xgmi_->all_reduce_sgd(xch_[0], ms_, sa, P, M, sh0, nullptr);
     } else {
       comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
     }
@@ -217,7 +217,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
       sh1.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
       sh1.count = 2;
-      xgmi_->all_reduce_sgd(1, ms_, sa, P, M, sh1, b_.step_ctr);  // the step's last kernel
+      xgmi_->all_reduce_sgd(xch_[1], ms_, sa, P, M, sh1, b_.step_ctr);  // the step's last kernel
     } else {
       comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
     }
@@ -236,13 +236,16 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   sgd_step(P, G, M, b_.n_params, sa, sh, b_.step_ctr, cs_);
 }
 
-void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x) {
+void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, int ch0, int ch1) {
   if (x) {
-    if (x->channels() != 2) throw std::runtime_error("engine: xgmi needs one channel per bucket (2)");
+    if (ch0 < 0 || ch1 < 0 || ch0 >= x->channels() || ch1 >= x->channels() || ch0 == ch1)
+      throw std::runtime_error("engine: xgmi channel indices (one per bucket) out of range");
     if (x->world() != cfg_.world) throw std::runtime_error("engine: xgmi world size mismatch");
   }
   destroy_graph();
   xgmi_ = std::move(x);
+  xch_[0] = ch0;
+  xch_[1] = ch1;
 }
 
 void SimpleCNNEngine::step(int batch, int batch_stride) {

@@ -70,7 +70,8 @@ class XgmiComm {
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
-  int add_channel(long off, long n);
+  int add_channel(long off, long n, bool oneshot = false);
+  bool oneshot(int channel) const { return ch_.at(channel).oneshot; }
   void set_data(float* data, long numel);
   std::string export_handles() const;
   void import_handles(const std::vector<std::string>& all);
@@ -88,6 +89,7 @@ class XgmiComm {
   struct Channel {
     long off = 0, n = 0, slice = 0;
     int blocks = 1;
+    bool oneshot = false;
     float* stage_local = nullptr;
     unsigned* sig_local = nullptr;
     float* stage[XGMI_MAX_RANKS] = {};
@@ -203,7 +205,8 @@ class SimpleCNNEngine {
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel (channel 0 = bucket 0, 1 = bucket 1)
   // instead of RCCL; set before capturing a graph
-  void set_xgmi(std::shared_ptr<XgmiComm> x);
+  // bucket all-reduces over the direct xGMI kernel: channel ch0 for bucket 0, ch1 for bucket 1
+  void set_xgmi(std::shared_ptr<XgmiComm> x, int ch0 = 0, int ch1 = 1);
 
  private:
   void launch_step(int batch, int batch_stride, bool first_momentum_step);
@@ -211,6 +214,7 @@ class SimpleCNNEngine {
   EngineBuffers b_;
   std::shared_ptr<Comm> comm_;
   std::shared_ptr<XgmiComm> xgmi_;
+  int xch_[2] = {0, 1};
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_;
   hipGraph_t graph_ = nullptr;

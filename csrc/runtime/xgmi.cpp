@@ -41,19 +41,21 @@ XgmiComm::~XgmiComm() {
   }
 }
 
-int XgmiComm::add_channel(long off, long n) {
+int XgmiComm::add_channel(long off, long n, bool oneshot) {
   if (imported_) throw std::runtime_error("xgmi: add channels before import_handles");
   Channel c;
   c.off = off;
   c.n = n;
+  c.oneshot = oneshot;
   c.slice = (n + world_ - 1) / world_;
-  c.blocks = xgmi_blocks(n, world_);
+  c.blocks = xgmi_blocks(n, world_, oneshot);
   if (c.blocks > XGMI_MAX_BLOCKS) throw std::runtime_error("xgmi: bucket too large for one channel");
-  DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c.stage_local), sizeof(float) * 2 * c.slice));
+  const long stage = oneshot ? n : c.slice;  // per parity
+  DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c.stage_local), sizeof(float) * 2 * stage));
   DDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c.sig_local),
                                       sizeof(unsigned) * XGMI_SIG_WORDS, hipDeviceMallocUncached));
   DDP_HIP_CHECK(hipMemset(c.sig_local, 0, sizeof(unsigned) * XGMI_SIG_WORDS));
-  DDP_HIP_CHECK(hipMemset(c.stage_local, 0, sizeof(float) * 2 * c.slice));
+  DDP_HIP_CHECK(hipMemset(c.stage_local, 0, sizeof(float) * 2 * stage));
   DDP_HIP_CHECK(hipDeviceSynchronize());
   ch_.push_back(c);
   return (int)ch_.size() - 1;
@@ -141,6 +143,7 @@ void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, fl
   a.off = c.off;
   a.n = c.n;
   a.slice = c.slice;
+  a.oneshot = c.oneshot ? 1 : 0;
   a.scale = scale;
   a.rank = rank_;
   a.world = world_;

@@ -27,6 +27,10 @@ from ..models.layers import flat_space
 from ..ops.functional import wgrad_rows
 from ..parallel.ddp import bucket_plan, bucket_ranges
 
+# buckets up to this many fp32 elements also get a one-shot xGMI channel (SimpleCNN's
+# conv bucket: 18,816 = 75 KB); the bucket must fit one kernel grid (1024 x 256)
+ONESHOT_MAX_ELEMS = 65536
+
 BF16 = torch.bfloat16
 
 
@@ -48,8 +52,10 @@ class EngineOptions:
     # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
     # wgrad role reads a1 tiles too
     store_a1: int = 0
-    # bucket all-reduce data plane at world size > 1: "xgmi" = the direct two-shot kernel
-    # (falls back to RCCL when its self-test fails), "rccl" = RCCL, "auto" = xgmi
+    # bucket all-reduce data plane at world size > 1 (the direct kernels fall back to RCCL
+    # when their self-test fails): "auto" = time two-shot xGMI, two-shot + one-shot for
+    # the small bucket, and RCCL on the node and keep the fastest; "xgmi" = the fastest
+    # of the two xGMI plans; "xgmi2" / "xgmi1" = that plan, forced; "rccl" = RCCL
     comm: str = "auto"
 
 
@@ -111,23 +117,36 @@ class FusedSimpleCNNEngine:
                    store_a1=int(self.opts.store_a1))
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
+        self.xgmi_plan = None
         self.allreduce_us = None
-        if use_comm and self.opts.comm in ("auto", "xgmi"):
-            from ..parallel.xgmi import create_xgmi, pick_data_plane
+        xch = (0, 1)
+        if use_comm and self.opts.comm in ("auto", "xgmi", "xgmi1", "xgmi2"):
+            from ..parallel.xgmi import channel_plan, create_xgmi, pick_data_plane
 
-            self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size)
-            if self.xgmi is not None and comm is not None and self.opts.comm == "auto":
-                # both data planes work here: measure one step's bucket all-reduces with
-                # each on this node and keep the faster (rank 0 decides for everyone)
-                use_x, self.allreduce_us = pick_data_plane(self.xgmi, comm, fs.grads, ranges, rank)
-                if not use_x:
+            # small buckets also get a one-shot channel (one cross-GPU barrier instead of two)
+            oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= ONESHOT_MAX_ELEMS)
+            self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size, oneshot=oneshot)
+            if self.xgmi is not None and self.opts.comm in ("xgmi1", "xgmi2"):
+                plan = "xgmi1" if self.opts.comm == "xgmi1" else "xgmi"  # forced (tests, sweeps)
+            elif self.xgmi is not None:
+                # measure one step's bucket all-reduces under each plan on this node and
+                # keep the fastest (rank 0 decides for everyone); RCCL competes in "auto"
+                plan, self.allreduce_us = pick_data_plane(
+                    self.xgmi, comm if self.opts.comm == "auto" else None, fs.grads, ranges, rank,
+                    oneshot=oneshot)
+            if self.xgmi is not None:
+                self.xgmi_plan = plan
+                if plan == "rccl":
                     self.xgmi = None
+                else:
+                    cp = channel_plan(len(ranges), oneshot)
+                    xch = tuple(cp[(b, plan == "xgmi1" and b in oneshot)] for b in range(len(ranges)))
         if use_comm and self.xgmi is None and comm is None:
             raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
-        self.comm_kind = "xgmi" if self.xgmi is not None else ("rccl" if use_comm else "none")
+        self.comm_kind = (self.xgmi_plan or "xgmi") if self.xgmi is not None else ("rccl" if use_comm else "none")
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.xgmi is not None:
-            self.eng.set_xgmi(self.xgmi)
+            self.eng.set_xgmi(self.xgmi, *xch)
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:
             self.eng.set_momentum_started(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)

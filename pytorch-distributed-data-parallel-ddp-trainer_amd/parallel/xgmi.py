@@ -1,14 +1,26 @@
 """Bootstrap of the direct xGMI all-reduce (csrc/runtime/xgmi.cpp, csrc/kernels/allreduce.hip).
 
-The data plane of the fused engine's bucket all-reduces at world size > 1: one kernel per
-bucket that pulls every peer's slice over its own xGMI link (two cross-GPU barriers, fixed
-rank order, bitwise identical on every rank) instead of an RCCL ring - see the kernel's
-header for the protocol.  SURVEY.md §5.8 (design items 3 and 4).
+The data plane of the fused engine's bucket all-reduces at world size > 1.  Each bucket
+gets one kernel that pulls over the xGMI links directly instead of running an RCCL ring:
 
-Bootstrap: every rank registers the flat gradient buffer and one channel per bucket,
-publishes its IPC handle blob in the c10d TCPStore, maps every peer's blob, then runs a
-self-test on exactly-representable patterns.  If any rank's self-test fails (or a
-barrier timed out) every rank gets ``None`` back and the caller falls back to RCCL.
+* two-shot: every rank pulls its own slice of the bucket from every peer over that peer's
+  link, sums in fixed rank order, then gathers the reduced slices back (two cross-GPU
+  barriers, bitwise identical on every rank);
+* one-shot (small buckets): every rank pulls every peer's whole bucket and sums it
+  itself (one barrier).
+
+See the kernel's header for the protocol.  SURVEY.md §5.8 (design items 3 and 4), §7.3
+step 7.
+
+Bootstrap:
+
+1. Every rank registers the flat gradient buffer and one channel per (bucket, mode).
+2. It publishes its IPC handle blob in the c10d TCPStore and maps every peer's blob.
+3. It runs a self-test on exactly-representable patterns on every channel.
+
+If any rank's self-test fails (or a barrier timed out), every rank gets ``None`` back and
+the caller falls back to RCCL.  :func:`pick_data_plane` then times the candidate plans on
+the node and keeps the fastest.
 """
 from __future__ import annotations
 
@@ -29,20 +41,27 @@ def _pattern(n: int, rank: int, device) -> torch.Tensor:
 
 
 def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
-                self_test: bool = True, verbose: bool = True):
-    """XgmiComm over ``grads`` (flat fp32, CUDA) with one channel per ``(offset, numel)``
-    bucket, or ``None`` when the direct path is unusable here (collective: every rank
-    must call it with the same buckets)."""
+                self_test: bool = True, verbose: bool = True, oneshot=()):
+    """Build an XgmiComm over ``grads`` (flat fp32, CUDA), or return ``None`` when the direct
+    path is unusable here.
+
+    Channels: ``0..len(buckets)-1`` are two-shot channels, one per ``(offset, numel)``
+    bucket. They are followed by one one-shot channel per bucket index listed in
+    ``oneshot`` (:func:`channel_plan` maps buckets to channels).
+
+    Collective: every rank must call it with the same buckets."""
     C = native.require()
     store = store or dist.distributed_c10d._get_default_store()
     gen = next(_gen)
     key = f"ddp_amd/xgmi/{gen}"
+    chans = [(int(o), int(n), False) for o, n in buckets] + \
+            [(int(buckets[b][0]), int(buckets[b][1]), True) for b in oneshot]
     ok = True
     x = None
     try:
         x = C.XgmiComm(rank, world, grads.device.index)
-        for off, n in buckets:
-            x.add_channel(int(off), int(n))
+        for off, n, one in chans:
+            x.add_channel(off, n, one)
         x.set_data(grads)
         store.set(f"{key}/h/{rank}", x.export_handles())
         blobs = [store.get(f"{key}/h/{r}") for r in range(world)]
@@ -52,7 +71,7 @@ def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
             print(f"[ddp_amd] rank {rank}: xGMI setup failed ({e}); using RCCL", file=sys.stderr)
         ok = False
     if ok and self_test:
-        ok = _self_test(x, grads, buckets, rank, world)
+        ok = _self_test(x, grads, chans, rank, world)
     store.set(f"{key}/ok/{rank}", b"1" if ok else b"0")
     agreed = all(store.get(f"{key}/ok/{r}") == b"1" for r in range(world))
     if not agreed:
@@ -62,24 +81,30 @@ def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
     return x
 
 
-def _self_test(x, grads, buckets, rank, world) -> bool:
+def channel_plan(nbuckets: int, oneshot=()) -> dict:
+    """``{(bucket, oneshot): channel}`` for a comm built by ``create_xgmi(..., oneshot=...)``."""
+    plan = {(b, False): b for b in range(nbuckets)}
+    for k, b in enumerate(oneshot):
+        plan[(b, True)] = nbuckets + k
+    return plan
+
+
+def _self_test(x, grads, chans, rank, world) -> bool:
     saved = grads.detach().clone()
     try:
         stream = torch.cuda.current_stream()
-        for rounds in range(3):  # exercises both stage-buffer parities
-            for ch, (off, n) in enumerate(buckets):
+        for ch, (off, n, _) in enumerate(chans):
+            for rounds in range(3):  # exercises both stage-buffer parities
                 grads[off:off + n].copy_(_pattern(n, rank + rounds, grads.device))
-            stream.synchronize()
-            for ch in range(len(buckets)):
+                stream.synchronize()
                 x.all_reduce(ch)
-            stream.synchronize()
-            if x.error_flags():
-                print(f"[ddp_amd] rank {rank}: xGMI barrier timeout in self-test", file=sys.stderr)
-                return False
-            for off, n in buckets:
+                stream.synchronize()
+                if x.error_flags():
+                    print(f"[ddp_amd] rank {rank}: xGMI barrier timeout in self-test", file=sys.stderr)
+                    return False
                 want = sum(_pattern(n, r + rounds, grads.device) for r in range(world))
                 if not torch.equal(grads[off:off + n], want):
-                    print(f"[ddp_amd] rank {rank}: xGMI self-test mismatch", file=sys.stderr)
+                    print(f"[ddp_amd] rank {rank}: xGMI self-test mismatch (channel {ch})", file=sys.stderr)
                     return False
         return True
     finally:
@@ -87,19 +112,36 @@ def _self_test(x, grads, buckets, rank, world) -> bool:
         torch.cuda.current_stream().synchronize()
 
 
-def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int = 30, store=None):
-    """Time the engine's two bucket all-reduces over the xGMI kernel and over RCCL on
-    this node (``iters`` back-to-back pairs each, after a warm-up); returns
-    ``(use_xgmi, {"xgmi": us, "rccl": us})`` with rank 0's measurement and decision
-    broadcast through the store, so every rank picks the same data plane.  The
-    gradient buffer's contents are clobbered (the engine rewrites every bucket each step)."""
+def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int = 30, store=None,
+                    oneshot=()):
+    """Time the engine's bucket all-reduces under every available plan on this node.
+
+    Candidates:
+
+    * ``"xgmi"``: two-shot kernels for every bucket;
+    * ``"xgmi1"``: the same, except the one-shot kernel for the buckets in ``oneshot``;
+    * ``"rccl"``: RCCL.
+
+    Each candidate runs ``iters`` back-to-back rounds after a warm-up.  Returns
+    ``(plan, {plan: us})``. ``plan`` is the fastest candidate by rank 0's measurement,
+    broadcast through the store so that every rank picks the same one.
+
+    The gradient buffer's contents are clobbered; the engine rewrites every bucket each
+    step."""
     store = store or dist.distributed_c10d._get_default_store()
     gen = next(_gen)
+    nb = len(buckets)
+    chans = channel_plan(nb, oneshot)
     views = [grads[off:off + n] for off, n in buckets]
+    plans = {"xgmi": [chans[(b, False)] for b in range(nb)]}
+    if oneshot:
+        plans["xgmi1"] = [chans[(b, b in oneshot)] for b in range(nb)]
 
-    def t_xgmi():
-        for ch in range(len(buckets)):
-            x.all_reduce(ch)
+    def run_x(chs):
+        def f():
+            for ch in chs:
+                x.all_reduce(ch)
+        return f
 
     def t_rccl():
         for v in views:
@@ -117,11 +159,16 @@ def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1000.0 / iters
 
-    tx = timed(t_xgmi)
-    tr = timed(t_rccl)
+    times = {name: timed(run_x(chs)) for name, chs in plans.items()}
+    if comm is not None:
+        times["rccl"] = timed(t_rccl)
     ok = x.error_flags() == 0
     key = f"ddp_amd/xgmi/pick/{gen}"
     if rank == 0:
-        store.set(key, f"{int(ok and tx <= tr)} {tx:.2f} {tr:.2f}".encode())
-    use, a, b = store.get(key).decode().split()
-    return use == "1", {"xgmi": float(a), "rccl": float(b)}
+        cand = {k: v for k, v in times.items() if ok or k == "rccl"}
+        best = min(cand, key=cand.get)
+        store.set(key, (best + " " + " ".join(f"{k}={v:.2f}" for k, v in times.items())).encode())
+    parts = store.get(key).decode().split()
+    best = parts[0]
+    measured = {k: float(v) for k, v in (p.split("=") for p in parts[1:])}
+    return best, measured

@@ -34,8 +34,9 @@ def _allreduce_worker(rank, world, port, q):
         n_total = 501_770 + 18_816 + 64
         buckets = [(0, 501_770), (501_770, 18_816)]
         grads = torch.zeros(n_total, device="cuda")
-        x = create_xgmi(grads, buckets, rank, world)
+        x = create_xgmi(grads, buckets, rank, world, oneshot=(1,))  # channel 2: one-shot bucket 1
         assert x is not None, "self-test failed"
+        assert x.channels == 3 and x.oneshot(2) and not x.oneshot(1)
         for it in range(4):
             g = torch.Generator().manual_seed(1000 * it + rank)
             mine = torch.randn(n_total, generator=g)
@@ -56,6 +57,15 @@ def _allreduce_worker(rank, world, port, q):
             s1 = slice(b1[0], b1[0] + b1[1])
             assert torch.equal(got[s1], want[s1] * 0.5), f"bucket 1 it {it}"
             assert torch.equal(got[b1[0] + b1[1]:], mine[b1[0] + b1[1]:]), "outside the buckets"
+            # the one-shot channel over bucket 1: same bits as the two-shot one
+            grads.copy_(mine.cuda())
+            torch.cuda.synchronize()
+            x.all_reduce(2, scale=0.5)
+            torch.cuda.synchronize()
+            assert x.error_flags() == 0
+            got1 = grads.cpu()
+            assert torch.equal(got1[s1], want[s1] * 0.5), f"one-shot bucket 1 it {it}"
+            assert torch.equal(got1[:b0[1]], mine[:b0[1]]), "one-shot touched bucket 0"
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok"))
@@ -63,7 +73,7 @@ def _allreduce_worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-def _engine_worker(rank, world, port, q):
+def _engine_worker(rank, world, port, q, comm="xgmi2"):
     try:
         _init(rank, world, port)
         from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -78,8 +88,8 @@ def _engine_worker(rank, world, port, q):
         opt = FusedSGD(model, lr=0.05, momentum=0.9)
         imgs, labels = synthetic_mnist(4096)
         eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, torch.device("cuda", 0)),
-                                   16, world, rank, None, EngineOptions(graph_steps=5, comm="xgmi"))
-        assert eng.comm_kind == "xgmi"
+                                   16, world, rank, None, EngineOptions(graph_steps=5, comm=comm))
+        assert eng.comm_kind == ("xgmi1" if comm == "xgmi1" else "xgmi"), eng.comm_kind
         eng.refresh()
         p0 = fs.params.detach().cpu().clone()
         eng.run_steps(1)
@@ -118,10 +128,10 @@ def _engine_worker(rank, world, port, q):
         q.put((rank, repr(e), None))
 
 
-def _run(worker, world, port):
+def _run(worker, world, port, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, q) + extra) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -138,8 +148,11 @@ def test_xgmi_allreduce_exact(world):
     assert all(r[1] == "ok" for r in res), res
 
 
-def test_engine_two_ranks_xgmi_identical_params():
+@pytest.mark.parametrize("comm", ["xgmi2", "xgmi1"])
+def test_engine_two_ranks_xgmi_identical_params(comm):
+    """Both xGMI plans: two-shot for both buckets, and the one-shot kernel for the small
+    conv bucket."""
     from ddp_amd.parallel import free_port
 
-    res = _run(_engine_worker, 2, free_port())
+    res = _run(_engine_worker, 2, free_port(), comm)
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]

@@ -48,9 +48,9 @@ def parse_args(argv=None):
     p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1],
                    help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
                         "1 = 4 kernels/step (default)")
-    p.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
-                   help="fused engine bucket all-reduce at world size > 1: direct xGMI kernel "
-                        "(RCCL fallback) or RCCL")
+    p.add_argument("--comm", choices=["auto", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
+                   help="fused engine bucket all-reduce at world size > 1: auto = fastest of the direct "
+                        "xGMI kernels (xgmi2 two-shot, xgmi1 + one-shot small bucket) and RCCL")
     p.add_argument("--grad_accum", type=int, default=1,
                    help="micro-batches per optimizer step (module/CPU path; DDP no_sync)")
     p.add_argument("--global_loss", action="store_true",
