@@ -184,7 +184,37 @@ void noop(int blocks, int* sink, hipStream_t s) {
   hipLaunchKernelGGL(noop_kernel, dim3(blocks), dim3(256), 0, s, sink);
 }
 
+// Few-row slabs (the ResNet weight gradients split over 1-16 pixel chunks): one thread
+// per 4 consecutive outputs summing rows 0..R-1 in order - the 64-output x 4-row-group
+// blocks of grad_reduce_kernel would leave most lanes idle and launch 10^4 tiny blocks.
+__global__ __launch_bounds__(256) void slab_reduce_rows_kernel(SlabSeg sg) {
+  const long n4 = sg.n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+    const float* src = sg.slab + sg.src_off + 4 * q;
+    float4 a = *reinterpret_cast<const float4*>(src);
+    for (int r = 1; r < sg.rows; ++r) {
+      const float4 b = *reinterpret_cast<const float4*>(src + (long)r * sg.row_stride);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    a.x *= sg.scale; a.y *= sg.scale; a.z *= sg.scale; a.w *= sg.scale;
+    float4* d = reinterpret_cast<float4*>(sg.dst + 4 * q);
+    if (sg.accum) {
+      const float4 o = *d;
+      a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+    }
+    *d = a;
+  }
+}
+
 void grad_reduce(const SlabSet& ss, hipStream_t s) {
+  if (ss.count == 1 && !ss.sgd.update && !ss.sys_store && !ss.step_ctr && ss.s[0].rows <= 16 &&
+      ss.s[0].n % 4 == 0 && ss.s[0].row_stride % 4 == 0 && ss.s[0].src_off % 4 == 0 &&
+      ((uintptr_t)ss.s[0].slab & 15) == 0 && ((uintptr_t)ss.s[0].dst & 15) == 0) {
+    const long b = (ss.s[0].n / 4 + 255) / 256;
+    hipLaunchKernelGGL(slab_reduce_rows_kernel, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, s, ss.s[0]);
+    return;
+  }
   long blocks = 0;
   for (int k = 0; k < ss.count; ++k) blocks += (ss.s[k].n + 63) / 64;
   if (blocks == 0) return;

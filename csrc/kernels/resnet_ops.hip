@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta, int accum) {
   __shared__ float sred[32][2][64];
-  __shared__ float shalf[2][128];
+  __shared__ float sfin[8][128];
   __shared__ int s_last;
   const int tg = threadIdx.x & 7, tp = threadIdx.x >> 3;
   const int cb = blockIdx.x * 64;
@@ -200,18 +200,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
   const int p0 = blockIdx.y * rpb, p1 = min(P, p0 + rpb);
-  for (int p = p0 + tp; p < p1; p += 32) {
-    const long off = (long)p * C + c0;
+  auto acc8 = [&](bf16x8 gd, bf16x8 gx, bf16x8 go) {
     float d[8], xv[8], ov[8];
-    unpack8(ld8(dout + off), d);
-    unpack8(ld8(x + off), xv);
-    if (RELU) unpack8(ld8(out + off), ov);
+    unpack8(gd, d);
+    unpack8(gx, xv);
+    if (RELU) unpack8(go, ov);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
       s[j] += d[j];
       q[j] = fmaf(d[j], (xv[j] - mu[j]) * is[j], q[j]);
     }
+  };
+  int p = p0 + tp;
+  for (; p + 32 < p1; p += 64) {  // two pixels' loads in flight
+    const long o0 = (long)p * C + c0, o1 = o0 + 32L * C;
+    const bf16x8 d0 = ld8(dout + o0), x0 = ld8(x + o0), d1 = ld8(dout + o1), x1 = ld8(x + o1);
+    const bf16x8 r0 = RELU ? ld8(out + o0) : zero8(), r1 = RELU ? ld8(out + o1) : zero8();
+    acc8(d0, x0, r0);
+    acc8(d1, x1, r1);
+  }
+  for (; p < p1; p += 32) {
+    const long o0 = (long)p * C + c0;
+    acc8(ld8(dout + o0), ld8(x + o0), RELU ? ld8(out + o0) : zero8());
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -227,23 +238,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     st_wt(ws + ((long)blockIdx.y * 2 + which) * C + cb + cc, a);
   }
   if (!last_arrival(&tickets[blockIdx.x], R, &s_last)) return;
-  const int h = threadIdx.x >> 7;
-  float a = 0.f;
+  // Fixed-order sum of the R partial rows: thread = 4 of the strip's 128 values (float4)
+  // x one of 8 row phases, up to 8 rows in flight.  Plain loads are coherent here: the
+  // rows were stored write-through and no block of this kernel read them before.
   {
-    int yy = h;
-    for (; yy + 14 < R; yy += 16) {
-      float t8[8];
+    const int vq = threadIdx.x & 31, ph = threadIdx.x >> 5;
+    const int wh = vq >> 4, c4 = (vq & 15) * 4;
+    const float* src = ws + (long)wh * C + cb + c4;
+    float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int yy = ph;
+    for (; yy + 56 < R; yy += 64) {
+      float4 t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t8[u] = ld_agent(ws + ((long)(yy + 2 * u) * 2 + which) * C + cb + cc);
+      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const float4*>(src + (long)(yy + 8 * u) * 2 * C);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a += t8[u];
+      for (int u = 0; u < 8; ++u) {
+        a4.x += t[u].x; a4.y += t[u].y; a4.z += t[u].z; a4.w += t[u].w;
+      }
     }
-    for (; yy < R; yy += 2) a += ld_agent(ws + ((long)yy * 2 + which) * C + cb + cc);
+    for (; yy < R; yy += 8) {
+      const float4 t = *reinterpret_cast<const float4*>(src + (long)yy * 2 * C);
+      a4.x += t.x; a4.y += t.y; a4.z += t.z; a4.w += t.w;
+    }
+    float* sp = &sfin[ph][wh * 64 + c4];
+    sp[0] = a4.x; sp[1] = a4.y; sp[2] = a4.z; sp[3] = a4.w;
   }
-  shalf[h][v] = a;
   __syncthreads();
   if (threadIdx.x < 128) {
-    const float tot = shalf[0][v] + shalf[1][v];
+    float tot = sfin[0][v];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) tot += sfin[k][v];
     const int c = cb + cc;
     sums[which * C + c] = tot;
     float* dst = which ? dgamma : dbeta;
