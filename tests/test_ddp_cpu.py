@@ -58,7 +58,7 @@ def _worker_ddp_equivalence(rank, ws, port, q):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("ws", [2, 3])
+@pytest.mark.parametrize("ws", [2, 3, 8])
 def test_ddp_matches_torch_ddp_gloo(ws):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
