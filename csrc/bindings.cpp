@@ -349,14 +349,15 @@ int op_conv_gemm_wgrad_chunks(const Tensor& X, const Tensor& dY, int KH, int KW,
 }
 
 void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& out, int KH, int KW, int stride,
-                        int pad, int ppc, bool accum) {
+                        int pad, int ppc, bool accum, int ks) {
   check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(out, "out", at::kFloat);
   const ConvGeom g = geom_of(X, dY, KH, KW, stride, pad);
   TORCH_CHECK((g.Cin % 64 == 0 || g.Cin == 4) && g.Cout % 64 == 0, "conv_gemm_wgrad: Cin % 64 (or 4), Cout % 64");
   TORCH_CHECK(ppc % 32 == 0 && ppc > 0, "pixels per chunk must be a multiple of 32");
   const long row = (long)g.Cout * KH * KW * (g.Cin == 4 ? 3 : g.Cin);
   TORCH_CHECK(out.numel() >= (long)conv_gemm_wgrad_chunks(g, ppc) * row, "wgrad output too small");
-  conv_gemm_wgrad(g, cbf(dY), cbf(X), out.data_ptr<float>(), ppc, accum, cur_stream());
+  TORCH_CHECK(ks == 0 || ks == 32 || ks == 64, "conv_gemm_wgrad: ks 0 (auto), 32 or 64");
+  conv_gemm_wgrad(g, cbf(dY), cbf(X), out.data_ptr<float>(), ppc, accum, cur_stream(), ks);
   kcheck();
 }
 
@@ -632,7 +633,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return conv_gemm_wgrad_ppc(geom_of(X, dY, KH, KW, st, pd));
   });
   m.def("conv_gemm_wgrad", &op_conv_gemm_wgrad, py::arg("dY"), py::arg("X"), py::arg("out"), py::arg("KH"),
-        py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("ppc"), py::arg("accum") = false);
+        py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("ppc"), py::arg("accum") = false,
+        py::arg("ks") = 0);
   m.def("conv_gemm_plan", &op_conv_gemm_plan, py::arg("X"), py::arg("Y"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("dgrad") = false, py::arg("bp") = 0, py::arg("bc") = 0,
         py::arg("splits") = 0, py::arg("parity") = -1);

@@ -479,17 +479,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // K-along-lane MFMA fragments are read with the hardware transpose.
 // STEM (Cin == 4 in X, BN = 64): the block's 64 columns are 16 taps x 4 channels (tap
 // group blockIdx.y); the output keeps only the 3 real channels: [Cout][T][3].
-template <int BM, int BN, bool STEM>
+template <int BM, int BN, bool STEM, int KS>
 __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                               const bf16_t* __restrict__ X,
                                                               float* __restrict__ out, int px_per_chunk,
                                                               int accum) {
   static_assert(!STEM || BN == 64, "stem: 16 taps x 4 channels per block");
   constexpr int RD = BM + 16, RX = BN + 16;
-  constexpr int DPT = BM / 64, XPT = BN / 64;  // 16-B staging chunks per thread
+  constexpr int DPT = BM * KS / 2048, XPT = BN * KS / 2048;  // 16-B staging chunks per thread
   constexpr int TA = BM / 32, TB = BN / 32;    // 16x16 tiles per wave
-  __shared__ __attribute__((aligned(16))) bf16_t sD[2][32 * RD];
-  __shared__ __attribute__((aligned(16))) bf16_t sX[2][32 * RX];
+  __shared__ __attribute__((aligned(16))) bf16_t sD[2][KS * RD];
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][KS * RX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int co0 = blockIdx.x * BM;
   const int T = g.KH * g.KW;
@@ -565,26 +565,29 @@ __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const 
   __syncthreads();
   int cur = 0;
   const int kA = 4 * gq + q, kB = 16 + 4 * gq + q;
-  for (int pk = pbeg; pk < pend; pk += 32) {
-    const bool more = pk + 32 < pend;
-    if (more) load(pk + 32, vd, vx);
-    bf16x8 fa[TA], fb[TB];
+  for (int pk = pbeg; pk < pend; pk += KS) {
+    const bool more = pk + KS < pend;
+    if (more) load(pk + KS, vd, vx);
 #pragma unroll
-    for (int a = 0; a < TA; ++a) {
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][kA * RD + wm + 16 * a + 4 * pq]);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][kB * RD + wm + 16 * a + 4 * pq]);
-      fa[a] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int kk = 0; kk < KS / 32; ++kk) {  // KS/32 MFMA K-steps per barrier
+      bf16x8 fa[TA], fb[TB];
+#pragma unroll
+      for (int a = 0; a < TA; ++a) {
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][(32 * kk + kA) * RD + wm + 16 * a + 4 * pq]);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sD[cur][(32 * kk + kB) * RD + wm + 16 * a + 4 * pq]);
+        fa[a] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int b = 0; b < TB; ++b) {
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][(32 * kk + kA) * RX + wn + 16 * b + 4 * pq]);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][(32 * kk + kB) * RX + wn + 16 * b + 4 * pq]);
+        fb[b] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int a = 0; a < TA; ++a)
+#pragma unroll
+        for (int b = 0; b < TB; ++b) acc[a][b] = mfma16(fa[a], fb[b], acc[a][b]);
     }
-#pragma unroll
-    for (int b = 0; b < TB; ++b) {
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][kA * RX + wn + 16 * b + 4 * pq]);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sX[cur][kB * RX + wn + 16 * b + 4 * pq]);
-      fb[b] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int a = 0; a < TA; ++a)
-#pragma unroll
-      for (int b = 0; b < TB; ++b) acc[a][b] = mfma16(fa[a], fb[b], acc[a][b]);
     if (more) store(cur ^ 1, vd, vx);
     __syncthreads();
     cur ^= 1;
@@ -780,22 +783,34 @@ int conv_gemm_wgrad_ppc(const ConvGeom& g) {
   return (int)(ppc < 32 ? 32 : ppc);
 }
 
+// ks: pixels staged per barrier (32 or 64; 0 = 32).  Staging 64 pixels halves the
+// barriers per MFMA but measured neutral on every ResNet-18 layer (conv_sweep.jsonl,
+// "auto/ks32" vs "auto/ks64"): the 64 x 64 tiles are bound by L2 traffic - dY and the
+// gathered X are re-read once per tap block - not by the barrier.
 void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out,
-                     int px_per_chunk, bool accum, hipStream_t s) {
+                     int px_per_chunk, bool accum, hipStream_t s, int ks) {
   const int ch = conv_gemm_wgrad_chunks(g, px_per_chunk);
   const int acc = (accum && ch == 1) ? 1 : 0;
   int bm, bn;
   wgrad_tile(g, &bm, &bn);
+  if (ks != 32 && ks != 64) ks = 32;
   if (g.Cin == 4) {
     const dim3 grid(g.Cout / bm, (g.KH * g.KW + 15) / 16, ch);
-    if (bm == 128) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<128, 64, true>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc);
-    else hipLaunchKernelGGL((conv_gemm_wgrad_kernel<64, 64, true>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc);
+#define CGWS(M, K) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, 64, true, K>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc)
+    if (bm == 128) { if (ks == 64) CGWS(128, 64); else CGWS(128, 32); }
+    else { if (ks == 64) CGWS(64, 64); else CGWS(64, 32); }
+#undef CGWS
     return;
   }
   const dim3 grid(g.Cout / bm, g.KH * g.KW * (g.Cin / bn), ch);
-#define CGW(M, N) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, N, false>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc)
-  if (bm == 128) { if (bn == 128) CGW(128, 128); else CGW(128, 64); }
-  else { if (bn == 128) CGW(64, 128); else CGW(64, 64); }
+#define CGW(M, N, K) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, N, false, K>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc)
+  if (ks == 64) {
+    if (bm == 128) { if (bn == 128) CGW(128, 128, 64); else CGW(128, 64, 64); }
+    else { if (bn == 128) CGW(64, 128, 64); else CGW(64, 64, 64); }
+  } else {
+    if (bm == 128) { if (bn == 128) CGW(128, 128, 32); else CGW(128, 64, 32); }
+    else { if (bn == 128) CGW(64, 128, 32); else CGW(64, 64, 32); }
+  }
 #undef CGW
 }
 

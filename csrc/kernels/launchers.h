@@ -65,7 +65,7 @@ int conv_gemm_wgrad_ppc(const ConvGeom& g);    // tuned pixels per chunk
 // one chunk: out = the gradient ([Cout][T][Cin], stem: [Cout][T][3]), `accum` adds to it;
 // several: out = slab [chunks][...] for grad_reduce
 void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out,
-                     int px_per_chunk, bool accum, hipStream_t s);
+                     int px_per_chunk, bool accum, hipStream_t s, int ks = 0);
 
 // ---- ResNet ops (resnet_ops.hip) -----------------------------------------------------
 int bn_finalize_groups(int rows);  // ws of bn_finalize: [groups][2][C]

@@ -98,8 +98,9 @@ def main():
         P = N * OH * OH
         res = {}
         auto_ppc = C.conv_gemm_wgrad_ppc(x, dy, K, K, st, pd)
-        for target in ("auto", 128, 256, 512, 1024, 2048):
-            if target == "auto":
+        for target in ("auto", "auto/ks32", "auto/ks64", 128, 256, 512, 1024, 2048):
+            ks = {"auto/ks32": 32, "auto/ks64": 64}.get(target, 0)
+            if isinstance(target, str):
                 ppc = auto_ppc
             else:
                 ppc = -(-P // max(1, target // tiles))  # ceil(P / chunks), rounded up to 32
@@ -111,9 +112,9 @@ def main():
 
             def fn():
                 if ch == 1:
-                    C.conv_gemm_wgrad(dy, x, g, K, K, st, pd, ppc, True)
+                    C.conv_gemm_wgrad(dy, x, g, K, K, st, pd, ppc, True, ks)
                 else:
-                    C.conv_gemm_wgrad(dy, x, slab, K, K, st, pd, ppc, False)
+                    C.conv_gemm_wgrad(dy, x, slab, K, K, st, pd, ppc, False, ks)
                     C.grad_reduce([(slab, row, 0, row, ch, g, 1.0, True)])
             res[target] = (round(timeit(fn, a.iters), 2), ch)
         flops = 2.0 * N * OH * OH * Cout * K * K * (3 if Cin == 4 else Cin)

@@ -93,9 +93,10 @@ def test_conv_gemm_wgrad(C, N, H, Cin, Cout, K, s, p):
     assert relerr((dw - prior).view(Cout, K, K, Cin), rdw) < 2e-3
     one = -(-P // 32) * 32
     assert C.conv_gemm_wgrad_chunks(x, dy, K, K, s, p, one) == 1
-    d1 = torch.full((row,), 7.0, device=dev)
-    C.conv_gemm_wgrad(dy, x, d1, K, K, s, p, one, False)
-    assert relerr(d1.view(Cout, K, K, Cin), rdw) < 2e-3
+    for ks in (32, 64):  # pixels staged per barrier
+        d1 = torch.full((row,), 7.0, device=dev)
+        C.conv_gemm_wgrad(dy, x, d1, K, K, s, p, one, False, ks)
+        assert relerr(d1.view(Cout, K, K, Cin), rdw) < 2e-3, ks
     d2 = prior.clone()
     C.conv_gemm_wgrad(dy, x, d2, K, K, s, p, one, True)
     assert relerr((d2 - prior).view(Cout, K, K, Cin), rdw) < 2e-3
