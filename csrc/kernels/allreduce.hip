@@ -84,9 +84,35 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
   __syncthreads();
 }
 
-// One element of the slice per thread and rank: all N loads of a thread are in flight
-// at once (RS: the N contributions; AG: the N reduced slices), so each phase is one
-// xGMI round trip.  Grid = ceil(slice / XGMI_THREADS) blocks (<= XGMI_MAX_BLOCKS).
+// Element i of the slice per thread and rank, blocks striding over 256-element chunks
+// (chunk c, c + gridDim.x, ...: the grid is capped at XGMI_GRID_CAP blocks so the
+// all-reduce, which overlaps the conv backward on its own stream, keeps few waves
+// resident while it waits in its barriers).  All N loads of a chunk - two chunks at a
+// time - are in flight at once, so each phase is about one xGMI round trip per two chunks.
+__device__ __forceinline__ float rank_sum(const XgmiArgs& a, float* const* src, long k, int N) {
+  float v[XGMI_MAX_RANKS];
+#pragma unroll
+  for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld_sys(src[p] + k) : 0.f;
+  float sum = v[0];
+#pragma unroll
+  for (int p = 1; p < XGMI_MAX_RANKS; ++p)
+    if (p < N) sum += v[p];
+  return sum;
+}
+
+// the reduced gradient g of flat bucket element k -> my gradient buffer (+ fused SGD)
+__device__ __forceinline__ void finish(const XgmiArgs& a, long k, float g) {
+  a.data[a.rank][a.off + k] = g;
+  if (a.sgd.update) {  // fused optimizer: same update on every rank
+    const long j = a.off + k;
+    float m = a.mbuf ? a.mbuf[j] : 0.f;
+    const float pn = sgd_one(a.params[j], g, &m, a.sgd);
+    a.params[j] = pn;
+    if (a.mbuf) a.mbuf[j] = m;
+    shadow_one(a.sh, j, pn);
+  }
+}
+
 __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
   __shared__ unsigned s_epoch, s_fail;
   const int N = a.world, r = a.rank;
@@ -105,78 +131,60 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
   }
   __syncthreads();
   const unsigned e = s_epoch;
-  const long slice = a.slice;  // elements per rank slice (the last rank's may be shorter)
-  const long i = (long)blockIdx.x * XGMI_THREADS + threadIdx.x;
-  const bool live = i < slice;
-  const long par = (long)(e & 1u) * slice;
+  const long G = (long)gridDim.x * XGMI_THREADS;     // elements per grid stride
+  const long i0 = (long)blockIdx.x * XGMI_THREADS + threadIdx.x;
 
   if (a.oneshot) {
-    // ---- publish my bucket element i, one barrier, sum every rank's copy in rank order
+    // ---- publish my whole bucket, one barrier, sum every rank's copy in rank order
     const long par1 = (long)(e & 1u) * a.n;
-    const bool in = i < a.n;
-    if (in) st_sys(a.stage[r] + par1 + i, a.data[r][a.off + i]);
+    for (long i = i0; i < a.n; i += G) st_sys(a.stage[r] + par1 + i, a.data[r][a.off + i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     xgmi_barrier(a, 2u * e, &s_fail);
-    if (!s_fail && in) {
-      float v[XGMI_MAX_RANKS];
+    if (!s_fail) {
+      float* src[XGMI_MAX_RANKS];
 #pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld_sys(a.stage[p] + par1 + i) : 0.f;
-      float sum = v[0];
-#pragma unroll
-      for (int p = 1; p < XGMI_MAX_RANKS; ++p)
-        if (p < N) sum += v[p];
-      const float g = sum * a.scale;
-      a.data[r][a.off + i] = g;
-      if (a.sgd.update) {
-        const long j = a.off + i;
-        float m = a.mbuf ? a.mbuf[j] : 0.f;
-        const float pn = sgd_one(a.params[j], g, &m, a.sgd);
-        a.params[j] = pn;
-        if (a.mbuf) a.mbuf[j] = m;
-        shadow_one(a.sh, j, pn);
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p) src[p] = p < N ? a.stage[p] + par1 : nullptr;
+      long i = i0;
+      for (; i + G < a.n; i += 2 * G) {
+        const float s0 = rank_sum(a, src, i, N), s1 = rank_sum(a, src, i + G, N);
+        finish(a, i, s0 * a.scale);
+        finish(a, i + G, s1 * a.scale);
       }
+      if (i < a.n) finish(a, i, rank_sum(a, src, i, N) * a.scale);
     }
     if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
     return;
   }
+  const long slice = a.slice;  // elements per rank slice (the last rank's may be shorter)
+  const long par = (long)(e & 1u) * slice;
   xgmi_barrier(a, 2u * e, &s_fail);  // B0
-  if (!s_fail && live) {
-    // ---- RS: element i of my slice, fixed-order sum over ranks 0..N-1
-    const long g = (long)r * slice + i;
-    if (g < a.n) {
-      float v[XGMI_MAX_RANKS];
+  if (!s_fail) {
+    // ---- RS: elements of my slice, fixed-order sum over ranks 0..N-1
+    float* src[XGMI_MAX_RANKS];
 #pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld_sys(a.data[p] + a.off + g) : 0.f;
-      float sum = v[0];
-#pragma unroll
-      for (int p = 1; p < XGMI_MAX_RANKS; ++p)
-        if (p < N) sum += v[p];
-      st_sys(a.stage[r] + par + i, sum);
+    for (int p = 0; p < XGMI_MAX_RANKS; ++p) src[p] = p < N ? a.data[p] + a.off + (long)r * slice : nullptr;
+    const long lim = min(slice, a.n - (long)r * slice);  // my slice's real length
+    long i = i0;
+    for (; i + G < lim; i += 2 * G) {
+      const float s0 = rank_sum(a, src, i, N), s1 = rank_sum(a, src, i + G, N);
+      st_sys(a.stage[r] + par + i, s0);
+      st_sys(a.stage[r] + par + i + G, s1);
     }
+    if (i < lim) st_sys(a.stage[r] + par + i, rank_sum(a, src, i, N));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   xgmi_barrier(a, 2u * e + 1u, &s_fail);  // B1
-  if (!s_fail && live) {
+  if (!s_fail) {
     // ---- AG: element i of every rank's reduced slice into my gradient buffer
-    float v[XGMI_MAX_RANKS];
+    for (long i = i0; i < slice; i += G) {
+      float v[XGMI_MAX_RANKS];
 #pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p)
-      v[p] = (p < N && (long)p * slice + i < a.n) ? ld_sys(a.stage[p] + par + i) : 0.f;
-    float* out = a.data[r] + a.off;
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p)
+        v[p] = (p < N && (long)p * slice + i < a.n) ? ld_sys(a.stage[p] + par + i) : 0.f;
 #pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
-      const long k = (long)p * slice + i;
-      if (p < N && k < a.n) {
-        const float g = v[p] * a.scale;
-        out[k] = g;
-        if (a.sgd.update) {  // fused optimizer: same update on every rank
-          const long j = a.off + k;
-          float m = a.mbuf ? a.mbuf[j] : 0.f;
-          const float pn = sgd_one(a.params[j], g, &m, a.sgd);
-          a.params[j] = pn;
-          if (a.mbuf) a.mbuf[j] = m;
-          shadow_one(a.sh, j, pn);
-        }
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
+        const long k = (long)p * slice + i;
+        if (p < N && k < a.n) finish(a, k, v[p] * a.scale);
       }
     }
   }
@@ -185,7 +193,8 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
 
 int xgmi_blocks(long n, int world, bool oneshot) {
   const long slice = oneshot ? n : (n + world - 1) / world;
-  const long b = (slice + XGMI_THREADS - 1) / XGMI_THREADS;
+  long b = (slice + XGMI_THREADS - 1) / XGMI_THREADS;
+  if (b > XGMI_GRID_CAP) b = XGMI_GRID_CAP;
   return (int)(b < 1 ? 1 : b);
 }
 

@@ -184,6 +184,7 @@ void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s
 
 // ---- direct two-shot xGMI all-reduce (allreduce.hip) ----------------------------------
 constexpr int XGMI_MAX_RANKS = 8, XGMI_THREADS = 256, XGMI_MAX_BLOCKS = 1024;
+constexpr int XGMI_GRID_CAP = 256;  // blocks per all-reduce launch: one per CU (block-strided chunks beyond)
 // signal words of one channel: [block][src rank] flags, [block] call counters, error word
 constexpr int XGMI_FLAG_OFF = 0;
 constexpr int XGMI_SEQ_OFF = XGMI_MAX_BLOCKS * XGMI_MAX_RANKS;
