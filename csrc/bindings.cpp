@@ -279,25 +279,25 @@ ConvGeom geom_of(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, i
   return g;
 }
 
-ConvPlan plan_of(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity = -1) {
+ConvPlan plan_of(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity = -1, int halo = -1) {
   TORCH_CHECK(bp == 0 || bp == 64 || bp == 128, "conv_gemm: pixel tile 64 or 128");
   TORCH_CHECK(bc == 0 || bc == 64 || bc == 128, "conv_gemm: channel tile 64 or 128");
   const int C = dgrad ? g.Cin : g.Cout;
   TORCH_CHECK(bc == 0 || C % bc == 0, "conv_gemm: channel tile must divide the channels");
-  return conv_gemm_plan(g, dgrad, bp, bc, splits, parity);
+  return conv_gemm_plan(g, dgrad, bp, bc, splits, parity, halo);
 }
 
 // (bp, bc, splits, stat_rows) of the plan; for dgrad X = dX-shaped layer input, Y = dY
 py::tuple op_conv_gemm_plan(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, int pad,
-                            bool dgrad, int bp, int bc, int splits, int parity) {
+                            bool dgrad, int bp, int bc, int splits, int parity, int halo) {
   const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
-  const ConvPlan pl = plan_of(g, dgrad, bp, bc, splits, parity);
-  return py::make_tuple(pl.bp, pl.bc, pl.splits, dgrad ? 0 : conv_gemm_stat_rows(g, pl), pl.parity);
+  const ConvPlan pl = plan_of(g, dgrad, bp, bc, splits, parity, halo);
+  return py::make_tuple(pl.bp, pl.bc, pl.splits, dgrad ? 0 : conv_gemm_stat_rows(g, pl), pl.parity, pl.halo);
 }
 
 void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> bias, Tensor& Y,
                       int KH, int KW, int stride, int pad, bool relu, std::optional<Tensor> stats,
-                      std::optional<Tensor> part, int bp, int bc, int splits) {
+                      std::optional<Tensor> part, int bp, int bc, int splits, int halo) {
   check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(Y, "Y", at::kBFloat16);
   const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
   TORCH_CHECK(g.Cin % 32 == 0 || (g.Cin == 4 && g.Cout % 64 == 0), "conv_gemm: Cin % 32 (or stem Cin=4)");
@@ -305,7 +305,7 @@ void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> b
   TORCH_CHECK(Wt.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm: weight shape");
   const float* bp_ = nullptr;
   if (bias) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == g.Cout, "bias"); bp_ = bias->data_ptr<float>(); }
-  ConvPlan pl = plan_of(g, false, bp, bc, (bias || relu) ? 1 : splits);
+  ConvPlan pl = plan_of(g, false, bp, bc, (bias || relu) ? 1 : splits, -1, (bias || relu) ? 0 : halo);
   float* st = nullptr;
   if (stats) {
     check(*stats, "stats", at::kFloat);
@@ -621,7 +621,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_gemm_fwd", &op_conv_gemm_fwd, py::arg("X"), py::arg("W"), py::arg("bias"), py::arg("Y"),
         py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("relu") = false,
         py::arg("stats") = py::none(), py::arg("part") = py::none(), py::arg("bp") = 0, py::arg("bc") = 0,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("halo") = -1);
   m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad, py::arg("dY"), py::arg("W"), py::arg("Xact"), py::arg("dX"),
         py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(),
         py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1);
@@ -637,7 +637,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ks") = 0);
   m.def("conv_gemm_plan", &op_conv_gemm_plan, py::arg("X"), py::arg("Y"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("dgrad") = false, py::arg("bp") = 0, py::arg("bc") = 0,
-        py::arg("splits") = 0, py::arg("parity") = -1);
+        py::arg("splits") = 0, py::arg("parity") = -1, py::arg("halo") = -1);
   m.def("bn_finalize", &op_bn_finalize);
   m.def("bn_apply", &op_bn_apply);
   m.def("bn_finalize_groups", &bn_finalize_groups);

@@ -1,0 +1,236 @@
+// Stride-1 3x3 forward convolution with an LDS halo tile (ResNet-18's 56/28/14-wide
+// 3x3 layers; conv_gemm_plan picks it, conv_gemm_fwd launches it).
+//
+// The implicit GEMM of conv_gemm.hip gathers the B operand per K-step (one tap x 32
+// input channels), so every input pixel is fetched from L2 once per tap - 9x.  Here a
+// block owns R full output rows of one image (R*W <= 128 pixels) and, per 32-channel
+// chunk, stages the (R+2) x (W+2) input halo into LDS once; the nine taps of the chunk
+// then read their B fragments straight from the halo at a tap offset.  Weights are
+// staged one kernel row (3 taps x [BC][32]) per barrier, so each barrier covers three
+// MFMA K-steps.  The next chunk's halo is loaded into registers at the chunk's first
+// barrier step and stored to the other halo buffer before the chunk switch.
+//
+// Same MFMA tiling as conv_gemm_fwd_kernel (4 waves = 2 co x 2 px, 16x16x32 bf16,
+// 128-pixel column tile of which R*W are live), same epilogues: bf16 NHWC store with the
+// per-block BatchNorm sum / sum-of-squares partials, or fp32 split-K partials for
+// splitk_reduce.  K splits run over channel chunks (grid.z).
+#include "kernels/common.h"
+#include "kernels/launchers.h"
+
+namespace ddp_amd {
+
+constexpr int HL_KS = 32;   // channels per chunk (one MFMA K-step per tap)
+constexpr int HL_RS = 40;   // LDS row stride (elements) per pixel / weight row
+constexpr int HL_BP = 128;  // pixel columns of the MFMA tile
+constexpr int HL_MAXPX = 232;     // largest halo: (R+2) x (W+2) = 4 x 58 at W = 56 (R = 2)
+
+template <int BC, int BP, bool STATS, bool PART>
+__global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
+                                                                 const bf16_t* __restrict__ Wt,
+                                                                 bf16_t* __restrict__ Y,
+                                                                 float* __restrict__ stats,
+                                                                 float* __restrict__ part, int R,
+                                                                 int chunks_per_split) {
+  constexpr int TCO = BC / 32, TPX = BP / 32;
+  constexpr int HCH = (HL_MAXPX * 4 + 255) / 256;  // 16-B halo chunks per thread
+  // weights of one kernel row (3 taps) per K-step: 3 MFMA K-steps between barriers
+  __shared__ __attribute__((aligned(16))) bf16_t sA[2][3 * BC * HL_RS];
+  __shared__ __attribute__((aligned(16))) bf16_t sH[2][HL_MAXPX * HL_RS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave >> 1, wpx = wave & 1;
+  const int W = g.W, H = g.H, Cin = g.Cin;
+  const int RG = (H + R - 1) / R;
+  const int n_ = blockIdx.x / RG, rg = blockIdx.x - n_ * RG;
+  const int oh0 = rg * R;
+  const int co0 = blockIdx.y * BC;
+  const int HW2 = W + 2, HR = R + 2, HPX = HR * HW2;
+  const int NPX = R * W;
+  const int nch = Cin / HL_KS;
+  const int c_beg = blockIdx.z * chunks_per_split;
+  const int c_end = min(nch, c_beg + chunks_per_split);
+  const int KWC = 9 * Cin;
+
+  // halo chunk h of this thread: pixel hp = (tid + 256u) / 4, quarter (8 channels) = & 3
+  auto load_halo = [&](int ch, bf16x8* rh) {
+#pragma unroll
+    for (int u = 0; u < HCH; ++u) {
+      const int e = tid + 256 * u;
+      const int hp = e >> 2, qq = e & 3;
+      rh[u] = zero8();
+      if (hp < HPX) {
+        const int hr = hp / HW2, hc = hp - hr * HW2;
+        const int ih = oh0 - 1 + hr, iw = hc - 1;
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          rh[u] = ld8(X + (((long)n_ * H + ih) * W + iw) * Cin + ch * HL_KS + qq * 8);
+      }
+    }
+  };
+  auto store_halo = [&](int buf, const bf16x8* rh) {
+#pragma unroll
+    for (int u = 0; u < HCH; ++u) {
+      const int e = tid + 256 * u;
+      const int hp = e >> 2, qq = e & 3;
+      if (hp < HPX) *reinterpret_cast<bf16x8*>(&sH[buf][hp * HL_RS + qq * 8]) = rh[u];
+    }
+  };
+  // weight rows of kernel row kh: sA row = t * BC + co (t = kw), 32 channels each
+  constexpr int WCH = 3 * BC * 4 / 256;  // 16-B weight chunks per thread
+  auto load_w = [&](int ch, int kh, bf16x8* ra) {
+#pragma unroll
+    for (int u = 0; u < WCH; ++u) {
+      const int c = tid + u * 256;
+      const int row = c >> 2, off = (c & 3) * 8;
+      const int t = row / BC, co = row - t * BC;
+      ra[u] = ld8(Wt + (long)(co0 + co) * KWC + (kh * 3 + t) * Cin + ch * HL_KS + off);
+    }
+  };
+  auto store_w = [&](int buf, const bf16x8* ra) {
+#pragma unroll
+    for (int u = 0; u < WCH; ++u) {
+      const int c = tid + u * 256;
+      *reinterpret_cast<bf16x8*>(&sA[buf][(c >> 2) * HL_RS + (c & 3) * 8]) = ra[u];
+    }
+  };
+
+  // per-lane halo base of each pixel column tile (tap offset added per K-step)
+  const int kofs = 8 * (lane >> 4), col = lane & 15;
+  int hbase[TPX];
+#pragma unroll
+  for (int j = 0; j < TPX; ++j) {
+    const int p = wpx * (BP / 2) + 16 * j + col;
+    const int r = p / W, c = p - r * W;
+    hbase[j] = p < NPX ? r * HW2 + c : 0;  // padding pixels read a valid row, masked later
+  }
+  f32x4 acc[TCO][TPX];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i)
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 ra[WCH], rh[HCH];
+  if (c_beg < c_end) {
+    load_halo(c_beg, rh);
+    load_w(c_beg, 0, ra);
+    store_halo(0, rh);
+    store_w(0, ra);
+  }
+  __syncthreads();
+  int step = 0;
+  for (int ch = c_beg; ch < c_end; ++ch) {
+    const int hb = (ch - c_beg) & 1;
+    const bool next_chunk = ch + 1 < c_end;
+    for (int kh = 0; kh < 3; ++kh, ++step) {  // one kernel row (3 taps) per barrier
+      const int cur = step & 1;
+      const bool last = kh == 2;
+      const bool more = !last || next_chunk;
+      if (more) load_w(last ? ch + 1 : ch, last ? 0 : kh + 1, ra);
+      if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int toff = kh * HW2 + kw;
+        bf16x8 a[TCO], b[TPX];
+#pragma unroll
+        for (int i = 0; i < TCO; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(kw * BC + wco * (BC / 2) + 16 * i + col) * HL_RS + kofs]);
+#pragma unroll
+        for (int j = 0; j < TPX; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
+#pragma unroll
+        for (int i = 0; i < TCO; ++i)
+#pragma unroll
+          for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      }
+      if (last && next_chunk) store_halo(hb ^ 1, rh);  // buffer hb^1 was last read a chunk ago
+      if (more) store_w(cur ^ 1, ra);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (block-local pixel p -> output row oh0 + p / W, column p % W)
+  const int Ptot = g.N * g.OH * g.OW;
+  float csum[TCO][4], csq[TCO][4];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) csum[i][r] = csq[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < TPX; ++j) {
+    const int p = wpx * (BP / 2) + 16 * j + col;
+    const int r = p / W;
+    const int oh = oh0 + r;
+    const bool ok = p < NPX && oh < g.OH;
+    const long P = ((long)n_ * g.OH + oh) * g.OW + (p - r * W);
+#pragma unroll
+    for (int i = 0; i < TCO; ++i) {
+      const int co = co0 + wco * (BC / 2) + 16 * i + 4 * (lane >> 4);
+      if (PART) {
+        if (ok)
+          *reinterpret_cast<float4*>(part + ((long)blockIdx.z * Ptot + P) * g.Cout + co) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        continue;
+      }
+      const uint2 pk = pack4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      if (ok) *reinterpret_cast<uint2*>(Y + P * g.Cout + co) = pk;
+      if (STATS) {
+        float q[4];
+        unpack4(pk, q);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const float x = ok ? q[rr] : 0.f;
+          csum[i][rr] += x;
+          csq[i][rr] = fmaf(x, x, csq[i][rr]);
+        }
+      }
+    }
+  }
+  if (STATS && !PART) {
+    __shared__ float s_st[2][2][BC];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float a = sum16(csum[i][rr]), b = sum16(csq[i][rr]);
+        if (col == 0) {
+          const int cl = wco * (BC / 2) + 16 * i + 4 * (lane >> 4) + rr;
+          s_st[wpx][0][cl] = a;
+          s_st[wpx][1][cl] = b;
+        }
+      }
+    __syncthreads();
+    for (int c = tid; c < BC; c += 256) {
+      float* dst = stats + (long)blockIdx.x * 2 * g.Cout;
+      dst[co0 + c] = s_st[0][0][c] + s_st[1][0][c];
+      dst[g.Cout + co0 + c] = s_st[0][1][c] + s_st[1][1][c];
+    }
+  }
+}
+
+// bp: pixel columns of the block's MFMA tile (128 or 64); R = bp / W full rows per block
+bool conv_halo_fits(const ConvGeom& g, int bp) {
+  if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad != 1 || g.Cin % HL_KS != 0) return false;
+  if (g.OH != g.H || g.OW != g.W || (bp != 64 && bp != 128)) return false;
+  const int R = bp / g.W;
+  return R >= 1 && (R + 2) * (g.W + 2) <= HL_MAXPX;
+}
+
+int conv_halo_rows(const ConvGeom& g, int bp) { return bp / g.W; }
+
+void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
+                   bf16_t* Y, float* stats, float* part, hipStream_t s) {
+  const int R = conv_halo_rows(g, bp);
+  const int RG = (g.H + R - 1) / R;
+  const int nch = g.Cin / HL_KS;
+  const int cps = (nch + splits - 1) / splits;
+  const dim3 grid(g.N * RG, g.Cout / bc, splits);
+#define HLF(BC, BP, ST, PT) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps)
+#define HLF_BP(BC, BP)                                  \
+  if (splits > 1) HLF(BC, BP, false, true);             \
+  else if (stats) HLF(BC, BP, true, false);             \
+  else HLF(BC, BP, false, false);
+  if (bp == 128) { if (bc == 128) { HLF_BP(128, 128) } else { HLF_BP(64, 128) } }
+  else { if (bc == 128) { HLF_BP(128, 64) } else { HLF_BP(64, 64) } }
+#undef HLF_BP
+#undef HLF
+}
+
+}  // namespace ddp_amd

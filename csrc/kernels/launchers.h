@@ -49,9 +49,15 @@ struct ConvGeom {
 struct ConvPlan {
   int bp, bc, splits, ks_per, grid_x, grid_y, grid_z;
   int parity;  // dgrad, stride 2: one dense GEMM per input-pixel parity class
+  int halo;    // fwd, stride-1 3x3: LDS halo-tile kernel (conv_halo.hip)
 };
-// bp / bc / splits = 0, parity = -1: chosen (tuned on ResNet-18, see conv_gemm.hip)
-ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity = -1);
+// bp / bc / splits = 0, parity / halo = -1: chosen (tuned on ResNet-18, see conv_gemm.hip)
+ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int parity = -1,
+                        int halo = -1);
+bool conv_halo_fits(const ConvGeom& g, int bp);
+int conv_halo_rows(const ConvGeom& g, int bp);
+void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
+                   bf16_t* Y, float* stats, float* part, hipStream_t s);
 int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl);  // BN stats slab rows (fwd)
 // splits > 1: `part` = fp32 workspace [splits][P][C]; no bias / ReLU on the split path
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,

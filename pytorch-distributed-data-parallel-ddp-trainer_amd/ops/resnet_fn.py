@@ -62,7 +62,7 @@ class _ConvBNAct(torch.autograd.Function):
         y = torch.empty(N, OH, OW, Cout, dtype=BF16, device=x.device)
         C = _C()
         P = N * OH * OW
-        _, _, splits, rows, _ = C.conv_gemm_plan(x, y, KH, KW, stride, pad)
+        _, _, splits, rows, _, _ = C.conv_gemm_plan(x, y, KH, KW, stride, pad)
         part = torch.empty(splits * P * Cout, device=x.device) if splits > 1 else None
         stats = torch.empty(rows, 2, Cout, device=x.device) if training else None
         C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part)
@@ -109,7 +109,7 @@ class _ConvBNAct(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0] and not stem:
             dx = torch.empty_like(x)
-            _, _, splits, _, _ = C.conv_gemm_plan(x, dout, KH, KW, stride, pad, True)
+            _, _, splits, _, _, _ = C.conv_gemm_plan(x, dout, KH, KW, stride, pad, True)
             part = torch.empty(splits * x.numel(), device=dev) if splits > 1 else None
             C.conv_gemm_dgrad(dy, wb, None, dx, KH, KW, stride, pad, part)
         # weight gradient

@@ -72,12 +72,12 @@ def main():
                 if bp == 0 and par != -1:
                     continue
                 if kind == "fwd":
-                    pbp, pbc, sp, nrows, used = C.conv_gemm_plan(x, y, K, K, st, pd, False, bp, bc, s)
+                    pbp, pbc, sp, nrows, _, used = C.conv_gemm_plan(x, y, K, K, st, pd, False, bp, bc, s)
                     stats = torch.empty(nrows, 2, Cout, device=dev)
                     part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
                     fn = lambda: C.conv_gemm_fwd(x, w, None, y, K, K, st, pd, False, stats, part, bp, bc, s)  # noqa: E731
                 else:
-                    pbp, pbc, sp, _, used = C.conv_gemm_plan(x, dy, K, K, st, pd, True, bp, bc, s, par)
+                    pbp, pbc, sp, _, used, _ = C.conv_gemm_plan(x, dy, K, K, st, pd, True, bp, bc, s, par)
                     part = torch.empty(sp * x.numel(), device=dev) if sp > 1 else None
                     fn = lambda: C.conv_gemm_dgrad(dy, w, None, dx, K, K, st, pd, part, bp, bc, s, par)  # noqa: E731
                 tag = f"{pbp}x{pbc}/s{sp}" + ("/par" if kind == "dgrad" and used else "")

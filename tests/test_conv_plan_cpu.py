@@ -32,14 +32,22 @@ def test_plans_are_valid(layer):
     C = native.require()
     name, N, H, Cin, Cout, K, s, p = layer
     x, y, OH = _shapes(N, H, Cin, Cout, K, s, p)
-    bp, bc, splits, rows, par = C.conv_gemm_plan(x, y, K, K, s, p, False)
+    bp, bc, splits, rows, par, halo = C.conv_gemm_plan(x, y, K, K, s, p, False)
     assert bp in (64, 128) and bc in (64, 128) and Cout % bc == 0 and par == 0
     nk = ((K * K + 7) // 8) if Cin == 4 else K * K * Cin // 32
     assert 1 <= splits <= min(8, nk)
     P = N * OH * OH
-    assert rows == (-(-P // bp) if splits == 1 else rows) and rows >= 1
+    # the halo-tile forward takes the stride-1 3x3 layers whose row-block grid fills the GPU
+    # (56/28 wide: 128-pixel tiles, 14 wide: 64-pixel tiles; not the 7-wide layer4)
+    assert halo == (1 if (K == 3 and s == 1 and H >= 14) else 0)
+    if halo:
+        R = bp // H
+        assert splits <= Cin // 32 and (splits > 1 or rows == N * -(-H // R))
+    elif splits == 1:
+        assert rows == -(-P // bp)
     if Cin != 4:
-        bp, bc, splits, _, par = C.conv_gemm_plan(x, y, K, K, s, p, True)
+        bp, bc, splits, _, par, halo = C.conv_gemm_plan(x, y, K, K, s, p, True)
+        assert halo == 0
         assert bc in (64, 128) and Cin % bc == 0
         assert par == (1 if s == 2 else 0)
         assert splits >= 1
@@ -59,9 +67,8 @@ def test_plans_match_sweep_winners():
         x, y, _ = _shapes(N, H, Cin, Cout, K, s, p)
         return C.conv_gemm_plan(x, y, K, K, s, p, dgrad)
 
-    assert plan("l1.3x3", False)[:3] == (128, 64, 1)
-    assert plan("l2.3x3", False)[:3] == (64, 128, 1)
-    assert plan("l4.3x3", False)[2] == 8          # long K (144 steps): split 8 ways
+    assert plan("l1.3x3", False)[5] == 1 and plan("l1.3x3", False)[2] == 1   # halo tile
+    assert plan("l4.3x3", False)[5] == 0 and plan("l4.3x3", False)[2] == 8   # 7 wide: split 8 ways
     assert plan("l3.1x1s2", False)[:3] == (64, 64, 1)
     assert plan("l2.3x3s2", True)[:3] == (128, 64, 1) and plan("l2.3x3s2", True)[4] == 1
     assert plan("l4.1x1s2", True)[:3] == (64, 64, 1)
@@ -71,6 +78,7 @@ def test_explicit_plan_overrides_and_bad_tiles():
     C = native.require()
     x, y, _ = _shapes(2, 14, 128, 256, 3, 1, 1)
     assert C.conv_gemm_plan(x, y, 3, 3, 1, 1, False, 64, 64, 3)[:3] == (64, 64, 3)
+    assert C.conv_gemm_plan(x, y, 3, 3, 1, 1, False, 0, 0, 0, -1, 0)[5] == 0  # halo off on request
     x2, y2, _ = _shapes(2, 14, 128, 256, 3, 2, 1)
     assert C.conv_gemm_plan(x2, y2, 3, 3, 2, 1, True, 0, 0, 0, 0)[4] == 0  # parity off on request
     with pytest.raises(RuntimeError):

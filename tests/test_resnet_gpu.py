@@ -21,12 +21,36 @@ def relerr(a, b):
 
 CASES = [  # N, H, Cin, Cout, K, stride, pad
     (4, 14, 64, 64, 3, 1, 1),
+    (2, 28, 64, 128, 3, 1, 1),     # halo-tile forward (W = 28, 4 rows per block)
+    (1, 56, 128, 64, 3, 1, 1),     # halo-tile forward (W = 56, 2 rows), 4 channel chunks
     (4, 14, 64, 128, 3, 2, 1),
     (4, 14, 64, 128, 1, 2, 0),
     (2, 8, 256, 512, 3, 2, 1),
     (2, 7, 512, 512, 3, 1, 1),
 ]
-PLANS = [(0, 0, 0), (64, 64, 1), (128, 128, 1), (64, 128, 3), (128, 64, 2)]  # (bp, bc, splits); 0 = auto
+PLANS = [(0, 0, 0), (64, 64, 1), (128, 128, 1), (64, 128, 3), (128, 64, 2), (0, 0, 2)]  # (bp, bc, splits); 0 = auto
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,splits,bc,bp", [(4, 14, 64, 64, 1, 64, 0), (4, 14, 64, 64, 1, 64, 128),
+                                                        (2, 28, 64, 128, 2, 128, 0), (2, 28, 64, 128, 1, 64, 64),
+                                                        (1, 56, 128, 64, 2, 64, 0), (3, 56, 64, 64, 1, 0, 0),
+                                                        (2, 7, 64, 128, 1, 0, 0)])
+def test_halo_fwd_forced(C, N, H, Cin, Cout, splits, bc, bp):
+    """The LDS halo-tile forward (conv_halo.hip), forced on: both pixel tiles, both channel
+    tiles, with and without K splits, down to the 7-wide layer."""
+    x = rnd(N, H, H, Cin, relu=True, seed=11)
+    w = rnd(Cout, 3, 3, Cin, scale=0.05, seed=12)
+    y = torch.empty(N, H, H, Cout, dtype=BF, device=dev)
+    pbp, _, sp, rows, _, halo = C.conv_gemm_plan(x, y, 3, 3, 1, 1, False, bp, bc, splits, -1, 1)
+    assert halo == 1 and sp == splits and (bp == 0 or pbp == bp)
+    stats = torch.empty(rows, 2, Cout, device=dev)
+    part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
+    C.conv_gemm_fwd(x, w, None, y, 3, 3, 1, 1, False, stats, part, bp, bc, splits, 1)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert relerr(y, ref) < 1e-2
+    st = stats.sum(0)
+    yb = y.float()
+    assert relerr(st[0], yb.sum((0, 1, 2))) < 1e-4 and relerr(st[1], (yb * yb).sum((0, 1, 2))) < 1e-4
 
 
 def _plan_ok(bp, bc, C):
@@ -45,7 +69,7 @@ def test_conv_gemm_fwd_dgrad(C, N, H, Cin, Cout, K, s, p, bp, bc, splits):
     wr = w.float().permute(0, 3, 1, 2)
     if _plan_ok(bp, bc, Cout):
         y = torch.empty(N, OH, OH, Cout, dtype=BF, device=dev)
-        _, _, sp, rows, _ = C.conv_gemm_plan(x, y, K, K, s, p, False, bp, bc, splits)
+        _, _, sp, rows, _, _ = C.conv_gemm_plan(x, y, K, K, s, p, False, bp, bc, splits)
         stats = torch.empty(rows, 2, Cout, device=dev)
         part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
         C.conv_gemm_fwd(x, w, None, y, K, K, s, p, False, stats, part, bp, bc, splits)
@@ -63,7 +87,7 @@ def test_conv_gemm_fwd_dgrad(C, N, H, Cin, Cout, K, s, p, bp, bc, splits):
         for par in ((-1, 0) if s == 2 else (-1,)):
             for mask in (None, x):
                 dx = torch.full_like(x, 3.0)  # every element must be written (zeros included)
-                _, _, sp, _, used = C.conv_gemm_plan(x, dy, K, K, s, p, True, bp, bc, splits, par)
+                _, _, sp, _, used, _ = C.conv_gemm_plan(x, dy, K, K, s, p, True, bp, bc, splits, par)
                 assert used == (1 if (s == 2 and par != 0) else 0)
                 part = torch.empty(sp * x.numel(), device=dev) if sp > 1 else None
                 C.conv_gemm_dgrad(dy, w, mask, dx, K, K, s, p, part, bp, bc, splits, par)
