@@ -325,13 +325,13 @@ void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> b
 
 void op_conv_gemm_dgrad(const Tensor& dY, const Tensor& W, std::optional<Tensor> Xact, Tensor& dX,
                         int KH, int KW, int stride, int pad, std::optional<Tensor> part, int bp, int bc,
-                        int splits, int parity) {
+                        int splits, int parity, int halo) {
   check(dY, "dY", at::kBFloat16); check(W, "W", at::kBFloat16); check(dX, "dX", at::kBFloat16);
   const ConvGeom g = geom_of(dX, dY, KH, KW, stride, pad);
   TORCH_CHECK(g.Cin % 64 == 0 && g.Cout % 32 == 0, "conv_gemm_dgrad: Cin % 64, Cout % 32");
   TORCH_CHECK(W.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_gemm_dgrad: OHWI weight shape");
   if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
-  const ConvPlan pl = plan_of(g, true, bp, bc, splits, parity);
+  const ConvPlan pl = plan_of(g, true, bp, bc, splits, parity, halo);
   float* pt = nullptr;
   if (pl.splits > 1) {
     TORCH_CHECK(part.has_value(), "conv_gemm_dgrad: split plan needs the fp32 `part` workspace");
@@ -624,7 +624,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splits") = 0, py::arg("halo") = -1);
   m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad, py::arg("dY"), py::arg("W"), py::arg("Xact"), py::arg("dX"),
         py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(),
-        py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1);
+        py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1,
+        py::arg("halo") = -1);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
   m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
     return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));

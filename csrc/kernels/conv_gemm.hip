@@ -631,24 +631,25 @@ ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int split
   // Auto-picked only when that grid fills the GPU without K splits; with splits the fp32
   // partial round trip cost more than the halo saved.  ResNet-18 (conv_sweep.jsonl):
   // layer1 24.4 -> 21.5 us, layer2 26.3 -> 17.2 us.  halo = 1 forces it.
+  // The stride-1 3x3 data gradient is the same halo GEMM over dY (conv_halo.hip).
+  const int hrows = dgrad ? g.Cin : g.Cout, hk = dgrad ? g.Cout : g.Cin;
   int hbp = 0;
   long hgrid = 0;
   for (int cand : {128, 64}) {
     if (bp && bp != cand) continue;
-    if (!conv_halo_fits(g, cand)) continue;
+    if (!conv_halo_fits(g, cand) || hk % CG_KS != 0) continue;
     const int r = conv_halo_rows(g, cand);
     hbp = cand;
-    hgrid = (long)g.N * ((g.H + r - 1) / r) * (g.Cout / 64);
+    hgrid = (long)g.N * ((g.H + r - 1) / r) * (hrows / 64);
     if (hgrid >= 384) break;
   }
-  if (!dgrad && hbp && !(bp && halo != 1) &&
-      (halo == 1 || (halo < 0 && hgrid >= 384 && splits <= 1))) {
+  if (hbp && !(bp && halo != 1) && (halo == 1 || (halo < 0 && hgrid >= 384 && splits <= 1))) {
     pl.halo = 1;
     pl.bp = hbp;
     pl.bc = bc ? bc : 64;
-    const int R = conv_halo_rows(g, hbp), RG = (g.H + R - 1) / R, nch = g.Cin / CG_KS;
+    const int R = conv_halo_rows(g, hbp), RG = (g.H + R - 1) / R, nch = hk / CG_KS;
     pl.grid_x = g.N * RG;
-    pl.grid_y = g.Cout / pl.bc;
+    pl.grid_y = hrows / pl.bc;
     const long base = (long)pl.grid_x * pl.grid_y;
     int s = splits;
     if (s <= 0) {
@@ -768,6 +769,11 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
 
 void conv_gemm_dgrad(const ConvGeom& g, const ConvPlan& pl, const bf16_t* dY, const bf16_t* W,
                      const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s) {
+  if (pl.halo) {
+    conv_halo_dgrad(g, pl.bp, pl.bc, pl.splits, dY, W, pl.splits > 1 ? nullptr : Xact, dX, part, s);
+    if (pl.splits > 1) splitk_reduce(part, pl.splits, (long)g.N * g.H * g.W, g.Cin, Xact, dX, nullptr, s);
+    return;
+  }
   const dim3 grid(pl.grid_x, pl.grid_y, pl.grid_z);
   const int kp = pl.ks_per, ns = pl.splits, par = pl.parity;
 #define CGD(BP, BC, MX, PT) hipLaunchKernelGGL((conv_gemm_dgrad_kernel<BP, BC, MX, PT>), grid, dim3(256), 0, s, g, dY, W, Xact, dX, part, kp, ns, par)

@@ -205,6 +205,192 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
   }
 }
 
+// ---------------------------------------------------------------- data gradient
+// Stride-1 3x3 data gradient = the forward convolution of dY with the weights transposed
+// (ci <-> co) and the taps flipped: dX[ih][iw][ci] = sum W[co][kh][kw][ci] *
+// dY[ih + 1 - kh][iw + 1 - kw][co].  Same halo tiling over dY rows; the weight tiles of
+// one kernel row are staged as stored ([32 co][BC ci] per tap) and read with
+// ds_read_b64_tr_b16, so the dY halo is stored in the transposed read's K order
+// (dtrk_pos, as conv_gemm_dgrad_kernel does for its gathered tile).
+__device__ __forceinline__ int dtrk_pos(int k4) { return k4 < 4 ? 8 * k4 : 8 * (k4 - 4) + 4; }
+
+template <int BC, int BP, bool MASK_X, bool PART>
+__global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
+                                                                   const bf16_t* __restrict__ Wt,
+                                                                   const bf16_t* __restrict__ Xact,
+                                                                   bf16_t* __restrict__ dX,
+                                                                   float* __restrict__ part, int R,
+                                                                   int chunks_per_split) {
+  constexpr int TCI = BC / 32, TPX = BP / 32;
+  constexpr int HCH = (HL_MAXPX * 4 + 255) / 256;
+  constexpr int AS = BC + 16;                  // [co][ci] weight row stride (odd multiple of 8 dwords)
+  constexpr int WCH = 3 * HL_KS * BC / 8 / 256;  // 16-B weight chunks per thread (one kernel row)
+  __shared__ __attribute__((aligned(16))) bf16_t sA[2][3 * HL_KS * AS];
+  __shared__ __attribute__((aligned(16))) bf16_t sH[2][HL_MAXPX * HL_RS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wci = wave >> 1, wpx = wave & 1;
+  const int W = g.W, H = g.H, Cout = g.Cout;
+  const int RG = (H + R - 1) / R;
+  const int n_ = blockIdx.x / RG, rg = blockIdx.x - n_ * RG;
+  const int ih0 = rg * R;
+  const int ci0 = blockIdx.y * BC;
+  const int HW2 = W + 2, HPX = (R + 2) * HW2;
+  const int NPX = R * W;
+  const int nch = Cout / HL_KS;
+  const int c_beg = blockIdx.z * chunks_per_split;
+  const int c_end = min(nch, c_beg + chunks_per_split);
+  const int KWC = 9 * g.Cin;
+
+  auto load_halo = [&](int ch, bf16x8* rh) {
+#pragma unroll
+    for (int u = 0; u < HCH; ++u) {
+      const int e = tid + 256 * u;
+      const int hp = e >> 2, qq = e & 3;
+      rh[u] = zero8();
+      if (hp < HPX) {
+        const int hr = hp / HW2, hc = hp - hr * HW2;
+        const int oh = ih0 - 1 + hr, ow = hc - 1;
+        if ((unsigned)oh < (unsigned)H && (unsigned)ow < (unsigned)W)
+          rh[u] = ld8(dY + (((long)n_ * H + oh) * W + ow) * Cout + ch * HL_KS + qq * 8);
+      }
+    }
+  };
+  auto store_halo = [&](int buf, const bf16x8* rh) {
+#pragma unroll
+    for (int u = 0; u < HCH; ++u) {
+      const int e = tid + 256 * u;
+      const int hp = e >> 2, qq = e & 3;
+      if (hp < HPX) {
+        const uint4 q = __builtin_bit_cast(uint4, rh[u]);
+        *reinterpret_cast<uint2*>(&sH[buf][hp * HL_RS + dtrk_pos(2 * qq)]) = make_uint2(q.x, q.y);
+        *reinterpret_cast<uint2*>(&sH[buf][hp * HL_RS + dtrk_pos(2 * qq + 1)]) = make_uint2(q.z, q.w);
+      }
+    }
+  };
+  // kernel row kh, co chunk ch: sA[(kw * 32 + co) * AS + ci] = W[co0 + co][kh][kw][ci0 + ci]
+  auto load_w = [&](int ch, int kh, bf16x8* ra) {
+#pragma unroll
+    for (int u = 0; u < WCH; ++u) {
+      const int c = tid + u * 256;
+      const int row = c / (BC / 8), off = (c % (BC / 8)) * 8;
+      const int kw = row / HL_KS, co = row - kw * HL_KS;
+      ra[u] = ld8(Wt + (long)(ch * HL_KS + co) * KWC + (kh * 3 + kw) * g.Cin + ci0 + off);
+    }
+  };
+  auto store_w = [&](int buf, const bf16x8* ra) {
+#pragma unroll
+    for (int u = 0; u < WCH; ++u) {
+      const int c = tid + u * 256;
+      const int row = c / (BC / 8), off = (c % (BC / 8)) * 8;
+      *reinterpret_cast<bf16x8*>(&sA[buf][row * AS + off]) = ra[u];
+    }
+  };
+
+  const int kofs = 8 * (lane >> 4), col = lane & 15;
+  const int gq = lane >> 4, q = col >> 2, pq = col & 3;
+  int hbase[TPX];
+#pragma unroll
+  for (int j = 0; j < TPX; ++j) {
+    const int p = wpx * (BP / 2) + 16 * j + col;
+    const int r = p / W, c = p - r * W;
+    hbase[j] = p < NPX ? r * HW2 + c : 0;
+  }
+  f32x4 acc[TCI][TPX];
+#pragma unroll
+  for (int i = 0; i < TCI; ++i)
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 ra[WCH], rh[HCH];
+  if (c_beg < c_end) {
+    load_halo(c_beg, rh);
+    load_w(c_beg, 0, ra);
+    store_halo(0, rh);
+    store_w(0, ra);
+  }
+  __syncthreads();
+  int step = 0;
+  for (int ch = c_beg; ch < c_end; ++ch) {
+    const int hb = (ch - c_beg) & 1;
+    const bool next_chunk = ch + 1 < c_end;
+    for (int kh = 0; kh < 3; ++kh, ++step) {
+      const int cur = step & 1;
+      const bool last = kh == 2;
+      const bool more = !last || next_chunk;
+      if (more) load_w(last ? ch + 1 : ch, last ? 0 : kh + 1, ra);
+      if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int toff = (2 - kh) * HW2 + (2 - kw);  // flipped tap
+        const bf16_t* wa = &sA[cur][kw * HL_KS * AS];
+        bf16x8 a[TCI], b[TPX];
+#pragma unroll
+        for (int i = 0; i < TCI; ++i) {
+          const int m = wci * (BC / 2) + 16 * i + 4 * pq;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(4 * gq + q) * AS + m]);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(16 + 4 * gq + q) * AS + m]);
+          a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < TPX; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
+#pragma unroll
+        for (int i = 0; i < TCI; ++i)
+#pragma unroll
+          for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      }
+      if (last && next_chunk) store_halo(hb ^ 1, rh);
+      if (more) store_w(cur ^ 1, ra);
+      __syncthreads();
+    }
+  }
+
+  const long Ptot = (long)g.N * H * W;
+#pragma unroll
+  for (int j = 0; j < TPX; ++j) {
+    const int p = wpx * (BP / 2) + 16 * j + col;
+    const int r = p / W;
+    const int ih = ih0 + r;
+    if (p >= NPX || ih >= H) continue;
+    const long P = ((long)n_ * H + ih) * W + (p - r * W);
+#pragma unroll
+    for (int i = 0; i < TCI; ++i) {
+      const int ci = ci0 + wci * (BC / 2) + 16 * i + 4 * (lane >> 4);
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (PART) {
+        *reinterpret_cast<float4*>(part + ((long)blockIdx.z * Ptot + P) * g.Cin + ci) =
+            make_float4(v[0], v[1], v[2], v[3]);
+        continue;
+      }
+      if (MASK_X) {
+        float xm[4];
+        unpack4(*reinterpret_cast<const uint2*>(Xact + P * g.Cin + ci), xm);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[rr] = xm[rr] > 0.f ? v[rr] : 0.f;
+      }
+      *reinterpret_cast<uint2*>(dX + P * g.Cin + ci) = pack4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* dY, const bf16_t* Wt,
+                     const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s) {
+  const int R = bp / g.W;
+  const int RG = (g.H + R - 1) / R;
+  const int nch = g.Cout / HL_KS;
+  const int cps = (nch + splits - 1) / splits;
+  const dim3 grid(g.N * RG, g.Cin / bc, splits);
+#define HLD(BC, BP, MX, PT) hipLaunchKernelGGL((conv3x3s1_halo_dgrad_kernel<BC, BP, MX, PT>), grid, dim3(256), 0, s, g, dY, Wt, Xact, dX, part, R, cps)
+#define HLD_BP(BC, BP)                                  \
+  if (splits > 1) HLD(BC, BP, false, true);             \
+  else if (Xact) HLD(BC, BP, true, false);              \
+  else HLD(BC, BP, false, false);
+  if (bp == 128) { if (bc == 128) { HLD_BP(128, 128) } else { HLD_BP(64, 128) } }
+  else { if (bc == 128) { HLD_BP(128, 64) } else { HLD_BP(64, 64) } }
+#undef HLD_BP
+#undef HLD
+}
+
 // bp: pixel columns of the block's MFMA tile (128 or 64); R = bp / W full rows per block
 bool conv_halo_fits(const ConvGeom& g, int bp) {
   if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad != 1 || g.Cin % HL_KS != 0) return false;

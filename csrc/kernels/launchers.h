@@ -58,6 +58,8 @@ bool conv_halo_fits(const ConvGeom& g, int bp);
 int conv_halo_rows(const ConvGeom& g, int bp);
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
                    bf16_t* Y, float* stats, float* part, hipStream_t s);
+void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* dY, const bf16_t* Wt,
+                     const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s);
 int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl);  // BN stats slab rows (fwd)
 // splits > 1: `part` = fp32 workspace [splits][P][C]; no bias / ReLU on the split path
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,

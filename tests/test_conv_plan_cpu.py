@@ -47,7 +47,7 @@ def test_plans_are_valid(layer):
         assert rows == -(-P // bp)
     if Cin != 4:
         bp, bc, splits, _, par, halo = C.conv_gemm_plan(x, y, K, K, s, p, True)
-        assert halo == 0
+        assert halo == (1 if (K == 3 and s == 1 and H >= 14) else 0)  # halo dgrad likewise
         assert bc in (64, 128) and Cin % bc == 0
         assert par == (1 if s == 2 else 0)
         assert splits >= 1

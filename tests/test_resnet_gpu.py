@@ -51,6 +51,19 @@ def test_halo_fwd_forced(C, N, H, Cin, Cout, splits, bc, bp):
     st = stats.sum(0)
     yb = y.float()
     assert relerr(st[0], yb.sum((0, 1, 2))) < 1e-4 and relerr(st[1], (yb * yb).sum((0, 1, 2))) < 1e-4
+    # the halo data gradient (dY halo, flipped taps, transposed weight reads), same tiles
+    if Cin % 64 == 0 and (bc == 0 or Cin % bc == 0):
+        dy = rnd(N, H, H, Cout, scale=0.5, seed=13)
+        rdx = torch.nn.grad.conv2d_input(x.shape[:1] + (Cin, H, H), w.float().permute(0, 3, 1, 2),
+                                         dy.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+        for mask in (None, x):
+            dx = torch.full_like(x, 3.0)
+            _, _, sd, _, _, hd = C.conv_gemm_plan(x, dy, 3, 3, 1, 1, True, bp, bc, splits, -1, 1)
+            assert hd == 1
+            partd = torch.empty(sd * x.numel(), device=dev) if sd > 1 else None
+            C.conv_gemm_dgrad(dy, w, mask, dx, 3, 3, 1, 1, partd, bp, bc, splits, -1, 1)
+            want = rdx if mask is None else torch.where(x.float() > 0, rdx, torch.zeros_like(rdx))
+            assert relerr(dx, want) < 1e-2, mask is not None
 
 
 def _plan_ok(bp, bc, C):
