@@ -29,7 +29,12 @@
 namespace ddp_amd {
 
 constexpr int CG_KS = 32;  // K-step (channels of one tap)
-constexpr int CG_RS = 40;  // LDS row stride (elements) of K-contiguous tiles
+// LDS row stride (elements) of K-contiguous tiles.  40 (20 dwords) shows 4.9-5.3 bank-
+// conflict cycles per LDS instruction in the forward (PMC SQ_LDS_BANK_CONFLICT,
+// profiles/r1_resnet); the conflict-free 48 (24 dwords, == 8 mod 16) measured no faster
+// over the ResNet-18 layers (stem +3 us, the rest within +-1 us): these kernels are not
+// LDS-bound, and 40 keeps the LDS footprint smaller.
+constexpr int CG_RS = 40;
 
 // K-slot permutation of the transposed (ds_read_b64_tr_b16) fragment read: fragment
 // element j of lane group g holds k = 4g + j (j < 4) or 16 + 4g + (j - 4).  The matching

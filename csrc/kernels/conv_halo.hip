@@ -20,7 +20,7 @@
 namespace ddp_amd {
 
 constexpr int HL_KS = 32;   // channels per chunk (one MFMA K-step per tap)
-constexpr int HL_RS = 40;   // LDS row stride (elements) per pixel / weight row
+constexpr int HL_RS = 48;   // LDS row stride (elements) per pixel / weight row: 24 dwords == 8 (mod 16)
 constexpr int HL_BP = 128;  // pixel columns of the MFMA tile
 constexpr int HL_MAXPX = 232;     // largest halo: (R+2) x (W+2) = 4 x 58 at W = 56 (R = 2)
 
@@ -184,7 +184,9 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
     }
   }
   if (STATS && !PART) {
-    __shared__ float s_st[2][2][BC];
+    // the weight tiles are dead after the K loop: their LDS holds the per-wave partials
+    // (keeps two blocks per CU resident)
+    float (*s_st)[2][BC] = reinterpret_cast<float (*)[2][BC]>(&sA[0][0]);
 #pragma unroll
     for (int i = 0; i < TCO; ++i)
 #pragma unroll
