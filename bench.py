@@ -222,9 +222,12 @@ def bench_resnet(args):
         opt.step()
         return loss
 
-    if not args.no_graph:
-        # whole-step hipGraph (engine/graph_step.py); its capture warm-up steps are
-        # part of the untimed warm-up
+    # whole-step hipGraph (engine/graph_step.py) on one GPU; with several ranks the step
+    # runs eagerly (the DDP buffer broadcasts and bucket all-reduces are validated
+    # graph-captured only at world size 1 - ranks can't share a GPU under RCCL here)
+    use_graph = not args.no_graph and ws == 1
+    if use_graph:
+        # its capture warm-up steps are part of the untimed warm-up
         from ddp_amd.engine import GraphedStep
 
         nwarm = max(1, min(3, args.warmup))
@@ -265,7 +268,7 @@ def bench_resnet(args):
             "config": {"model": f"ResNet-18 ({param_count(model):,} params)", "global_batch": ws * B,
                        "per_rank_batch": B, "seq_len": None, "parallelism": f"dp{ws}",
                        "engine": "module path (HIP autograd + native reducer)"
-                                 + (", eager" if args.no_graph else ", whole step in one hipGraph"),
+                                 + (", whole step in one hipGraph" if use_graph else ", eager"),
                        "loss": round(float(loss.item()), 4)},
         }), flush=True)
     dist.destroy_process_group()
