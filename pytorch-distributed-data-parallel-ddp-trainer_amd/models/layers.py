@@ -250,9 +250,13 @@ class FlatSpace:
             self._bf16_version = self.params._version
         return self._bf16
 
-    def bf16_view(self, p: torch.Tensor) -> torch.Tensor:
-        """The bf16 copy of parameter ``p`` (a view of this flat space), same shape."""
-        off = (p.data_ptr() - self.params.data_ptr()) // self.params.element_size()
+    def bf16_view(self, p: torch.Tensor):
+        """The bf16 copy of parameter ``p``, same shape; ``None`` if ``p`` no longer lives
+        in this flat space (e.g. its ``.data`` was replaced) or is not contiguous."""
+        es = self.params.element_size()
+        off, rem = divmod(p.data_ptr() - self.params.data_ptr(), es)
+        if rem or off < 0 or off + p.numel() > self.numel or not p.is_contiguous() or p.dtype != torch.float32:
+            return None
         return self.bf16_params()[off:off + p.numel()].view(p.shape)
 
     def mark_bf16_fresh(self):

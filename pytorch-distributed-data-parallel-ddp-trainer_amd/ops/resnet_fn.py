@@ -44,9 +44,8 @@ def to_nhwc4(x: torch.Tensor) -> torch.Tensor:
 
 def _weight_bf16(w: torch.Tensor) -> torch.Tensor:
     fs = getattr(w, "_ddp_amd_fs", None)
-    if fs is not None:
-        return fs.bf16_view(w)
-    return w.detach().to(BF16)
+    v = fs.bf16_view(w) if fs is not None else None
+    return v if v is not None else w.detach().to(BF16).contiguous()
 
 
 class _ConvBNAct(torch.autograd.Function):
