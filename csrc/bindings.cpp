@@ -627,6 +627,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1,
         py::arg("halo") = -1);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
+  m.def("conv_gemm_wgrad_force_tile", &conv_gemm_wgrad_force_tile);
   m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
     return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));
   });
@@ -644,6 +645,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize_groups", &bn_finalize_groups);
   m.def("bn_bwd_rows", [](long P, int C) { return bn_bwd_rows(P, C, nullptr); });
   m.def("bn_bwd", &op_bn_bwd);
+  m.def("bn_bwd_set_px_per_block", &bn_bwd_set_px_per_block);
   m.def("maxpool_fwd", &op_maxpool_fwd);
   m.def("maxpool_bwd", &op_maxpool_bwd);
   m.def("avgpool_fwd", &op_avgpool_fwd);

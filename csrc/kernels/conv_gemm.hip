@@ -798,16 +798,29 @@ int conv_gemm_wgrad_chunks(const ConvGeom& g, int px_per_chunk) {
   return (int)((P + px_per_chunk - 1) / px_per_chunk);
 }
 
-// Block tile of the weight gradient (scripts/resnet_conv_sweep.py, profiles/r1_resnet):
+// Block tile of the weight gradient (scripts/resnet_conv_sweep.py, wgrad_tile_sweep.py,
+// profiles/r1_resnet):
 // 128-wide tiles only while the 128-tile grid is small (< 64 tiles: those layers are
 // chunked over pixels anyway and the wider tile halves the slab traffic); otherwise
 // 64 x 64, whose 4x larger grid fills the CUs without chunking.
+static int g_wgrad_force_bm = 0, g_wgrad_force_bn = 0;  // sweep override (0 = auto)
+void conv_gemm_wgrad_force_tile(int bm, int bn) {
+  g_wgrad_force_bm = (bm == 64 || bm == 128) ? bm : 0;
+  g_wgrad_force_bn = (bn == 64 || bn == 128) ? bn : 0;
+}
+
 static void wgrad_tile(const ConvGeom& g, int* bm, int* bn) {
   const int T = g.KH * g.KW;
   *bm = 64;
   *bn = 64;
   if (g.Cin == 4 || T == 1) return;
-  const int bm2 = g.Cout % 128 == 0 ? 128 : 64, bn2 = g.Cin % 128 == 0 ? 128 : 64;
+  if (g_wgrad_force_bm && g.Cout % g_wgrad_force_bm == 0 && g.Cin % g_wgrad_force_bn == 0) {
+    *bm = g_wgrad_force_bm;
+    *bn = g_wgrad_force_bn;
+    return;
+  }
+  // stride 2: the narrower X tile (l3 3x3/s2: 27.7 -> 22.8 us, scripts/wgrad_tile_sweep.py)
+  const int bm2 = g.Cout % 128 == 0 ? 128 : 64, bn2 = (g.Cin % 128 == 0 && g.stride == 1) ? 128 : 64;
   if ((long)(g.Cout / bm2) * T * (g.Cin / bn2) < 64) {
     *bm = bm2;
     *bn = bn2;

@@ -68,6 +68,7 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
 void conv_gemm_dgrad(const ConvGeom& g, const ConvPlan& pl, const bf16_t* dY, const bf16_t* W,
                      const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s);
 int conv_gemm_wgrad_chunks(const ConvGeom& g, int px_per_chunk);
+void conv_gemm_wgrad_force_tile(int bm, int bn);  // 0, 0 = auto
 int conv_gemm_wgrad_tiles(const ConvGeom& g);  // blocks per pixel chunk
 int conv_gemm_wgrad_ppc(const ConvGeom& g);    // tuned pixels per chunk
 // one chunk: out = the gradient ([Cout][T][Cin], stem: [Cout][T][3]), `accum` adds to it;
@@ -83,6 +84,7 @@ void bn_finalize(const float* slab, int rows, int C, float count, float eps, flo
 void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* invstd,
               const float* gamma, const float* beta, const bf16_t* res, bool relu, bf16_t* y,
               hipStream_t s);
+void bn_bwd_set_px_per_block(int px);
 int bn_bwd_rows(long P, int C, int* rpb);  // ws of bn_bwd: [rows][2][C]
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,

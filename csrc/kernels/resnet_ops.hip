@@ -528,12 +528,19 @@ void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* in
 #undef BA
 }
 
+// Rows of the reduce grid: about 392 pixels per block.  The last-arrival tail (write-through
+// partials, R same-address ticket increments, the last block's R-row sum) grows with R,
+// so small layers want few fat blocks: scripts/bn_sweep.py at batch 32 measured
+// 13.1 -> 8.5 us (7x7x512), 14.9 -> 10.8 us (14x14x256), 19.8 -> 15.4 us (28x28x128)
+// against a fixed 512-block grid.  Settable for the sweep; ws is sized by bn_bwd_rows at
+// the same setting.
+static int g_bn_bwd_px = 392;
+void bn_bwd_set_px_per_block(int px) { g_bn_bwd_px = px < 32 ? 32 : px; }
+
 int bn_bwd_rows(long P, int C, int* rpb) {
-  const int strips = C / 64;
-  long R = 512 / strips;
+  (void)C;
+  long R = P / g_bn_bwd_px;
   if (R > 256) R = 256;
-  const long maxr = (P + 31) / 32;
-  if (R > maxr) R = maxr;
   if (R < 1) R = 1;
   const long r = (P + R - 1) / R;
   if (rpb) *rpb = (int)r;
