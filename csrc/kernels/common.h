@@ -66,6 +66,23 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs (linear id
+// % 8 = the XCD group), each with a private L2.  The remap gives XCD group k one
+// contiguous range of the logical linear order, so blocks that share operand rows (e.g.
+// every tile of one pixel chunk) hit one L2 instead of eight.  Bijective for any grid
+// size: the first nb % 8 groups take one extra block.  Placement only changes speed.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int per = nb >> 3, rem = nb & 7, x = b & 7, i = b >> 3;
+  return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+}
+// The logical (x, y, z) block of this workgroup after xcd_remap (x fastest).
+__device__ __forceinline__ int3 xcd_block3() {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int b = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int l = xcd_remap(b, gx * gy * gridDim.z);
+  return make_int3(l % gx, (l / gx) % gy, l / (gx * gy));
+}
+
 // 8 contiguous bytes = 4 bf16 packed from 4 floats
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
   uint2 r;

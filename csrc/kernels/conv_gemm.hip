@@ -61,14 +61,15 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
   constexpr int TPX = BP / 32;  // 16-col tiles per wave (px)
   constexpr int TPR = 256 / BP;          // staging threads per pixel row
   constexpr int EPT = CG_KS / TPR;       // elements per thread (16 or 8)
+  const int3 bk = xcd_block3();  // XCD-contiguous block order (pixel tiles share an L2)
   const int OHW = g.OH * g.OW;
   const int Ptot = g.N * OHW;
-  const int p0 = blockIdx.x * BP;
-  const int co0 = blockIdx.y * BC;
+  const int p0 = bk.x * BP;
+  const int co0 = bk.y * BC;
   const int KWC = g.KH * g.KW * g.Cin;
   const int T = g.KH * g.KW;
   const int nk = STEM ? (T + 7) / 8 : T * (g.Cin / CG_KS);
-  const int kb = blockIdx.z * ks_per;
+  const int kb = bk.z * ks_per;
   const int ke = min(nk, kb + ks_per);
 
   const int bp = tid / TPR, bh = (tid % TPR) * EPT;  // pixel row, element offset
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
 
   // ---- epilogue
   if (PART) {  // fp32 split partial [z][P][Cout]: 4 consecutive channels per lane = 16 B
-    float* dst = part + (long)blockIdx.z * Ptot * g.Cout;
+    float* dst = part + (long)bk.z * Ptot * g.Cout;
 #pragma unroll
     for (int j = 0; j < TPX; ++j) {
       const int Pj = p0 + wpx * (BP / 2) + 16 * j + col;
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
     __syncthreads();
     // stats slab: [blocks_x][2][Cout]
     for (int c = tid; c < BC; c += 256) {
-      float* dst = stats + (long)blockIdx.x * 2 * g.Cout;
+      float* dst = stats + (long)bk.x * 2 * g.Cout;
       dst[co0 + c] = s_st[0][0][c] + s_st[1][0][c];
       dst[g.Cout + co0 + c] = s_st[0][1][c] + s_st[1][1][c];
     }
@@ -266,18 +267,21 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
   // Stride-2 parity classes: input pixel (ih, iw) only meets taps with kh = ih + pad
   // (mod 2), kw likewise, so each class (ih % 2, iw % 2) is a dense GEMM over its own
   // 1..4 taps (3x3) instead of all 9 with 3/4 structural zeros.  grid.z = class x split.
-  int cls = 0, zs = blockIdx.z;
+  // hardware block order: the XCD remap measured worse here (stride-2 parity classes leave
+  // whole blocks idle and contiguous ranges pile them on a few XCDs: 1x1/s2 8.7 -> 14.8 us)
+  const int3 bk = make_int3(blockIdx.x, blockIdx.y, blockIdx.z);
+  int cls = 0, zs = bk.z;
   if (parity) {
-    cls = blockIdx.z / nsplit;
-    zs = blockIdx.z - cls * nsplit;
+    cls = bk.z / nsplit;
+    zs = bk.z - cls * nsplit;
   }
   const int ph = cls >> 1, pw = cls & 1, ts = parity ? 2 : 1;
   const int Hc = (g.H - ph + ts - 1) / ts, Wc = (g.W - pw + ts - 1) / ts;
   const int HWc = Hc * Wc;
   const int Pc = g.N * HWc;  // pixels of this class
-  const int p0 = blockIdx.x * BP;
+  const int p0 = bk.x * BP;
   if (p0 >= Pc) return;  // block-uniform (a smaller class), before any barrier
-  const int ci0b = blockIdx.y * BC;
+  const int ci0b = bk.y * BC;
   const int kh0 = parity ? (ph + g.pad) & 1 : 0, kw0 = parity ? (pw + g.pad) & 1 : 0;
   const int nth = (g.KH - kh0 + ts - 1) / ts, ntw = (g.KW - kw0 + ts - 1) / ts;
   const int CK = g.Cout / CG_KS;
@@ -496,15 +500,18 @@ __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const 
   __shared__ __attribute__((aligned(16))) bf16_t sD[2][KS * RD];
   __shared__ __attribute__((aligned(16))) bf16_t sX[2][KS * RX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int co0 = blockIdx.x * BM;
+  // hardware block order: an XCD-contiguous remap (whole pixel chunks per L2) measured
+  // +1..+4 us on 6 of 9 layers (scripts/wgrad_tile_sweep.py); the L2 misses are not the bound
+  const int3 bk = make_int3(blockIdx.x, blockIdx.y, blockIdx.z);
+  const int co0 = bk.x * BM;
   const int T = g.KH * g.KW;
-  const int tap = STEM ? 0 : blockIdx.y / (g.Cin / BN);
-  const int ci0 = STEM ? 0 : (blockIdx.y - tap * (g.Cin / BN)) * BN;
+  const int tap = STEM ? 0 : bk.y / (g.Cin / BN);
+  const int ci0 = STEM ? 0 : (bk.y - tap * (g.Cin / BN)) * BN;
   const int kh = tap / g.KW, kw = tap - kh * g.KW;
-  const int tg0 = STEM ? blockIdx.y * 16 : 0;  // first tap of this block (STEM)
+  const int tg0 = STEM ? bk.y * 16 : 0;  // first tap of this block (STEM)
   const int OHW = g.OH * g.OW;
   const int Ptot = g.N * OHW;
-  const int pbeg = blockIdx.z * px_per_chunk;
+  const int pbeg = bk.z * px_per_chunk;
   const int pend = min(Ptot, pbeg + px_per_chunk);
   auto load = [&](int pk, bf16x8* vd, bf16x8* vx) {
 #pragma unroll
@@ -598,25 +605,49 @@ __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const 
     cur ^= 1;
   }
   const int ocin = STEM ? 3 : g.Cin;
-  float* o = out + (long)blockIdx.z * g.Cout * T * ocin;
+  float* o = out + (long)bk.z * g.Cout * T * ocin;
+  // output index of accumulator element (a, b, r); -1 = a padding column of the stem
+  auto out_idx = [&](int a, int b, int r) -> long {
+    const int co = co0 + wm + 16 * a + 4 * gq + r;
+    if (STEM) {
+      const int j = wn + 16 * b + i16;  // column = tap offset * 4 + channel
+      const int t = tg0 + j / 4;
+      if (t >= T || (j & 3) == 3) return -1;
+      return ((long)co * T + t) * 3 + (j & 3);
+    }
+    return ((long)co * T + tap) * g.Cin + ci0 + wn + 16 * b + i16;
+  };
+  if (accum) {  // all old values in flight at once, then the stores
+    float old[TA][TB][4];
 #pragma unroll
-  for (int a = 0; a < TA; ++a)
+    for (int a = 0; a < TA; ++a)
 #pragma unroll
-    for (int b = 0; b < TB; ++b)
+      for (int b = 0; b < TB; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm + 16 * a + 4 * gq + r;
-        long idx;
-        if (STEM) {
-          const int j = wn + 16 * b + i16;  // column = tap offset * 4 + channel
-          const int t = tg0 + j / 4;
-          if (t >= T || (j & 3) == 3) continue;
-          idx = ((long)co * T + t) * 3 + (j & 3);
-        } else {
-          idx = ((long)co * T + tap) * g.Cin + ci0 + wn + 16 * b + i16;
+        for (int r = 0; r < 4; ++r) {
+          const long idx = out_idx(a, b, r);
+          old[a][b][r] = idx >= 0 ? o[idx] : 0.f;
         }
-        o[idx] = accum ? o[idx] + acc[a][b][r] : acc[a][b][r];
-      }
+#pragma unroll
+    for (int a = 0; a < TA; ++a)
+#pragma unroll
+      for (int b = 0; b < TB; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long idx = out_idx(a, b, r);
+          if (idx >= 0) o[idx] = old[a][b][r] + acc[a][b][r];
+        }
+  } else {
+#pragma unroll
+    for (int a = 0; a < TA; ++a)
+#pragma unroll
+      for (int b = 0; b < TB; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long idx = out_idx(a, b, r);
+          if (idx >= 0) o[idx] = acc[a][b][r];
+        }
+  }
 }
 
 // ---------------------------------------------------------------- host side

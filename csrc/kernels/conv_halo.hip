@@ -40,13 +40,14 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
   const int wco = wave >> 1, wpx = wave & 1;
   const int W = g.W, H = g.H, Cin = g.Cin;
   const int RG = (H + R - 1) / R;
-  const int n_ = blockIdx.x / RG, rg = blockIdx.x - n_ * RG;
+  const int3 bk = xcd_block3();  // XCD-contiguous block order
+  const int n_ = bk.x / RG, rg = bk.x - n_ * RG;
   const int oh0 = rg * R;
-  const int co0 = blockIdx.y * BC;
+  const int co0 = bk.y * BC;
   const int HW2 = W + 2, HR = R + 2, HPX = HR * HW2;
   const int NPX = R * W;
   const int nch = Cin / HL_KS;
-  const int c_beg = blockIdx.z * chunks_per_split;
+  const int c_beg = bk.z * chunks_per_split;
   const int c_end = min(nch, c_beg + chunks_per_split);
   const int KWC = 9 * Cin;
 
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
       const int co = co0 + wco * (BC / 2) + 16 * i + 4 * (lane >> 4);
       if (PART) {
         if (ok)
-          *reinterpret_cast<float4*>(part + ((long)blockIdx.z * Ptot + P) * g.Cout + co) =
+          *reinterpret_cast<float4*>(part + ((long)bk.z * Ptot + P) * g.Cout + co) =
               make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
         continue;
       }
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
       }
     __syncthreads();
     for (int c = tid; c < BC; c += 256) {
-      float* dst = stats + (long)blockIdx.x * 2 * g.Cout;
+      float* dst = stats + (long)bk.x * 2 * g.Cout;
       dst[co0 + c] = s_st[0][0][c] + s_st[1][0][c];
       dst[g.Cout + co0 + c] = s_st[0][1][c] + s_st[1][1][c];
     }
@@ -233,13 +234,14 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, c
   const int wci = wave >> 1, wpx = wave & 1;
   const int W = g.W, H = g.H, Cout = g.Cout;
   const int RG = (H + R - 1) / R;
-  const int n_ = blockIdx.x / RG, rg = blockIdx.x - n_ * RG;
+  const int3 bk = xcd_block3();  // XCD-contiguous block order
+  const int n_ = bk.x / RG, rg = bk.x - n_ * RG;
   const int ih0 = rg * R;
-  const int ci0 = blockIdx.y * BC;
+  const int ci0 = bk.y * BC;
   const int HW2 = W + 2, HPX = (R + 2) * HW2;
   const int NPX = R * W;
   const int nch = Cout / HL_KS;
-  const int c_beg = blockIdx.z * chunks_per_split;
+  const int c_beg = bk.z * chunks_per_split;
   const int c_end = min(nch, c_beg + chunks_per_split);
   const int KWC = 9 * g.Cin;
 
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, c
       const int ci = ci0 + wci * (BC / 2) + 16 * i + 4 * (lane >> 4);
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (PART) {
-        *reinterpret_cast<float4*>(part + ((long)blockIdx.z * Ptot + P) * g.Cin + ci) =
+        *reinterpret_cast<float4*>(part + ((long)bk.z * Ptot + P) * g.Cin + ci) =
             make_float4(v[0], v[1], v[2], v[3]);
         continue;
       }
