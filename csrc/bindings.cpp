@@ -452,6 +452,7 @@ void op_avgpool_fwd(const Tensor& x, Tensor& y) {
   check(x, "x", at::kBFloat16); check(y, "y", at::kFloat);
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   TORCH_CHECK(y.numel() == (long)N * C, "avgpool out size");
+  TORCH_CHECK(C % 64 == 0 && N < 65536, "avgpool: C % 64 (one block per 64 channels)");
   avgpool_fwd(cbf(x), N, HW, C, y.data_ptr<float>(), cur_stream());
   kcheck();
 }

@@ -145,6 +145,10 @@ void xent(const float* part, int G, const float* bias, int C, int B, const long 
           const int* labels32, BatchIdx bi, float* logits_out, float* dlogits, float* loss_out,
           float* dbias, float gscale, float dbias_scale, hipStream_t s);
 
+// ResNet-width heads (C > 64, labels64, no bias fold): one wave per row; false if unsupported
+bool xent_wave_rows(const float* logits, int C, int B, const long long* labels, float* dlogits,
+                    float* loss_out, float gscale, hipStream_t s);
+
 void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int B,
                const int* labels32, BatchIdx bi, float* dlogits, float* loss_rows, float gscale,
                hipStream_t s);

@@ -352,60 +352,97 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
       make_uint2(bi[0] | bi[1] << 8 | bi[2] << 16 | bi[3] << 24, bi[4] | bi[5] << 8 | bi[6] << 16 | bi[7] << 24);
 }
 
-// Gather form of the backward (deterministic): each input element sums dy over the
-// (at most 4) windows that selected it, in window order.  8 channels per thread.
+// Gather form of the backward (deterministic).  One thread per 2x2 input quad (rows 2a,
+// 2a+1 x cols 2b, 2b+1) and 8 channels: with stride 2 the quad's pixels are covered only
+// by the windows (a|a+1, b|b+1), so the thread loads those four dy / argmax vectors once
+// (a per-pixel gather loads 9 per quad) and sums each pixel's matches in the window order
+// kh, kw = 0..2 (bitwise equal to the per-pixel form).
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const unsigned char* __restrict__ amax,
                                                           int N, int H, int W, int C, int OH, int OW,
                                                           bf16_t* __restrict__ dx) {
   const int cg = C / 8;
-  const int total = N * H * W * cg;
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2;
+  const int total = N * QH * QW * cg;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int g8 = (i % cg) * 8;
-  const int p = i / cg;
-  const int n = p / (H * W);
-  const int r = p - n * H * W;
-  const int ih = r / W, iw = r - ih * W;
+  const int q = i / cg;
+  const int n = q / (QH * QW);
+  const int r = q - n * QH * QW;
+  const int qa = r / QW, qb = r - qa * QW;
+  float d[2][2][8];
+  uint2 am[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int oh = qa + u, ow = qb + v;
+      if (oh < OH && ow < OW) {
+        const long o = (((long)n * OH + oh) * OW + ow) * C + g8;
+        am[u][v] = *reinterpret_cast<const uint2*>(amax + o);
+        unpack8(ld8(dy + o), d[u][v]);
+      } else {
+        am[u][v] = make_uint2(0xffffffffu, 0xffffffffu);  // matches no tap
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[u][v][j] = 0.f;
+      }
+    }
+#pragma unroll
+  for (int dr = 0; dr < 2; ++dr) {
+    const int ih = 2 * qa + dr;
+    if (ih >= H) continue;
+#pragma unroll
+    for (int dc = 0; dc < 2; ++dc) {
+      const int iw = 2 * qb + dc;
+      if (iw >= W) continue;
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      // even row: window row qa at kh = 1; odd row: qa + 1 at kh = 0, then qa at kh = 2
+#pragma unroll
+      for (int ru = 0; ru < (dr ? 2 : 1); ++ru) {
+        const int u = dr ? 1 - ru : 0, kh = dr ? 2 * ru : 1;
+#pragma unroll
+        for (int cv = 0; cv < (dc ? 2 : 1); ++cv) {
+          const int v = dc ? 1 - cv : 0, kw = dc ? 2 * cv : 1;
+          const unsigned kk = kh * 3 + kw;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned bsel = ((j < 4 ? am[u][v].x : am[u][v].y) >> (8 * (j & 3))) & 0xffu;
+            if (bsel == kk) acc[j] += d[u][v][j];
+          }
+        }
+      }
+      *reinterpret_cast<uint4*>(dx + (((long)n * H + ih) * W + iw) * C + g8) = pack8(acc);
+    }
+  }
+}
+
+// global average pool: [N][HW][C] bf16 -> [N][C] fp32.  Block = (n, 64 channels): 8 channel
+// groups (16-B loads) x 32 pixel lanes, lanes summed in fixed order through LDS.
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int HW,
+                                                          int C, float* __restrict__ y) {
+  __shared__ float s_p[32][65];
+  const int n = blockIdx.x, c0 = blockIdx.y * 64;
+  const int cgp = threadIdx.x & 7, pl = threadIdx.x >> 3;
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int p = pl; p < HW; p += 32) {
+    float v[8];
+    unpack8(ld8(x + ((long)n * HW + p) * C + c0 + cgp * 8), v);
 #pragma unroll
-  for (int kh = 0; kh < 3; ++kh) {
-    const int th = ih + 1 - kh;
-    if (th < 0 || (th & 1)) continue;
-    const int oh = th >> 1;
-    if (oh >= OH) continue;
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int tw = iw + 1 - kw;
-      if (tw < 0 || (tw & 1)) continue;
-      const int ow = tw >> 1;
-      if (ow >= OW) continue;
-      const long o = (((long)n * OH + oh) * OW + ow) * C + g8;
-      const uint2 am = *reinterpret_cast<const uint2*>(amax + o);
-      float d[8];
-      unpack8(ld8(dy + o), d);
-      const unsigned kk = kh * 3 + kw;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const unsigned b = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
-        if (b == kk) acc[j] += d[j];
-      }
-    }
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
   }
-  *reinterpret_cast<uint4*>(dx + (long)p * C + g8) = pack8(acc);
-}
-
-// global average pool: [N][HW][C] bf16 -> [N][C] fp32 (thread per (n, c), fixed order)
-__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int HW, int C,
-                                   float* __restrict__ y) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N * C) return;
-  const int n = i / C, c = i - (i / C) * C;
-  float s = 0.f;
-  for (int p = 0; p < HW; ++p) s += bf2f(x[((long)n * HW + p) * C + c]);
-  y[i] = s / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s_p[pl][cgp * 8 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+    for (int l = 0; l < 32; ++l) t += s_p[l][threadIdx.x];
+    y[(long)n * C + c0 + threadIdx.x] = t / (float)HW;
+  }
 }
 
 __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int HW, int C,
@@ -415,6 +452,56 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int HW, 
   const int c = (int)(i % C);
   const int n = (int)(i / ((long)HW * C));
   dx[i] = f2bf(dy[(long)n * C + c] / (float)HW);
+}
+
+// ---------------------------------------------------------------- classifier loss
+// Mean softmax cross-entropy over [B][C] fp32 logits (C <= 1024) for wide heads: one wave
+// per row (4 rows per block, B/4 blocks) instead of one block looping over the rows.
+// Per-row losses go out write-through; the last block sums them in row order.
+constexpr int XR_M = 16;
+__global__ __launch_bounds__(256) void xent_wave_rows_kernel(const float* __restrict__ logits, int C,
+                                                             int B, const long long* __restrict__ labels,
+                                                             float* __restrict__ dlogits,
+                                                             float* __restrict__ loss_out,
+                                                             float* __restrict__ ws, int* __restrict__ ticket,
+                                                             float gscale) {
+  __shared__ int s_last;
+  const int lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b < B) {
+    const int label = (int)labels[b];
+    float x[XR_M];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < XR_M; ++m) {
+      const int c = lane + 64 * m;
+      x[m] = c < C ? logits[(long)b * C + c] : -INFINITY;
+      mx = fmaxf(mx, x[m]);
+    }
+    mx = wave_max(mx);
+    float se = 0.f, xl = 0.f;
+#pragma unroll
+    for (int m = 0; m < XR_M; ++m) {
+      const int c = lane + 64 * m;
+      if (c == label) xl = x[m];
+      x[m] = c < C ? __expf(x[m] - mx) : 0.f;
+      se += x[m];
+    }
+    se = wave_sum(se);
+    xl = wave_sum(xl);  // logit[label]
+    const float inv = 1.f / se;
+#pragma unroll
+    for (int m = 0; m < XR_M; ++m) {
+      const int c = lane + 64 * m;
+      if (c < C) dlogits[(long)b * C + c] = (x[m] * inv - (c == label ? 1.f : 0.f)) * gscale;
+    }
+    if (lane == 0) st_wt(ws + b, mx + __logf(se) - xl);
+  }
+  if (!last_arrival(ticket, gridDim.x, &s_last)) return;
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int r = 0; r < B; ++r) t += ld_agent(ws + r);
+    loss_out[0] = t / (float)B;
+  }
 }
 
 // ---------------------------------------------------------------- input pipeline
@@ -574,7 +661,7 @@ void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf
 
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
                  int OW, bf16_t* dx, hipStream_t s) {
-  const long total = (long)N * H * W * (C / 8);
+  const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, dy,
                      amax, N, H, W, C, OH, OW, dx);
 }
@@ -587,7 +674,21 @@ void image_gather_nhwc4(const unsigned char* imgs, const long long* idx, int B, 
 }
 
 void avgpool_fwd(const bf16_t* x, int N, int HW, int C, float* y, hipStream_t s) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * C + 255) / 256), dim3(256), 0, s, x, N, HW, C, y);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(N, C / 64), dim3(256), 0, s, x, N, HW, C, y);
+}
+
+bool xent_wave_rows(const float* logits, int C, int B, const long long* labels, float* dlogits,
+                    float* loss_out, float gscale, hipStream_t s) {
+  constexpr int kMaxB = 8192;
+  if (C > 64 * XR_M || B > kMaxB || B < 1) return false;
+  static float* wsp[64] = {};
+  int dev = 0;
+  RN_CHECK(hipGetDevice(&dev));
+  dev &= 63;
+  if (!wsp[dev]) RN_CHECK(hipMalloc(reinterpret_cast<void**>(&wsp[dev]), sizeof(float) * kMaxB));
+  hipLaunchKernelGGL(xent_wave_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, logits, C, B, labels,
+                     dlogits, loss_out, wsp[dev], ticket_slots(1), gscale);
+  return true;
 }
 
 void avgpool_bwd(const float* dy, int N, int HW, int C, bf16_t* dx, hipStream_t s) {

@@ -122,6 +122,9 @@ void xent(const float* part, int G, const float* bias, int C, int B, const long 
           const int* labels32, BatchIdx bi, float* logits_out, float* dlogits, float* loss_out,
           float* dbias, float gscale, float dbias_scale, hipStream_t s) {
   // one wave per row when there is no bias gradient to fold (it is reduced over 4 waves)
+  if (G == 1 && !bias && !dbias && !logits_out && labels64 && !bi.step_ctr && C > 64 &&
+      xent_wave_rows(part, C, B, labels64, dlogits, loss_out, gscale, s))
+    return;
   const int waves = dbias ? 4 : (B < 16 ? (B < 4 ? 4 : B) : 16);
   hipLaunchKernelGGL(xent_kernel, dim3(1), dim3(64 * waves), 0, s, part, G, bias, C, B, labels64, labels32,
                      bi, logits_out, dlogits, loss_out, dbias, gscale, dbias_scale);

@@ -219,6 +219,46 @@ def test_batchnorm_fwd_bwd_matches_torch(C, P_img, Cc):
     assert torch.equal(sums, sums2)
 
 
+@pytest.mark.parametrize("H,W", [(56, 56), (8, 11)])
+def test_maxpool_bwd_quad_shapes(C, H, W):
+    """maxpool backward (one thread per 2x2 input quad) on even and odd / non-square inputs."""
+    N, Cc = 2, 64
+    x = rnd(N, H, W, Cc, seed=21)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty(N, OH, OW, Cc, dtype=BF, device=dev)
+    am = torch.empty(N, OH, OW, Cc, dtype=torch.uint8, device=dev)
+    C.maxpool_fwd(x, y, am)
+    xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    dy = rnd(N, OH, OW, Cc, seed=22)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    dx = torch.empty_like(x)
+    C.maxpool_bwd(dy, am, dx)
+    assert relerr(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    dx2 = torch.full_like(x, 7.0)
+    C.maxpool_bwd(dy, am, dx2)  # every input element written, deterministically
+    assert torch.equal(dx, dx2)
+
+
+@pytest.mark.parametrize("B,NC", [(32, 1000), (5, 1000), (64, 100)])
+def test_xent_wide_head_wave_rows(C, B, NC):
+    """ResNet-width cross-entropy (one wave per row, last-block mean) vs fp32 PyTorch."""
+    g = torch.Generator().manual_seed(B + NC)
+    lg = (torch.randn(B, NC, generator=g) * 3).to(dev)
+    y = torch.randint(0, NC, (B,), generator=g).to(dev)
+    dl = torch.empty_like(lg)
+    loss = torch.empty(1, device=dev)
+    C.xent(lg, 1, None, y, None, dl, loss, None, 1.0 / B, 0.0)
+    lr = lg.clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, y)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
+    assert relerr(dl, lr.grad) < 1e-4
+    loss2 = torch.empty(1, device=dev)
+    C.xent(lg, 1, None, y, None, dl, loss2, None, 1.0 / B, 0.0)
+    assert torch.equal(loss, loss2)  # fixed-order row sum
+
+
 def test_pools_and_head(C):
     N, H, Cc = 2, 9, 64
     x = rnd(N, H, H, Cc, seed=9)
