@@ -8,6 +8,8 @@
 // (hipIpcOpenMemHandle: xGMI peer mappings on a multi-GPU node, a second mapping of the
 // same memory when several ranks share one GPU in tests).  all_reduce() is one kernel
 // launch on the caller's stream, capturable in a hipGraph.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "runtime/runtime.h"
@@ -30,6 +32,8 @@ XgmiComm::XgmiComm(int rank, int world, int device) : rank_(rank), world_(world)
     throw std::runtime_error("xgmi: world size must be 1.." + std::to_string(XGMI_MAX_RANKS));
   if (rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad rank");
   DDP_HIP_CHECK(hipSetDevice(device));
+  // rehearsal knobs (several ranks sharing one GPU): a longer barrier bound
+  if (const char* e = std::getenv("DDP_AMD_XGMI_TIMEOUT_S")) timeout_s_ = std::atof(e);
 }
 
 XgmiComm::~XgmiComm() {
@@ -49,6 +53,9 @@ int XgmiComm::add_channel(long off, long n, bool oneshot) {
   c.oneshot = oneshot;
   c.slice = (n + world_ - 1) / world_;
   c.blocks = xgmi_blocks(n, world_, oneshot);
+  // and a smaller grid, so the ranks' spinning blocks leave CUs to the others' kernels
+  // (the kernel is block-strided; every rank must see the same value)
+  if (const char* e = std::getenv("DDP_AMD_XGMI_GRID_CAP")) c.blocks = std::max(1, std::min(c.blocks, std::atoi(e)));
   if (c.blocks > XGMI_MAX_BLOCKS) throw std::runtime_error("xgmi: bucket too large for one channel");
   const long stage = oneshot ? n : c.slice;  // per parity
   DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c.stage_local), sizeof(float) * 2 * stage));
