@@ -497,9 +497,13 @@ ShadowSet make_shadows(const py::list& shadows) {
     Tensor dst = t[2].cast<Tensor>();
     check(dst, "shadow dst", at::kBFloat16);
     const long n = t[1].cast<long>();
-    TORCH_CHECK(dst.numel() == n, "shadow dst size mismatch");
     const int kind = t[3].cast<int>(), a = t[4].cast<int>(), b = t[5].cast<int>(), c = t[6].cast<int>();
-    TORCH_CHECK(kind >= SHADOW_BF16 && kind <= SHADOW_BF16_FCFRAG, "unknown shadow kind");
+    TORCH_CHECK(kind >= SHADOW_BF16 && kind <= SHADOW_BF16_PAD4, "unknown shadow kind");
+    if (kind == SHADOW_BF16_PAD4) {
+      TORCH_CHECK(n % 3 == 0 && dst.numel() == n / 3 * 4, "PAD4 shadow: dst must hold n/3 x 4");
+    } else {
+      TORCH_CHECK(dst.numel() == n, "shadow dst size mismatch");
+    }
     if (kind == SHADOW_BF16_TAPT) TORCH_CHECK((long)a * b * c == n, "TAPT shadow: Co*T*Ci != n");
     if (kind == SHADOW_BF16_FCFRAG)
       TORCH_CHECK(a % 16 == 0 && b % 16 == 0 && n % ((long)a * b) == 0 && n < (1L << 31),

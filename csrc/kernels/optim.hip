@@ -59,6 +59,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
                 sh.r[r].dst[jj] = f2bf(e[u]);
               } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
                 sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(e[u]);
+              } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
+                sh.r[r].dst[(jj / 3) * 4 + jj % 3] = f2bf(e[u]);
               } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
                 const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
                 const long co = jj / ((long)T * Ci);
@@ -88,6 +90,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
         sh.r[r].dst[j] = f2bf(v);
       } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
         sh.r[r].dst[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = f2bf(v);
+      } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
+        sh.r[r].dst[(j / 3) * 4 + j % 3] = f2bf(v);
       } else {
         const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
         const long co = j / ((long)T * Ci);

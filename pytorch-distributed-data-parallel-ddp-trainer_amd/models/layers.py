@@ -234,6 +234,7 @@ class FlatSpace:
         module._ddp_amd_flat = self
         self._bf16 = None
         self._bf16_version = -1
+        self._pad4: dict = {}  # flat offset -> bf16 [..][4] copy of a [..][3] parameter
 
     def bf16_params(self) -> torch.Tensor:
         """bf16 copy of the flat parameters (the MFMA kernels' weight operand).
@@ -247,8 +248,34 @@ class FlatSpace:
         if self._bf16_version != self.params._version:
             with torch.no_grad():
                 self._bf16.copy_(self.params)
+                for off, buf in self._pad4.items():
+                    self._fill_pad4(off, buf)
             self._bf16_version = self.params._version
         return self._bf16
+
+    def _fill_pad4(self, off: int, buf: torch.Tensor):
+        n = buf.numel() // 4 * 3
+        buf.view(-1, 4)[:, :3].copy_(self.params[off:off + n].view(-1, 3))
+
+    def bf16_pad4_view(self, p: torch.Tensor):
+        """bf16 copy of a ``[..., 3]`` parameter zero-padded to ``[..., 4]`` (the ResNet stem
+        weight as its conv kernel loads it), kept fresh exactly like :meth:`bf16_params`:
+        FusedSGD rewrites it in its update pass (a SHADOW_BF16_PAD4 region) and any other
+        write rebuilds it with the flat copy.  ``None`` if ``p`` is not a flat-space view."""
+        if p.shape[-1] != 3 or self.bf16_view(p) is None:  # bf16_view also refreshes
+            return None
+        off = (p.data_ptr() - self.params.data_ptr()) // self.params.element_size()
+        buf = self._pad4.get(off)
+        if buf is None:
+            buf = torch.zeros(*p.shape[:-1], 4, dtype=torch.bfloat16, device=self.device)
+            with torch.no_grad():
+                self._fill_pad4(off, buf)
+            self._pad4[off] = buf
+        return buf
+
+    def pad4_shadows(self) -> list:
+        """SGD shadow regions (off, n, dst, kind=4, 0, 0, 0) of the padded copies."""
+        return [(off, buf.numel() // 4 * 3, buf, 4, 0, 0, 0) for off, buf in self._pad4.items()]
 
     def bf16_view(self, p: torch.Tensor):
         """The bf16 copy of parameter ``p``, same shape; ``None`` if ``p`` no longer lives

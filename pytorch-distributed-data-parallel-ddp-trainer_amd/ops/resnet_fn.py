@@ -57,7 +57,12 @@ class _ConvBNAct(torch.autograd.Function):
         stem = Cin == 4 and wcin == 3
         OH, OW = (H + 2 * pad - KH) // stride + 1, (W_ + 2 * pad - KW) // stride + 1
         wb = _weight_bf16(w)
-        wk = torch.nn.functional.pad(wb, (0, 1)) if stem else wb
+        wk = wb
+        if stem:  # the padded copy FusedSGD keeps, else a per-call pad
+            fs = getattr(w, "_ddp_amd_fs", None)
+            wk = fs.bf16_pad4_view(w) if fs is not None else None
+            if wk is None:
+                wk = torch.nn.functional.pad(wb, (0, 1))
         y = torch.empty(N, OH, OW, Cout, dtype=BF16, device=x.device)
         C = _C()
         P = N * OH * OW

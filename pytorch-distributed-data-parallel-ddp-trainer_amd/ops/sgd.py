@@ -62,7 +62,7 @@ class FusedSGD:
 
             shadows = self.shadows
             if fs._bf16 is not None:  # the model's bf16 weight copy, refreshed in the same pass
-                shadows = shadows + [(0, fs.numel, fs._bf16, 1, 0, 0, 0)]
+                shadows = shadows + [(0, fs.numel, fs._bf16, 1, 0, 0, 0)] + fs.pad4_shadows()
             native.require().sgd(fs.params, fs.grads, self.momentum_buffer, g["lr"], g["momentum"],
                                  g["dampening"], g["weight_decay"], g["nesterov"], g["maximize"],
                                  first, True, shadows)

@@ -355,11 +355,17 @@ def test_resnet18_direct_grads_and_bf16_weight_copy():
         opt.step()
         assert fs._bf16_version == fs.params._version
         assert torch.equal(fs._bf16, fs.params.to(torch.bfloat16))
+        # the stem's zero-padded bf16 weight (PAD4 shadow) is rewritten in the same pass
+        pad_ref = F.pad(b.conv1.weight.detach().to(torch.bfloat16), (0, 1))
+        assert len(fs._pad4) == 1
+        assert torch.equal(next(iter(fs._pad4.values())), pad_ref)
     # a torch-side write to the parameters invalidates the copy; the next use rebuilds it
     with torch.no_grad():
         b.conv1.weight.mul_(0.5)
     assert fs._bf16_version != fs.params._version
     assert torch.equal(fs.bf16_view(b.conv1.weight), b.conv1.weight.to(torch.bfloat16))
+    assert torch.equal(fs.bf16_pad4_view(b.conv1.weight),
+                       F.pad(b.conv1.weight.detach().to(torch.bfloat16), (0, 1)))
 
 
 def test_graphed_step_equals_eager():
