@@ -4,6 +4,18 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+``--gpus N`` (N > 1) without a launcher environment SELF-LAUNCHES: the parent never
+touches the GPU (no torch.cuda call, no native import); it starts
+``torch.distributed.run`` with N fresh worker processes (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT) as a child process - the
+reference's launcher derives N processes from world_size the same way
+(``/root/reference/train_ddp.py:221-224``) - and, unless ``--no_scaling_ref``, first a
+1-rank child run of the same config, so its ONE JSON line carries
+``scaling_efficiency`` = value(N) / (N * value(1)).  Workers assert
+``dist.get_world_size() == N`` and the native RCCL communicator's nranks == N and report
+both (``ranks_seen``, ``rccl_nranks``), plus the data plane (``bucket_allreduce``) and
+each bucket's isolated all-reduce time (``bucket_allreduce_us``).
+
 Metric/config are BASELINE.json's: images/sec of the reference's SimpleCNN
 (520,586 params) DDP training step at the reference's default per-rank batch
 (32), weak scaling (per-GPU batch fixed), synthetic MNIST-shaped uint8 data and
@@ -25,6 +37,7 @@ so its best measured aggregate at any batch, 3,670 img/s, is used).
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -44,6 +57,88 @@ def graph_chunk(k: int, cap: int = 100) -> int:
     return 1
 
 
+LAUNCH_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _child_json(cmd, env, timeout):
+    """Run one launcher child; return its last JSON stdout line (stderr passes through)."""
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True,
+                       timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        sys.stdout.write(p.stdout)
+        raise SystemExit(f"[bench] launcher child failed (rc={p.returncode}): {' '.join(cmd)}")
+    return json.loads(lines[-1])
+
+
+def self_launch(args, argv):
+    """``--gpus N`` without a launcher env: N fresh worker processes via torch.distributed.run
+    (a child process - this parent never initialises the GPU and never execs)."""
+    n = args.gpus
+    here = os.path.abspath(__file__)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / xGMI peer mappings)
+
+    def run(nproc, extra=()):
+        port = _free_port()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={port}",
+               here, *_with_gpus(argv, nproc), *extra]
+        return _child_json(cmd, env, args.launch_timeout)
+
+    if args.dry_launch:
+        rec = run(n)
+        print(json.dumps(rec), flush=True)
+        return
+    ref = None
+    if not args.no_scaling_ref:
+        ref = run(1)
+    rec = run(n)
+    rec.setdefault("config", {})["launcher"] = "self (torch.distributed.run child)"
+    if ref is not None and ref.get("value"):
+        rec["config"]["n1_value"] = ref["value"]
+        rec["config"]["scaling_efficiency"] = round(rec["value"] / (n * ref["value"]), 4)
+    print(json.dumps(rec), flush=True)
+
+
+def _with_gpus(argv, n):
+    """argv with --gpus forced to n (both "--gpus N" and "--gpus=N" spellings)."""
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a == "--gpus":
+            skip = True
+            continue
+        if a.startswith("--gpus="):
+            continue
+        out.append(a)
+    return ["--gpus", str(n), *out]
+
+
+def dry_worker(args):
+    """--dry_launch inside a worker: report what the launcher gave this rank, gathered on
+    rank 0 over a gloo group (no GPU)."""
+    rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    mine = {k: os.environ.get(k) for k in LAUNCH_ENV}
+    allenv = [None] * ws
+    dist.all_gather_object(allenv, mine)
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "n_gpus": args.gpus, "ranks_seen": dist.get_world_size(),
+                          "children": allenv}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,9 +154,10 @@ def main():
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
     ap.add_argument("--store_a1", type=int, default=None, choices=[0, 1, 2],
                     help="fused engine: conv1 output for the backward recomputed (0) / stored for dgrad (1) / for both (2)")
-    ap.add_argument("--comm", choices=["auto", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
-                    help="bucket all-reduce at N>1: auto = fastest of xGMI two-shot (xgmi2), xGMI with the "
-                         "one-shot kernel for the small bucket (xgmi1) and RCCL, timed on the node")
+    ap.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
+                    help="bucket all-reduce at N>1: auto = direct xGMI kernels (one-shot for the small "
+                         "bucket), RCCL if their self-test fails; tune = fastest of xgmi2 / xgmi1 / RCCL "
+                         "timed on the node")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="control-plane process group (nccl = RCCL); gloo + --comm xgmi rehearses "
                          "N ranks on ONE GPU (RCCL refuses duplicate GPUs)")
@@ -69,7 +165,21 @@ def main():
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
     ap.add_argument("--image_size", type=int, default=224, help="resnet18 input size")
-    args = ap.parse_args()
+    ap.add_argument("--dry_launch", action="store_true",
+                    help="self-launch test hook: workers report their launcher env and exit (no GPU)")
+    ap.add_argument("--no_scaling_ref", action="store_true",
+                    help="self-launch: skip the 1-rank reference run (scaling_efficiency null)")
+    ap.add_argument("--launch_timeout", type=float, default=900.0, help="self-launch: per-child seconds")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    launched = all(k in os.environ for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"))
+    if not launched and args.gpus > 1:
+        return self_launch(args, argv)
+    if args.dry_launch:
+        if launched:
+            return dry_worker(args)
+        print(json.dumps({"dry_launch": True, "n_gpus": 1, "ranks_seen": 1, "children": []}))
+        return
     if args.model == "resnet18":
         return bench_resnet(args)
 
@@ -84,18 +194,23 @@ def main():
     native.require()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if ws != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    if ws != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
     lrank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "gloo":  # rehearsal: several ranks may share the visible GPUs
         lrank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(lrank)
     dev = torch.device("cuda", lrank)
     comm = None
+    ranks_seen, rccl_nranks = 1, None
     if ws > 1:
         setup(rank, ws, backend=args.backend, verbose=False)
+        ranks_seen = dist.get_world_size()
+        assert ranks_seen == ws == args.gpus, (ranks_seen, ws, args.gpus)
         if args.backend == "nccl":
             comm = native_comm()
+            rccl_nranks = comm.world
+            assert rccl_nranks == ws, f"native RCCL communicator has {rccl_nranks} ranks, expected {ws}"
         elif args.comm == "rccl":
             raise SystemExit("--backend gloo has no RCCL data plane: use --comm xgmi")
 
@@ -147,6 +262,7 @@ def main():
         dt = float(t.item())
     ms = dt * 1000.0 / args.steps
     img_s = ws * args.batch_size * args.steps / dt
+    bucket_us = eng.measure_bucket_allreduce() if ws > 1 else None  # after the timed region
     finite = bool(torch.isfinite(fs.params).all().item())
     same = True
     if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
@@ -180,8 +296,11 @@ def main():
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
                                   "wgrad_rows": eng.wgrad_rows, "store_a1": eo.store_a1},
                        "params_finite": finite,
-                       "bucket_allreduce": eng.comm_kind, "params_identical_across_ranks": same,
-                       "allreduce_pair_us": eng.allreduce_us},
+                       "bucket_allreduce": eng.comm_kind, "bucket_allreduce_us": bucket_us,
+                       "buckets_elems": [n for _, n in eng.ranges],
+                       "params_identical_across_ranks": same, "ranks_seen": ranks_seen,
+                       "rccl_nranks": rccl_nranks, "backend": args.backend if ws > 1 else None,
+                       "scaling_efficiency": None, "tuned_planes_us": eng.allreduce_us},
         }), flush=True)
     if ws > 1:
         barrier()

@@ -158,7 +158,8 @@ void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int
 // read by the conv3x3_fwd FC epilogue, [o][hw/16][c/16][(c/4)%4][hw%16][c%4], so each
 // wave-instruction of that epilogue loads 512 contiguous bytes.
 // SHADOW_BF16_PAD4: a [..][3] weight (the ResNet stem) -> [..][4] with the 4th channel left
-// at its zero fill (the stem conv's 16-B weight loads read it); sgd_kernel only.
+// at its zero fill (the stem conv's 16-B weight loads read it); sgd_kernel and the xGMI
+// fused-SGD all-gather (shadow_one).
 enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2, SHADOW_BF16_FCFRAG = 3, SHADOW_BF16_PAD4 = 4 };
 constexpr int MAX_SHADOWS = 4;
 struct ShadowRegion {

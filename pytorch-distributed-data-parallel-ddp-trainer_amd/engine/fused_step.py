@@ -53,9 +53,10 @@ class EngineOptions:
     # wgrad role reads a1 tiles too
     store_a1: int = 0
     # bucket all-reduce data plane at world size > 1 (the direct kernels fall back to RCCL
-    # when their self-test fails): "auto" = time two-shot xGMI, two-shot + one-shot for
-    # the small bucket, and RCCL on the node and keep the fastest; "xgmi" = the fastest
-    # of the two xGMI plans; "xgmi2" / "xgmi1" = that plan, forced; "rccl" = RCCL
+    # when their self-test fails): "auto"/"xgmi" = the direct xGMI kernels, one-shot for
+    # buckets <= ONESHOT_MAX_ELEMS (deterministic: same plane on every start, so resumes
+    # reduce in the same order); "tune" = time two-shot, two-shot + one-shot and RCCL on
+    # the node and keep the fastest; "xgmi2" / "xgmi1" = that plan, forced; "rccl" = RCCL
     comm: str = "auto"
 
 
@@ -120,7 +121,7 @@ class FusedSimpleCNNEngine:
         self.xgmi_plan = None
         self.allreduce_us = None
         xch = (0, 1)
-        if use_comm and self.opts.comm in ("auto", "xgmi", "xgmi1", "xgmi2"):
+        if use_comm and self.opts.comm in ("auto", "tune", "xgmi", "xgmi1", "xgmi2"):
             from ..parallel.xgmi import channel_plan, create_xgmi, pick_data_plane
 
             # small buckets also get a one-shot channel (one cross-GPU barrier instead of two)
@@ -128,12 +129,17 @@ class FusedSimpleCNNEngine:
             self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size, oneshot=oneshot)
             if self.xgmi is not None and self.opts.comm in ("xgmi1", "xgmi2"):
                 plan = "xgmi1" if self.opts.comm == "xgmi1" else "xgmi"  # forced (tests, sweeps)
+            elif self.xgmi is not None and self.opts.comm in ("auto", "xgmi"):
+                # deterministic: the plane depends only on the self-test outcome and the bucket
+                # sizes, never on timing noise, so an uninterrupted run and a resumed run
+                # reduce in the same order (BASELINE config 4).  Both xGMI plans sum in fixed
+                # rank order 0..N-1, so they are bitwise interchangeable; RCCL is not.
+                plan = "xgmi1" if oneshot else "xgmi"
             elif self.xgmi is not None:
-                # measure one step's bucket all-reduces under each plan on this node and
-                # keep the fastest (rank 0 decides for everyone); RCCL competes in "auto"
+                # "tune": measure one step's bucket all-reduces under each plan on this node
+                # and keep the fastest (rank 0 decides for everyone); RCCL competes
                 plan, self.allreduce_us = pick_data_plane(
-                    self.xgmi, comm if self.opts.comm == "auto" else None, fs.grads, ranges, rank,
-                    oneshot=oneshot)
+                    self.xgmi, comm, fs.grads, ranges, rank, oneshot=oneshot)
             if self.xgmi is not None:
                 self.xgmi_plan = plan
                 if plan == "rccl":
@@ -144,6 +150,7 @@ class FusedSimpleCNNEngine:
         if use_comm and self.xgmi is None and comm is None:
             raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
         self.comm_kind = (self.xgmi_plan or "xgmi") if self.xgmi is not None else ("rccl" if use_comm else "none")
+        self.ranges, self.xch, self.comm = ranges, xch, (comm if use_comm else None)
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.xgmi is not None:
             self.eng.set_xgmi(self.xgmi, *xch)
@@ -175,6 +182,33 @@ class FusedSimpleCNNEngine:
         if self.opts.use_graph and self._captured != k:
             self.eng.capture(k)
             self._captured = k
+
+    def measure_bucket_allreduce(self, iters: int = 20) -> list | None:
+        """Device time (us) of each bucket's all-reduce on the engine's data plane, in
+        isolation (collective: every rank calls it).  Clobbers the gradient buffer - the
+        step rewrites every bucket, so call it between steps only."""
+        if self.comm_kind == "none":
+            return None
+        self.synchronize()
+        out = []
+        for b, (off, n) in enumerate(self.ranges):
+            if self.xgmi is not None:
+                fn = lambda ch=self.xch[b]: self.xgmi.all_reduce(ch)  # noqa: E731
+            else:
+                view = self.fs.grads[off:off + n]
+                fn = lambda v=view: self.comm.all_reduce(v)  # noqa: E731
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                fn()
+            e1.record()
+            e1.synchronize()
+            out.append(round(e0.elapsed_time(e1) * 1000.0 / iters, 2))
+        if self.xgmi is not None and self.xgmi.error_flags():
+            raise RuntimeError("xGMI all-reduce: a cross-GPU barrier timed out while timing buckets")
+        return out
 
     # ------------------------------------------------------------------ epoch
     def start_epoch(self, epoch: int):

@@ -26,7 +26,7 @@ import torch.distributed as dist
 from ..data import (DeviceImageLoader, DeviceImages, DeviceMNIST, DeviceMNISTLoader, get_dataloader,
                     load_mnist, synthetic_imagenet)
 from ..models import SimpleCNN, resnet18
-from ..models.layers import flat_space
+from ..models.layers import buffer_space, flat_space
 from ..ops import CrossEntropyLoss, FusedSGD
 from ..parallel import DistributedDataParallel as DDP
 from ..parallel import cleanup, local_rank, native_comm, setup
@@ -39,6 +39,7 @@ class TrainOptions:
     momentum: float = 0.0
     weight_decay: float = 0.0
     backend: str | None = None        # rccl|nccl|gloo (default: rccl on GPU, gloo on CPU)
+    device: str | None = None         # auto|gpu|cpu: "gpu" fails loudly without a usable HIP device
     engine: str = "fused"             # fused | module   (GPU only)
     data: str = "auto"                # auto | mnist | synthetic
     data_root: str = "./data"
@@ -68,7 +69,7 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
               opts: TrainOptions | None = None):
     opts = opts or TrainOptions()
     backend = setup(rank=rank, world_size=world_size, backend=opts.backend,
-                    timeout_s=opts.pg_timeout_s)
+                    timeout_s=opts.pg_timeout_s, device=opts.device)
     on_gpu = backend == "nccl"
     device = torch.device("cuda", local_rank(rank)) if on_gpu else torch.device("cpu")
     print(f"Rank {rank} initialized", flush=True)
@@ -161,7 +162,8 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
         if on_gpu:
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        _record_metrics(opts, rank, world_size, epoch, nsteps, batch_size, dt, len(sampler))
+        _record_metrics(opts, rank, world_size, epoch, nsteps, batch_size, dt,
+                        samples_processed(nsteps, batch_size, len(sampler)))
 
         if rank == 0 and opts.save:
             save_checkpoint(opts.checkpoint_dir, epoch, model, opt)
@@ -196,9 +198,10 @@ def _verify_and_broadcast(fs, model, world_size):
     if any(m != allm[0] for m in allm):
         raise RuntimeError(f"parameter shapes differ across ranks: {allm}")
     with torch.no_grad():
-        dist.broadcast(fs.params, src=0)
-        for b in model.buffers():
-            dist.broadcast(b, src=0)
+        dist.broadcast(fs.params, src=0)  # one flat collective (SimpleCNN has no buffers)
+        bs = buffer_space(model)
+        if bs is not None:
+            dist.broadcast(bs.bytes, src=0)
 
 
 def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_steps,
@@ -284,7 +287,15 @@ def _run_graphed_epoch(model, loader, loss_fn, opt, log, log_every, max_steps):
     return n
 
 
+def samples_processed(nsteps: int, batch: int, samples_per_rank: int) -> int:
+    """Images a rank actually trained on in ``nsteps`` steps of an epoch of
+    ``samples_per_rank`` (full batches, then the ragged tail; ``--max_steps`` /
+    ``--fault_at`` truncate the epoch)."""
+    return min(nsteps * batch, samples_per_rank)
+
+
 def _record_metrics(opts, rank, ws, epoch, nsteps, batch, dt, samples):
+    """``samples``: images this rank processed in the epoch (:func:`samples_processed`)."""
     if not opts.metrics_json or rank != 0:
         return
     import json

@@ -316,6 +316,79 @@ class FlatSpace:
         self.reattach_grads()
 
 
+class BufferSpace:
+    """Every buffer of a module (BatchNorm running stats, ``num_batches_tracked``, ...) as a
+    typed view into ONE contiguous byte buffer, so DDP's ``broadcast_buffers`` is a single
+    collective per forward instead of one per tensor (torch DDP coalesces the same way,
+    ``torch/nn/parallel/distributed.py:1557-1558``; ResNet-18 has 60 buffers).
+
+    Each buffer starts on a 64-byte boundary; the module's ``_buffers`` entries are
+    replaced by views, so in-place kernel updates land in the flat bytes.
+    :meth:`rehome` copies back any buffer that was REPLACED by a new tensor since
+    (``module.buf = t``) and re-points it at its view."""
+
+    def __init__(self, module: nn.Module, align: int = 64):
+        self.module = module
+        self.names = [n for n, _ in module.named_buffers()]
+        named = dict(module.named_buffers())
+        self.offsets, self.nbytes, self.meta = {}, {}, {}
+        off = 0
+        for n in self.names:
+            b = named[n]
+            nb = b.numel() * b.element_size()
+            self.offsets[n], self.nbytes[n] = off, nb
+            self.meta[n] = (b.dtype, tuple(b.shape))
+            off += (nb + align - 1) // align * align
+        self.total = off
+        dev = named[self.names[0]].device if self.names else torch.device("cpu")
+        self.bytes = torch.zeros(max(off, 1), dtype=torch.uint8, device=dev)
+        self._views = {}
+        for n in self.names:
+            v = self.view(n)
+            with torch.no_grad():
+                v.copy_(named[n])
+            self._views[n] = v
+            mod, attr = _resolve(module, n)
+            mod._buffers[attr] = v
+        module._ddp_amd_bufs = self
+
+    def view(self, name: str) -> torch.Tensor:
+        """Alias of the buffer's bytes with its OWN version counter (``set_`` on the
+        storage, not an autograd view): BatchNorm saves running stats for backward, and
+        a version counter shared by all 60 buffers would make every later layer's
+        in-place stat update look like a modification of the saved tensor."""
+        dt, shape = self.meta[name]
+        es = torch.empty(0, dtype=dt).element_size()
+        t = torch.empty(0, dtype=dt, device=self.bytes.device)
+        t.set_(self.bytes.untyped_storage(), self.offsets[name] // es, shape)
+        return t
+
+    def rehome(self) -> int:
+        """Pull replaced buffers back into the flat bytes; returns how many moved."""
+        moved = 0
+        for n in self.names:
+            mod, attr = _resolve(self.module, n)
+            cur, v = mod._buffers.get(attr), self._views[n]
+            if cur is None or cur.data_ptr() == v.data_ptr():
+                continue
+            with torch.no_grad():
+                v.copy_(cur)
+            mod._buffers[attr] = v
+            moved += 1
+        return moved
+
+
+def buffer_space(module: nn.Module) -> BufferSpace | None:
+    """The module's BufferSpace (created on first use); ``None`` if it has no buffers."""
+    bs = getattr(module, "_ddp_amd_bufs", None)
+    if bs is None:
+        if not any(True for _ in module.buffers()):
+            return None
+        bs = BufferSpace(module)
+    bs.rehome()
+    return bs
+
+
 def _resolve(module: nn.Module, name: str):
     parts = name.split(".")
     mod = module

@@ -114,8 +114,18 @@ class FusedSGD:
                    if "momentum_buffer" in v}
             _from_reference_layout(self.model, self.flat, ref, buf)
             self.momentum_buffer = buf
+            # torch only creates a momentum buffer in its first step: a loaded buffer means
+            # the next step is a regular update (buf = m*buf + (1-d)*g), never the
+            # initialisation step (buf = g) - the fused engine keys that off ``steps``
+            self.steps = max(self.steps, 1)
         else:
             self.momentum_buffer = None
+            self.steps = 0
+
+    def mark_started(self):
+        """A momentum buffer arrived from elsewhere (resume broadcast): treat as started."""
+        if self.momentum_buffer is not None:
+            self.steps = max(self.steps, 1)
 
 
 def _owner(model, name):

@@ -10,7 +10,10 @@ Behaviour kept from the reference's DDP:
 * a bucket is all-reduced as soon as its last gradient is accumulated (overlap
   with the rest of backward); ``loss.backward()`` returns with averaged
   gradients (sum_r g_r / ws);
-* ``broadcast_buffers``: rank 0's buffers are broadcast before each forward;
+* ``broadcast_buffers``: rank 0's buffers are broadcast before each forward - ONE
+  collective over a flat byte buffer that every module buffer is a view into
+  (``BufferSpace``; torch coalesces the same way), stream-ordered RCCL from our native
+  communicator on the GPU, so the whole step stays hipGraph-capturable at any world size;
 * ``no_sync()`` for gradient accumulation; ``.module`` for the wrapped model.
 
 MI355X-first differences: parameters and gradients live in one flat fp32 buffer
@@ -28,7 +31,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..models.layers import FlatSpace, flat_space
+from ..models.layers import FlatSpace, buffer_space, flat_space
 
 
 def bucket_plan(fs: FlatSpace, bucket_cap_mb: float = 25.0, first_bucket_mb: float = 1.0):
@@ -111,8 +114,12 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
         self.fs = flat_space(module)
+        self.bufs = buffer_space(module)
         self.world_size = dist.get_world_size(process_group)
         self.rank = dist.get_rank(process_group)
+        # global rank of the group's rank 0: the source of every DDP broadcast
+        self._src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+        self.buffer_broadcasts = 0
         self._verify_params()
         self._sync_module_states()
         self.buckets = bucket_plan(self.fs, bucket_cap_mb, first_bucket_mb)
@@ -146,10 +153,20 @@ class DistributedDataParallel(nn.Module):
     def _sync_module_states(self):
         if self.world_size == 1:
             return
-        src = dist.get_global_rank(self.process_group, 0) if self.process_group else 0
-        dist.broadcast(self.fs.params, src=src, group=self.process_group)
-        for b in self.module.buffers():
-            dist.broadcast(b, src=src, group=self.process_group)
+        self._broadcast(self.fs.params)
+        if self.bufs is not None:
+            self._broadcast(self.bufs.bytes)
+
+    def _broadcast(self, t: torch.Tensor):
+        """One broadcast of a flat buffer from the group's rank 0: our native RCCL
+        communicator on the current HIP stream (graph-capturable) for device tensors in the
+        default group, c10d otherwise."""
+        if t.is_cuda and self.process_group is None and dist.get_backend() == "nccl":
+            from .process_group import native_comm
+
+            native_comm().broadcast(t, self._src, 0)
+        else:
+            dist.broadcast(t, src=self._src, group=self.process_group)
 
     # ---------------------------------------------------------------- hooks
     def _make_hook(self, name):
@@ -197,12 +214,11 @@ class DistributedDataParallel(nn.Module):
             self._sync_enabled = old
 
     def forward(self, *args, **kwargs):
-        if self.broadcast_buffers and self.world_size > 1:
-            bufs = list(self.module.buffers())
-            if bufs:
-                with torch.no_grad():
-                    for b in bufs:
-                        dist.broadcast(b, src=0, group=self.process_group)
+        if self.broadcast_buffers and self.world_size > 1 and self.bufs is not None:
+            self.bufs.rehome()
+            with torch.no_grad():
+                self._broadcast(self.bufs.bytes)
+            self.buffer_broadcasts += 1
         return self.module(*args, **kwargs)
 
 

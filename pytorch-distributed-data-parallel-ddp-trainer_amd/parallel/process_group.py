@@ -9,7 +9,10 @@ explicit about the transport instead of silently auto-selecting:
   (:func:`native_comm`) is bootstrapped over the same TCPStore for the data
   plane (bucket all-reduces issued from C++ on our own HIP streams);
 * CPU only -> ``"gloo"`` (the reference's only working configuration, BASELINE
-  config 1).
+  config 1) - but only when no GPU run was asked for: ``device="gpu"`` (the CLI's
+  ``--device gpu``, ``DDP_AMD_DEVICE=gpu``) or a host that exposes a GPU (``/dev/kfd``)
+  whose HIP runtime then fails to come up raise instead of quietly training on the CPU
+  (the reference's ``utils.py:6`` auto-select would silently fall back to gloo).
 
 ``MASTER_ADDR``/``MASTER_PORT`` default to 127.0.0.1 and a free port when unset
 (bug B2), and the PG timeout is configurable (``DDP_AMD_PG_TIMEOUT`` seconds).
@@ -50,12 +53,52 @@ def default_backend() -> str:
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
-def setup(rank: int, world_size: int, backend: str | None = None, verbose: bool = True,
-          timeout_s: float | None = None) -> str:
-    """Join the process group; returns the backend used."""
-    backend = backend or os.environ.get("DDP_AMD_BACKEND") or default_backend()
+def _gpu_host() -> bool:
+    """The host exposes an AMD GPU (the KFD device node) - a GPU run is the expected one."""
+    return os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != ""
+
+
+def resolve_backend(backend: str | None = None, device: str | None = None) -> str:
+    """The c10d backend for this run, explicit about the transport.
+
+    ``backend``: ``rccl``/``nccl`` | ``gloo`` | None (from ``DDP_AMD_BACKEND`` or the device).
+    ``device``: ``gpu`` | ``cpu`` | ``auto``/None (from ``DDP_AMD_DEVICE``).  Raises
+    ``RuntimeError`` when a GPU run was requested (``device="gpu"``, ``backend="rccl"``, or
+    a GPU host in ``auto`` mode) but no HIP device is usable, instead of silently
+    training on the CPU over gloo."""
+    backend = backend or os.environ.get("DDP_AMD_BACKEND") or None
+    device = (device or os.environ.get("DDP_AMD_DEVICE") or "auto").lower()
+    if device not in ("auto", "gpu", "cpu"):
+        raise ValueError(f"device must be auto|gpu|cpu, got {device!r}")
     if backend == "rccl":
         backend = "nccl"
+    if backend not in (None, "nccl", "gloo"):
+        raise ValueError(f"unknown backend {backend!r} (rccl|nccl|gloo)")
+    have_gpu = torch.cuda.is_available()
+    if device == "cpu":
+        if backend == "nccl":
+            raise RuntimeError("--device cpu with backend rccl: RCCL needs HIP devices")
+        return "gloo"
+    if backend == "nccl" or device == "gpu":
+        if not have_gpu:
+            raise RuntimeError("a GPU run was requested (backend rccl / --device gpu) but no HIP "
+                               "device is usable (torch.cuda.is_available() is False)")
+        return backend or "nccl"
+    if backend is not None:
+        return backend
+    if have_gpu:
+        return "nccl"
+    if _gpu_host():
+        raise RuntimeError("this host exposes a GPU (/dev/kfd) but the HIP runtime is not usable; "
+                           "refusing to fall back to CPU/gloo silently (pass --device cpu to "
+                           "train on the CPU)")
+    return "gloo"
+
+
+def setup(rank: int, world_size: int, backend: str | None = None, verbose: bool = True,
+          timeout_s: float | None = None, device: str | None = None) -> str:
+    """Join the process group; returns the backend used (see :func:`resolve_backend`)."""
+    backend = resolve_backend(backend, device)
     ensure_master_env()
     if backend == "nccl":
         if not torch.cuda.is_available():

@@ -127,8 +127,11 @@ def resume(model, optimizer, ckpt_dir="./checkpoints", rank: int = 0, world_size
             else:
                 for p in model.parameters():
                     dist.broadcast(p.data, src=0)
-            for b in model.buffers():
-                dist.broadcast(b, src=0)
+            from ..models.layers import buffer_space
+
+            bs = buffer_space(model)  # every buffer in one flat byte broadcast
+            if bs is not None:
+                dist.broadcast(bs.bytes, src=0)
         hp = [optimizer.param_groups[0] if rank == 0 else None]
         dist.broadcast_object_list(hp, src=0)
         optimizer.param_groups[0].update(hp[0])
@@ -139,4 +142,6 @@ def resume(model, optimizer, ckpt_dir="./checkpoints", rank: int = 0, world_size
             if optimizer.momentum_buffer is None:
                 optimizer.momentum_buffer = torch.zeros_like(flat.params)
             dist.broadcast(optimizer.momentum_buffer, src=0)
+            if hasattr(optimizer, "mark_started"):
+                optimizer.mark_started()
     return int(flag[1]), (str(latest) if latest is not None else "(broadcast from rank 0)")

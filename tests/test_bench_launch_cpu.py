@@ -1,0 +1,49 @@
+"""bench.py's self-launch path: ``python bench.py --gpus N`` without a
+launcher environment must start N fresh worker processes itself - through a
+``torch.distributed.run`` CHILD process, never an exec from a process that touched the GPU -
+and every worker must see a consistent RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set.
+Reference: the launcher derives N processes from world_size (/root/reference/train_ddp.py:221-224).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
+                                                              "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout + p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout  # ONE JSON line for the whole run
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n", [2, 3])
+def test_self_launch_spawns_n_ranks(n):
+    rec = _run(["--gpus", str(n), "--backend", "gloo", "--comm", "xgmi", "--dry_launch"])
+    assert rec["dry_launch"] and rec["ranks_seen"] == n
+    kids = rec["children"]
+    assert len(kids) == n
+    assert sorted(int(k["RANK"]) for k in kids) == list(range(n))
+    assert sorted(int(k["LOCAL_RANK"]) for k in kids) == list(range(n))
+    assert all(int(k["WORLD_SIZE"]) == n for k in kids)
+    assert all(k["MASTER_ADDR"] == "127.0.0.1" for k in kids)
+    assert len({k["MASTER_PORT"] for k in kids}) == 1
+
+
+def test_with_gpus_rewrites_argv():
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench._with_gpus(["--gpus", "8", "--steps", "5"], 1) == ["--gpus", "1", "--steps", "5"]
+    assert bench._with_gpus(["--gpus=4", "--warmup", "2"], 4) == ["--gpus", "4", "--warmup", "2"]
+    assert bench._with_gpus(["--steps", "5"], 2) == ["--gpus", "2", "--steps", "5"]

@@ -1,0 +1,90 @@
+"""The default GPU CLI end to end on one MI355X (SURVEY §7.4 minimum
+slice, BASELINE config 4 at world size 1): ``train_ddp.py`` on the fused native engine trains,
+prints the reference's log lines (/root/reference/train_ddp.py:32-202, utils.py:14,19),
+saves ``./checkpoints/epoch_N.pt`` in the reference schema (train_ddp.py:204-209),
+auto-resumes on a re-run (train_ddp.py:45-185), and a crash + resume reproduces the
+uninterrupted run's final checkpoint byte for byte (all zip records but the random
+serialization_id), with and without momentum."""
+import os
+import subprocess
+import sys
+import zipfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference/checkpoints/epoch_0.pt"
+
+
+def _train(cwd, *args, expect_rc=0, timeout=180):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, "-u", os.path.join(REPO, "train_ddp.py"), "--world_size", "1",
+           "--data", "synthetic", "--device", "gpu", *args]
+    p = subprocess.run(cmd, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=timeout)
+    assert p.returncode == expect_rc, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    return p.stdout
+
+
+def test_cli_train_save_resume(tmp_path):
+    out = _train(tmp_path, "--epochs", "1", "--batch_size", "32", "--max_steps", "50",
+                 "--log_every", "20")
+    for line in ["Rank: 0 has initialized its process group with world size 1", "Rank 0 initialized",
+                 "Rank 0 model wrapped in DDP", "Rank 0: Dataloader ready",
+                 "Rank 0: Loss and Optimizer ready", "Rank 0: No checkpoint found, starting from scratch.",
+                 "Rank 0: Starting epoch 0", "Epoch 0 | Batch 0 | Loss:", "Epoch 0 | Batch 40 | Loss:",
+                 "Rank 0 cleaned up."]:
+        assert line in out, (line, out)
+    ck_dir = tmp_path / "checkpoints"
+    assert sorted(os.listdir(ck_dir)) == ["epoch_0.pt"]
+    ck = torch.load(ck_dir / "epoch_0.pt", weights_only=True)
+    assert ck["epoch"] == 0 and list(ck) == ["epoch", "model", "optimizer"]
+    for k, v in ck["model"].items():
+        assert v.device.type == "cpu" and v.dtype == torch.float32 and torch.isfinite(v).all(), k
+    if os.path.exists(REF):  # schema identical to the reference's own checkpoint
+        ref = torch.load(REF, weights_only=True)
+        assert list(ck["model"].keys()) == list(ref["model"].keys())
+        assert ck["model"]._metadata == ref["model"]._metadata
+        for k, v in ref["model"].items():
+            assert ck["model"][k].shape == v.shape and ck["model"][k].stride() == v.stride(), k
+        assert ck["optimizer"] == {"state": {}, "param_groups": ref["optimizer"]["param_groups"]}
+        za, zb = zipfile.ZipFile(REF), zipfile.ZipFile(ck_dir / "epoch_0.pt")
+        assert [i.filename for i in za.infolist()] == [i.filename for i in zb.infolist()]
+    # re-run with more epochs: auto-resume at epoch 1
+    out2 = _train(tmp_path, "--epochs", "2", "--batch_size", "32", "--max_steps", "30")
+    assert "Rank 0: Starting epoch 1" in out2 and "Starting epoch 0" not in out2
+    assert "No checkpoint found" not in out2
+    assert sorted(os.listdir(ck_dir)) == ["epoch_0.pt", "epoch_1.pt"]
+    ck1 = torch.load(ck_dir / "epoch_1.pt", weights_only=True)
+    assert ck1["epoch"] == 1
+    assert any(not torch.equal(ck1["model"][k], ck["model"][k]) for k in ck["model"])
+    # nothing left to do: starts at epoch 2 >= epochs, no training, no new file
+    out3 = _train(tmp_path, "--epochs", "2", "--batch_size", "32", "--max_steps", "30")
+    assert "Starting epoch" not in out3 and sorted(os.listdir(ck_dir)) == ["epoch_0.pt", "epoch_1.pt"]
+
+
+@pytest.mark.parametrize("momentum", ["0", "0.9"])
+def test_cli_fault_resume_byte_identical(tmp_path, momentum):
+    """Crash at epoch 1 step 20, re-run: epoch_2.pt == the uninterrupted run's.  The fused
+    engine replays 16-step hipGraphs plus eager steps (--graph_steps 16, 40 steps/epoch)."""
+    common = ["--epochs", "3", "--batch_size", "32", "--max_steps", "40", "--graph_steps", "16",
+              "--momentum", momentum, "--log_every", "1000"]
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _train(a, *common)
+    out = _train(b, *common, "--fault_at", "1:20", expect_rc=17)
+    assert "injected fault at epoch 1 step 20" in out
+    assert sorted(os.listdir(b / "checkpoints")) == ["epoch_0.pt"]
+    out = _train(b, *common)
+    assert "Rank 0: Starting epoch 1" in out and "Starting epoch 0" not in out
+    za = zipfile.ZipFile(a / "checkpoints" / "epoch_2.pt")
+    zb = zipfile.ZipFile(b / "checkpoints" / "epoch_2.pt")
+    diff = [i.filename for i in za.infolist() if za.read(i.filename) != zb.read(i.filename)]
+    assert diff == ["epoch_2/.data/serialization_id"], diff
+    ck = torch.load(a / "checkpoints" / "epoch_2.pt", weights_only=True)
+    assert bool(ck["optimizer"]["state"]) == (momentum != "0")

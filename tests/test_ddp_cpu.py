@@ -115,29 +115,32 @@ def test_train_save_and_resume_ws2(tmp_path, capfd):
     assert ck1["epoch"] == 1
 
 
-def _worker_fault(rank, ws, port, ckdir, epochs, fault):
+def _worker_fault(rank, ws, port, ckdir, epochs, fault, momentum=0.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from ddp_amd.engine.trainer import TrainOptions, ddp_train
 
     opts = TrainOptions(backend="gloo", checkpoint_dir=ckdir, max_steps=12, num_workers=0,
-                        log_every=1000, data="synthetic", fault=fault)
+                        log_every=1000, data="synthetic", fault=fault, momentum=momentum)
     ddp_train(rank, ws, epochs, 32, opts)
 
 
 @pytest.mark.slow
-def test_fault_then_resume_is_byte_identical(tmp_path):
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_fault_then_resume_is_byte_identical(tmp_path, momentum):
     """BASELINE config 4 on CPU/gloo: crash mid-epoch, auto-resume, final checkpoint equals
-    the uninterrupted run's (every zip record except the random serialization_id)."""
+    the uninterrupted run's (every zip record except the random serialization_id) - with
+    momentum the resumed ranks (rank 0 loads, rank 1 receives the broadcast) continue the
+    momentum buffer instead of re-initialising it."""
     import zipfile
 
     a, b = str(tmp_path / "a"), str(tmp_path / "b")
-    mp.start_processes(_worker_fault, args=(2, free_port(), a, 3, None), nprocs=2,
+    mp.start_processes(_worker_fault, args=(2, free_port(), a, 3, None, momentum), nprocs=2,
                        start_method="spawn", join=True)
     with pytest.raises(Exception):
-        mp.start_processes(_worker_fault, args=(2, free_port(), b, 3, (1, 5, 1)), nprocs=2,
+        mp.start_processes(_worker_fault, args=(2, free_port(), b, 3, (1, 5, 1), momentum), nprocs=2,
                            start_method="spawn", join=True)
     assert sorted(os.listdir(b)) == ["epoch_0.pt"]
-    mp.start_processes(_worker_fault, args=(2, free_port(), b, 3, None), nprocs=2,
+    mp.start_processes(_worker_fault, args=(2, free_port(), b, 3, None, momentum), nprocs=2,
                        start_method="spawn", join=True)
     za, zb = zipfile.ZipFile(os.path.join(a, "epoch_2.pt")), zipfile.ZipFile(os.path.join(b, "epoch_2.pt"))
     diff = [i.filename for i in za.infolist() if za.read(i.filename) != zb.read(i.filename)]

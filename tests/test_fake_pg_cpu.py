@@ -68,3 +68,40 @@ def test_no_sync_skips_allreduce(fake_world):
         torch.nn.functional.cross_entropy(ddp(x), y).backward()
         n_sync = sum(1 for e in tr.log if e[0] == "all_reduce")
     assert n_nosync == 0 and n_sync == 2
+
+
+@pytest.mark.parametrize("fake_world", [(2, 8)], indirect=True)
+def test_broadcast_buffers_one_collective_per_forward(fake_world):
+    """``broadcast_buffers=True`` (the reference's DDP default) costs ONE flat broadcast per
+    forward for ResNet-18's 60 BatchNorm buffers (torch DDP coalesces likewise), and the
+    BN kernels' in-place running-stat updates land in the flat bytes."""
+    from ddp_amd.models import resnet18
+    from ddp_amd.parallel import DistributedDataParallel
+    from ddp_amd.utils.debug import CollectiveTracer
+
+    torch.manual_seed(0)
+    model = resnet18(num_classes=10)
+    nbuf = sum(1 for _ in model.buffers())
+    assert nbuf == 60
+    with CollectiveTracer() as tr:
+        ddp = DistributedDataParallel(model)
+        ctor = len(tr.log)
+        x = torch.randn(2, 3, 32, 32)
+        for _ in range(3):
+            ddp(x).sum().backward()
+        steps = tr.log[ctor:]
+    bc = [e for e in steps if e[0] == "broadcast"]
+    assert len(bc) == 3 and ddp.buffer_broadcasts == 3
+    assert all(e[1][0] == "torch.uint8" and e[2] == 0 for e in bc)
+    total = sum(b.numel() * b.element_size() for b in model.buffers())
+    assert bc[0][1][1][0] >= total
+    # every buffer is a view of the flat bytes; running stats moved off their init values
+    base = ddp.bufs.bytes.data_ptr()
+    for b in model.buffers():
+        assert base <= b.data_ptr() < base + ddp.bufs.bytes.numel()
+    bn = model.bn1
+    assert int(bn.num_batches_tracked) == 3 and bn.running_mean.abs().sum() > 0
+    # a buffer replaced by a new tensor is pulled back into the flat bytes before the next broadcast
+    bn.running_var = torch.full_like(bn.running_var, 2.0)
+    ddp(x)
+    assert base <= bn.running_var.data_ptr() < base + ddp.bufs.bytes.numel()

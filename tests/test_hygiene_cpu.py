@@ -1,0 +1,70 @@
+"""Small correctness fixes from the round-1 review."""
+import pytest
+import torch
+
+
+def test_samples_processed_counts_truncated_epochs():
+    from ddp_amd.engine.trainer import samples_processed
+
+    assert samples_processed(1875, 32, 60000) == 60000       # full epoch, ws1
+    assert samples_processed(938, 32, 30000) == 30000        # ragged tail (16) included
+    assert samples_processed(50, 32, 60000) == 1600          # --max_steps 50
+    assert samples_processed(0, 32, 60000) == 0
+
+
+def test_backend_resolution_never_silently_falls_back(monkeypatch):
+    from ddp_amd.parallel import process_group as pg
+
+    monkeypatch.delenv("DDP_AMD_BACKEND", raising=False)
+    monkeypatch.delenv("DDP_AMD_DEVICE", raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    monkeypatch.setattr(pg, "_gpu_host", lambda: False)
+    assert pg.resolve_backend() == "gloo"                    # CPU host: the plumbing config
+    assert pg.resolve_backend(device="cpu") == "gloo"
+    assert pg.resolve_backend("gloo") == "gloo"
+    with pytest.raises(RuntimeError, match="GPU run was requested"):
+        pg.resolve_backend(device="gpu")
+    with pytest.raises(RuntimeError, match="GPU run was requested"):
+        pg.resolve_backend("rccl")
+    with pytest.raises(RuntimeError):
+        pg.resolve_backend("rccl", device="cpu")
+    monkeypatch.setenv("DDP_AMD_DEVICE", "gpu")
+    with pytest.raises(RuntimeError):
+        pg.resolve_backend()
+    monkeypatch.delenv("DDP_AMD_DEVICE")
+    # a GPU host whose HIP runtime is unusable: refuse instead of training on the CPU
+    monkeypatch.setattr(pg, "_gpu_host", lambda: True)
+    with pytest.raises(RuntimeError, match="refusing to fall back"):
+        pg.resolve_backend()
+    assert pg.resolve_backend(device="cpu") == "gloo"        # explicit CPU run is fine
+    # GPU usable: RCCL
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    assert pg.resolve_backend() == "nccl"
+    assert pg.resolve_backend("rccl") == "nccl"
+    assert pg.resolve_backend(device="gpu") == "nccl"
+
+
+def test_loaded_momentum_state_means_started():
+    """a checkpoint's momentum buffer must resume as a regular update,
+    never as the buf = grad initialisation step (the fused engine keys off ``steps``)."""
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+
+    torch.manual_seed(0)
+    m = SimpleCNN()
+    opt = FusedSGD(m, lr=0.01, momentum=0.9)
+    for p in m.parameters():
+        p.grad.normal_()
+    opt.step()
+    sd = opt.state_dict()
+    assert sd["state"]
+    m2 = SimpleCNN()
+    opt2 = FusedSGD(m2, lr=0.01, momentum=0.9)
+    assert opt2.steps == 0
+    opt2.load_state_dict(sd)
+    assert opt2.steps >= 1 and opt2.momentum_buffer is not None
+    assert torch.equal(opt2.momentum_buffer, opt.momentum_buffer)
+    # no state -> not started
+    opt3 = FusedSGD(SimpleCNN(), lr=0.01, momentum=0.9)
+    opt3.load_state_dict(FusedSGD(SimpleCNN(), lr=0.01, momentum=0.9).state_dict())
+    assert opt3.steps == 0 and opt3.momentum_buffer is None

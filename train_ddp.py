@@ -28,6 +28,9 @@ def parse_args(argv=None):
                    help="processes to spawn when not under torchrun (default: #GPUs, or 2 on CPU)")
     p.add_argument("--backend", choices=["rccl", "nccl", "gloo"], default=None,
                    help="collective backend (default: rccl on GPU, gloo on CPU)")
+    p.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto",
+                   help="gpu: fail unless a HIP device is usable; cpu: gloo plumbing run; auto: the GPU "
+                        "when usable, CPU only on a host without one (never a silent fallback on a GPU host)")
     p.add_argument("--engine", choices=["fused", "module"], default="fused",
                    help="GPU step: fused native engine (hipGraph) or module path (autograd)")
     p.add_argument("--data", choices=["auto", "mnist", "synthetic"], default="auto",
@@ -48,9 +51,10 @@ def parse_args(argv=None):
     p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1],
                    help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
                         "1 = 4 kernels/step (default)")
-    p.add_argument("--comm", choices=["auto", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
-                   help="fused engine bucket all-reduce at world size > 1: auto = fastest of the direct "
-                        "xGMI kernels (xgmi2 two-shot, xgmi1 + one-shot small bucket) and RCCL")
+    p.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
+                   help="fused engine bucket all-reduce at world size > 1: auto = the direct xGMI kernels "
+                        "(one-shot for the small bucket; RCCL if their self-test fails) - deterministic, so "
+                        "resumes reduce in the same order; tune = fastest of xgmi2 / xgmi1 / RCCL on the node")
     p.add_argument("--grad_accum", type=int, default=1,
                    help="micro-batches per optimizer step (module/CPU path; DDP no_sync)")
     p.add_argument("--global_loss", action="store_true",
@@ -72,7 +76,7 @@ def parse_args(argv=None):
 def main(argv=None):
     a = parse_args(argv)
     opts = TrainOptions(lr=a.lr, momentum=a.momentum, weight_decay=a.weight_decay,
-                        backend=a.backend, engine=a.engine, data=a.data, data_root=a.data_root,
+                        backend=a.backend, device=a.device, engine=a.engine, data=a.data, data_root=a.data_root,
                         checkpoint_dir=a.checkpoint_dir, save=not a.no_save, seed=a.seed,
                         log_every=a.log_every, graph_steps=a.graph_steps,
                         bucket_cap_mb=a.bucket_cap_mb, num_workers=a.num_workers,
