@@ -85,6 +85,6 @@ def test_cli_fault_resume_byte_identical(tmp_path, momentum):
     za = zipfile.ZipFile(a / "checkpoints" / "epoch_2.pt")
     zb = zipfile.ZipFile(b / "checkpoints" / "epoch_2.pt")
     diff = [i.filename for i in za.infolist() if za.read(i.filename) != zb.read(i.filename)]
-    assert diff == ["epoch_2/.data/serialization_id"], diff
+    assert set(diff) <= {"epoch_2/.data/serialization_id"}, diff  # (the id may even coincide)
     ck = torch.load(a / "checkpoints" / "epoch_2.pt", weights_only=True)
     assert bool(ck["optimizer"]["state"]) == (momentum != "0")
