@@ -162,6 +162,9 @@ def main():
                     help="control-plane process group (nccl = RCCL); gloo + --comm xgmi rehearses "
                          "N ranks on ONE GPU (RCCL refuses duplicate GPUs)")
     ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="compute precision: bf16 MFMA operands (default) or exact fp32 MFMA (the "
+                         "reference's precision)")
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
     ap.add_argument("--image_size", type=int, default=224, help="resnet18 input size")
@@ -228,7 +231,7 @@ def main():
     imgs, labels = synthetic_mnist()
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
     k = args.graph_steps or graph_chunk(args.steps)
-    eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph)
+    eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=args.dtype)
     eo.comm = args.comm
     for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1"):
         if getattr(args, f) is not None:
@@ -286,7 +289,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(img_s / base, 2) if base else None,
-            "dtype": "bf16",
+            "dtype": eng.dtype,
             "data": "synthetic (MNIST-shaped uint8 60000x28x28, random-init weights)",
             "config": {"model": f"SimpleCNN ({param_count(model):,} params)",
                        "global_batch": ws * args.batch_size, "per_rank_batch": args.batch_size,

@@ -34,6 +34,26 @@ const bf16_t* obf(const std::optional<Tensor>& t, const char* name) {
   return cbf(*t);
 }
 
+// Activation dtype of an op: bf16 (default path) or fp32 (--dtype fp32, exact-fp32 MFMA).
+// Every activation / weight-operand tensor of one call must share it.
+bool act_f32(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name,
+              " must be bfloat16 or float32, got ", t.scalar_type());
+  return t.scalar_type() == at::kFloat;
+}
+void check_act(const Tensor& t, const char* name, bool f32) {
+  check(t, name, f32 ? at::kFloat : at::kBFloat16);
+}
+template <typename T>
+T* tp(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+const T* otp(const std::optional<Tensor>& t, const char* name, bool f32) {
+  if (!t) return nullptr;
+  check_act(*t, name, f32);
+  return tp<T>(*t);
+}
+
 BatchIdx make_bi(const std::optional<Tensor>& idx, const std::optional<Tensor>& ctr, int stride,
                  int offset, long n_rows = 0x7fffffff) {
   BatchIdx bi{nullptr, nullptr, stride, offset};
@@ -59,7 +79,8 @@ void op_conv1_fwd(const Tensor& x, std::optional<Tensor> idx, std::optional<Tens
   check_cuda(x, "x");
   const bool u8 = x.scalar_type() == at::kByte;
   TORCH_CHECK(u8 || x.scalar_type() == at::kFloat, "x must be uint8 or float32");
-  check(w, "w", at::kFloat); check(b, "b", at::kFloat); check(y, "y", at::kBFloat16);
+  check(w, "w", at::kFloat); check(b, "b", at::kFloat);
+  const bool f32 = act_f32(y, "y");
   const int Cout = (int)b.numel();
   TORCH_CHECK(Cout % 8 == 0 && 256 % (Cout / 8) == 0, "conv1: Cout must be 8..256, power of two");
   TORCH_CHECK(w.numel() == (long)Cout * 9, "conv1: weight must be [Cout,1,3,3]");
@@ -69,8 +90,9 @@ void op_conv1_fwd(const Tensor& x, std::optional<Tensor> idx, std::optional<Tens
   } else {
     TORCH_CHECK(x.numel() % ((long)H * W) == 0, "conv1: dataset must be [N,H,W]");
   }
-  conv1_fwd(x.data_ptr(), u8, make_bi(idx, ctr, stride, offset, x.numel() / ((long)H * W)), w.data_ptr<float>(),
-            b.data_ptr<float>(), bf(y), B, H, W, Cout, cur_stream());
+  const BatchIdx bi = make_bi(idx, ctr, stride, offset, x.numel() / ((long)H * W));
+  if (f32) conv1_fwd(x.data_ptr(), u8, bi, w.data_ptr<float>(), b.data_ptr<float>(), tp<float>(y), B, H, W, Cout, cur_stream());
+  else conv1_fwd(x.data_ptr(), u8, bi, w.data_ptr<float>(), b.data_ptr<float>(), bf(y), B, H, W, Cout, cur_stream());
   kcheck();
 }
 
@@ -79,47 +101,58 @@ void op_conv1_wgrad(const Tensor& x, std::optional<Tensor> idx, std::optional<Te
                     Tensor& slab, int B, int H, int W, int Cout, int chunk) {
   check_cuda(x, "x");
   const bool u8 = x.scalar_type() == at::kByte;
-  check(dy, "dy", at::kBFloat16); check(slab, "slab", at::kFloat);
+  const bool f32 = act_f32(dy, "dy");
+  check(slab, "slab", at::kFloat);
   TORCH_CHECK(dy.numel() == (long)B * H * W * Cout, "conv1_wgrad: bad dy size");
   TORCH_CHECK(Cout * 10 <= 320 * 4, "conv1_wgrad: Cout too large");
   TORCH_CHECK(slab.numel() >= (long)conv1_wgrad_blocks(B, H, W, chunk) * Cout * 10, "slab too small");
-  conv1_wgrad(x.data_ptr(), u8, make_bi(idx, ctr, stride, offset, x.numel() / ((long)H * W)), cbf(dy), obf(yact, "yact"),
-              slab.data_ptr<float>(), B, H, W, Cout, chunk, cur_stream());
+  const BatchIdx bi = make_bi(idx, ctr, stride, offset, x.numel() / ((long)H * W));
+  if (f32)
+    conv1_wgrad(x.data_ptr(), u8, bi, tp<float>(dy), otp<float>(yact, "yact", true), slab.data_ptr<float>(), B, H,
+                W, Cout, chunk, cur_stream());
+  else
+    conv1_wgrad(x.data_ptr(), u8, bi, cbf(dy), obf(yact, "yact"), slab.data_ptr<float>(), B, H, W, Cout, chunk,
+                cur_stream());
   kcheck();
 }
 
 void op_conv3x3_fwd(const Tensor& X, const Tensor& Wt, const Tensor& bias, Tensor& Y, bool relu,
                     std::optional<Tensor> wfc, std::optional<Tensor> fc_part, int NO, int pxt) {
-  check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(bias, "bias", at::kFloat);
-  check(Y, "Y", at::kBFloat16);
+  const bool f32 = act_f32(X, "X");
+  check_act(Wt, "Wt", f32); check(bias, "bias", at::kFloat); check_act(Y, "Y", f32);
   TORCH_CHECK(X.dim() == 4 && Y.dim() == 4, "conv3x3_fwd: X, Y must be NHWC 4-d");
   const int B = X.size(0), H = X.size(1), W = X.size(2), Cin = X.size(3), Cout = Y.size(3);
   TORCH_CHECK(Y.size(0) == B && Y.size(1) == H && Y.size(2) == W, "conv3x3_fwd: Y shape");
   TORCH_CHECK(Cin % 32 == 0 && Cout % 64 == 0, "conv3x3_fwd: Cin%32, Cout%64 required");
   TORCH_CHECK(Wt.numel() == (long)Cout * 9 * Cin && bias.numel() == Cout, "conv3x3_fwd: weight shape");
   TORCH_CHECK(pxt == 1 || pxt == 2, "pxt must be 1 or 2");
-  TORCH_CHECK(conv3x3_fwd_lds(W, Cin, pxt) <= 160 * 1024, "conv3x3_fwd: LDS budget exceeded");
-  const bf16_t* wf = nullptr;
+  TORCH_CHECK(conv3x3_fwd_lds(W, Cin, pxt, false, f32 ? 4 : 2) <= 160 * 1024, "conv3x3_fwd: LDS budget exceeded");
+  const void* wf = nullptr;
   float* part = nullptr;
   if (wfc) {
-    check(*wfc, "wfc", at::kBFloat16);
+    check_act(*wfc, "wfc", f32);
     TORCH_CHECK(fc_part.has_value(), "fc_part required with wfc");
     check(*fc_part, "fc_part", at::kFloat);
     TORCH_CHECK(Cout == 64 && (H * W) % 16 == 0 && NO == 10, "fused fc: Cout==64, HW%16==0, NO==10");
     TORCH_CHECK(wfc->numel() == (long)NO * H * W * Cout, "fused fc: wfc shape");
     TORCH_CHECK(fc_part->numel() >= 2L * conv3x3_dgrad_blocks(B, H, W, pxt) * NO,
                 "fused fc: fc_part too small ([blocks][2][NO])");
-    wf = cbf(*wfc);
+    wf = wfc->data_ptr();
     part = fc_part->data_ptr<float>();
   }
-  conv3x3_fwd(cbf(X), cbf(Wt), bias.data_ptr<float>(), bf(Y), B, H, W, Cin, Cout, relu, wf, part,
-              NO, pxt, cur_stream());
+  if (f32)
+    conv3x3_fwd(tp<float>(X), tp<float>(Wt), bias.data_ptr<float>(), tp<float>(Y), B, H, W, Cin, Cout, relu,
+                (const float*)wf, part, NO, pxt, cur_stream());
+  else
+    conv3x3_fwd(cbf(X), cbf(Wt), bias.data_ptr<float>(), bf(Y), B, H, W, Cin, Cout, relu, (const bf16_t*)wf,
+                part, NO, pxt, cur_stream());
   kcheck();
 }
 
 void op_conv3x3_dgrad(const Tensor& dY, std::optional<Tensor> Yact, const Tensor& WT,
                       std::optional<Tensor> Xact, Tensor& dX, int pxt) {
-  check(dY, "dY", at::kBFloat16); check(WT, "WT", at::kBFloat16); check(dX, "dX", at::kBFloat16);
+  const bool f32 = act_f32(dY, "dY");
+  check_act(WT, "WT", f32); check_act(dX, "dX", f32);
   TORCH_CHECK(dY.dim() == 4 && dX.dim() == 4, "conv3x3_dgrad: NHWC 4-d");
   const int B = dY.size(0), H = dY.size(1), W = dY.size(2), Cout = dY.size(3), Cin = dX.size(3);
   TORCH_CHECK(dX.size(0) == B && dX.size(1) == H && dX.size(2) == W, "conv3x3_dgrad: dX shape");
@@ -128,10 +161,14 @@ void op_conv3x3_dgrad(const Tensor& dY, std::optional<Tensor> Yact, const Tensor
   if (Yact) TORCH_CHECK(Yact->sizes() == dY.sizes(), "Yact shape");
   if (Xact) TORCH_CHECK(Xact->sizes() == dX.sizes(), "Xact shape");
   TORCH_CHECK(pxt == 1 || pxt == 2, "pxt must be 1 or 2");
-  TORCH_CHECK(conv3x3_dgrad_lds(W, Cout, pxt, false) <= 160 * 1024, "conv3x3_dgrad: LDS budget");
+  TORCH_CHECK(conv3x3_dgrad_lds(W, Cout, pxt, false, f32 ? 4 : 2) <= 160 * 1024, "conv3x3_dgrad: LDS budget");
   BatchIdx bi{nullptr, nullptr, 0, 0};
-  conv3x3_dgrad(cbf(dY), obf(Yact, "Yact"), cbf(WT), obf(Xact, "Xact"), bf(dX), B, H, W, Cin, Cout,
-                nullptr, false, bi, nullptr, pxt, cur_stream());
+  if (f32)
+    conv3x3_dgrad(tp<float>(dY), otp<float>(Yact, "Yact", true), tp<float>(WT), otp<float>(Xact, "Xact", true),
+                  tp<float>(dX), B, H, W, Cin, Cout, nullptr, false, bi, nullptr, pxt, cur_stream());
+  else
+    conv3x3_dgrad(cbf(dY), obf(Yact, "Yact"), cbf(WT), obf(Xact, "Xact"), bf(dX), B, H, W, Cin, Cout,
+                  nullptr, false, bi, nullptr, pxt, cur_stream());
   kcheck();
 }
 
@@ -153,30 +190,37 @@ void op_conv3x3_dgrad_fused_w1(const Tensor& dY, const Tensor& WT, const Tensor&
 
 void op_conv3x3_wgrad(const Tensor& dY, std::optional<Tensor> Yact, const Tensor& X, Tensor& slab,
                       int R) {
-  check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(slab, "slab", at::kFloat);
+  const bool f32 = act_f32(dY, "dY");
+  check_act(X, "X", f32); check(slab, "slab", at::kFloat);
   const int B = dY.size(0), H = dY.size(1), W = dY.size(2), Cout = dY.size(3), Cin = X.size(3);
   TORCH_CHECK(X.size(0) == B && X.size(1) == H && X.size(2) == W, "conv3x3_wgrad: X shape");
   TORCH_CHECK(Cout % 32 == 0 && Cin % 16 == 0 && ((Cout / 32) * (Cin / 16)) % 4 == 0,
               "conv3x3_wgrad: unsupported channel counts");
   TORCH_CHECK(R >= 1 && R <= H, "conv3x3_wgrad: bad row chunk");
-  TORCH_CHECK(conv3x3_wgrad_lds(W, Cin, Cout, R) <= 160 * 1024, "conv3x3_wgrad: LDS too large");
+  TORCH_CHECK(conv3x3_wgrad_lds(W, Cin, Cout, R, false, f32 ? 4 : 2) <= 160 * 1024, "conv3x3_wgrad: LDS too large");
   TORCH_CHECK(slab.numel() >= (long)conv3x3_wgrad_blocks(B, H, R) * ((long)Cout * 9 * Cin + Cout),
               "conv3x3_wgrad: slab too small");
   if (Yact) TORCH_CHECK(Yact->sizes() == dY.sizes(), "Yact shape");
-  conv3x3_wgrad(cbf(dY), obf(Yact, "Yact"), cbf(X), slab.data_ptr<float>(), B, H, W, Cin, Cout, R,
-                cur_stream());
+  if (f32)
+    conv3x3_wgrad(tp<float>(dY), otp<float>(Yact, "Yact", true), tp<float>(X), slab.data_ptr<float>(), B, H, W,
+                  Cin, Cout, R, cur_stream());
+  else
+    conv3x3_wgrad(cbf(dY), obf(Yact, "Yact"), cbf(X), slab.data_ptr<float>(), B, H, W, Cin, Cout, R,
+                  cur_stream());
   kcheck();
 }
 
 void op_fc_partial(const Tensor& X, const Tensor& Wf, Tensor& part) {
-  check(X, "X", at::kBFloat16); check(Wf, "Wf", at::kBFloat16); check(part, "part", at::kFloat);
+  const bool f32 = act_f32(X, "X");
+  check_act(Wf, "Wf", f32); check(part, "part", at::kFloat);
   TORCH_CHECK(X.dim() == 4, "fc_partial: X must be NHWC");
   const int B = X.size(0), HW = X.size(1) * X.size(2), C = X.size(3);
   TORCH_CHECK(HW % 16 == 0 && C % 8 == 0, "fc_partial: HW%16, C%8");
   const int NO = (int)(Wf.numel() / ((long)HW * C));
   TORCH_CHECK((long)NO * HW * C == Wf.numel() && NO <= 16, "fc_partial: weight shape");
   TORCH_CHECK(part.numel() >= (long)B * (HW / 16) * NO, "fc_partial: part too small");
-  fc_partial(cbf(X), cbf(Wf), part.data_ptr<float>(), B, HW, C, NO, cur_stream());
+  if (f32) fc_partial(tp<float>(X), tp<float>(Wf), part.data_ptr<float>(), B, HW, C, NO, cur_stream());
+  else fc_partial(cbf(X), cbf(Wf), part.data_ptr<float>(), B, HW, C, NO, cur_stream());
   kcheck();
 }
 
@@ -192,8 +236,9 @@ void op_fc_reduce(const Tensor& part, std::optional<Tensor> bias, Tensor& out, i
 void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, Tensor& dW,
                double scale, bool mask, std::optional<Tensor> dbias, std::optional<Tensor> loss_rows,
                std::optional<Tensor> loss_out) {
-  check(dL, "dL", at::kFloat); check(X, "X", at::kBFloat16); check(Wf, "Wf", at::kBFloat16);
-  check(dX, "dX", at::kBFloat16); check(dW, "dW", at::kFloat);
+  check(dL, "dL", at::kFloat);
+  const bool f32 = act_f32(X, "X");
+  check_act(Wf, "Wf", f32); check_act(dX, "dX", f32); check(dW, "dW", at::kFloat);
   const int B = dL.size(0), NO = dL.size(1);
   const long K = X.numel() / B;
   TORCH_CHECK(X.numel() == (long)B * K && dX.numel() == X.numel(), "fc_bwd: X/dX shape");
@@ -219,8 +264,12 @@ void op_fc_bwd(const Tensor& dL, const Tensor& X, const Tensor& Wf, Tensor& dX, 
     ex.loss_rows = loss_rows->data_ptr<float>();
     ex.loss_out = loss_out->data_ptr<float>();
   }
-  fc_bwd(dL.data_ptr<float>(), cbf(X), cbf(Wf), bf(dX), dW.data_ptr<float>(), (float)scale, B, K,
-         NO, mask, cur_stream(), ex);
+  if (f32)
+    fc_bwd(dL.data_ptr<float>(), tp<float>(X), tp<float>(Wf), tp<float>(dX), dW.data_ptr<float>(), (float)scale,
+           B, K, NO, mask, cur_stream(), ex);
+  else
+    fc_bwd(dL.data_ptr<float>(), cbf(X), cbf(Wf), bf(dX), dW.data_ptr<float>(), (float)scale, B, K,
+           NO, mask, cur_stream(), ex);
   kcheck();
 }
 
@@ -749,11 +798,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_level = cfgd.contains("fuse_level") ? cfgd["fuse_level"].cast<int>() : 0;
              c.fuse_opt = cfgd.contains("fuse_opt") ? (int)cfgd["fuse_opt"].cast<bool>() : 1;
              c.store_a1 = cfgd.contains("store_a1") ? cfgd["store_a1"].cast<int>() : 0;
+             c.f32 = cfgd.contains("f32") ? (int)cfgd["f32"].cast<bool>() : 0;
+             const int es = c.f32 ? 4 : 2;
              TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");
              TORCH_CHECK(c.fuse_level == 0 || c.fuse_level == 1, "engine: fuse_level must be 0 or 1");
-             TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0) <= 160 * 1024 &&
-                             conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0) <= 160 * 1024 &&
-                             conv3x3_dgrad_lds(c.W, c.C2, c.pxt_dgrad, true) <= 160 * 1024,
+             TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0, es) <= 160 * 1024 &&
+                             conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0, es) <= 160 * 1024 &&
+                             conv3x3_dgrad_lds(c.W, c.C2, c.pxt_dgrad, true, es) <= 160 * 1024,
                          "engine: LDS budget exceeded for this tiling");
              auto T = [&](const char* k) { return t[k].cast<Tensor>(); };
              auto need = [&](const char* k, at::ScalarType st, long n) {
@@ -777,15 +828,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              TORCH_CHECK(b.off_wfc + (long)c.NO * HW * c.C2 <= b.n_params && b.off_w1 + 9L * c.C1 <= b.n_params &&
                          b.bucket0_off + b.bucket0_n <= b.n_params && b.bucket1_off + b.bucket1_n <= b.n_params,
                          "engine: parameter offsets out of range");
-             b.w2_bf16 = bf(need("w2_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
-             b.w2t_bf16 = bf(need("w2t_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
-             b.wfc_bf16 = bf(need("wfc_bf16", at::kBFloat16, (long)c.NO * HW * c.C2));
-             b.wfc_frag = bf(need("wfc_frag", at::kBFloat16, (long)c.NO * HW * c.C2));
              TORCH_CHECK(fc_bwd_lds(c.max_batch, c.NO, true) <= 160 * 1024, "engine: batch too large for fc_bwd LDS");
-             b.a1 = bf(need("a1", at::kBFloat16, B * HW * c.C1));
-             b.a2 = bf(need("a2", at::kBFloat16, B * HW * c.C2));
-             b.dz2 = bf(need("dz2", at::kBFloat16, B * HW * c.C2));
-             b.dz1 = bf(need("dz1", at::kBFloat16, B * HW * c.C1));
+             if (c.f32) {  // exact fp32: fp32 activations + the conv2 weight's fp32 [tap][ci][co] copy
+               TORCH_CHECK(c.fuse_level == 1 && c.store_a1 == 0, "engine: fp32 needs fuse_level 1, store_a1 0");
+               b.a2_f32 = need("a2", at::kFloat, B * HW * c.C2).data_ptr<float>();
+               b.dz2_f32 = need("dz2", at::kFloat, B * HW * c.C2).data_ptr<float>();
+               b.w2t_f32 = need("w2t_f32", at::kFloat, 9L * c.C1 * c.C2).data_ptr<float>();
+             } else {
+               b.w2_bf16 = bf(need("w2_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
+               b.w2t_bf16 = bf(need("w2t_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
+               b.wfc_bf16 = bf(need("wfc_bf16", at::kBFloat16, (long)c.NO * HW * c.C2));
+               b.wfc_frag = bf(need("wfc_frag", at::kBFloat16, (long)c.NO * HW * c.C2));
+               b.a1 = bf(need("a1", at::kBFloat16, B * HW * c.C1));
+               b.a2 = bf(need("a2", at::kBFloat16, B * HW * c.C2));
+               b.dz2 = bf(need("dz2", at::kBFloat16, B * HW * c.C2));
+               b.dz1 = bf(need("dz1", at::kBFloat16, B * HW * c.C1));
+             }
              b.fc_part = need("fc_part", at::kFloat, 2L * conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_fwd) * c.NO).data_ptr<float>();
              b.dlogits = need("dlogits", at::kFloat, B * c.NO).data_ptr<float>();
              b.loss_rows = need("loss_rows", at::kFloat, B).data_ptr<float>();
@@ -803,7 +861,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.idx = idx.data_ptr<int>();
              b.n_idx = (int)idx.numel();
              b.n_rows = (int)std::min<long>(images.numel() / HW, labels.numel());
-             TORCH_CHECK(conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows) <= 160 * 1024, "wgrad rows too large");
+             TORCH_CHECK(conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, true, es) <= 160 * 1024, "wgrad rows too large");
              return std::make_shared<SimpleCNNEngine>(c, b, comm);
            }),
            py::arg("config"), py::arg("tensors"), py::arg("offsets"), py::arg("comm") = nullptr)

@@ -56,6 +56,10 @@ __device__ __forceinline__ void shadow_one(const ShadowSet& sh, long j, float v)
       sh.r[r].dst[fcfrag_index((int)k, sh.r[r].a, sh.r[r].b)] = b;
     } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {  // [..][3] -> [..][4], 4th stays zero
       sh.r[r].dst[(k / 3) * 4 + k % 3] = b;
+    } else if (sh.r[r].kind == SHADOW_F32_TAPT) {  // exact fp32 [tap][ci][co] copy
+      const long per = (long)sh.r[r].b * sh.r[r].c;
+      const long co = k / per;
+      sh.r[r].dst32[(k - co * per) * sh.r[r].a + co] = v;
     } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
       const long per = (long)sh.r[r].b * sh.r[r].c;
       const long co = k / per;

@@ -66,6 +66,59 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// ---- 16-byte blobs (staging copies, any element type) --------------------------------
+__device__ __forceinline__ bf16x8 ld16(const void* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void st16(void* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
+
+// ---- element-type traits of the MFMA convolution kernels ------------------------------
+// The conv kernels are written once over an activation/weight element type T:
+//  * bf16_t: one v_mfma_f32_16x16x32_bf16 per 32-wide K step; lane l's fragment is the 8
+//    contiguous elements k = 8(l>>4) + j (common.h header);
+//  * float (exact fp32, the reference's precision): eight v_mfma_f32_16x16x4_f32 per
+//    32-wide K step; lane l's fragment is k = 4(l>>4) + j (lo) and 16 + 4(l>>4) + j (hi),
+//    j = 0..3 - MFMA j pairs A[row][k] with B[k][col] from the SAME lane group, so the
+//    eight products sum the whole K step.  Two ds_read_b128 per fragment, each with the
+//    bf16 form's 4-dword-per-lane-group offsets, so the same "row stride = 8 mod 16
+//    dwords" padding keeps both conflict-free.  Result = an exact k-ordered fp32 fma chain
+//    (cdna_hip_programming.md §3 'FP32-input MFMA'); no xf32 on gfx950.
+struct F32Frag {
+  f32x4 lo, hi;
+};
+template <typename T>
+struct Prec;
+template <>
+struct Prec<bf16_t> {
+  using Frag = bf16x8;
+  static constexpr int CE = 8;    // elements per 16-byte chunk
+  static constexpr int PAD = 16;  // LDS row pad (elements): 8 dwords
+  static __device__ __forceinline__ int kofs(int lane) { return 8 * (lane >> 4); }
+  static __device__ __forceinline__ Frag frag(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+  static __device__ __forceinline__ Frag zero() { return zero8(); }
+  static __device__ __forceinline__ f32x4 mma(const Frag& a, const Frag& b, f32x4 c) { return mfma16(a, b, c); }
+};
+template <>
+struct Prec<float> {
+  using Frag = F32Frag;
+  static constexpr int CE = 4;
+  static constexpr int PAD = 8;
+  static __device__ __forceinline__ int kofs(int lane) { return 4 * (lane >> 4); }
+  static __device__ __forceinline__ Frag frag(const float* p) {
+    return Frag{*reinterpret_cast<const f32x4*>(p), *reinterpret_cast<const f32x4*>(p + 16)};
+  }
+  static __device__ __forceinline__ Frag zero() { return Frag{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}; }
+  static __device__ __forceinline__ f32x4 mma(const Frag& a, const Frag& b, f32x4 c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], c, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], c, 0, 0, 0);
+    return c;
+  }
+};
+template <typename F>
+__device__ __forceinline__ F fsel(bool ok, const F& v, const F& z) {
+  return ok ? v : z;
+}
+
 // XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs (linear id
 // % 8 = the XCD group), each with a private L2.  The remap gives XCD group k one
 // contiguous range of the logical linear order, so blocks that share operand rows (e.g.
@@ -110,6 +163,22 @@ __device__ __forceinline__ bf16x8 mask8(bf16x8 g, bf16x8 y) {
   return r;
 }
 
+// ReLU mask of a 16-byte blob of gradients by the matching blob of activations (y > 0)
+template <typename T>
+__device__ __forceinline__ bf16x8 mask16(bf16x8 g, bf16x8 y);
+template <>
+__device__ __forceinline__ bf16x8 mask16<bf16_t>(bf16x8 g, bf16x8 y) {
+  return mask8(g, y);
+}
+template <>
+__device__ __forceinline__ bf16x8 mask16<float>(bf16x8 g, bf16x8 y) {
+  const f32x4 gf = __builtin_bit_cast(f32x4, g), yf = __builtin_bit_cast(f32x4, y);
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = yf[j] > 0.f ? gf[j] : 0.f;  // threshold_backward
+  return __builtin_bit_cast(bf16x8, r);
+}
+
 // SimpleCNN conv1 (Cin = 1, 3x3): relu(b1[c] + sum_k w1[c*9+k] * v[k]) with exactly the
 // FMA order of conv1_fwd_kernel, so kernels that recompute a1 instead of reading it
 // from memory reproduce the stored bf16 values bit for bit.
@@ -152,7 +221,7 @@ __device__ __forceinline__ float conv1_eval_g(const Conv1Group& cg, const float*
   for (int k = 0; k < 9; ++k) acc = fmaf(cg.w[j][k], v[k], acc);  // == conv1_eval
   return fmaxf(acc, 0.f);
 }
-template <typename ValidFn, typename TapFn, typename DstFn>
+template <typename T = bf16_t, typename ValidFn, typename TapFn, typename DstFn>
 __device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group& cg, int g, int pos0,
                                                      int pstride, ValidFn valid, TapFn tap, DstFn dst) {
   for (int pos = pos0 + (threadIdx.x & 63); pos < npos; pos += pstride) {
@@ -164,10 +233,16 @@ __device__ __forceinline__ void conv1_recompute_tile(int npos, const Conv1Group&
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = conv1_eval_g(cg, v, j);
     }
-    uint4 pk;
-    const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
-    pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-    *reinterpret_cast<uint4*>(dst(pos, g)) = pk;
+    if constexpr (sizeof(T) == 4) {  // exact fp32 rows
+      float* d = reinterpret_cast<float*>(dst(pos, g));
+      *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      uint4 pk;
+      const uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
+      pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
+      *reinterpret_cast<uint4*>(dst(pos, g)) = pk;
+    }
   }
 }
 
@@ -197,6 +272,15 @@ __device__ __forceinline__ void st_wt(uint2* p, uint2 v) {
 }
 __device__ __forceinline__ void st_wt(bf16_t* p, bf16_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(float2* p, float2 v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(float4* p, float4 v) {  // two 8-byte write-through stores
+  st_wt(reinterpret_cast<float2*>(p), make_float2(v.x, v.y));
+  st_wt(reinterpret_cast<float2*>(p) + 1, make_float2(v.z, v.w));
 }
 
 // ---- optimizer element update (torch/optim/sgd.py _single_tensor_sgd semantics)

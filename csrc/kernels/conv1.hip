@@ -15,11 +15,11 @@
 
 namespace ddp_amd {
 
-template <bool U8>
+template <typename T, bool U8>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__ x, BatchIdx bi,
                                                         const float* __restrict__ w,
                                                         const float* __restrict__ bias,
-                                                        bf16_t* __restrict__ y, int B, int H, int W,
+                                                        T* __restrict__ y, int B, int H, int W,
                                                         int Cout) {
   extern __shared__ __attribute__((aligned(16))) float s_w[];  // [Cout][9] then [Cout]
   const int t = threadIdx.x;
@@ -60,19 +60,28 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
   float o[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) o[c] = conv1_eval(s_w, s_w + Cout * 9, v, cg * 8 + c);
-  uint4 pk;
-  uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
-  pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
-  *reinterpret_cast<uint4*>(y + P * Cout + cg * 8) = pk;
+  if constexpr (sizeof(T) == 4) {  // exact fp32 activations (--dtype fp32)
+    float* d = reinterpret_cast<float*>(y + P * Cout + cg * 8);
+    *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<float4*>(d + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  } else {
+    uint4 pk;
+    uint2 lo = pack4(o[0], o[1], o[2], o[3]), hi = pack4(o[4], o[5], o[6], o[7]);
+    pk.x = lo.x; pk.y = lo.y; pk.z = hi.x; pk.w = hi.y;
+    *reinterpret_cast<uint4*>(y + P * Cout + cg * 8) = pk;
+  }
 }
+
+__device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
+__device__ __forceinline__ float to_f(float v) { return v; }
 
 // Partial weight/bias gradient of conv1 over a chunk of CHUNK pixels per block:
 //   slab[blk][co*9 + tap] = sum_P dZ[P][co] * x[P shifted by tap],  slab[blk][Cout*9 + co] = sum_P dZ[P][co]
 // dZ = dY * (Y > 0) when MASK (Y = conv1's ReLU output).  Reduced in fixed order by grad_reduce.
-template <bool U8, bool MASK>
+template <typename T, bool U8, bool MASK>
 __global__ __launch_bounds__(320) void conv1_wgrad_kernel(const void* __restrict__ x, BatchIdx bi,
-                                                          const bf16_t* __restrict__ dy,
-                                                          const bf16_t* __restrict__ yact,
+                                                          const T* __restrict__ dy,
+                                                          const T* __restrict__ yact,
                                                           float* __restrict__ slab, int B, int H,
                                                           int W, int Cout, int chunk) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -102,8 +111,8 @@ __global__ __launch_bounds__(320) void conv1_wgrad_kernel(const void* __restrict
     float g = 0.f;
     if (P < Ptot) {
       const long off = P0 * Cout + i;
-      g = bf2f(dy[off]);
-      if (MASK && !(bf2f(yact[off]) > 0.f)) g = 0.f;
+      g = to_f(dy[off]);
+      if (MASK && !(to_f(yact[off]) > 0.f)) g = 0.f;
     }
     s_dz[i] = g;
   }
@@ -122,16 +131,25 @@ __global__ __launch_bounds__(320) void conv1_wgrad_kernel(const void* __restrict
   }
 }
 
-void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, bf16_t* y,
-               int B, int H, int W, int Cout, hipStream_t s) {
+template <typename T>
+static void conv1_fwd_launch(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b,
+                             T* y, int B, int H, int W, int Cout, hipStream_t s) {
   const int ppb = 256 / (Cout / 8);
   const long P = (long)B * H * W;
   const dim3 grid((unsigned)((P + ppb - 1) / ppb));
   const size_t lds = sizeof(float) * Cout * 10;
   if (x_is_u8)
-    hipLaunchKernelGGL(conv1_fwd_kernel<true>, grid, dim3(256), lds, s, x, bi, w, b, y, B, H, W, Cout);
+    hipLaunchKernelGGL((conv1_fwd_kernel<T, true>), grid, dim3(256), lds, s, x, bi, w, b, y, B, H, W, Cout);
   else
-    hipLaunchKernelGGL(conv1_fwd_kernel<false>, grid, dim3(256), lds, s, x, bi, w, b, y, B, H, W, Cout);
+    hipLaunchKernelGGL((conv1_fwd_kernel<T, false>), grid, dim3(256), lds, s, x, bi, w, b, y, B, H, W, Cout);
+}
+void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, bf16_t* y,
+               int B, int H, int W, int Cout, hipStream_t s) {
+  conv1_fwd_launch<bf16_t>(x, x_is_u8, bi, w, b, y, B, H, W, Cout, s);
+}
+void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, float* y,
+               int B, int H, int W, int Cout, hipStream_t s) {
+  conv1_fwd_launch<float>(x, x_is_u8, bi, w, b, y, B, H, W, Cout, s);
 }
 
 int conv1_wgrad_blocks(int B, int H, int W, int chunk) {
@@ -139,15 +157,24 @@ int conv1_wgrad_blocks(int B, int H, int W, int chunk) {
   return (int)((P + chunk - 1) / chunk);
 }
 
-void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const bf16_t* dy, const bf16_t* yact,
-                 float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s) {
+template <typename T>
+static void conv1_wgrad_launch(const void* x, bool x_is_u8, BatchIdx bi, const T* dy, const T* yact,
+                               float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s) {
   const dim3 grid(conv1_wgrad_blocks(B, H, W, chunk));
   const size_t lds = sizeof(float) * chunk * (9 + Cout);
   const bool mask = yact != nullptr;
-#define L1W(U, M) hipLaunchKernelGGL((conv1_wgrad_kernel<U, M>), grid, dim3(320), lds, s, x, bi, dy, yact, slab, B, H, W, Cout, chunk)
+#define L1W(U, M) hipLaunchKernelGGL((conv1_wgrad_kernel<T, U, M>), grid, dim3(320), lds, s, x, bi, dy, yact, slab, B, H, W, Cout, chunk)
   if (x_is_u8) { if (mask) L1W(true, true); else L1W(true, false); }
   else { if (mask) L1W(false, true); else L1W(false, false); }
 #undef L1W
+}
+void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const bf16_t* dy, const bf16_t* yact,
+                 float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s) {
+  conv1_wgrad_launch<bf16_t>(x, x_is_u8, bi, dy, yact, slab, B, H, W, Cout, chunk, s);
+}
+void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const float* dy, const float* yact,
+                 float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s) {
+  conv1_wgrad_launch<float>(x, x_is_u8, bi, dy, yact, slab, B, H, W, Cout, chunk, s);
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv1)

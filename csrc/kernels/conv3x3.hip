@@ -1,5 +1,8 @@
-// 3x3 / stride 1 / padding 1 convolution on NHWC bf16 activations with MFMA
-// (v_mfma_f32_16x16x32_bf16): forward, data gradient and weight gradient.
+// 3x3 / stride 1 / padding 1 convolution on NHWC activations with MFMA: forward, data
+// gradient and weight gradient, in two precisions (element type T, common.h Prec<T>):
+//  * bf16 operands on v_mfma_f32_16x16x32_bf16 (fp32 accumulate) - the default;
+//  * exact fp32 operands on v_mfma_f32_16x16x4_f32 - the reference's precision
+//    (--dtype fp32): same tiling, LDS staging and fusions, 8 MFMAs per 32-wide K step.
 //
 // Reference op: model.py:11-12 (nn.Conv2d(32,64,3,padding=1) -> nn.ReLU()), i.e.
 // the layer that carries 95% of SimpleCNN's FLOPs.
@@ -9,8 +12,9 @@
 //   dgrad D[ci][px] += WT[tap][ci][co]  . dY[px-tap][co]       K = 9*Cout
 //   wgrad D[co][ci] += dY[px][co]       . X[px+tap][ci]        K = pixels (per tap)
 // A K-step of 32 is one tap x 32 contiguous channels, so every A/B fragment is a
-// single 16-byte load of 8 contiguous bf16.  Each lane finishes with 4
-// consecutive channels of one pixel -> one 8-byte NHWC store per 16x16 tile.
+// single 16-byte load of 8 contiguous bf16 (fp32: two 16-byte loads).  Each lane
+// finishes with 4 consecutive channels of one pixel -> one 8-byte (fp32: 16-byte) NHWC
+// store per 16x16 tile.
 //
 // Fusions (templates):
 //  * fwd:   bias + ReLU epilogue; FUSE_FC additionally dots the bf16 output tile
@@ -78,9 +82,10 @@ __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
 
 // LDS bytes of the forward's staging area (weights, input rows, conv1 recompute
 // scratch), rounded to 16; the fused-fc epilogue's per-tile partials follow it.
-__host__ __device__ inline size_t fwd_stage_lds(int W, int Cin, int pxt, bool a1x) {
+__host__ __device__ inline size_t fwd_stage_lds(int W, int Cin, int pxt, bool a1x, int es = 2) {
   const size_t XR = 64 * pxt + 2 * W + 2;  // a block covers CH = 64 * pxt pixels
-  const size_t b = sizeof(bf16_t) * ((size_t)64 * (9 * Cin + 16) + XR * (Cin + 16)) +
+  const int pad = es == 2 ? 16 : 8;        // Prec<T>::PAD
+  const size_t b = (size_t)es * ((size_t)64 * (9 * Cin + pad) + XR * (Cin + pad)) +
                    (a1x ? sizeof(float) * ((XR + 2 * W + 2) + Cin * 10) : 0);
   return (b + 15) & ~(size_t)15;
 }
@@ -95,11 +100,14 @@ __host__ __device__ inline size_t fc_epi_lds(int pxt, int nof) { return sizeof(f
 // NW waves per block, PXT 16-pixel tiles per wave: a block covers CH = 16 * NW * PXT
 // pixels (64 * pxt in launcher terms).  With NW = 8 two waves share each SIMD, which
 // doubles the VALU issue rate of the conv1 recompute and the fc epilogue.
-template <int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO>
+template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO>
 __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
-    bf16_t* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
-    const bf16_t* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
+    const T* __restrict__ X, const T* __restrict__ Wt, const float* __restrict__ bias,
+    T* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
+    const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
+  using P = Prec<T>;
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int CE = P::CE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DDP_STAMP(STAMP_K_CONV_FWD, 0);
   DDP_GEOM_OVERRIDE();
@@ -108,28 +116,29 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   const int HW = H * W;
   const long Ptot = (long)B * HW;
   const int co0 = blockIdx.y * 64;
-  const int KW = 9 * Cin, WS = KW + 16, XS = Cin + 16;  // row strides = 8 mod 16 dwords: conflict-free b128 fragment reads
+  // row strides = 8 mod 16 dwords: conflict-free b128 fragment reads
+  const int KW = 9 * Cin, WS = KW + P::PAD, XS = Cin + P::PAD;
   const int XR = CH + 2 * W + 2;
-  bf16_t* sW = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* sX = sW + 64 * WS;
+  T* sW = reinterpret_cast<T*>(smem);
+  T* sX = sW + 64 * WS;
   const long P0 = (long)blockIdx.x * CH;
   const long Pbase = P0 - W - 1;
 
-  const int wc = KW / 8;
-  const int xc = Cin / 8;
+  const int wc = KW / CE;
+  const int xc = Cin / CE;
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave & 3);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
-  stage2<64 / NW, NT>(64 * wc,
-             [&](int i) { const int r = i / wc, c = (i - r * wc) * 8; return ld8(Wt + (long)(co0 + r) * KW + c); },
-             [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sW + r * WS + c) = v; },
+  stage2<(64 / NW) * (F32 ? 2 : 1), NT>(64 * wc,
+             [&](int i) { const int r = i / wc, c = (i - r * wc) * CE; return ld16(Wt + (long)(co0 + r) * KW + c); },
+             [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * CE; st16(sW + r * WS + c, v); },
              A1X ? 0 : XR * xc,
              [&](int i) {
-               const int r = i / xc, c = (i - r * xc) * 8;
-               const long P = Pbase + r;
-               return (P >= 0 && P < Ptot) ? ld8(X + P * Cin + c) : zero8();
+               const int r = i / xc, c = (i - r * xc) * CE;
+               const long Pq = Pbase + r;
+               return (Pq >= 0 && Pq < Ptot) ? ld16(X + Pq * Cin + c) : zero8();
              },
-             [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * 8; *reinterpret_cast<bf16x8*>(sX + r * XS + c) = v; });
+             [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * CE; st16(sX + r * XS + c, v); });
   if (A1X) {
     // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), then a1 (conv1 recompute).
     // The block also writes its own pixels (and the labels of images starting in them)
@@ -138,15 +147,15 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     const int NXX = XR + 2 * W + 2;
     const int base = c1.bi.base();
     for (int r = threadIdx.x; r < NXX; r += NT) {
-      const long P = Pbase - W - 1 + r;
+      const long Pq = Pbase - W - 1 + r;
       float v = 0.f;
-      if (P >= 0 && P < Ptot) {
-        const int n = (int)(P / HW), rm = (int)(P - (long)n * HW);
+      if (Pq >= 0 && Pq < Ptot) {
+        const int n = (int)(Pq / HW), rm = (int)(Pq - (long)n * HW);
         const int row = c1.bi.row(n, base);
         const unsigned char u = c1.x[(long)row * HW + rm];
         v = (float)u / 255.0f;
-        if (c1.xb_out && P >= P0 && P < P0 + CH) {
-          c1.xb_out[P] = u;
+        if (c1.xb_out && Pq >= P0 && Pq < P0 + CH) {
+          c1.xb_out[Pq] = u;
           if (rm == 0) c1.yb_out[n] = c1.labels[row];
         }
       }
@@ -154,12 +163,12 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     }
     __syncthreads();
     DDP_STAMP(STAMP_K_CONV_FWD, 1);
-    conv1_recompute_tile(
+    conv1_recompute_tile<T>(
         XR, cg, wave & 3, 64 * (wave >> 2), 64 * (NW / 4),
-        [&](int r) { const long P = Pbase + r; return P >= 0 && P < Ptot; },
+        [&](int r) { const long Pq = Pbase + r; return Pq >= 0 && Pq < Ptot; },
         [&](int r, int k) {
-          const long P = Pbase + r;
-          const int rm = (int)(P % HW);
+          const long Pq = Pbase + r;
+          const int rm = (int)(Pq % HW);
           const int hh = rm / W, ww = rm - (rm / W) * W;
           const int dh = k / 3 - 1, dw = k % 3 - 1;
           const bool ok = (unsigned)(hh + dh) < (unsigned)H && (unsigned)(ww + dw) < (unsigned)W;
@@ -169,7 +178,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     DDP_STAMP(STAMP_K_CONV_FWD, 5);
   }
 
-  const int kofs = 8 * (lane >> 4);
+  const int kofs = P::kofs(lane);
   const int col = lane & 15;
   int h[PXT], w[PXT], rowc[PXT], rem[PXT];
   bool valid[PXT];
@@ -186,9 +195,10 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     w[pt] = rem[pt] - h[pt] * W;
     rowc[pt] = lp + W + 1;  // sX row of the pixel itself
   }
-  // fc weight prefetch (lands while the MFMAs run)
-  uint2 wv[NOF > 0 ? PXT : 1][4][NOF > 0 ? NOF : 1];
-  if (NOF > 0) {
+  // fc weight prefetch (lands while the MFMAs run); fp32 reads its native-layout weight
+  // in the epilogue instead (160 more VGPRs would not fit next to the fp32 fragments)
+  uint2 wv[NOF > 0 && !F32 ? PXT : 1][4][NOF > 0 && !F32 ? NOF : 1];
+  if (NOF > 0 && !F32) {
 #pragma unroll
     for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
@@ -200,7 +210,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   }
   __syncthreads();
   DDP_STAMP(STAMP_K_CONV_FWD, 2);
-  if (A1X && c1.a1_out) {
+  if (A1X && !F32 && c1.a1_out) {
     // the block's own a1 rows (LDS rows W+1 .. W+CH) -> a1_out, 16 bytes per thread-step
     const int xc8 = Cin / 8;
     for (int i = threadIdx.x; i < CH * xc8; i += NT) {
@@ -208,7 +218,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       const long P = P0 + lp;
       if (P < Ptot)
         *reinterpret_cast<bf16x8*>(c1.a1_out + P * Cin + c) =
-            *reinterpret_cast<const bf16x8*>(sX + (lp + W + 1) * XS + c);
+            *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(sX) + (lp + W + 1) * XS + c);
     }
   }
 
@@ -218,35 +228,34 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[pt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const bf16_t* wrow = sW + col * WS + kofs;
+  const T* wrow = sW + col * WS + kofs;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int dh = tap / 3 - 1, dw = tap % 3 - 1;
     for (int ci0 = 0; ci0 < Cin; ci0 += 32) {
-      bf16x8 a[4], b[PXT];
+      typename P::Frag a[4], b[PXT];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        a[t] = *reinterpret_cast<const bf16x8*>(wrow + 16 * t * WS + tap * Cin + ci0);
+      for (int t = 0; t < 4; ++t) a[t] = P::frag(wrow + 16 * t * WS + tap * Cin + ci0);
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {
         const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
         // unconditional read (the row is always inside the staged range), then a select:
         // no exec-masked LDS read, so the reads of a tap pipeline ahead of the MFMAs
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sX + (rowc[pt] + dh * W + dw) * XS + ci0 + kofs);
-        b[pt] = ok ? v : zero8();
+        const typename P::Frag v = P::frag(sX + (rowc[pt] + dh * W + dw) * XS + ci0 + kofs);
+        b[pt] = fsel(ok, v, P::zero());
       }
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[pt][t] = mfma16(a[t], b[pt], acc[pt][t]);
+        for (int t = 0; t < 4; ++t) acc[pt][t] = P::mma(a[t], b[pt], acc[pt][t]);
     }
   }
 
   DDP_STAMP(STAMP_K_CONV_FWD, 3);
   // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
-  float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X));
+  float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X, (int)sizeof(T)));
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -259,15 +268,24 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       float v0 = acc[pt][t][0] + bv.x, v1 = acc[pt][t][1] + bv.y;
       float v2 = acc[pt][t][2] + bv.z, v3 = acc[pt][t][3] + bv.w;
       if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
-      const uint2 pk = pack4(v0, v1, v2, v3);
-      if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
+      float q[4] = {v0, v1, v2, v3};  // the values actually stored (what backward re-reads)
+      if constexpr (F32) {
+        if (valid[pt]) st_wt(reinterpret_cast<float4*>(Y + Pp[pt] * Cout + co), make_float4(v0, v1, v2, v3));
+      } else {
+        const uint2 pk = pack4(v0, v1, v2, v3);
+        if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
+        unpack4(pk, q);
+      }
       if (NOF > 0) {
-        float q[4];
-        unpack4(pk, q);  // the bf16 values actually stored (what backward re-reads)
 #pragma unroll
         for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
           float wf[4];
-          unpack4(wv[pt][t][o], wf);
+          if constexpr (F32) {  // native [o][hw][c] fp32 weight: 4 consecutive channels
+            const float4 w4 = *reinterpret_cast<const float4*>(wfc + ((long)o * HW + rem[pt]) * Cout + co);
+            wf[0] = w4.x; wf[1] = w4.y; wf[2] = w4.z; wf[3] = w4.w;
+          } else {
+            unpack4(wv[pt][t][o], wf);
+          }
           float s = fcs[o];
           s = fmaf(q[0], wf[0], s); s = fmaf(q[1], wf[1], s);
           s = fmaf(q[2], wf[2], s); s = fmaf(q[3], wf[3], s);
@@ -310,11 +328,15 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 // ---------------------------------------------------------------- data gradient
 // A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
 // being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
-template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI, int GCO>
+template <typename T, int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI,
+          int GCO>
 __device__ __forceinline__ void dgrad_body(
-    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
-    const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
+    const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ WT,
+    const T* __restrict__ Xact, T* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by) {
+  using P = Prec<T>;
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int CE = P::CE;
   DDP_STAMP(STAMP_K_DGRAD, 0);
   DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
@@ -322,10 +344,10 @@ __device__ __forceinline__ void dgrad_body(
   const int HW = H * W;
   const long Ptot = (long)B * HW;
   const int ci_blk = by * 32;
-  const int KW = 9 * Cout, WS = KW + 16, DS = Cout + 16;  // row strides = 8 mod 16 dwords (conflict-free)
+  const int KW = 9 * Cout, WS = KW + P::PAD, DS = Cout + P::PAD;  // row strides = 8 mod 16 dwords (conflict-free)
   const int XR = CH + 2 * W + 2;
-  bf16_t* sWT = reinterpret_cast<bf16_t*>(smem);        // [32 ci][9*Cout]
-  bf16_t* sDY = sWT + 32 * WS;                           // [XR][Cout]
+  T* sWT = reinterpret_cast<T*>(smem);                   // [32 ci][9*Cout]
+  T* sDY = sWT + 32 * WS;                                // [XR][Cout]
   float* sx0 = reinterpret_cast<float*>(sDY + XR * DS);  // [XR] conv1 input (FUSE_W1)
   float* s_w1 = sx0 + XR;                                // [4][320] (FUSE_W1)
   unsigned char* s_m1 = reinterpret_cast<unsigned char*>(s_w1 + 4 * 320);  // [CH][4] a1>0 bits (A1X)
@@ -347,26 +369,26 @@ __device__ __forceinline__ void dgrad_body(
   const float x0_pre = (FUSE_W1 && (int)threadIdx.x < XR) ? x0_at(threadIdx.x) : 0.f;
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
-  const int wc = KW / 8, cpc = Cout / 8;
-  stage2<16>(32 * wc,
+  const int wc = KW / CE, cpc = Cout / CE;
+  stage2<F32 ? 32 : 16>(32 * wc,
           [&](int i) {
-            const int r = i / wc, rest = (i - r * wc) * 8;  // rest = tap*Cout + co
+            const int r = i / wc, rest = (i - r * wc) * CE;  // rest = tap*Cout + co
             const int tap = rest / Cout, co = rest - tap * Cout;
-            return ld8(WT + ((long)tap * Cin + ci_blk + r) * Cout + co);
+            return ld16(WT + ((long)tap * Cin + ci_blk + r) * Cout + co);
           },
-          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * 8; *reinterpret_cast<bf16x8*>(sWT + r * WS + c) = v; },
+          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * CE; st16(sWT + r * WS + c, v); },
           XR * cpc,
           [&](int i) {
-            const int r = i / cpc, c = (i - r * cpc) * 8;
-            const long P = Pbase + r;
+            const int r = i / cpc, c = (i - r * cpc) * CE;
+            const long Pq = Pbase + r;
             bf16x8 v = zero8();
-            if (P >= 0 && P < Ptot) {
-              v = ld8(dY + P * Cout + c);
-              if (MASK_DY) v = mask8(v, ld8(Yact + P * Cout + c));
+            if (Pq >= 0 && Pq < Ptot) {
+              v = ld16(dY + Pq * Cout + c);
+              if (MASK_DY) v = mask16<T>(v, ld16(Yact + Pq * Cout + c));
             }
             return v;
           },
-          [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * 8; *reinterpret_cast<bf16x8*>(sDY + r * DS + c) = v; });
+          [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * CE; st16(sDY + r * DS + c, v); });
   DDP_STAMP(STAMP_K_CONV1, 0);  // stage2 done (weights + dY in LDS, own waves)
   if (FUSE_W1) {
     if ((int)threadIdx.x < XR) sx0[threadIdx.x] = x0_pre;
@@ -392,20 +414,22 @@ __device__ __forceinline__ void dgrad_body(
           v[k] = ok ? sx0[lp + W + 1 + dh * W + dw] : 0.f;
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          m |= (bf2f(f2bf(conv1_eval_g(cg, v, j))) > 0.f ? 1u : 0u) << j;
+        for (int j = 0; j < 8; ++j) {
+          const float a1v = conv1_eval_g(cg, v, j);  // the value the forward stored
+          m |= ((F32 ? a1v : bf2f(f2bf(a1v))) > 0.f ? 1u : 0u) << j;
+        }
       }
       s_m1[lp * 4 + g] = (unsigned char)m;
     }
     DDP_STAMP(STAMP_K_CONV1, 2);  // mask computed
   }
 
-  const int kofs = 8 * (lane >> 4);
+  const int kofs = P::kofs(lane);
   const int col = lane & 15;
   int h[PXT], w[PXT], rowc[PXT];
   bool valid[PXT];
   long Pp[PXT];
-  uint2 xa[PXT][2] = {};
+  float xa[PXT][2][4] = {};  // ReLU-input values of this lane's 2 x 4 outputs (MASK_X && !A1X)
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     const int lp = (wave * PXT + pt) * 16 + col;
@@ -419,8 +443,15 @@ __device__ __forceinline__ void dgrad_body(
     rowc[pt] = lp + W + 1;
     if (MASK_X && !A1X) {  // prefetch the ReLU-input mask (lands during the MFMAs)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        xa[pt][t] = *reinterpret_cast<const uint2*>(Xact + Pc * Cin + ci_blk + 16 * t + 4 * (lane >> 4));
+      for (int t = 0; t < 2; ++t) {
+        const T* xp = Xact + Pc * Cin + ci_blk + 16 * t + 4 * (lane >> 4);
+        if constexpr (F32) {
+          const float4 x4 = *reinterpret_cast<const float4*>(xp);
+          xa[pt][t][0] = x4.x; xa[pt][t][1] = x4.y; xa[pt][t][2] = x4.z; xa[pt][t][3] = x4.w;
+        } else {
+          unpack4(*reinterpret_cast<const uint2*>(xp), xa[pt][t]);
+        }
+      }
     }
   }
   __syncthreads();
@@ -429,25 +460,25 @@ __device__ __forceinline__ void dgrad_body(
   f32x4 acc[PXT][2];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) acc[pt][0] = acc[pt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bf16_t* wrow = sWT + col * WS + kofs;
+  const T* wrow = sWT + col * WS + kofs;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int dh = 1 - tap / 3, dw = 1 - tap % 3;  // dY pixel = (h + 1 - kh, w + 1 - kw)
     for (int co0 = 0; co0 < Cout; co0 += 32) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(wrow + tap * Cout + co0);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wrow + 16 * WS + tap * Cout + co0);
-      bf16x8 b[PXT];
+      const typename P::Frag a0 = P::frag(wrow + tap * Cout + co0);
+      const typename P::Frag a1 = P::frag(wrow + 16 * WS + tap * Cout + co0);
+      typename P::Frag b[PXT];
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {
         const int hh = h[pt] + dh, ww = w[pt] + dw;
         const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs);
-        b[pt] = ok ? v : zero8();  // unconditional read + select (see the forward)
+        const typename P::Frag v = P::frag(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs);
+        b[pt] = fsel(ok, v, P::zero());  // unconditional read + select (see the forward)
       }
 #pragma unroll
       for (int pt = 0; pt < PXT; ++pt) {
-        acc[pt][0] = mfma16(a0, b[pt], acc[pt][0]);
-        acc[pt][1] = mfma16(a1, b[pt], acc[pt][1]);
+        acc[pt][0] = P::mma(a0, b[pt], acc[pt][0]);
+        acc[pt][1] = P::mma(a1, b[pt], acc[pt][1]);
       }
     }
   }
@@ -484,16 +515,18 @@ __device__ __forceinline__ void dgrad_body(
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = ((m >> j) & 1u) ? v[j] : 0.f;
       } else if (MASK_X) {
-        float xm[4];
-        unpack4(xa[pt][t], xm);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = xm[j] > 0.f ? v[j] : 0.f;
+        for (int j = 0; j < 4; ++j) v[j] = xa[pt][t][j] > 0.f ? v[j] : 0.f;
       }
-      const uint2 pk = pack4(v[0], v[1], v[2], v[3]);
-      if (dX && valid[pt]) *reinterpret_cast<uint2*>(dX + Pp[pt] * Cin + ci) = pk;  // dX null: only the fused w1 grad needs it
-      if (FUSE_W1) {
-        float q[4];
+      float q[4] = {v[0], v[1], v[2], v[3]};  // the values stored (fp32: exact)
+      if constexpr (F32) {
+        if (dX && valid[pt]) *reinterpret_cast<float4*>(dX + Pp[pt] * Cin + ci) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        const uint2 pk = pack4(v[0], v[1], v[2], v[3]);
+        if (dX && valid[pt]) *reinterpret_cast<uint2*>(dX + Pp[pt] * Cin + ci) = pk;  // dX null: only the fused w1 grad needs it
         unpack4(pk, q);
+      }
+      if (FUSE_W1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float d = valid[pt] ? q[j] : 0.f;
@@ -531,13 +564,14 @@ __device__ __forceinline__ void dgrad_body(
   DDP_STAMP(STAMP_K_DGRAD, 4);
 }
 
-template <int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI, int GCO>
+template <typename T, int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI,
+          int GCO>
 __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
-    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ WT,
-    const bf16_t* __restrict__ Xact, bf16_t* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
+    const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ WT,
+    const T* __restrict__ Xact, T* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  dgrad_body<PXT, MASK_DY, MASK_X, FUSE_W1, A1X, GH, GW, GCI, GCO>(
+  dgrad_body<T, PXT, MASK_DY, MASK_X, FUSE_W1, A1X, GH, GW, GCI, GCO>(
       dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, x0_u8, bi, w1slab, c1, smem, blockIdx.x, blockIdx.y);
 }
 
@@ -552,10 +586,16 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // so the two 16-lane groups of a half-wave read 8 consecutive rows (conflict-free).
 // A1X: the X tile (a1 rows r0-1 .. r0+R) is recomputed from the uint8 images (rows
 // r0-2 .. r0+R+1) instead of being read from a stored a1 tensor.
-template <bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
+// fp32 (exact) variant: the K dimension (pixel slots) is strided in NHWC for both operands,
+// so each lane reads single floats - MFMA j takes slot s0 + 4j + (lane >> 4) - with row
+// strides of 16 mod 32 dwords (Cout + 16, Cin + 16), conflict-free for ds_read_b32's two
+// 32-lane groups (lanes l and l + 16 read adjacent slots).
+template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
 __device__ __forceinline__ void wgrad_body(
-    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
+    const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ X,
     float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by) {
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int CE = Prec<T>::CE;
   DDP_STAMP(STAMP_K_WGRAD, 0);
   DDP_GEOM_OVERRIDE();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -565,42 +605,42 @@ __device__ __forceinline__ void wgrad_body(
   const int Wp = (W + 7) & ~7;
   const int DS = Cout + 16, XS = Cin + 16;  // LDS row strides (elements)
   const int nslot = ((R * Wp + 31) / 32) * 32;
-  bf16_t* sdY = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* sX = sdY + (long)nslot * DS;
+  T* sdY = reinterpret_cast<T*>(smem);
+  T* sX = sdY + (long)nslot * DS;
   const int XW = Wp + 2;
 
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
   // ---- stage dY rows (masked) and X rows with halo: one round of loads
-  const int cpy_dy = Cout / 8, cpy_x = Cin / 8;
-  stage2<16>(nslot * cpy_dy,
+  const int cpy_dy = Cout / CE, cpy_x = Cin / CE;
+  stage2<F32 ? 32 : 16>(nslot * cpy_dy,
           [&](int i) {
-            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
+            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
             const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
             const int hh = r0 + r;
             bf16x8 v = zero8();
             if (r < R && hh < H && c < W) {
               const long off = (((long)n * H + hh) * W + c) * Cout + ch;
-              v = ld8(dY + off);
-              if (MASK_DY) v = mask8(v, ld8(Yact + off));
+              v = ld16(dY + off);
+              if (MASK_DY) v = mask16<T>(v, ld16(Yact + off));
             }
             return v;
           },
           [&](int i, bf16x8 v) {
-            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * 8;
-            *reinterpret_cast<bf16x8*>(sdY + (long)slot * DS + ch) = v;
+            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
+            st16(sdY + (long)slot * DS + ch, v);
           },
           A1X ? 0 : (R + 2) * XW * cpy_x,
           [&](int i) {
-            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
+            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * CE;
             const int rr = pos / XW, cc = pos - (pos / XW) * XW;
             const int hh = r0 - 1 + rr, ww = cc - 1;
             return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                       ? ld8(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
+                       ? ld16(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
           },
           [&](int i, bf16x8 v) {
-            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * 8;
-            *reinterpret_cast<bf16x8*>(sX + (long)pos * XS + ch) = v;
+            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * CE;
+            st16(sX + (long)pos * XS + ch, v);
           });
   if (A1X) {
     // uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, then a1 (conv1 recompute)
@@ -615,7 +655,7 @@ __device__ __forceinline__ void wgrad_body(
     }
     __syncthreads();
     DDP_STAMP(STAMP_K_WGRAD, 1);
-    conv1_recompute_tile(
+    conv1_recompute_tile<T>(
         (R + 2) * XW, cg, wave, 0, 64,
         [&](int pos) {
           const int rr = pos / XW, cc = pos - (pos / XW) * XW;
@@ -644,38 +684,61 @@ __device__ __forceinline__ void wgrad_body(
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc[c][k] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  bf16x8 ones;
+  if constexpr (F32) {
+#pragma unroll 1
+    for (int s0 = 0; s0 < nslot; s0 += 32) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
+      for (int j = 0; j < 8; ++j) {
+        const int sl = s0 + 4 * j + g;  // this lane's K slot of MFMA j
+        const float a0 = sdY[(long)sl * DS + coT + i16];
+        const float a1 = sdY[(long)sl * DS + coT + 16 + i16];
+        // padding slots (r >= R) carry dY == 0; clamp their row into initialised LDS
+        const int rs0 = sl / Wp, cs = sl - rs0 * Wp, rs = min(rs0, R - 1);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int kh = tap / 3, kw = tap % 3;
+          const float bx_ = sX[(long)((rs + kh) * XW + cs + kw) * XS + ciT + i16];
+          acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bx_, acc[0][tap], 0, 0, 0);
+          acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bx_, acc[1][tap], 0, 0, 0);
+        }
+        accb[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, 1.f, accb[0], 0, 0, 0);
+        accb[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, 1.f, accb[1], 0, 0, 0);
+      }
+    }
+  } else {
+    bf16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
 
-  for (int s0 = 0; s0 < nslot; s0 += 32) {
-    const int sA = s0 + 4 * g + q, sB = s0 + 16 + 4 * g + q;  // this lane's tr-read rows
-    bf16x8 a[2];
+    for (int s0 = 0; s0 < nslot; s0 += 32) {
+      const int sA = s0 + 4 * g + q, sB = s0 + 16 + 4 * g + q;  // this lane's tr-read rows
+      bf16x8 a[2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const bf16_t* pA = sdY + (long)sA * DS + coT + 16 * c + 4 * p;
-      const bf16_t* pB = sdY + (long)sB * DS + coT + 16 * c + 4 * p;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
-      a[c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-    // X position of slot s for tap (kh,kw): sX row (r+kh), col (c+kw).  Padding slots
-    // (r >= R) carry dY == 0; clamp their row so the read stays inside initialised LDS.
-    const int rA0 = sA / Wp, cA = sA - rA0 * Wp, rB0 = sB / Wp, cB = sB - rB0 * Wp;
-    const int rA = min(rA0, R - 1), rB = min(rB0, R - 1);
+      for (int c = 0; c < 2; ++c) {
+        const bf16_t* pA = sdY + (long)sA * DS + coT + 16 * c + 4 * p;
+        const bf16_t* pB = sdY + (long)sB * DS + coT + 16 * c + 4 * p;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
+        a[c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      // X position of slot s for tap (kh,kw): sX row (r+kh), col (c+kw).  Padding slots
+      // (r >= R) carry dY == 0; clamp their row so the read stays inside initialised LDS.
+      const int rA0 = sA / Wp, cA = sA - rA0 * Wp, rB0 = sB / Wp, cB = sB - rB0 * Wp;
+      const int rA = min(rA0, R - 1), rB = min(rB0, R - 1);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int kh = tap / 3, kw = tap % 3;
-      const bf16_t* pA = sX + (long)((rA + kh) * XW + cA + kw) * XS + ciT + 4 * p;
-      const bf16_t* pB = sX + (long)((rB + kh) * XW + cB + kw) * XS + ciT + 4 * p;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
-      const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      acc[0][tap] = mfma16(a[0], b, acc[0][tap]);
-      acc[1][tap] = mfma16(a[1], b, acc[1][tap]);
+      for (int tap = 0; tap < 9; ++tap) {
+        const int kh = tap / 3, kw = tap % 3;
+        const bf16_t* pA = sX + (long)((rA + kh) * XW + cA + kw) * XS + ciT + 4 * p;
+        const bf16_t* pB = sX + (long)((rB + kh) * XW + cB + kw) * XS + ciT + 4 * p;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
+        const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[0][tap] = mfma16(a[0], b, acc[0][tap]);
+        acc[1][tap] = mfma16(a[1], b, acc[1][tap]);
+      }
+      accb[0] = mfma16(a[0], ones, accb[0]);
+      accb[1] = mfma16(a[1], ones, accb[1]);
     }
-    accb[0] = mfma16(a[0], ones, accb[0]);
-    accb[1] = mfma16(a[1], ones, accb[1]);
   }
 
   DDP_STAMP(STAMP_K_WGRAD, 3);
@@ -693,12 +756,12 @@ __device__ __forceinline__ void wgrad_body(
   DDP_STAMP(STAMP_K_WGRAD, 4);
 }
 
-template <bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
+template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
 __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
-    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ Yact, const bf16_t* __restrict__ X,
+    const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ X,
     float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  wgrad_body<MASK_DY, A1X, GH, GW, GCI, GCO>(dY, Yact, X, slab, B, H, W, Cin, Cout, R, c1, smem,
+  wgrad_body<T, MASK_DY, A1X, GH, GW, GCI, GCO>(dY, Yact, X, slab, B, H, W, Cin, Cout, R, c1, smem,
                                               blockIdx.x, blockIdx.y);
 }
 
@@ -713,29 +776,33 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // uint8 batch; otherwise it reads the a1 the forward stored (Xact).  Measured: the dgrad
 // role only needs a1's ReLU mask of its own pixels and gets ~2 us faster reading it; the
 // wgrad role needs full a1 tiles with halo and is as fast recomputing as loading.
-template <int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO>
-__global__ __launch_bounds__(256, 2) void conv3x3_bwd_kernel(
-    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ WT, bf16_t* __restrict__ dX,
+// bf16: 2 blocks per CU (<= 256 VGPR+AGPR per lane); fp32 tiles take ~135 KiB of LDS, so
+// one block per CU and the full register file
+template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kernel(
+    const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
-    int R, int nd, C1Src c1, const bf16_t* __restrict__ Xact) {
+    int R, int nd, C1Src c1, const T* __restrict__ Xact) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < nd)
-    dgrad_body<PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
+    dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
         dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem,
         blockIdx.x, 0);
   else
-    wgrad_body<false, WA1X, GH, GW, GCI, GCO>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H, W, Cin,
-                                              Cout, R, c1, smem, blockIdx.x - nd, 0);
+    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H, W, Cin,
+                                                 Cout, R, c1, smem, blockIdx.x - nd, 0);
 }
 
 // ---------------------------------------------------------------- launchers
-size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x) {
-  return fwd_stage_lds(W, Cin, pxt, a1x) + fc_epi_lds(pxt, FC_MAX_NOF);
+// es = element size (2: bf16, 4: exact fp32)
+size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x, int es) {
+  return fwd_stage_lds(W, Cin, pxt, a1x, es) + fc_epi_lds(pxt, FC_MAX_NOF);
 }
 
-size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1) {
+size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1, int es) {
   const size_t XR = 64 * pxt + 2 * W + 2;
-  return sizeof(bf16_t) * ((size_t)32 * (9 * Cout + 16) + XR * (Cout + 16)) +
+  const int pad = es == 2 ? 16 : 8;  // Prec<T>::PAD
+  return (size_t)es * ((size_t)32 * (9 * Cout + pad) + XR * (Cout + pad)) +
          (fuse_w1 ? sizeof(float) * (XR + 4 * 320) + 4 * 64 * pxt : 0);
 }
 
@@ -743,26 +810,40 @@ static inline bool simplecnn_geom(int H, int W, int Cin, int Cout) {
   return H == 28 && W == 28 && Cin == 32 && Cout == 64;
 }
 
-void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
-                 int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s, const C1Src* c1) {
+// Kernels whose dynamic LDS exceeds the 64 KiB default must opt in once per
+// instantiation (fp32 tiles use up to ~135 KiB of the CU's 160 KiB).
+template <typename K>
+static void lds_optin(K kernel, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <typename T>
+static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, int H, int W, int Cin,
+                       int Cout, bool relu, const T* wfc, float* fc_part, int pxt, hipStream_t s,
+                       const C1Src* c1) {
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cout / 64);
   const bool a1x = c1 != nullptr;
-  const size_t lds = conv3x3_fwd_lds(W, Cin, pxt, a1x);
+  const size_t lds = conv3x3_fwd_lds(W, Cin, pxt, a1x, (int)sizeof(T));
   const bool fc = wfc != nullptr;  // host guarantees NO == 10 when fused
   const C1Src cs = a1x ? *c1 : C1Src();
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   // one 16-pixel tile per wave: pxt 2 -> 8 waves (2 per SIMD), pxt 1 -> 4 waves
-#define LF(PX, RL, NF, AX)                                                                             \
-  do {                                                                                                 \
-    if (g) hipLaunchKernelGGL((conv3x3_fwd_kernel<1, 4 * PX, RL, NF, AX, 28, 28, 32, 64>), grid,     \
-                              dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,      \
-                              fc_part, cs);                                                         \
-    else hipLaunchKernelGGL((conv3x3_fwd_kernel<1, 4 * PX, RL, NF, AX, 0, 0, 0, 0>), grid,           \
-                            dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, \
-                            cs);                                                                    \
+#define LF(PX, RL, NF, AX)                                                                          \
+  do {                                                                                              \
+    if (g) {                                                                                        \
+      auto k = conv3x3_fwd_kernel<T, 1, 4 * PX, RL, NF, AX, 28, 28, 32, 64>;                        \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, grid, dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,  \
+                         fc_part, cs);                                                              \
+    } else {                                                                                        \
+      auto k = conv3x3_fwd_kernel<T, 1, 4 * PX, RL, NF, AX, 0, 0, 0, 0>;                            \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, grid, dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,  \
+                         fc_part, cs);                                                              \
+    }                                                                                               \
   } while (0)
   if (pxt == 2) {
     if (fc && a1x) LF(2, true, 10, true);
@@ -772,27 +853,45 @@ void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y
     else if (fc) LF(1, true, 10, false); else if (relu) LF(1, true, 0, false); else LF(1, false, 0, false);
   }
 #undef LF
-  (void)NO;
 }
 
-void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
-                   bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
-                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1) {
+void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
+                 int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
+                 int pxt, hipStream_t s, const C1Src* c1) {
+  (void)NO;
+  fwd_launch<bf16_t>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1);
+}
+void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
+                 int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
+                 int pxt, hipStream_t s, const C1Src* c1) {
+  (void)NO;
+  fwd_launch<float>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1);
+}
+
+template <typename T>
+static void dgrad_launch(const T* dY, const T* Yact, const T* WT, const T* Xact, T* dX, int B, int H,
+                         int W, int Cin, int Cout, const void* x0, bool x0_u8, BatchIdx bi,
+                         float* w1slab, int pxt, hipStream_t s, const C1Src* c1) {
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cin / 32);
   const bool mdy = Yact != nullptr, mx = Xact != nullptr || c1 != nullptr, w1 = w1slab != nullptr;
-  const size_t lds = conv3x3_dgrad_lds(W, Cout, pxt, w1);
+  const size_t lds = conv3x3_dgrad_lds(W, Cout, pxt, w1, (int)sizeof(T));
   const C1Src cs = c1 ? *c1 : C1Src();
   const bool g = simplecnn_geom(H, W, Cin, Cout);
-#define LD(PX, A, Bm, C, AX)                                                                              \
-  do {                                                                                                    \
-    if (g) hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C, AX, 28, 28, 32, 64>), grid, dim3(256), \
-                              lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi,   \
-                              w1slab, cs);                                                              \
-    else hipLaunchKernelGGL((conv3x3_dgrad_kernel<PX, A, Bm, C, AX, 0, 0, 0, 0>), grid, dim3(256), lds,  \
-                            s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, (int)x0_u8, bi, w1slab,   \
-                            cs);                                                                        \
+#define LD(PX, A, Bm, C, AX)                                                                        \
+  do {                                                                                              \
+    if (g) {                                                                                        \
+      auto k = conv3x3_dgrad_kernel<T, PX, A, Bm, C, AX, 28, 28, 32, 64>;                           \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0,  \
+                         (int)x0_u8, bi, w1slab, cs);                                               \
+    } else {                                                                                        \
+      auto k = conv3x3_dgrad_kernel<T, PX, A, Bm, C, AX, 0, 0, 0, 0>;                               \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0,  \
+                         (int)x0_u8, bi, w1slab, cs);                                               \
+    }                                                                                               \
   } while (0)
   if (pxt == 2) {
     if (w1 && c1) LD(2, false, true, true, true);
@@ -812,6 +911,17 @@ void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const
 #undef LD
 }
 
+void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
+                   bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
+                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1) {
+  dgrad_launch<bf16_t>(dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, x0_u8, bi, w1slab, pxt, s, c1);
+}
+void conv3x3_dgrad(const float* dY, const float* Yact, const float* WT, const float* Xact,
+                   float* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
+                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1) {
+  dgrad_launch<float>(dY, Yact, WT, Xact, dX, B, H, W, Cin, Cout, x0, x0_u8, bi, w1slab, pxt, s, c1);
+}
+
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt) {
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
@@ -820,55 +930,89 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt) {
 
 int conv3x3_wgrad_blocks(int B, int H, int R) { return B * ((H + R - 1) / R); }
 
-size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x) {
+size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x, int es) {
   const int Wp = (W + 7) & ~7;
   const int nslot = ((R * Wp + 31) / 32) * 32;
-  return sizeof(bf16_t) * ((size_t)nslot * (Cout + 16) + (size_t)(R + 2) * (Wp + 2) * (Cin + 16)) +
+  return (size_t)es * ((size_t)nslot * (Cout + 16) + (size_t)(R + 2) * (Wp + 2) * (Cin + 16)) +
          (a1x ? sizeof(float) * ((size_t)(R + 4) * (Wp + 4) + Cin * 10) : 0);
 }
 
-void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
-                   int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1) {
+template <typename T>
+static void wgrad_launch(const T* dY, const T* Yact, const T* X, float* slab, int B, int H, int W,
+                         int Cin, int Cout, int R, hipStream_t s, const C1Src* c1) {
   const dim3 grid(conv3x3_wgrad_blocks(B, H, R), (Cout / 32) * (Cin / 16) / 4);
-  const size_t lds = conv3x3_wgrad_lds(W, Cin, Cout, R, c1 != nullptr);
+  const size_t lds = conv3x3_wgrad_lds(W, Cin, Cout, R, c1 != nullptr, (int)sizeof(T));
   const C1Src cs = c1 ? *c1 : C1Src();
   const bool g = simplecnn_geom(H, W, Cin, Cout);
 #define LW(M, AX)                                                                                   \
   do {                                                                                              \
-    if (g) hipLaunchKernelGGL((conv3x3_wgrad_kernel<M, AX, 28, 28, 32, 64>), grid, dim3(256), lds, s, \
-                              dY, Yact, X, slab, B, H, W, Cin, Cout, R, cs);                      \
-    else hipLaunchKernelGGL((conv3x3_wgrad_kernel<M, AX, 0, 0, 0, 0>), grid, dim3(256), lds, s, dY,  \
-                            Yact, X, slab, B, H, W, Cin, Cout, R, cs);                            \
+    if (g) {                                                                                        \
+      auto k = conv3x3_wgrad_kernel<T, M, AX, 28, 28, 32, 64>;                                      \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, dY, Yact, X, slab, B, H, W, Cin, Cout, R, cs);  \
+    } else {                                                                                        \
+      auto k = conv3x3_wgrad_kernel<T, M, AX, 0, 0, 0, 0>;                                          \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, grid, dim3(256), lds, s, dY, Yact, X, slab, B, H, W, Cin, Cout, R, cs);  \
+    }                                                                                               \
   } while (0)
   if (c1) { if (Yact) LW(true, true); else LW(false, true); }
   else { if (Yact) LW(true, false); else LW(false, false); }
 #undef LW
 }
 
-size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R) {
-  const size_t a = conv3x3_dgrad_lds(W, Cout, pxt, true), b = conv3x3_wgrad_lds(W, Cin, Cout, R, true);
+void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
+                   int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1) {
+  wgrad_launch<bf16_t>(dY, Yact, X, slab, B, H, W, Cin, Cout, R, s, c1);
+}
+void conv3x3_wgrad(const float* dY, const float* Yact, const float* X, float* slab, int B,
+                   int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1) {
+  wgrad_launch<float>(dY, Yact, X, slab, B, H, W, Cin, Cout, R, s, c1);
+}
+
+size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es) {
+  const size_t a = conv3x3_dgrad_lds(W, Cout, pxt, true, es), b = conv3x3_wgrad_lds(W, Cin, Cout, R, true, es);
   return a > b ? a : b;
 }
 
-void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
-                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
-                 bool wgrad_load_a1, hipStream_t s) {
+template <typename T>
+static void bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
+                       int Cin, int Cout, int pxt, int R, const C1Src& c1, const T* Xact,
+                       bool wgrad_load_a1, hipStream_t s) {
   const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = conv3x3_wgrad_blocks(B, H, R);
-  const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R);
+  const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
-#define LBW(PX, DA, WA)                                                                                     \
-  do {                                                                                                      \
-    if (g) hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, DA, WA, 28, 28, 32, 64>), dim3(nd + nw), dim3(256),   \
-                              lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1, Xact);       \
-    else hipLaunchKernelGGL((conv3x3_bwd_kernel<PX, DA, WA, 0, 0, 0, 0>), dim3(nd + nw), dim3(256), lds, s, \
-                            dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R, nd, c1, Xact);                 \
+#define LBW(PX, DA, WA)                                                                             \
+  do {                                                                                              \
+    if (g) {                                                                                        \
+      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64>;                                   \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
+                         Cout, R, nd, c1, Xact);                                                    \
+    } else {                                                                                        \
+      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0>;                                       \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
+                         Cout, R, nd, c1, Xact);                                                    \
+    }                                                                                               \
   } while (0)
   // Xact given: the dgrad role reads it; the wgrad role reads it only if wgrad_load_a1
   if (!Xact) { if (pxt == 2) LBW(2, true, true); else LBW(1, true, true); }
   else if (wgrad_load_a1) { if (pxt == 2) LBW(2, false, false); else LBW(1, false, false); }
   else { if (pxt == 2) LBW(2, false, true); else LBW(1, false, true); }
 #undef LBW
+}
+
+void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
+                 bool wgrad_load_a1, hipStream_t s) {
+  bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s);
+}
+void conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
+                 bool wgrad_load_a1, hipStream_t s) {
+  bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s);
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv3x3)

@@ -14,16 +14,29 @@ void stamps_set(void* buf);
 // ---- conv1 (Cin = 1) ---------------------------------------------------------------
 void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, bf16_t* y,
                int B, int H, int W, int Cout, hipStream_t s);
+void conv1_fwd(const void* x, bool x_is_u8, BatchIdx bi, const float* w, const float* b, float* y,
+               int B, int H, int W, int Cout, hipStream_t s);
 int conv1_wgrad_blocks(int B, int H, int W, int chunk);
 void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const bf16_t* dy, const bf16_t* yact,
                  float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s);
+void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const float* dy, const float* yact,
+                 float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s);
 
 // ---- 3x3 / s1 / p1 NHWC conv (MFMA) --------------------------------------------------
+// bf16 operands (v_mfma_f32_16x16x32_bf16) or exact fp32 operands (v_mfma_f32_16x16x4_f32,
+// the float overloads); `es` = element size of the LDS-size helpers (2 or 4).
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
                  int pxt, hipStream_t s, const C1Src* c1 = nullptr);
+// fp32: wfc (fused fc epilogue) is the fc weight in its native [NO][H*W][C] layout
+void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
+                 int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
+                 int pxt, hipStream_t s, const C1Src* c1 = nullptr);
 void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
                    bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
+                   BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1 = nullptr);
+void conv3x3_dgrad(const float* dY, const float* Yact, const float* WT, const float* Xact,
+                   float* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
                    BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1 = nullptr);
 int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // fused level-1 conv backward (dgrad + conv1 wgrad slabs, and conv2 wgrad slabs) in one
@@ -33,12 +46,17 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s);
-size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R);
+void conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
+                 int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
+                 bool wgrad_load_a1, hipStream_t s);
+size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2);
 int conv3x3_wgrad_blocks(int B, int H, int R);
-size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false);
-size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x = false);
-size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1);
+size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false, int es = 2);
+size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x = false, int es = 2);
+size_t conv3x3_dgrad_lds(int W, int Cout, int pxt, bool fuse_w1, int es = 2);
 void conv3x3_wgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* X, float* slab, int B,
+                   int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1 = nullptr);
+void conv3x3_wgrad(const float* dY, const float* Yact, const float* X, float* slab, int B,
                    int H, int W, int Cin, int Cout, int R, hipStream_t s, const C1Src* c1 = nullptr);
 
 // ---- general NHWC implicit-GEMM convolution (conv_gemm.hip) ------------------------
@@ -105,6 +123,8 @@ void transpose_w(const float* w, int Co, int T, int Ci, bf16_t* wt, hipStream_t 
 // ---- Linear over NHWC-flattened activations -----------------------------------------
 void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
                 hipStream_t s);
+void fc_partial(const float* X, const float* Wf, float* part, int B, int HW, int C, int NO,
+                hipStream_t s);
 void fc_reduce(const float* part, const float* bias, float* out, int B, int G, int NO,
                hipStream_t s);
 // Optional extras of fc_bwd's first block: fc bias gradient and the batch-mean loss
@@ -139,6 +159,8 @@ size_t fc_bwd_lds(int B, int NO, bool xent);
 void noop(int blocks, int* sink, hipStream_t s);
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
+void fc_bwd(const float* dL, const float* X, const float* Wf, float* dX, float* dW, float scale,
+            int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
 
 // ---- cross-entropy --------------------------------------------------------------------
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,
@@ -160,12 +182,16 @@ void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int
 // SHADOW_BF16_PAD4: a [..][3] weight (the ResNet stem) -> [..][4] with the 4th channel left
 // at its zero fill (the stem conv's 16-B weight loads read it); sgd_kernel and the xGMI
 // fused-SGD all-gather (shadow_one).
-enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2, SHADOW_BF16_FCFRAG = 3, SHADOW_BF16_PAD4 = 4 };
+// SHADOW_F32_TAPT: the exact-fp32 engine's [tap][ci][co] copy of the conv2 weight (the
+// data-gradient operand), a transposed fp32 copy - not a reduced-precision shadow; dst32.
+enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2, SHADOW_BF16_FCFRAG = 3, SHADOW_BF16_PAD4 = 4,
+       SHADOW_F32_TAPT = 5 };
 constexpr int MAX_SHADOWS = 4;
 struct ShadowRegion {
   long off, n;
   bf16_t* dst;
   int kind, a, b, c;  // TAPT: a = Cout, b = taps, c = Cin
+  float* dst32 = nullptr;  // SHADOW_F32_TAPT destination
 };
 struct ShadowSet {
   ShadowRegion r[MAX_SHADOWS];
@@ -183,6 +209,7 @@ struct SlabSeg {
   float* m = nullptr;
   bf16_t* sh = nullptr;
   bf16_t* sh_t = nullptr;
+  float* sh_t32 = nullptr;  // exact-fp32 engine: fp32 [tap][ci][co] copy (same t_* geometry)
   int t_co = 0, t_taps = 0, t_ci = 0;
   int accum = 0;  // dst += reduced * scale (gradient accumulation) instead of dst =
 };

@@ -1,5 +1,6 @@
-// Skinny Linear layer over an NHWC-flattened bf16 activation (SimpleCNN's fc,
-// reference model.py:16,19: nn.Linear(50176, 10)).
+// Skinny Linear layer over an NHWC-flattened bf16 or fp32 activation (SimpleCNN's fc,
+// reference model.py:16,19: nn.Linear(50176, 10)).  The fp32 instantiations (--dtype fp32)
+// read the fp32 master weight itself - no shadow copy.
 //
 // The weight is kept in the activation's memory order, [out][H*W][C] (bf16
 // shadow of the fp32 master), so both passes stream it contiguously.  The
@@ -21,8 +22,19 @@ namespace ddp_amd {
 
 constexpr int FC_MAXO = 16;
 
-__global__ __launch_bounds__(256) void fc_partial_kernel(const bf16_t* __restrict__ X,
-                                                         const bf16_t* __restrict__ Wf,
+__device__ __forceinline__ void ld8f(const bf16_t* p, float* o) {
+  const bf16x8 v = ld8(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f((bf16_t)v[j]);
+}
+__device__ __forceinline__ void ld8f(const float* p, float* o) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void fc_partial_kernel(const T* __restrict__ X,
+                                                         const T* __restrict__ Wf,
                                                          float* __restrict__ part, int B, int HW,
                                                          int C, int NO) {
   const int lane = threadIdx.x & 63;
@@ -37,14 +49,16 @@ __global__ __launch_bounds__(256) void fc_partial_kernel(const bf16_t* __restric
 #pragma unroll
   for (int o = 0; o < FC_MAXO; ++o) s[o] = 0.f;
   for (int e = lane * 8; e < te; e += 512) {
-    const bf16x8 xv = ld8(X + xoff + e);
+    float xv[8];
+    ld8f(X + xoff + e, xv);
 #pragma unroll
     for (int o = 0; o < FC_MAXO; ++o) {
       if (o < NO) {
-        const bf16x8 wv = ld8(Wf + (long)o * HW * C + woff + e);
+        float wv[8];
+        ld8f(Wf + (long)o * HW * C + woff + e, wv);
         float a = s[o];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a = fmaf(bf2f((bf16_t)xv[j]), bf2f((bf16_t)wv[j]), a);
+        for (int j = 0; j < 8; ++j) a = fmaf(xv[j], wv[j], a);
         s[o] = a;
       }
     }
@@ -78,11 +92,24 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __
 constexpr int FCB_COLS = 128;
 constexpr int FCB_RB = 8;  // rows in flight per wave
 
-template <bool MASK, bool XENT, int NOT, int WPB>
+// 2 consecutive columns of one row as floats (bf16: one 4-byte load, fp32: one 8-byte load)
+__device__ __forceinline__ float2 ld2f(const bf16_t* p) {
+  const unsigned u = *reinterpret_cast<const unsigned*>(p);
+  return make_float2(__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u));
+}
+__device__ __forceinline__ float2 ld2f(const float* p) { return *reinterpret_cast<const float2*>(p); }
+__device__ __forceinline__ void st2_wt(bf16_t* p, float a, float b) {
+  st_wt(reinterpret_cast<unsigned*>(p), (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16));
+}
+__device__ __forceinline__ void st2_wt(float* p, float a, float b) {
+  st_wt(reinterpret_cast<float2*>(p), make_float2(a, b));
+}
+
+template <typename T, bool MASK, bool XENT, int NOT, int WPB>
 __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restrict__ dL,
-                                                          const bf16_t* __restrict__ X,
-                                                          const bf16_t* __restrict__ Wf,
-                                                          bf16_t* __restrict__ dX,
+                                                          const T* __restrict__ X,
+                                                          const T* __restrict__ Wf,
+                                                          T* __restrict__ dX,
                                                           float* __restrict__ dW, float scale,
                                                           int B, long K, int NO_rt,
                                                           FcBwdExtras ex) {
@@ -100,15 +127,15 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
   const bool active = col < K;  // host guarantees K % 2 == 0
   const long cc = active ? col : 0;
   // ---- this block's loads first (independent of the prologue)
-  unsigned wr[NOT];
+  float2 wr[NOT];
 #pragma unroll
-  for (int o = 0; o < NOT; ++o) wr[o] = (o < NO) ? *reinterpret_cast<const unsigned*>(Wf + (long)o * K + cc) : 0u;
+  for (int o = 0; o < NOT; ++o) wr[o] = (o < NO) ? ld2f(Wf + (long)o * K + cc) : make_float2(0.f, 0.f);
   const int nr = B > wave ? (B - wave + WPB - 1) / WPB : 0;  // rows of this wave (uniform)
-  unsigned xr[FCB_RB];
+  float2 xr[FCB_RB];
 #pragma unroll
   for (int u = 0; u < FCB_RB; ++u) {
     const int b = min(wave + WPB * u, B - 1);
-    xr[u] = *reinterpret_cast<const unsigned*>(X + (long)b * K + cc);
+    xr[u] = ld2f(X + (long)b * K + cc);
   }
   // fused-SGD operands of this thread's dW outputs (final loop below): requested now so
   // the optimizer tail has no dependent global round trip
@@ -154,8 +181,8 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
   float w0[NOT], w1[NOT], dw0[NOT], dw1[NOT];
 #pragma unroll
   for (int o = 0; o < NOT; ++o) {
-    w0[o] = __builtin_bit_cast(float, wr[o] << 16);
-    w1[o] = __builtin_bit_cast(float, wr[o] & 0xffff0000u);
+    w0[o] = wr[o].x;
+    w1[o] = wr[o].y;
     dw0[o] = 0.f;
     dw1[o] = 0.f;
   }
@@ -164,15 +191,15 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
 #pragma unroll
       for (int u = 0; u < FCB_RB; ++u) {
         const int b = min(wave + WPB * (u0 + u), B - 1);
-        xr[u] = *reinterpret_cast<const unsigned*>(X + (long)b * K + cc);
+        xr[u] = ld2f(X + (long)b * K + cc);
       }
     }
 #pragma unroll
     for (int u = 0; u < FCB_RB; ++u) {
       if (u0 + u < nr) {  // wave-uniform
         const int b = wave + WPB * (u0 + u);
-        const float x0 = __builtin_bit_cast(float, xr[u] << 16);
-        const float x1 = __builtin_bit_cast(float, xr[u] & 0xffff0000u);
+        const float x0 = xr[u].x;
+        const float x1 = xr[u].y;
         const float* dl = s_dl + b * NO;
         float dz0 = 0.f, dz1 = 0.f;
 #pragma unroll
@@ -188,9 +215,7 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
           dz0 = x0 > 0.f ? dz0 : 0.f;
           dz1 = x1 > 0.f ? dz1 : 0.f;
         }
-        if (active)
-          st_wt(reinterpret_cast<unsigned*>(dX + (long)b * K + col),
-                (unsigned)f2bf(dz0) | ((unsigned)f2bf(dz1) << 16));  // dZ2: write-through
+        if (active) st2_wt(dX + (long)b * K + col, dz0, dz1);  // dZ2: write-through
       }
     }
   }
@@ -235,7 +260,13 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
 void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
                 hipStream_t s) {
   const long tiles = (long)B * (HW / 16);
-  hipLaunchKernelGGL(fc_partial_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, X, Wf,
+  hipLaunchKernelGGL(fc_partial_kernel<bf16_t>, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, X, Wf,
+                     part, B, HW, C, NO);
+}
+void fc_partial(const float* X, const float* Wf, float* part, int B, int HW, int C, int NO,
+                hipStream_t s) {
+  const long tiles = (long)B * (HW / 16);
+  hipLaunchKernelGGL(fc_partial_kernel<float>, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s, X, Wf,
                      part, B, HW, C, NO);
 }
 
@@ -253,12 +284,13 @@ size_t fc_bwd_lds(int B, int NO, bool xent) {
   return sizeof(float) * (head + (size_t)FCB_WPB * NOT * FCB_COLS);
 }
 
-void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
-            int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
+template <typename T>
+static void fc_bwd_launch(const float* dL, const T* X, const T* Wf, T* dX, float* dW, float scale,
+                          int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
   const dim3 grid((unsigned)((K + FCB_COLS - 1) / FCB_COLS));
   const bool xe = ex.part != nullptr;
   const size_t lds = fc_bwd_lds(B, NO, xe);
-#define LB(M, XE, N) hipLaunchKernelGGL((fc_bwd_kernel<M, XE, N, FCB_WPB>), grid, dim3(FCB_WPB * 64), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
+#define LB(M, XE, N) hipLaunchKernelGGL((fc_bwd_kernel<T, M, XE, N, FCB_WPB>), grid, dim3(FCB_WPB * 64), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
   if (NO == 10) {
     if (xe) { if (mask) LB(true, true, 10); else LB(false, true, 10); }
     else { if (mask) LB(true, false, 10); else LB(false, false, 10); }
@@ -267,6 +299,15 @@ void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, floa
     else { if (mask) LB(true, false, FC_MAXO); else LB(false, false, FC_MAXO); }
   }
 #undef LB
+}
+
+void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
+            int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
+  fc_bwd_launch<bf16_t>(dL, X, Wf, dX, dW, scale, B, K, NO, mask, s, ex);
+}
+void fc_bwd(const float* dL, const float* X, const float* Wf, float* dX, float* dW, float scale,
+            int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex) {
+  fc_bwd_launch<float>(dL, X, Wf, dX, dW, scale, B, K, NO, mask, s, ex);
 }
 
 DDP_STAMPS_SETTER(stamps_set_linear)

@@ -61,6 +61,10 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
                 sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(e[u]);
               } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
                 sh.r[r].dst[(jj / 3) * 4 + jj % 3] = f2bf(e[u]);
+              } else if (sh.r[r].kind == SHADOW_F32_TAPT) {
+                const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
+                const long co = jj / ((long)T * Ci);
+                sh.r[r].dst32[(jj - co * T * Ci) * Co + co] = e[u];
               } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
                 const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
                 const long co = jj / ((long)T * Ci);
@@ -92,6 +96,10 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
         sh.r[r].dst[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = f2bf(v);
       } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
         sh.r[r].dst[(j / 3) * 4 + j % 3] = f2bf(v);
+      } else if (sh.r[r].kind == SHADOW_F32_TAPT) {
+        const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
+        const long co = j / ((long)T * Ci);
+        sh.r[r].dst32[(j - co * T * Ci) * Co + co] = v;
       } else {
         const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
         const long co = j / ((long)T * Ci);
@@ -153,10 +161,11 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
       sg.p[i] = pn;
       if (sg.m) sg.m[i] = m;
       if (sg.sh) sg.sh[i] = f2bf(pn);
-      if (sg.sh_t) {  // OHWI [co][tap][ci] -> [tap][ci][co]
+      if (sg.sh_t || sg.sh_t32) {  // OHWI [co][tap][ci] -> [tap][ci][co]
         const long per = (long)sg.t_taps * sg.t_ci;
         const long co = i / per;
-        sg.sh_t[(i - co * per) * sg.t_co + co] = f2bf(pn);
+        if (sg.sh_t) sg.sh_t[(i - co * per) * sg.t_co + co] = f2bf(pn);
+        if (sg.sh_t32) sg.sh_t32[(i - co * per) * sg.t_co + co] = pn;
       }
     }
   }

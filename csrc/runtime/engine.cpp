@@ -22,6 +22,11 @@
 // fc_bwd runs the softmax cross-entropy in its prologue -> 6 kernels per step,
 // bit-identical to level 0 (same FMA orders, same fixed-order reductions).
 //
+// f32 = 1 (--dtype fp32) runs the same level-1 chain with exact fp32 operands
+// (launch_step_f32): fp32 a2 / dZ2, the fp32 master weights read directly by the conv
+// forward and fc kernels, and one fp32 [tap][ci][co] copy of the conv2 weight (kept by
+// the optimizer pass, like the bf16 shadows) for the data gradient.
+//
 // Buckets follow the reference DDP's rebuilt layout:
 // bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB).
 #include "runtime/runtime.h"
@@ -35,6 +40,10 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   if (cfg_.C2 % 64 != 0) throw std::runtime_error("engine: C2 must be a multiple of 64");
   if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
   if (cfg_.NO != 10) throw std::runtime_error("engine: the fused fc epilogue is built for 10 classes");
+  if (cfg_.f32 && (cfg_.fuse_level != 1 || cfg_.store_a1 != 0))
+    throw std::runtime_error("engine: fp32 mode needs fuse_level 1 and store_a1 0");
+  if (cfg_.f32 && !(b_.a2_f32 && b_.dz2_f32 && b_.w2t_f32))
+    throw std::runtime_error("engine: fp32 mode needs the a2 / dz2 / w2t fp32 buffers");
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
@@ -64,6 +73,13 @@ void SimpleCNNEngine::refresh_shadows() {
   SgdArgs a{0.f, 0.f, 0.f, 0.f, 0, 0, 0, /*update=*/0};
   ShadowSet sh{};
   const long n_w2 = (long)cfg_.C2 * 9 * cfg_.C1;
+  if (cfg_.f32) {
+    sh.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, cfg_.C2, 9, cfg_.C1, b_.w2t_f32};
+    sh.count = 1;
+    sgd_step(b_.params, b_.grads, nullptr, b_.n_params, a, sh, nullptr, cs_);
+    DDP_HIP_CHECK(hipGetLastError());
+    return;
+  }
   sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
   sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, cfg_.C2, 9, cfg_.C1};
   sh.r[2] = ShadowRegion{b_.off_wfc, (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, b_.wfc_bf16,
@@ -76,6 +92,10 @@ void SimpleCNNEngine::refresh_shadows() {
 }
 
 void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
+  if (cfg_.f32) {
+    launch_step_f32(B, stride, first_momentum_step);
+    return;
+  }
   const int H = cfg_.H, W = cfg_.W, HW = H * W, C1 = cfg_.C1, C2 = cfg_.C2, NO = cfg_.NO;
   if (B <= 0 || B > cfg_.max_batch) throw std::runtime_error("engine: bad batch size");
   const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
@@ -234,6 +254,126 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   sh.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
   sh.count = 4;
   sgd_step(P, G, M, b_.n_params, sa, sh, b_.step_ctr, cs_);
+}
+
+// The exact-fp32 step: same kernel chain as level 1 (conv2 fwd + fused fc partials with
+// conv1 recomputed from the uint8 batch; fc backward with the cross-entropy prologue;
+// one fused conv backward; slab reduction) on fp32 operands.
+void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_step) {
+  const int H = cfg_.H, W = cfg_.W, HW = H * W, C1 = cfg_.C1, C2 = cfg_.C2, NO = cfg_.NO;
+  if (B <= 0 || B > cfg_.max_batch) throw std::runtime_error("engine: bad batch size");
+  const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
+  const bool dist = use_x || (comm_ && (comm_->world() > 1 || cfg_.force_allreduce));
+  const float inv_ws = 1.f / (float)cfg_.world;
+  BatchIdx bi{b_.idx, b_.step_ctr, stride, 0};
+  bi.n_idx = b_.n_idx;
+  bi.n_rows = b_.n_rows;
+  float* P = b_.params;
+  float* G = b_.grads;
+  float* M = b_.momentum;
+  C1Src c1;
+  c1.x = b_.images;
+  c1.bi = bi;
+  c1.w = P + b_.off_w1;
+  c1.b = P + b_.off_b1;
+  c1.xb_out = b_.xb;
+  c1.yb_out = b_.yb;
+  c1.labels = b_.labels;
+  BatchIdx bid{nullptr, nullptr, 0, 0};
+  bid.n_rows = B;
+  C1Src c1b;
+  c1b.x = b_.xb;
+  c1b.bi = bid;
+  c1b.w = c1.w;
+  c1b.b = c1.b;
+  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
+  const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
+                   cfg_.maximize, first_momentum_step ? 1 : 0, 1};
+  const bool fopt = !dist && cfg_.fuse_opt;
+
+  // ---- forward: conv1 (recomputed) + conv2 + bias + ReLU -> a2, fused fc partial logits
+  conv3x3_fwd(static_cast<const float*>(nullptr), P + b_.off_w2, P + b_.off_b2, b_.a2_f32, B, H, W, C1, C2,
+              true, P + b_.off_wfc, b_.fc_part, NO, cfg_.pxt_fwd, cs_, &c1);
+  // ---- loss + fc backward (bucket 0)
+  FcBwdExtras ex;
+  ex.dbias = G + b_.off_bfc;
+  ex.dbias_scale = inv_ws;
+  ex.loss_out = b_.loss_hist;
+  ex.step_ctr = b_.step_ctr;
+  ex.part = b_.fc_part;
+  ex.HW = HW;
+  ex.CH = 64 * cfg_.pxt_fwd;
+  ex.fc_bias = P + b_.off_bfc;
+  ex.labels32 = b_.yb;
+  ex.bi = bid;
+  ex.gscale = 1.f / (float)B;
+  ex.sys_store = use_x ? 1 : 0;
+  if (fopt) {  // each block updates only the fc columns it alone reads: race free in place
+    ex.sgd = sa;
+    ex.p_w = P + b_.off_wfc;
+    ex.m_w = M ? M + b_.off_wfc : nullptr;
+  }
+  fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
+         (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+  if (dist) {
+    DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
+    if (use_x) {
+      ShadowSet none{};
+      xgmi_->all_reduce_sgd(xch_[0], ms_, sa, P, M, none, nullptr);
+    } else {
+      comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
+    }
+    DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
+  }
+  // ---- conv backward (bucket 1)
+  conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
+              cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr), false, cs_);
+  SlabSet ss{};
+  const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
+  ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, n_w2, wblk, G + b_.off_w2, inv_ws};
+  ss.s[1] = SlabSeg{b_.w2slab, w2row, n_w2, (long)C2, wblk, G + b_.off_b2, inv_ws};
+  const int dblk = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_dgrad);
+  ss.s[2] = SlabSeg{b_.w1slab, 320, 0, (long)C1 * 9, dblk, G + b_.off_w1, inv_ws};
+  ss.s[3] = SlabSeg{b_.w1slab, 320, (long)C1 * 9, (long)C1, dblk, G + b_.off_b1, inv_ws};
+  ss.count = 4;
+  if (fopt) {
+    auto opt = [&](SlabSeg& sg, long off) {
+      sg.p = P + off;
+      sg.m = M ? M + off : nullptr;
+    };
+    opt(ss.s[0], b_.off_w2);
+    ss.s[0].sh_t32 = b_.w2t_f32;
+    ss.s[0].t_co = C2; ss.s[0].t_taps = 9; ss.s[0].t_ci = C1;
+    opt(ss.s[1], b_.off_b2);
+    opt(ss.s[2], b_.off_w1);
+    opt(ss.s[3], b_.off_b1);
+    ss.s[4] = SlabSeg{G + b_.off_bfc, (long)NO, 0, (long)NO, 1, G + b_.off_bfc, 1.f};
+    opt(ss.s[4], b_.off_bfc);
+    ss.count = 5;
+    ss.sgd = sa;
+    ss.step_ctr = b_.step_ctr;
+  }
+  ss.sys_store = use_x ? 1 : 0;
+  grad_reduce(ss, cs_);
+  if (fopt) return;
+  ShadowSet sh1{};
+  sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
+  sh1.count = 1;
+  if (dist) {
+    DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
+    if (use_x) {
+      xgmi_->all_reduce_sgd(xch_[1], ms_, sa, P, M, sh1, b_.step_ctr);
+    } else {
+      comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
+    }
+    DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
+    if (use_x) return;
+  }
+  sgd_step(P, G, M, b_.n_params, sa, sh1, b_.step_ctr, cs_);
 }
 
 void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, int ch0, int ch1) {

@@ -153,6 +153,9 @@ struct EngineBuffers {
   long bucket0_off, bucket0_n, bucket1_off, bucket1_n;
   // bf16 shadows
   bf16_t *w2_bf16, *w2t_bf16, *wfc_bf16, *wfc_frag;  // wfc_frag: FCFRAG order (conv2 fwd FC epilogue)
+  // exact-fp32 engine (EngineConfig::f32): fp32 activations and the conv2 weight's
+  // [tap][ci][co] fp32 copy (the data-gradient operand); the bf16 buffers are unused
+  float *a2_f32 = nullptr, *dz2_f32 = nullptr, *w2t_f32 = nullptr;
   // activations / scratch (sized for max batch)
   bf16_t *a1, *a2, *dz2, *dz1;
   float *fc_part, *dlogits, *loss_rows, *loss_hist, *w2slab, *w1slab;
@@ -184,6 +187,9 @@ struct EngineConfig {
   // forward also stores a1 (own pixels) and the dgrad role reads its ReLU mask from it;
   // 2 = the wgrad role reads a1 tiles too
   int store_a1 = 0;
+  // 1: exact fp32 operands everywhere (v_mfma_f32_16x16x4_f32 conv2, fp32 fc, fp32
+  //    activations), the reference's precision; needs fuse_level 1 and store_a1 0
+  int f32 = 0;
 };
 
 class SimpleCNNEngine {
@@ -210,6 +216,7 @@ class SimpleCNNEngine {
 
  private:
   void launch_step(int batch, int batch_stride, bool first_momentum_step);
+  void launch_step_f32(int batch, int batch_stride, bool first_momentum_step);
   EngineConfig cfg_;
   EngineBuffers b_;
   std::shared_ptr<Comm> comm_;

@@ -58,6 +58,10 @@ class EngineOptions:
     # reduce in the same order); "tune" = time two-shot, two-shot + one-shot and RCCL on
     # the node and keep the fastest; "xgmi2" / "xgmi1" = that plan, forced; "rccl" = RCCL
     comm: str = "auto"
+    # compute precision: "bf16" (bf16 MFMA operands, fp32 master weights / gradients /
+    # optimizer) or "fp32" (exact fp32 operands on v_mfma_f32_16x16x4_f32 - the
+    # reference's precision; always the level-1 kernel chain)
+    dtype: str = "bf16"
 
 
 class FusedSimpleCNNEngine:
@@ -84,19 +88,28 @@ class FusedSimpleCNNEngine:
         self.sampler = ShardedSampler(len(data), world_size, rank, shuffle=True, seed=seed)
         n_rank = len(self.sampler)
         B, HW = self.B, 28 * 28
-        R = self.wgrad_rows = self.opts.wgrad_rows or wgrad_rows(28, B)
+        if self.opts.dtype not in ("bf16", "fp32"):
+            raise ValueError(f"engine dtype must be bf16 or fp32, got {self.opts.dtype!r}")
+        f32 = self.opts.dtype == "fp32"
+        if f32 and (self.opts.fuse_level != 1 or self.opts.store_a1 != 0):
+            raise ValueError("the fp32 engine runs the level-1 chain (fuse_level 1, store_a1 0)")
+        R = self.wgrad_rows = self.opts.wgrad_rows or wgrad_rows(28, B, torch.float32 if f32 else BF16)
         g = self.opt.param_groups[0]
         if g["momentum"] != 0 and self.opt.momentum_buffer is None:
             self.opt.momentum_buffer = torch.zeros_like(fs.params)
         e = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
         self.steps_per_epoch = math.ceil(n_rank / B)
+        if f32:  # fp32 activations + the conv2 weight's fp32 [tap][ci][co] copy; no bf16 buffers
+            act = dict(a2=e(B * HW * 64), dz2=e(B * HW * 64), w2t_f32=e(64 * 9 * 32))
+        else:
+            act = dict(w2_bf16=e(64 * 9 * 32, dt=BF16), w2t_bf16=e(64 * 9 * 32, dt=BF16),
+                       wfc_bf16=e(10 * HW * 64, dt=BF16), wfc_frag=e(10 * HW * 64, dt=BF16),
+                       a1=e(B * HW * 32, dt=BF16), a2=e(B * HW * 64, dt=BF16),
+                       dz2=e(B * HW * 64, dt=BF16), dz1=e(B * HW * 32, dt=BF16))
         self.t = dict(
             params=fs.params, grads=fs.grads,
             momentum=self.opt.momentum_buffer if self.opt.momentum_buffer is not None else e(1),
-            w2_bf16=e(64 * 9 * 32, dt=BF16), w2t_bf16=e(64 * 9 * 32, dt=BF16),
-            wfc_bf16=e(10 * HW * 64, dt=BF16), wfc_frag=e(10 * HW * 64, dt=BF16),
-            a1=e(B * HW * 32, dt=BF16), a2=e(B * HW * 64, dt=BF16),
-            dz2=e(B * HW * 64, dt=BF16), dz1=e(B * HW * 32, dt=BF16),
+            **act,
             fc_part=e(2 * self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_fwd) * 10),  # [blk][2][10]
             dlogits=e(B * 10), loss_rows=e(B),
             loss_hist=torch.zeros(self.steps_per_epoch + 1, device=dev),
@@ -115,7 +128,8 @@ class FusedSimpleCNNEngine:
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
-                   store_a1=int(self.opts.store_a1))
+                   store_a1=int(self.opts.store_a1), f32=f32)
+        self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
         self.xgmi_plan = None

@@ -63,6 +63,7 @@ class TrainOptions:
     num_classes: int = 1000           # resnet18
     dataset_size: int = 2048          # resnet18: synthetic images resident per rank
     graph_module: bool = False        # module path on GPU: capture each step in a hipGraph
+    dtype: str = "bf16"               # GPU compute precision: bf16 | fp32 (exact fp32 MFMA, reference precision)
 
 
 def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
@@ -79,11 +80,15 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
     if opts.seed is not None:
         torch.manual_seed(opts.seed)  # B15: reproducible init (rank 0's weights win anyway)
     if opts.model == "resnet18":
+        if on_gpu and opts.dtype != "bf16":
+            raise ValueError("resnet18 on the GPU runs bf16 MFMA kernels only (--dtype bf16)")
         model = resnet18(num_classes=opts.num_classes).to(device)
         if on_gpu and opts.engine == "fused" and rank == 0:
             print("Rank 0: resnet18 runs on the module path (the fused engine is SimpleCNN's)", flush=True)
     elif opts.model == "simplecnn":
-        model = SimpleCNN().to(device)
+        if opts.dtype not in ("bf16", "fp32"):
+            raise ValueError(f"--dtype must be bf16 or fp32, got {opts.dtype!r}")
+        model = SimpleCNN(compute_dtype=torch.float32 if opts.dtype == "fp32" else torch.bfloat16).to(device)
     else:
         raise ValueError(f"unknown model {opts.model!r}")
     fused = on_gpu and opts.engine == "fused" and opts.model == "simplecnn"
@@ -131,7 +136,7 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
 
         comm = native_comm() if world_size > 1 and dist.get_backend() == "nccl" else None
         eo = EngineOptions(graph_steps=opts.graph_steps, bucket_cap_mb=opts.bucket_cap_mb,
-                           comm=opts.comm)
+                           comm=opts.comm, dtype=opts.dtype)
         if opts.fuse_level is not None:
             eo.fuse_level = opts.fuse_level
         engine = FusedSimpleCNNEngine(model, opt, ddata, batch_size, world_size, rank, comm, eo)

@@ -11,8 +11,10 @@ linear_nhwc          fc_partial + fc_reduce (split-K, fixed)     fc_bwd (dgrad+w
 cross_entropy        xent (softmax-xent fwd+bwd fused)           scale of the saved dlogits
 ===================  ==========================================  ==============================
 
-Activations are NHWC bf16; weights fp32 masters in native layouts (see
-``models/layers.py``) converted to bf16 on the fly for the MFMA operands.
+Activations are NHWC in the compute dtype: bf16 (default; fp32 masters converted to bf16
+on the fly for the MFMA operands) or fp32 (``dtype=torch.float32``: exact-fp32 MFMA
+``v_mfma_f32_16x16x4_f32`` conv2, fp32 fc, the reference's precision - the weights are
+read as they are).
 These functions require CUDA tensors and the native extension: there is no
 silent PyTorch fallback on the GPU.
 """
@@ -29,13 +31,14 @@ def _C():
     return native.require()
 
 
-def wgrad_rows(H: int, B: int) -> int:
+def wgrad_rows(H: int, B: int, dtype=BF16) -> int:
     """Rows per wgrad block: the largest chunk that still gives >= 128 split-K blocks.
 
     Fewer, fatter blocks mean fewer fp32 slab rows to write and re-read; 128 blocks
-    keep half the CUs busy.  LDS bounds R at 14 for a 28x28x(32,64) layer.
+    keep half the CUs busy.  LDS bounds R at 14 for a 28x28x(32,64) layer in bf16 and at
+    7 in fp32 (twice the bytes per staged element).
     """
-    for R in (14, 7, 4, 2, 1):
+    for R in ((14, 7, 4, 2, 1) if dtype == BF16 else (7, 4, 2, 1)):
         if R <= H and B * ((H + R - 1) // R) >= 128:
             return R
     return 1
@@ -43,12 +46,12 @@ def wgrad_rows(H: int, B: int) -> int:
 
 class _Conv1ReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, dtype=BF16):
         B = x.shape[0]
         H, W = x.shape[-2], x.shape[-1]
         Cout = b.numel()
         xf = x.reshape(B, H * W).float().contiguous()
-        y = torch.empty(B, H, W, Cout, dtype=BF16, device=x.device)
+        y = torch.empty(B, H, W, Cout, dtype=dtype, device=x.device)
         _C().conv1_fwd(xf, None, None, 0, 0, w.contiguous(), b.contiguous(), y, B, H, W)
         ctx.save_for_backward(xf, y, w)
         ctx.dims = (B, H, W, Cout, tuple(x.shape))
@@ -58,7 +61,7 @@ class _Conv1ReLU(torch.autograd.Function):
     def backward(ctx, gy):
         xf, y, w = ctx.saved_tensors
         B, H, W, Cout, xshape = ctx.dims
-        gy = gy.to(BF16).contiguous()
+        gy = gy.to(y.dtype).contiguous()
         chunk = 256
         nblk = _C().conv1_wgrad_blocks(B, H, W, chunk)
         slab = torch.empty(nblk, Cout * 10, dtype=torch.float32, device=gy.device)
@@ -72,17 +75,17 @@ class _Conv1ReLU(torch.autograd.Function):
             dz = (gy.float() * (y.float() > 0)).permute(0, 3, 1, 2)
             gx = torch.nn.functional.conv_transpose2d(dz, w.permute(0, 3, 1, 2), padding=1)
             gx = gx.reshape(xshape)
-        return gx, gw.view(Cout, 3, 3, 1), gb
+        return gx, gw.view(Cout, 3, 3, 1), gb, None
 
 
 class _Conv3x3ReLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, relu):
+    def forward(ctx, x, w, b, relu, dtype=BF16):
         B, H, W, Cin = x.shape
         Cout = w.shape[0]
-        xb = x.to(BF16).contiguous()
-        wb = w.to(BF16).contiguous()
-        y = torch.empty(B, H, W, Cout, dtype=BF16, device=x.device)
+        xb = x.to(dtype).contiguous()
+        wb = w.to(dtype).contiguous()
+        y = torch.empty(B, H, W, Cout, dtype=dtype, device=x.device)
         _C().conv3x3_fwd(xb, wb, b.contiguous(), y, bool(relu), None, None, 0, 2)
         ctx.save_for_backward(xb, wb, y)
         ctx.relu = bool(relu)
@@ -93,14 +96,14 @@ class _Conv3x3ReLU(torch.autograd.Function):
         xb, wb, y = ctx.saved_tensors
         B, H, W, Cin = xb.shape
         Cout = wb.shape[0]
-        gy = gy.to(BF16).contiguous()
+        gy = gy.to(xb.dtype).contiguous()
         yact = y if ctx.relu else None
         dx = None
         if ctx.needs_input_grad[0]:
             wt = wb.view(Cout, 9, Cin).permute(1, 2, 0).contiguous()  # [tap][ci][co]
             dx = torch.empty_like(xb)
             _C().conv3x3_dgrad(gy, yact, wt, None, dx, 2)
-        R = wgrad_rows(H, B)
+        R = wgrad_rows(H, B, xb.dtype)
         nblk = _C().conv3x3_wgrad_blocks(B, H, R)
         row = Cout * 9 * Cin + Cout
         slab = torch.empty(nblk, row, dtype=torch.float32, device=gy.device)
@@ -109,16 +112,16 @@ class _Conv3x3ReLU(torch.autograd.Function):
         gb = torch.empty(Cout, dtype=torch.float32, device=gy.device)
         _C().grad_reduce([(slab, row, 0, Cout * 9 * Cin, nblk, gw, 1.0),
                           (slab, row, Cout * 9 * Cin, Cout, nblk, gb, 1.0)])
-        return dx, gw.view(Cout, 3, 3, Cin), gb, None
+        return dx, gw.view(Cout, 3, 3, Cin), gb, None, None
 
 
 class _LinearNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, dtype=BF16):
         B, H, W, C = x.shape
         NO = w.shape[0]
-        xb = x.to(BF16).contiguous()
-        wb = w.to(BF16).contiguous()
+        xb = x.to(dtype).contiguous()
+        wb = w.to(dtype).contiguous()
         G = (H * W) // 16
         part = torch.empty(B, G, NO, dtype=torch.float32, device=x.device)
         _C().fc_partial(xb, wb, part)
@@ -136,7 +139,7 @@ class _LinearNHWC(torch.autograd.Function):
         dw = torch.empty(wb.shape, dtype=torch.float32, device=go.device)
         _C().fc_bwd(go, xb, wb, dx, dw, 1.0, False)
         db = go.sum(0) if ctx.has_bias else None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _CrossEntropy(torch.autograd.Function):
@@ -156,16 +159,16 @@ class _CrossEntropy(torch.autograd.Function):
         return dl * g, None
 
 
-def conv1_relu(x, w, b):
-    return _Conv1ReLU.apply(x, w, b)
+def conv1_relu(x, w, b, dtype=BF16):
+    return _Conv1ReLU.apply(x, w, b, dtype)
 
 
-def conv3x3_relu(x, w, b, relu=True):
-    return _Conv3x3ReLU.apply(x, w, b, relu)
+def conv3x3_relu(x, w, b, relu=True, dtype=BF16):
+    return _Conv3x3ReLU.apply(x, w, b, relu, dtype)
 
 
-def linear_nhwc(x, w, b):
-    return _LinearNHWC.apply(x, w, b)
+def linear_nhwc(x, w, b, dtype=BF16):
+    return _LinearNHWC.apply(x, w, b, dtype)
 
 
 def cross_entropy(logits, labels):

@@ -14,6 +14,11 @@ def bf16r(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.bfloat16).float()
 
 
+def _f(t: torch.Tensor) -> torch.Tensor:
+    """fp32 view of ``t`` - float64 stays float64 (the exact-fp32 path's oracle)."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
 def nhwc_to_nchw(x):
     return x.permute(0, 3, 1, 2)
 
@@ -43,8 +48,8 @@ def conv3x3_dgrad(dy_nhwc, w_ohwi):
 
 def conv3x3_wgrad(dy_nhwc, x_nhwc):
     """(dW OHWI, db) of a 3x3/s1/p1 conv."""
-    x = nhwc_to_nchw(x_nhwc).float()
-    dy = nhwc_to_nchw(dy_nhwc).float()
+    x = _f(nhwc_to_nchw(x_nhwc))
+    dy = _f(nhwc_to_nchw(dy_nhwc))
     cin, cout = x.shape[1], dy.shape[1]
     dw = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), dy, padding=1)
     return dw.permute(0, 2, 3, 1).contiguous(), dy.sum(dim=(0, 2, 3))
@@ -52,22 +57,22 @@ def conv3x3_wgrad(dy_nhwc, x_nhwc):
 
 def conv1_wgrad(dz_nhwc, x):
     """(dW [Cout,3,3,1], db) of conv1 given its pre-activation gradient dZ (NHWC)."""
-    dy = nhwc_to_nchw(dz_nhwc).float()
-    dw = torch.nn.grad.conv2d_weight(x.unsqueeze(1).float(), (dy.shape[1], 1, 3, 3), dy, padding=1)
+    dy = _f(nhwc_to_nchw(dz_nhwc))
+    dw = torch.nn.grad.conv2d_weight(_f(x.unsqueeze(1)), (dy.shape[1], 1, 3, 3), dy, padding=1)
     return dw.permute(0, 2, 3, 1).contiguous(), dy.sum(dim=(0, 2, 3))
 
 
 def fc_nhwc(x_nhwc, w_native, b):
     """logits = flatten_nhwc(x) @ w_native.reshape(out,-1).T + b."""
     B = x_nhwc.shape[0]
-    return x_nhwc.reshape(B, -1).float() @ w_native.reshape(w_native.shape[0], -1).float().t() + b
+    return _f(x_nhwc.reshape(B, -1)) @ _f(w_native.reshape(w_native.shape[0], -1)).t() + b
 
 
 def fc_bwd(dl, x_nhwc, w_native, mask=True):
     """(dX NHWC [masked by X>0], dW native) of fc_nhwc."""
     B = x_nhwc.shape[0]
-    xf = x_nhwc.reshape(B, -1).float()
-    wf = w_native.reshape(w_native.shape[0], -1).float()
+    xf = _f(x_nhwc.reshape(B, -1))
+    wf = _f(w_native.reshape(w_native.shape[0], -1))
     dx = dl @ wf
     if mask:
         dx = dx * (xf > 0)
@@ -77,7 +82,7 @@ def fc_bwd(dl, x_nhwc, w_native, mask=True):
 
 def cross_entropy(logits, labels):
     """(mean loss, dlogits = (softmax - onehot)/B)."""
-    lp = torch.log_softmax(logits.float(), dim=1)
+    lp = torch.log_softmax(_f(logits), dim=1)
     loss = F.nll_loss(lp, labels)
     d = lp.exp()
     d[torch.arange(logits.shape[0]), labels] -= 1.0
@@ -105,6 +110,29 @@ def simple_cnn_step_bf16(params: dict, x: torch.Tensor, labels: torch.Tensor, ws
     dw2, db2 = conv3x3_wgrad(dz2, a1)
     dz1 = bf16r(conv3x3_dgrad(dz2, w2b)) * (a1 > 0)
     dw1, db1 = conv1_wgrad(dz1, x.float())
+    s = 1.0 / ws
+    return loss, {"w1": dw1 * s, "b1": db1 * s, "w2": dw2 * s, "b2": db2 * s,
+                  "wfc": dwfc * s, "bfc": dl.sum(0) * s}
+
+
+def simple_cnn_step_exact(params: dict, x: torch.Tensor, labels: torch.Tensor, ws: int = 1,
+                          dtype: torch.dtype = torch.float64):
+    """The same step without any bf16 rounding, evaluated in ``dtype`` (float64 by
+    default): the oracle of the exact-fp32 path (``--dtype fp32``), whose MFMA results
+    are plain fp32 fma chains.  Same arguments / returns as :func:`simple_cnn_step_bf16`."""
+    B = x.shape[0]
+    p = {k: v.to(dtype) for k, v in params.items()}
+    w1, b1, w2, b2, wfc, bfc = p["w1"], p["b1"], p["w2"], p["b2"], p["wfc"], p["bfc"]
+    x = x.to(dtype)
+    a1 = conv1_relu(x, w1, b1)
+    a2 = conv3x3(a1, w2, b2, relu=True)
+    logits = fc_nhwc(a2, wfc, bfc)
+    loss, dl = cross_entropy(logits, labels)
+    dz2 = (dl @ wfc.reshape(wfc.shape[0], -1)).view_as(a2) * (a2 > 0)
+    dwfc = (dl.t() @ a2.reshape(B, -1)).view_as(wfc)
+    dw2, db2 = conv3x3_wgrad(dz2, a1)
+    dz1 = conv3x3_dgrad(dz2, w2) * (a1 > 0)
+    dw1, db1 = conv1_wgrad(dz1, x)
     s = 1.0 / ws
     return loss, {"w1": dw1 * s, "b1": db1 * s, "w2": dw2 * s, "b2": db2 * s,
                   "wfc": dwfc * s, "bfc": dl.sum(0) * s}

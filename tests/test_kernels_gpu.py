@@ -290,7 +290,9 @@ def test_simple_cnn_module_path_matches_references():
     loss_g.backward()
     assert abs(loss_g.item() - loss_c.item()) < 2e-2
     for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
-        relclose(pg.grad, pc.grad, 1.5e-1)  # bf16 activations vs fp32: loose by construction
+        # bf16 operands vs the fp32 model: the float64 comparison of the two rounding models
+        # (ops/reference.py simple_cnn_step_bf16 vs _exact) differs by ~3e-2 on conv grads
+        relclose(pg.grad, pc.grad, 3e-2)
     p = {k: v.cpu() for k, v in _native_params(gpu).items()}
     loss_e, ge = R.simple_cnn_step_bf16(p, x.view(16, 28, 28), y)
     assert abs(loss_g.item() - loss_e.item()) < 1e-4

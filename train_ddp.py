@@ -31,6 +31,9 @@ def parse_args(argv=None):
     p.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto",
                    help="gpu: fail unless a HIP device is usable; cpu: gloo plumbing run; auto: the GPU "
                         "when usable, CPU only on a host without one (never a silent fallback on a GPU host)")
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                   help="GPU compute precision: bf16 MFMA operands (fp32 masters/grads/optimizer) or "
+                        "exact fp32 MFMA (the reference's fp32 nn.Conv2d/nn.Linear precision)")
     p.add_argument("--engine", choices=["fused", "module"], default="fused",
                    help="GPU step: fused native engine (hipGraph) or module path (autograd)")
     p.add_argument("--data", choices=["auto", "mnist", "synthetic"], default="auto",
@@ -76,7 +79,7 @@ def parse_args(argv=None):
 def main(argv=None):
     a = parse_args(argv)
     opts = TrainOptions(lr=a.lr, momentum=a.momentum, weight_decay=a.weight_decay,
-                        backend=a.backend, device=a.device, engine=a.engine, data=a.data, data_root=a.data_root,
+                        backend=a.backend, device=a.device, engine=a.engine, dtype=a.dtype, data=a.data, data_root=a.data_root,
                         checkpoint_dir=a.checkpoint_dir, save=not a.no_save, seed=a.seed,
                         log_every=a.log_every, graph_steps=a.graph_steps,
                         bucket_cap_mb=a.bucket_cap_mb, num_workers=a.num_workers,
