@@ -289,10 +289,20 @@ def test_simple_cnn_module_path_matches_references():
     loss_g = CrossEntropyLoss()(gpu(x.to(dev)), y.to(dev))
     loss_g.backward()
     assert abs(loss_g.item() - loss_c.item()) < 2e-2
+    # bf16-justified bound: the bf16 rounding model itself (ops/reference.py
+    # simple_cnn_step_bf16, float math) deviates from the exact step (simple_cnn_step_exact,
+    # float64) by e_k per parameter (measured here: 4.8e-2 / 5.5e-2 on conv1 w / b, 3e-3 on
+    # fc); the HIP path may deviate from the fp32 model by at most 1.25 e_k + 1e-3.
+    # (The exact-fp32 path is held to 1e-4: tests/test_fp32_gpu.py.)
+    pe = {k: v.detach().cpu() for k, v in _native_params(cpu).items()}
+    _, g_b = R.simple_cnn_step_bf16(pe, x.view(16, 28, 28), y)
+    _, g_x = R.simple_cnn_step_exact(pe, x.view(16, 28, 28), y)
+    key = {"net.0.weight": "w1", "net.0.bias": "b1", "net.2.weight": "w2", "net.2.bias": "b2",
+           "fl.weight": "wfc", "fl.bias": "bfc"}
     for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
-        # bf16 operands vs the fp32 model: the float64 comparison of the two rounding models
-        # (ops/reference.py simple_cnn_step_bf16 vs _exact) differs by ~3e-2 on conv grads
-        relclose(pg.grad, pc.grad, 3e-2)
+        k = key[n]
+        e_k = ((g_b[k].double() - g_x[k]).norm() / g_x[k].norm()).item()
+        relclose(pg.grad, pc.grad, 1.25 * e_k + 1e-3)
     p = {k: v.cpu() for k, v in _native_params(gpu).items()}
     loss_e, ge = R.simple_cnn_step_bf16(p, x.view(16, 28, 28), y)
     assert abs(loss_g.item() - loss_e.item()) < 1e-4
