@@ -162,6 +162,9 @@ def main():
                     help="control-plane process group (nccl = RCCL); gloo + --comm xgmi rehearses "
                          "N ranks on ONE GPU (RCCL refuses duplicate GPUs)")
     ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--bucket_cap_mb", type=float, default=25.0,
+                    help="DDP bucket cap (torch rule: first bucket 1 MiB, then this cap)")
+    ap.add_argument("--first_bucket_mb", type=float, default=1.0)
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
                     help="compute precision: bf16 MFMA operands (default) or exact fp32 MFMA (the "
                          "reference's precision)")
@@ -231,7 +234,8 @@ def main():
     imgs, labels = synthetic_mnist()
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
     k = args.graph_steps or graph_chunk(args.steps)
-    eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=args.dtype)
+    eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=args.dtype,
+                       bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
     eo.comm = args.comm
     for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1"):
         if getattr(args, f) is not None:

@@ -823,10 +823,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              auto O = [&](const char* k) { return offs[k].cast<long>(); };
              b.off_w1 = O("w1"); b.off_b1 = O("b1"); b.off_w2 = O("w2"); b.off_b2 = O("b2");
              b.off_wfc = O("wfc"); b.off_bfc = O("bfc");
-             b.bucket0_off = O("bucket0_off"); b.bucket0_n = O("bucket0_n");
-             b.bucket1_off = O("bucket1_off"); b.bucket1_n = O("bucket1_n");
+             std::vector<EngineBucket> buckets;
+             for (auto item : offs["buckets"].cast<py::list>()) {
+               auto pr = item.cast<std::pair<long, long>>();
+               buckets.push_back(EngineBucket{pr.first, pr.second});
+             }
              TORCH_CHECK(b.off_wfc + (long)c.NO * HW * c.C2 <= b.n_params && b.off_w1 + 9L * c.C1 <= b.n_params &&
-                         b.bucket0_off + b.bucket0_n <= b.n_params && b.bucket1_off + b.bucket1_n <= b.n_params,
+                         b.off_b2 + c.C2 <= b.n_params && b.off_w2 + 9L * c.C1 * c.C2 <= b.n_params,
                          "engine: parameter offsets out of range");
              TORCH_CHECK(fc_bwd_lds(c.max_batch, c.NO, true) <= 160 * 1024, "engine: batch too large for fc_bwd LDS");
              if (c.f32) {  // exact fp32: fp32 activations + the conv2 weight's fp32 [tap][ci][co] copy
@@ -862,7 +865,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.n_idx = (int)idx.numel();
              b.n_rows = (int)std::min<long>(images.numel() / HW, labels.numel());
              TORCH_CHECK(conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, true, es) <= 160 * 1024, "wgrad rows too large");
-             return std::make_shared<SimpleCNNEngine>(c, b, comm);
+             return std::make_shared<SimpleCNNEngine>(c, b, comm, buckets);
            }),
            py::arg("config"), py::arg("tensors"), py::arg("offsets"), py::arg("comm") = nullptr)
       .def("step", &SimpleCNNEngine::step, py::arg("batch"), py::arg("batch_stride"))
@@ -873,7 +876,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("destroy_graph", &SimpleCNNEngine::destroy_graph)
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
-      .def("set_xgmi", &SimpleCNNEngine::set_xgmi, py::arg("xgmi"), py::arg("ch0") = 0, py::arg("ch1") = 1)
+      .def("set_xgmi", &SimpleCNNEngine::set_xgmi, py::arg("xgmi"), py::arg("channels"))
+      .def_property_readonly("num_buckets", &SimpleCNNEngine::num_buckets)
+      .def("bucket_stage", &SimpleCNNEngine::bucket_stage)
       .def_property_readonly("graph_steps", &SimpleCNNEngine::graph_steps)
       .def_property_readonly("stream", [](SimpleCNNEngine& e) { return (uint64_t)e.stream(); });
 }

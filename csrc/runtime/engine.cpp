@@ -29,13 +29,15 @@
 //
 // Buckets follow the reference DDP's rebuilt layout:
 // bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB).
+#include <algorithm>
+
 #include "runtime/runtime.h"
 
 namespace ddp_amd {
 
 SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& buf,
-                                 std::shared_ptr<Comm> comm)
-    : cfg_(cfg), b_(buf), comm_(std::move(comm)) {
+                                 std::shared_ptr<Comm> comm, std::vector<EngineBucket> buckets)
+    : cfg_(cfg), b_(buf), comm_(std::move(comm)), buckets_(std::move(buckets)) {
   if (cfg_.C1 != 32) throw std::runtime_error("engine: fused conv1 wgrad needs C1 == 32");
   if (cfg_.C2 % 64 != 0) throw std::runtime_error("engine: C2 must be a multiple of 64");
   if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
@@ -44,6 +46,20 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
     throw std::runtime_error("engine: fp32 mode needs fuse_level 1 and store_a1 0");
   if (cfg_.f32 && !(b_.a2_f32 && b_.dz2_f32 && b_.w2t_f32))
     throw std::runtime_error("engine: fp32 mode needs the a2 / dz2 / w2t fp32 buffers");
+  // bucket plan: in-range, ordered, non-overlapping; stage by the first conv gradient
+  const long conv0 = std::min(std::min(b_.off_w2, b_.off_b2), std::min(b_.off_w1, b_.off_b1));
+  const long fc_hi = std::max(b_.off_wfc + (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, b_.off_bfc + cfg_.NO);
+  if (fc_hi > conv0) throw std::runtime_error("engine: fc gradients must precede the conv gradients");
+  long prev_end = 0;
+  for (const EngineBucket& bk : buckets_) {
+    if (bk.n <= 0 || bk.off < prev_end || bk.off + bk.n > b_.n_params)
+      throw std::runtime_error("engine: bucket plan out of range / overlapping / unordered");
+    prev_end = bk.off + bk.n;
+    stage_.push_back(bk.off + bk.n <= conv0 ? 0 : 1);
+  }
+  last_bucket_ = (int)buckets_.size() - 1;
+  for (int s : stage_) stage_used_[s] = true;
+  xch_.assign(buckets_.size(), -1);
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
@@ -174,21 +190,15 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // (fused optimizer: the fc weight gradient is consumed in registers and not stored)
   fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
          (long)HW * C2, NO, /*mask=*/true, cs_, ex);
-  if (dist) {
-    DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
-    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
-    if (use_x) {
-      // SGD of bucket 0 (fc weight + bias) fused into the all-gather: no optimizer kernel
-      ShadowSet sh0{};
-      sh0.r[0] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
-      sh0.r[1] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
-      sh0.count = 2;
-      xgmi_->all_reduce_sgd(xch_[0], ms_, sa, P, M, sh0, nullptr);
-    } else {
-      comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
-    }
-    DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
-  }
+  // every bf16 shadow; a bucket's fused SGD refreshes the ones inside its range
+  ShadowSet sh_all{};
+  sh_all.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
+  sh_all.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
+  sh_all.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
+  sh_all.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+  sh_all.count = 4;
+  // fc-only buckets: all-reduce (and, over xGMI, the fused SGD) overlaps the conv backward
+  if (dist) launch_buckets(0, use_x, sa, M, sh_all);
   // ---- conv backward (bucket 1)
   if (f1) {
     // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
@@ -230,30 +240,33 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   grad_reduce(ss, cs_);
   if (fopt) return;
   if (dist) {
-    DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
-    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
-    if (use_x) {
-      ShadowSet sh1{};
-      sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
-      sh1.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
-      sh1.count = 2;
-      xgmi_->all_reduce_sgd(xch_[1], ms_, sa, P, M, sh1, b_.step_ctr);  // the step's last kernel
-    } else {
-      comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
-    }
-    DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
-    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
-    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
+    launch_buckets(1, use_x, sa, M, sh_all);
+    join_buckets();
     if (use_x) return;  // the optimizer ran inside the all-reduces
   }
   // ---- optimizer + bf16 shadows + next batch window
-  ShadowSet sh{};
-  sh.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
-  sh.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
-  sh.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
-  sh.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
-  sh.count = 4;
-  sgd_step(P, G, M, b_.n_params, sa, sh, b_.step_ctr, cs_);
+  sgd_step(P, G, M, b_.n_params, sa, sh_all, b_.step_ctr, cs_);
+}
+
+void SimpleCNNEngine::launch_buckets(int stage, bool use_x, const SgdArgs& sa, float* M, const ShadowSet& sh) {
+  if (!stage_used_[stage]) return;
+  hipEvent_t ready = stage == 0 ? e_b0_ : e_b1_;
+  DDP_HIP_CHECK(hipEventRecord(ready, cs_));
+  DDP_HIP_CHECK(hipStreamWaitEvent(ms_, ready, 0));
+  for (int b = 0; b < (int)buckets_.size(); ++b) {
+    if (stage_[b] != stage) continue;
+    if (use_x) {
+      xgmi_->all_reduce_sgd(xch_[b], ms_, sa, b_.params, M, sh, b == last_bucket_ ? b_.step_ctr : nullptr);
+    } else {
+      comm_->all_reduce(b_.grads + buckets_[b].off, (size_t)buckets_[b].n, 0, 0, ms_);
+    }
+  }
+  DDP_HIP_CHECK(hipEventRecord(stage == 0 ? e_d0_ : e_d1_, ms_));
+}
+
+void SimpleCNNEngine::join_buckets() {
+  // the comm stream is in order: its last recorded event covers every earlier bucket
+  DDP_HIP_CHECK(hipStreamWaitEvent(cs_, stage_used_[1] ? e_d1_ : e_d0_, 0));
 }
 
 // The exact-fp32 step: same kernel chain as level 1 (conv2 fwd + fused fc partials with
@@ -315,17 +328,10 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   }
   fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
          (long)HW * C2, NO, /*mask=*/true, cs_, ex);
-  if (dist) {
-    DDP_HIP_CHECK(hipEventRecord(e_b0_, cs_));
-    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b0_, 0));
-    if (use_x) {
-      ShadowSet none{};
-      xgmi_->all_reduce_sgd(xch_[0], ms_, sa, P, M, none, nullptr);
-    } else {
-      comm_->all_reduce(G + b_.bucket0_off, (size_t)b_.bucket0_n, 0, 0, ms_);
-    }
-    DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
-  }
+  ShadowSet sh1{};
+  sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
+  sh1.count = 1;
+  if (dist) launch_buckets(0, use_x, sa, M, sh1);
   // ---- conv backward (bucket 1)
   conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
               cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr), false, cs_);
@@ -357,35 +363,29 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   ss.sys_store = use_x ? 1 : 0;
   grad_reduce(ss, cs_);
   if (fopt) return;
-  ShadowSet sh1{};
-  sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
-  sh1.count = 1;
   if (dist) {
-    DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
-    DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
-    if (use_x) {
-      xgmi_->all_reduce_sgd(xch_[1], ms_, sa, P, M, sh1, b_.step_ctr);
-    } else {
-      comm_->all_reduce(G + b_.bucket1_off, (size_t)b_.bucket1_n, 0, 0, ms_);
-    }
-    DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
-    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
-    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
+    launch_buckets(1, use_x, sa, M, sh1);
+    join_buckets();
     if (use_x) return;
   }
   sgd_step(P, G, M, b_.n_params, sa, sh1, b_.step_ctr, cs_);
 }
 
-void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, int ch0, int ch1) {
+void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> channels) {
   if (x) {
-    if (ch0 < 0 || ch1 < 0 || ch0 >= x->channels() || ch1 >= x->channels() || ch0 == ch1)
-      throw std::runtime_error("engine: xgmi channel indices (one per bucket) out of range");
+    if (channels.size() != buckets_.size())
+      throw std::runtime_error("engine: one xgmi channel per bucket required");
+    for (size_t i = 0; i < channels.size(); ++i) {
+      if (channels[i] < 0 || channels[i] >= x->channels())
+        throw std::runtime_error("engine: xgmi channel index out of range");
+      for (size_t j = 0; j < i; ++j)
+        if (channels[j] == channels[i]) throw std::runtime_error("engine: xgmi channels must be distinct");
+    }
     if (x->world() != cfg_.world) throw std::runtime_error("engine: xgmi world size mismatch");
   }
   destroy_graph();
   xgmi_ = std::move(x);
-  xch_[0] = ch0;
-  xch_[1] = ch1;
+  xch_ = xgmi_ ? channels : std::vector<int>(buckets_.size(), -1);
 }
 
 void SimpleCNNEngine::step(int batch, int batch_stride) {

@@ -149,8 +149,6 @@ struct EngineBuffers {
   float* momentum;  // may be null (momentum == 0)
   long n_params;
   long off_w1, off_b1, off_w2, off_b2, off_wfc, off_bfc;
-  // gradient buckets (reference rebuilt order: [fl.*], [net.2.*, net.0.*])
-  long bucket0_off, bucket0_n, bucket1_off, bucket1_n;
   // bf16 shadows
   bf16_t *w2_bf16, *w2t_bf16, *wfc_bf16, *wfc_frag;  // wfc_frag: FCFRAG order (conv2 fwd FC epilogue)
   // exact-fp32 engine (EngineConfig::f32): fp32 activations and the conv2 weight's
@@ -192,9 +190,18 @@ struct EngineConfig {
   int f32 = 0;
 };
 
+// Gradient bucket of the engine's data plane: a [off, off + n) range of the flat gradient
+// buffer.  Any plan works (DDP's bucket_cap_mb rule, sub-parameter chunks): a bucket is
+// all-reduced as soon as every gradient in it is final - right after fc_bwd when it lies
+// inside the fc parameters (overlapping the conv backward), after grad_reduce otherwise.
+struct EngineBucket {
+  long off, n;
+};
+
 class SimpleCNNEngine {
  public:
-  SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& buf, std::shared_ptr<Comm> comm);
+  SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& buf, std::shared_ptr<Comm> comm,
+                  std::vector<EngineBucket> buckets);
   ~SimpleCNNEngine();
   // eager launches of one full training step on the engine's compute stream
   void step(int batch, int batch_stride);
@@ -209,19 +216,31 @@ class SimpleCNNEngine {
   hipStream_t stream() const { return cs_; }
   void synchronize();
   void set_momentum_started(bool v) { momentum_started_ = v; }
-  // bucket all-reduces over the direct xGMI kernel (channel 0 = bucket 0, 1 = bucket 1)
-  // instead of RCCL; set before capturing a graph
-  // bucket all-reduces over the direct xGMI kernel: channel ch0 for bucket 0, ch1 for bucket 1
-  void set_xgmi(std::shared_ptr<XgmiComm> x, int ch0 = 0, int ch1 = 1);
+  // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
+  // bucket b; set before capturing a graph
+  void set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> channels);
+  int num_buckets() const { return (int)buckets_.size(); }
+  int bucket_stage(int b) const { return stage_.at(b); }
 
  private:
   void launch_step(int batch, int batch_stride, bool first_momentum_step);
   void launch_step_f32(int batch, int batch_stride, bool first_momentum_step);
+  // enqueue the all-reduces of the buckets of `stage` (0: after fc_bwd, 1: after
+  // grad_reduce) on the comm stream behind an event of the compute stream; with xGMI the
+  // optimizer (+ the shadows in `sh`) runs inside each bucket's all-gather and the last
+  // bucket of the step advances the step counter
+  void launch_buckets(int stage, bool use_x, const SgdArgs& sa, float* M, const ShadowSet& sh);
+  // compute stream waits for every launched stage
+  void join_buckets();
   EngineConfig cfg_;
   EngineBuffers b_;
   std::shared_ptr<Comm> comm_;
   std::shared_ptr<XgmiComm> xgmi_;
-  int xch_[2] = {0, 1};
+  std::vector<EngineBucket> buckets_;
+  std::vector<int> stage_;  // 0: final after fc_bwd, 1: after grad_reduce
+  std::vector<int> xch_;    // xGMI channel of each bucket
+  int last_bucket_ = -1;    // the step's last collective (advances the step counter)
+  bool stage_used_[2] = {false, false};
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_;
   hipGraph_t graph_ = nullptr;

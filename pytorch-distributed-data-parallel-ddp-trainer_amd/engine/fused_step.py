@@ -42,6 +42,7 @@ class EngineOptions:
     pxt_dgrad: int = 2
     wgrad_rows: int | None = None
     bucket_cap_mb: float = 25.0
+    first_bucket_mb: float = 1.0   # torch DDP's first-bucket cap (the rest use bucket_cap_mb)
     force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
     # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd)
@@ -78,13 +79,12 @@ class FusedSimpleCNNEngine:
             raise RuntimeError("the fused engine runs on a HIP device")
         names = {"w1": "net.0.weight", "b1": "net.0.bias", "w2": "net.2.weight",
                  "b2": "net.2.bias", "wfc": "fl.weight", "bfc": "fl.bias"}
-        self.buckets = bucket_plan(fs, self.opts.bucket_cap_mb)
+        # any DDP bucket plan: each bucket's all-reduce starts as soon as its gradients are
+        # final (fc-only buckets right after fc_bwd, overlapping the conv backward)
+        self.buckets = bucket_plan(fs, self.opts.bucket_cap_mb, self.opts.first_bucket_mb)
         ranges = bucket_ranges(fs, self.buckets)
-        if len(ranges) != 2:
-            raise RuntimeError(f"expected the reference's 2 gradient buckets, got {self.buckets}")
         offs = {k: fs.offsets[v] for k, v in names.items()}
-        offs.update(bucket0_off=ranges[0][0], bucket0_n=ranges[0][1],
-                    bucket1_off=ranges[1][0], bucket1_n=ranges[1][1])
+        offs["buckets"] = [(int(o), int(n)) for o, n in ranges]
         self.sampler = ShardedSampler(len(data), world_size, rank, shuffle=True, seed=seed)
         n_rank = len(self.sampler)
         B, HW = self.B, 28 * 28
@@ -134,7 +134,7 @@ class FusedSimpleCNNEngine:
         self.xgmi = None
         self.xgmi_plan = None
         self.allreduce_us = None
-        xch = (0, 1)
+        xch = list(range(len(ranges)))
         if use_comm and self.opts.comm in ("auto", "tune", "xgmi", "xgmi1", "xgmi2"):
             from ..parallel.xgmi import channel_plan, create_xgmi, pick_data_plane
 
@@ -160,14 +160,14 @@ class FusedSimpleCNNEngine:
                     self.xgmi = None
                 else:
                     cp = channel_plan(len(ranges), oneshot)
-                    xch = tuple(cp[(b, plan == "xgmi1" and b in oneshot)] for b in range(len(ranges)))
+                    xch = [cp[(b, plan == "xgmi1" and b in oneshot)] for b in range(len(ranges))]
         if use_comm and self.xgmi is None and comm is None:
             raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
         self.comm_kind = (self.xgmi_plan or "xgmi") if self.xgmi is not None else ("rccl" if use_comm else "none")
         self.ranges, self.xch, self.comm = ranges, xch, (comm if use_comm else None)
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.xgmi is not None:
-            self.eng.set_xgmi(self.xgmi, *xch)
+            self.eng.set_xgmi(self.xgmi, xch)
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:
             self.eng.set_momentum_started(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)

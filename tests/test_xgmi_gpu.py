@@ -156,3 +156,63 @@ def test_engine_two_ranks_xgmi_identical_params(comm):
 
     res = _run(_engine_worker, 2, free_port(), comm)
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
+
+
+def _plan_worker(rank, world, port, q, cap_mb, first_mb, dtype):
+    try:
+        _init(rank, world, port)
+        import hashlib
+
+        from ddp_amd.data import DeviceMNIST, synthetic_mnist
+        from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+        from ddp_amd.models import SimpleCNN
+        from ddp_amd.models.layers import flat_space
+        from ddp_amd.ops import FusedSGD
+
+        torch.manual_seed(0)
+        model = SimpleCNN().cuda()
+        fs = flat_space(model)
+        opt = FusedSGD(model, lr=0.05, momentum=0.9)
+        imgs, labels = synthetic_mnist(4096)
+        eo = EngineOptions(graph_steps=4, comm="xgmi", bucket_cap_mb=cap_mb, first_bucket_mb=first_mb,
+                           dtype=dtype)
+        eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, torch.device("cuda", 0)),
+                                   16, world, rank, None, eo)
+        assert eng.comm_kind in ("xgmi", "xgmi1"), eng.comm_kind
+        nb = eng.eng.num_buckets
+        stages = [eng.eng.bucket_stage(b) for b in range(nb)]
+        eng.refresh()
+        eng.run_steps(10)
+        eng.synchronize()
+        p = fs.params.detach().cpu()
+        allp = [None] * world
+        dist.all_gather_object(allp, p)
+        same = all(torch.equal(allp[r], allp[0]) for r in range(world))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok" if same and torch.isfinite(p).all() else "ranks differ", nb, stages,
+               hashlib.sha256(p.numpy().tobytes()).hexdigest()))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, None, None))
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_engine_any_bucket_plan_bitwise(dtype):
+    """the fused engine takes ANY DDP bucket plan (--bucket_cap_mb):
+    2, 3, 4 and 6 buckets at 2 ranks.  Every bucket is all-reduced (with the fused SGD) as
+    soon as its gradients are final: fc-only buckets after fc_bwd, the rest after the conv
+    backward.  The xGMI sum order is per element (fixed rank order), so every plan must
+    give bit-identical parameters - across ranks and across plans."""
+    from ddp_amd.parallel import free_port
+
+    plans = [(25.0, 1.0, 2), (0.01, 1.0, 3), (0.05, 1e-6, 4), (1e-6, 1e-6, 6)]
+    digests = set()
+    for cap, first, want_nb in plans:
+        res = _run(_plan_worker, 2, free_port(), cap, first, dtype)
+        assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
+        nb, stages = res[0][2], res[0][3]
+        assert nb == want_nb, (cap, first, nb)
+        assert stages[0] == 0 and stages[-1] == 1, stages  # fc first, conv last
+        digests.add(res[0][4])
+        digests.add(res[1][4])
+    assert len(digests) == 1, "bucket plans changed the parameters"
