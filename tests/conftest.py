@@ -13,9 +13,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: multi-process / longer-running CPU test")
 
 
+# Multi-process GPU tests first: their ranks share the box's one GPU and spin on
+# cross-process barriers, which needs every rank's kernels resident at once.  Once this
+# process has run the in-process GPU tests it owns many (idle) HIP queues, and with three
+# or more processes' queues the GPU time-slices them - barrier rounds then stall for
+# seconds (tests/test_xgmi_gpu.py header).
+_FIRST = ("test_xgmi_gpu.py", "test_cli_gpu.py")
+
+
 def pytest_collection_modifyitems(config, items):
     import torch
 
+    def rank(it):
+        name = os.path.basename(str(it.fspath))
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+
+    items.sort(key=rank)  # stable: keeps the file's own order
     if torch.cuda.is_available():
         return
     skip = pytest.mark.skip(reason="no HIP device in this environment")

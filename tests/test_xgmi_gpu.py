@@ -182,7 +182,7 @@ def _plan_worker(rank, world, port, q, cap_mb, first_mb, dtype):
         nb = eng.eng.num_buckets
         stages = [eng.eng.bucket_stage(b) for b in range(nb)]
         eng.refresh()
-        eng.run_steps(10)
+        eng.run_steps(6)  # 1 momentum-init step + a 4-step graph replay + 1 eager step
         eng.synchronize()
         p = fs.params.detach().cpu()
         allp = [None] * world
