@@ -111,10 +111,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   DDP_STAMP(STAMP_K_SGD, 1);
 }
 
-// Block = 64 consecutive outputs x 4 row groups: thread (c, g) sums rows g, g+4, ...
-// (8 loads in flight), then the 4 group sums are added in fixed order via LDS.
-__global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
-  __shared__ float part[4][64];
+// Block = 64 consecutive outputs x GR row groups (GR waves): thread (c, g) sums rows g,
+// g + GR, ... with up to 8 loads in flight, then the GR group sums are added in fixed
+// order via LDS (bitwise reproducible).  GR = 16 (1024 threads) puts a whole 128-row
+// slab column block in flight at once: the kernel reads ~9.5 MB of split-K slabs per
+// SimpleCNN step, and with 4 groups it was latency-bound at ~4.7 GB/s per CU.
+template <int GR>
+__global__ __launch_bounds__(64 * GR) void grad_reduce_kernel(SlabSet ss) {
+  __shared__ float part[GR][64];
   DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
   const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
   // segments are laid out back to back, each padded to a multiple of 64 outputs, so
@@ -139,19 +143,22 @@ __global__ __launch_bounds__(256) void grad_reduce_kernel(SlabSet ss) {
     const float* src = sg.slab + sg.src_off + i;
     float a[8];
     int r = grp;
-    for (; r + 28 < sg.rows; r += 32) {
+    for (; r + 7 * GR < sg.rows; r += 8 * GR) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = src[(long)(r + 4 * u) * sg.row_stride];
+      for (int u = 0; u < 8; ++u) a[u] = src[(long)(r + GR * u) * sg.row_stride];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += a[u];
     }
-    for (; r < sg.rows; r += 4) acc += src[(long)r * sg.row_stride];
+    for (; r < sg.rows; r += GR) acc += src[(long)r * sg.row_stride];
   }
   part[grp][c] = acc;
   __syncthreads();
   if (grp == 0 && live) {
     const SlabSeg& sg = ss.s[k];  // k is block-uniform
-    float g = (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]) * sg.scale;
+    float g = part[0][c];
+#pragma unroll
+    for (int q = 1; q < GR; ++q) g += part[q][c];
+    g *= sg.scale;
     if (sg.accum) g += sg.dst[i];
     if (ss.sys_store) st_sys(sg.dst + i, g);
     else sg.dst[i] = g;
@@ -229,9 +236,17 @@ void grad_reduce(const SlabSet& ss, hipStream_t s) {
     return;
   }
   long blocks = 0;
-  for (int k = 0; k < ss.count; ++k) blocks += (ss.s[k].n + 63) / 64;
+  int max_rows = 0;
+  for (int k = 0; k < ss.count; ++k) {
+    blocks += (ss.s[k].n + 63) / 64;
+    max_rows = ss.s[k].rows > max_rows ? ss.s[k].rows : max_rows;
+  }
   if (blocks == 0) return;
-  hipLaunchKernelGGL(grad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ss);
+  // deep slabs: 16 row groups per block (all rows in flight); shallow ones: 4
+  if (max_rows >= 64)
+    hipLaunchKernelGGL(grad_reduce_kernel<16>, dim3((unsigned)blocks), dim3(1024), 0, s, ss);
+  else
+    hipLaunchKernelGGL(grad_reduce_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, ss);
 }
 
 void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s) {
