@@ -324,15 +324,23 @@ def bench_resnet(args):
     from ddp_amd.parallel import DistributedDataParallel, setup
 
     native.require()
+    if args.dtype != "bf16":
+        raise SystemExit("--model resnet18 runs the bf16 MFMA kernels only")
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if ws != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
     lrank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":  # rehearsal: several ranks share the visible GPUs
+        lrank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(lrank)
     dev = torch.device("cuda", lrank)
-    setup(rank, ws, backend="nccl", verbose=False)
+    setup(rank, ws, backend=args.backend, verbose=False)
     torch.manual_seed(0)
     model = resnet18().to(dev)
-    ddp = DistributedDataParallel(model)
+    # gloo rehearsal: no buffer broadcast (a c10d gloo call is not graph-capturable)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb,
+                                  broadcast_buffers=args.backend == "nccl")
     opt = FusedSGD(model, lr=args.lr, momentum=0.9)
     lossf = CrossEntropyLoss()
     B, S = args.batch_size, args.image_size
@@ -348,10 +356,10 @@ def bench_resnet(args):
         opt.step()
         return loss
 
-    # whole-step hipGraph (engine/graph_step.py) on one GPU; with several ranks the step
-    # runs eagerly (the DDP buffer broadcasts and bucket all-reduces are validated
-    # graph-captured only at world size 1 - ranks can't share a GPU under RCCL here)
-    use_graph = not args.no_graph and ws == 1
+    # whole-step hipGraph (engine/graph_step.py) at any world size: the DDP buffer
+    # broadcast (native RCCL on the current stream) and the bucket all-reduces (native
+    # reducer's comm stream, forked / joined by events) are captured with the step
+    use_graph = not args.no_graph
     if use_graph:
         # its capture warm-up steps are part of the untimed warm-up
         from ddp_amd.engine import GraphedStep
@@ -370,7 +378,10 @@ def bench_resnet(args):
 
     def barrier():
         if ws > 1:
-            dist.barrier(device_ids=[lrank])
+            if args.backend == "nccl":
+                dist.barrier(device_ids=[lrank])
+            else:
+                dist.barrier()
         torch.cuda.synchronize()
 
     barrier()
@@ -380,7 +391,7 @@ def bench_resnet(args):
     barrier()
     dt = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     img_s = ws * B * args.steps / dt
@@ -395,6 +406,8 @@ def bench_resnet(args):
                        "per_rank_batch": B, "seq_len": None, "parallelism": f"dp{ws}",
                        "engine": "module path (HIP autograd + native reducer)"
                                  + (", whole step in one hipGraph" if use_graph else ", eager"),
+                       "bucket_allreduce": ddp.comm_kind if ws > 1 else "none",
+                       "buckets": len(ddp.buckets), "ranks_seen": dist.get_world_size(),
                        "loss": round(float(loss.item()), 4)},
         }), flush=True)
     dist.destroy_process_group()

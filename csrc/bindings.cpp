@@ -752,9 +752,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         for (const auto& b : all) v.emplace_back(b);
         x.import_handles(v);
       })
-      .def("all_reduce", [](XgmiComm& x, int ch, double scale) {
-        x.all_reduce(ch, cur_stream(), (float)scale);
-      }, py::arg("channel"), py::arg("scale") = 1.0)
+      .def("all_reduce", [](XgmiComm& x, int ch, double scale, bool publish) {
+        x.all_reduce(ch, cur_stream(), (float)scale, publish);
+      }, py::arg("channel"), py::arg("scale") = 1.0, py::arg("publish") = false)
       .def("error_flags", &XgmiComm::error_flags)
       .def("set_timeout", &XgmiComm::set_timeout)
       .def_property_readonly("rank", &XgmiComm::rank)
@@ -777,6 +777,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              r.mark_ready(param, src, cur_stream());
            })
       .def("finalize", [](Reducer& r) { r.finalize(cur_stream()); })
+      .def("set_xgmi", &Reducer::set_xgmi, py::arg("xgmi"), py::arg("channels"))
+      .def_property_readonly("world", &Reducer::world)
       .def("reset", &Reducer::reset)
       .def_property_readonly("num_buckets", &Reducer::num_buckets)
       .def_property_readonly("allreduce_calls", &Reducer::allreduce_calls);

@@ -163,6 +163,16 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
   }
   const long slice = a.slice;  // elements per rank slice (the last rank's may be shorter)
   const long par = (long)(e & 1u) * slice;
+  if (a.publish) {
+    // the peers' block b reads element i of every slice of my bucket for exactly this
+    // block's i: make those elements system-visible (write-through) before arriving
+    float* mine = a.data[r] + a.off;
+    for (int p = 0; p < N; ++p) {
+      const long lim = min(slice, a.n - (long)p * slice);
+      for (long i = i0; i < lim; i += G) st_sys(mine + (long)p * slice + i, mine[(long)p * slice + i]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   xgmi_barrier(a, 2u * e, &s_fail);  // B0
   if (!s_fail) {
     // ---- RS: elements of my slice, fixed-order sum over ranks 0..N-1

@@ -240,6 +240,8 @@ struct XgmiArgs {
   unsigned* sig[XGMI_MAX_RANKS];  // every rank's signal words (uncached)
   long off, n, slice;             // bucket offset / length in the gradient buffer; n / world rounded up
   int oneshot;                    // 1: publish whole bucket, one barrier, every rank sums all (small buckets)
+  int publish;                    // two-shot: re-store my bucket system-scope before B0 (producers used
+                                  // plain stores, e.g. autograd kernels in the module path)
   float scale;                    // applied to the result (1: producers prescaled by 1/world)
   int rank, world;
   unsigned long long timeout_ticks;  // per barrier spin, 100 MHz ticks

@@ -7,7 +7,9 @@
 // last gradient is ready (overlapping backward), and the optimizer only runs
 // after every bucket finished.  What differs: buckets are views of one flat fp32
 // gradient buffer owned by the model, the all-reduce runs on a dedicated HIP
-// stream ordered by hipEvents (capturable), and the collective is RCCL directly.
+// stream ordered by hipEvents (capturable), and the collective is RCCL directly - or,
+// per bucket, the direct xGMI kernel (set_xgmi; two-shot with an in-kernel publish pass,
+// since autograd produced the gradients with plain stores).
 #include "runtime/runtime.h"
 
 namespace ddp_amd {
@@ -46,10 +48,29 @@ Reducer::~Reducer() {
 
 void Reducer::reset() { state_.reset(); }
 
+void Reducer::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> channels) {
+  if (x && channels.size() != bucket_off_.size())
+    throw std::runtime_error("reducer: one xgmi channel per bucket required");
+  if (x)
+    for (int ch : channels)
+      if (ch < 0 || ch >= x->channels()) throw std::runtime_error("reducer: xgmi channel out of range");
+  xgmi_ = std::move(x);
+  xch_ = std::move(channels);
+}
+
+int Reducer::world() const {
+  if (xgmi_) return xgmi_->world();
+  return comm_ ? comm_->world() : 1;
+}
+
 void Reducer::launch_bucket(int b, hipStream_t compute) {
   DDP_HIP_CHECK(hipEventRecord(ready_[b], compute));
   DDP_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_[b], 0));
-  if (comm_ && comm_->world() > 1) {
+  if (xgmi_ && xgmi_->world() > 1) {
+    // fixed rank-order sum, then the mean (unless the gradients were prescaled)
+    xgmi_->all_reduce(xch_[b], comm_stream_, prescale_ ? 1.f : 1.f / (float)xgmi_->world(), true);
+    ++calls_;
+  } else if (comm_ && comm_->world() > 1) {
     // prescaled gradients -> SUM == mean; otherwise let RCCL average
     comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, prescale_ ? 0 : 1,
                       comm_stream_);
@@ -62,7 +83,7 @@ void Reducer::launch_bucket(int b, hipStream_t compute) {
 void Reducer::mark_ready(int param, const float* grad_src, hipStream_t compute) {
   if (param < 0 || param >= (int)poff_.size()) throw std::runtime_error("reducer: bad param index");
   float* dst = flat_ + poff_[param];
-  const float scale = (prescale_ && comm_) ? 1.f / (float)comm_->world() : 1.f;
+  const float scale = prescale_ ? 1.f / (float)world() : 1.f;
   if (grad_src != nullptr && grad_src != dst) scale_copy(dst, grad_src, pnum_[param], scale, compute);
   else if (scale != 1.f) scale_copy(dst, dst, pnum_[param], scale, compute);
   const int b = state_.mark_ready(param);

@@ -75,10 +75,13 @@ class XgmiComm {
   void set_data(float* data, long numel);
   std::string export_handles() const;
   void import_handles(const std::vector<std::string>& all);
-  void all_reduce(int channel, hipStream_t s, float scale = 1.f);
+  // publish: the bucket's producers used plain stores (module path): each block re-stores
+  // its part system-scope before the entry barrier (no effect on one-shot channels, which
+  // always copy the bucket to their stage buffer that way)
+  void all_reduce(int channel, hipStream_t s, float scale = 1.f, bool publish = false);
   // the same, with SGD fused into the all-gather (see XgmiArgs)
   void all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
-                      const ShadowSet& sh, int* step_ctr, float scale = 1.f);
+                      const ShadowSet& sh, int* step_ctr, float scale = 1.f, bool publish = false);
   unsigned error_flags() const;  // != 0: a barrier timed out (result invalid)
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   int rank() const { return rank_; }
@@ -114,11 +117,16 @@ class XgmiComm {
 // communication of early buckets overlaps the rest of backward.  finalize()
 // makes the compute stream wait for every bucket.  All of it is stream-ordered
 // and therefore capturable into a hipGraph.
+// comm == null with an XgmiComm (set_xgmi) reduces over the direct xGMI kernels only
+// (e.g. ranks bootstrapped over gloo); world() comes from whichever data plane is set.
 class Reducer {
  public:
   Reducer(std::shared_ptr<Comm> comm, float* flat_grad, std::vector<long> param_offsets,
           std::vector<long> param_numels, std::vector<int> param_bucket,
           std::vector<long> bucket_offsets, std::vector<long> bucket_numels, bool prescale);
+  // bucket b all-reduced by xGMI channel channels[b] (its range must match the bucket)
+  void set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> channels);
+  int world() const;
   ~Reducer();
   // grad_src == nullptr: gradient already written in place (bucket view)
   void mark_ready(int param, const float* grad_src, hipStream_t compute);
@@ -130,6 +138,8 @@ class Reducer {
  private:
   void launch_bucket(int b, hipStream_t compute);
   std::shared_ptr<Comm> comm_;
+  std::shared_ptr<XgmiComm> xgmi_;
+  std::vector<int> xch_;
   float* flat_;
   std::vector<long> poff_, pnum_;
   std::vector<int> pbucket_;

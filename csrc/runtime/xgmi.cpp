@@ -132,12 +132,12 @@ void XgmiComm::import_handles(const std::vector<std::string>& all) {
   imported_ = true;
 }
 
-void XgmiComm::all_reduce(int channel, hipStream_t s, float scale) {
-  all_reduce_sgd(channel, s, SgdArgs{}, nullptr, nullptr, ShadowSet{}, nullptr, scale);
+void XgmiComm::all_reduce(int channel, hipStream_t s, float scale, bool publish) {
+  all_reduce_sgd(channel, s, SgdArgs{}, nullptr, nullptr, ShadowSet{}, nullptr, scale, publish);
 }
 
 void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params,
-                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale) {
+                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale, bool publish) {
   if (!imported_) throw std::runtime_error("xgmi: import_handles first");
   if (channel < 0 || channel >= (int)ch_.size()) throw std::runtime_error("xgmi: bad channel");
   const Channel& c = ch_[channel];
@@ -151,6 +151,7 @@ void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, fl
   a.n = c.n;
   a.slice = c.slice;
   a.oneshot = c.oneshot ? 1 : 0;
+  a.publish = publish ? 1 : 0;
   a.scale = scale;
   a.rank = rank_;
   a.world = world_;

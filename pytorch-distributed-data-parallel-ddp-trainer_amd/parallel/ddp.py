@@ -82,18 +82,39 @@ class _PyReducer:
 
 
 class _NativeReducer:
-    """Native C++ reducer (GPU): RCCL all-reduce (avg) on a dedicated HIP stream."""
+    """Native C++ reducer (GPU): per-bucket all-reduce (mean) on a dedicated HIP stream -
+    RCCL, or the direct xGMI kernels (``comm="xgmi"``: fixed rank-order sums, bitwise
+    identical on every rank; the only data plane when the ranks bootstrapped over gloo)."""
 
-    def __init__(self, fs: FlatSpace, buckets, ranges):
+    ONESHOT_MAX_ELEMS = 65536  # small buckets: one-shot kernel (one cross-GPU barrier)
+
+    def __init__(self, fs: FlatSpace, buckets, ranges, comm: str = "rccl"):
         from .. import native
         from .process_group import native_comm
 
         C = native.require()
         names = fs.names
         pb = {n: i for i, b in enumerate(buckets) for n in b}
-        self.r = C.Reducer(native_comm(), fs.grads, [fs.offsets[n] for n in names],
+        rccl = dist.get_backend() == "nccl"
+        self.kind = "rccl"
+        self.xgmi = None
+        if comm == "xgmi":
+            from .xgmi import channel_plan, create_xgmi
+
+            oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= self.ONESHOT_MAX_ELEMS)
+            self.xgmi = create_xgmi(fs.grads, ranges, dist.get_rank(), dist.get_world_size(),
+                                    oneshot=oneshot)
+            if self.xgmi is None and not rccl:
+                raise RuntimeError("xGMI self-test failed and the gloo group has no RCCL plane")
+            if self.xgmi is not None:
+                cp = channel_plan(len(ranges), oneshot)
+                self.channels = [cp[(b, b in oneshot)] for b in range(len(ranges))]
+                self.kind = "xgmi"
+        self.r = C.Reducer(native_comm() if rccl else None, fs.grads, [fs.offsets[n] for n in names],
                            [fs.numels[n] for n in names], [pb[n] for n in names],
                            [o for o, _ in ranges], [n for _, n in ranges], False)
+        if self.xgmi is not None:
+            self.r.set_xgmi(self.xgmi, self.channels)
         self.index = {n: i for i, n in enumerate(names)}
 
     def mark_ready(self, name):
@@ -107,7 +128,10 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None,
                  broadcast_buffers: bool = True, bucket_cap_mb: float = 25.0,
                  find_unused_parameters: bool = False, process_group=None,
-                 first_bucket_mb: float = 1.0, native: bool | None = None):
+                 first_bucket_mb: float = 1.0, native: bool | None = None, comm: str = "auto"):
+        """``comm`` (GPU, default group): ``"rccl"``, ``"xgmi"`` (the direct kernels) or
+        ``"auto"`` - RCCL under the nccl backend, xGMI when the ranks bootstrapped over gloo
+        (several ranks on one GPU rehearse the multi-GPU path that way)."""
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -127,7 +151,20 @@ class DistributedDataParallel(nn.Module):
         self._bucket_of = {n: i for i, b in enumerate(self.buckets) for n in b}
         self._pending = [len(b) for b in self.buckets]
         use_native = native if native is not None else (self.fs.params.is_cuda and process_group is None)
-        self._native = _NativeReducer(self.fs, self.buckets, self.ranges) if use_native else None
+        if comm not in ("auto", "rccl", "xgmi"):
+            raise ValueError(f"comm must be auto|rccl|xgmi, got {comm!r}")
+        if comm == "auto":
+            comm = "rccl" if dist.get_backend(process_group) == "nccl" else "xgmi"
+        if use_native and comm == "rccl" and dist.get_backend(process_group) != "nccl":
+            raise ValueError("comm='rccl' needs the nccl (RCCL) backend")
+        if use_native and self.world_size == 1:
+            comm = "rccl" if dist.get_backend(process_group) == "nccl" else "none"
+        self._native = None
+        if use_native and comm != "none":
+            self._native = _NativeReducer(self.fs, self.buckets, self.ranges, comm)
+        elif use_native and comm == "none":
+            use_native = False  # world size 1 over gloo: nothing to reduce
+        self.comm_kind = self._native.kind if self._native is not None else "c10d"
         self._py = None if use_native else _PyReducer(self.fs, self.ranges, process_group)
         self._sync_enabled = True
         self._queued = False
