@@ -176,6 +176,7 @@ class DistributedDataParallel(nn.Module):
                 # also fires for gradients the HIP Functions wrote in place (ops/direct_grad.py)
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(n)))
         self.allreduce_buckets_launched = 0
+        self._stream = torch.cuda.current_stream(self.fs.params.device) if self.fs.params.is_cuda else None
 
     # ---------------------------------------------------------------- construction sync
     def _verify_params(self):
@@ -219,7 +220,11 @@ class DistributedDataParallel(nn.Module):
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             b = self._bucket_of[name]
             if self._native is not None:
-                self._native.mark_ready(name)
+                # the forward's stream, not the hook's: autograd may run AccumulateGrad
+                # hooks with another current stream (a leaf's stream), which under hipGraph
+                # capture would leave the bucket all-reduce outside the captured graph
+                with torch.cuda.stream(self._stream):
+                    self._native.mark_ready(name)
             self._pending[b] -= 1
             if self._pending[b] == 0:
                 self._launched[b] = True
@@ -230,7 +235,8 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         if self._native is not None:
-            self._native.finalize()
+            with torch.cuda.stream(self._stream):
+                self._native.finalize()
         else:
             for b, done in enumerate(self._launched):
                 if not done:
@@ -251,6 +257,9 @@ class DistributedDataParallel(nn.Module):
             self._sync_enabled = old
 
     def forward(self, *args, **kwargs):
+        if self.fs.params.is_cuda:
+            # the step's compute stream: the bucket all-reduces order after it (see the hooks)
+            self._stream = torch.cuda.current_stream(self.fs.params.device)
         if self.broadcast_buffers and self.world_size > 1 and self.bufs is not None:
             self.bufs.rehome()
             with torch.no_grad():
