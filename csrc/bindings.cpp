@@ -442,7 +442,7 @@ void op_bn_apply(const Tensor& x, const Tensor& mean, const Tensor& invstd, cons
 void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
                const Tensor& invstd, const Tensor& gamma, double count, Tensor& ws, Tensor& sums,
                std::optional<Tensor> dgamma, std::optional<Tensor> dbeta, bool accum, Tensor& dx,
-               std::optional<Tensor> dres) {
+               std::optional<Tensor> dres, std::optional<Tensor> dout2) {
   check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(dx, "dx", at::kBFloat16);
   check(sums, "sums", at::kFloat); check(ws, "ws", at::kFloat);
   const int C = x.size(-1);
@@ -459,9 +459,10 @@ void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, c
   if (dbeta) { check(*dbeta, "dbeta", at::kFloat); TORCH_CHECK(dbeta->numel() == C, "dbeta"); db = dbeta->data_ptr<float>(); }
   bf16_t* dr = nullptr;
   if (dres) { check(*dres, "dres", at::kBFloat16); TORCH_CHECK(dres->sizes() == x.sizes(), "dres"); dr = bf(*dres); }
+  if (dout2) TORCH_CHECK(dout2->sizes() == x.sizes(), "dout2 shape");
   bn_bwd(cbf(dout), obf(out, "out"), cbf(x), P, C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
          gamma.data_ptr<float>(), (float)count, ws.data_ptr<float>(), sums.data_ptr<float>(), dg, db,
-         accum, bf(dx), dr, cur_stream());
+         accum, bf(dx), dr, cur_stream(), obf(dout2, "dout2"));
   kcheck();
 }
 
@@ -475,12 +476,14 @@ void op_maxpool_fwd(const Tensor& x, Tensor& y, Tensor& amax) {
   kcheck();
 }
 
-void op_maxpool_bwd(const Tensor& dy, const Tensor& amax, Tensor& dx) {
+void op_maxpool_bwd(const Tensor& dy, const Tensor& amax, Tensor& dx, std::optional<Tensor> dy2) {
   check(dy, "dy", at::kBFloat16); check(dx, "dx", at::kBFloat16); check(amax, "amax", at::kByte);
   const int N = dx.size(0), H = dx.size(1), W = dx.size(2), C = dx.size(3), OH = dy.size(1), OW = dy.size(2);
   TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && amax.numel() == dy.numel(), "maxpool bwd shape");
   TORCH_CHECK(C % 8 == 0 && dy.size(3) == C && dx.numel() / 8 < (1L << 31), "maxpool bwd: C % 8");
-  maxpool_bwd(cbf(dy), amax.data_ptr<unsigned char>(), N, H, W, C, OH, OW, bf(dx), cur_stream());
+  if (dy2) TORCH_CHECK(dy2->sizes() == dy.sizes(), "dy2 shape");
+  maxpool_bwd(cbf(dy), amax.data_ptr<unsigned char>(), N, H, W, C, OH, OW, bf(dx), cur_stream(),
+              obf(dy2, "dy2"));
   kcheck();
 }
 
@@ -516,7 +519,7 @@ void op_avgpool_bwd(const Tensor& dy, Tensor& dx) {
 
 // C[M][N] = alpha * A(m,k) B(k,n) + bias; strides in elements (A/B: fp32 or bf16)
 void op_sgemm(int M, int N, int K, const Tensor& A, long sam, long sak, const Tensor& B, long sbk,
-              long sbn, Tensor& Cm, std::optional<Tensor> bias, double alpha) {
+              long sbn, Tensor& Cm, std::optional<Tensor> bias, double alpha, bool accum) {
   check_cuda(A, "A"); check_cuda(B, "B"); check(Cm, "C", at::kFloat);
   const bool abf = A.scalar_type() == at::kBFloat16, bbf = B.scalar_type() == at::kBFloat16;
   TORCH_CHECK(abf || A.scalar_type() == at::kFloat, "A dtype");
@@ -527,7 +530,7 @@ void op_sgemm(int M, int N, int K, const Tensor& A, long sam, long sak, const Te
   const float* bp = nullptr;
   if (bias) { check(*bias, "bias", at::kFloat); TORCH_CHECK(bias->numel() == N, "bias"); bp = bias->data_ptr<float>(); }
   sgemm(M, N, K, A.data_ptr(), abf, sam, sak, B.data_ptr(), bbf, sbk, sbn, Cm.data_ptr<float>(), N,
-        bp, (float)alpha, cur_stream());
+        bp, (float)alpha, cur_stream(), accum);
   kcheck();
 }
 
@@ -698,14 +701,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &op_bn_apply);
   m.def("bn_finalize_groups", &bn_finalize_groups);
   m.def("bn_bwd_rows", [](long P, int C) { return bn_bwd_rows(P, C, nullptr); });
-  m.def("bn_bwd", &op_bn_bwd);
+  m.def("bn_bwd", &op_bn_bwd, py::arg("dout"), py::arg("out"), py::arg("x"), py::arg("mean"),
+        py::arg("invstd"), py::arg("gamma"), py::arg("count"), py::arg("ws"), py::arg("sums"),
+        py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dx"), py::arg("dres"),
+        py::arg("dout2") = py::none());
   m.def("bn_bwd_set_px_per_block", &bn_bwd_set_px_per_block);
   m.def("maxpool_fwd", &op_maxpool_fwd);
-  m.def("maxpool_bwd", &op_maxpool_bwd);
+  m.def("maxpool_bwd", &op_maxpool_bwd, py::arg("dy"), py::arg("amax"), py::arg("dx"),
+        py::arg("dy2") = py::none());
   m.def("avgpool_fwd", &op_avgpool_fwd);
   m.def("image_gather_nhwc4", &op_image_gather_nhwc4);
   m.def("avgpool_bwd", &op_avgpool_bwd);
-  m.def("sgemm", &op_sgemm);
+  m.def("sgemm", &op_sgemm, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("sam"),
+        py::arg("sak"), py::arg("B"), py::arg("sbk"), py::arg("sbn"), py::arg("C"), py::arg("bias"),
+        py::arg("alpha"), py::arg("accum") = false);
   m.def("transpose_w", &op_transpose_w);
   m.def("rccl_version", []() { int v = 0; ncclGetVersion(&v); return v; });
 

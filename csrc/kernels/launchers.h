@@ -104,20 +104,24 @@ void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* in
               hipStream_t s);
 void bn_bwd_set_px_per_block(int px);
 int bn_bwd_rows(long P, int C, int* rpb);  // ws of bn_bwd: [rows][2][C]
+// dout2 (optional): a second upstream gradient of the same tensor, summed on load
+// (bf16-rounded, == autograd's add) - the ResNet block input's two consumers
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,
-            float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s);
+            float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s,
+            const bf16_t* dout2 = nullptr);
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
                  unsigned char* amax, hipStream_t s);
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
-                 int OW, bf16_t* dx, hipStream_t s);
+                 int OW, bf16_t* dx, hipStream_t s, const bf16_t* dy2 = nullptr);
 void image_gather_nhwc4(const unsigned char* imgs, const long long* idx, int B, int HW, long N,
                         bf16_t* out, hipStream_t s);
 void avgpool_fwd(const bf16_t* x, int N, int HW, int C, float* y, hipStream_t s);
 void avgpool_bwd(const float* dy, int N, int HW, int C, bf16_t* dx, hipStream_t s);
+// accum: C += alpha A.B (+ bias) instead of C =
 void sgemm(int M, int N, int K, const void* A, bool a_bf16, long sam, long sak, const void* B,
            bool b_bf16, long sbk, long sbn, float* C, long ldc, const float* bias, float alpha,
-           hipStream_t s);
+           hipStream_t s, bool accum = false);
 void transpose_w(const float* w, int Co, int T, int Ci, bf16_t* wt, hipStream_t s);
 
 // ---- Linear over NHWC-flattened activations -----------------------------------------

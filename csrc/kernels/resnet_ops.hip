@@ -130,6 +130,18 @@ __device__ __forceinline__ void unpack8(bf16x8 v, float* o) {
   unpack4(make_uint2(u.x, u.y), o);
   unpack4(make_uint2(u.z, u.w), o + 4);
 }
+// Upstream gradient of a tensor with two consumers (ResNet block input: the conv branch and
+// the residual branch): d = bf16(d1 + d2), the exact value autograd's separate bf16 add
+// kernel would have produced - fused into the loads of the kernel that consumes the sum.
+__device__ __forceinline__ void unpack8_sum(bf16x8 a, const bf16_t* b2, long off, float* o) {
+  unpack8(a, o);
+  if (b2) {
+    float t[8];
+    unpack8(ld8(b2 + off), t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf16_round(o[j] + t[j]);
+  }
+}
 __device__ __forceinline__ uint4 pack8(const float* v) {
   const uint2 lo = pack4(v[0], v[1], v[2], v[3]), hi = pack4(v[4], v[5], v[6], v[7]);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -180,6 +192,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 // affine gradients (dbeta = sum dy, dgamma = sum dy*xhat; `accum` adds to them).
 template <bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
+                                                            const bf16_t* __restrict__ dout2,
                                                             const bf16_t* __restrict__ out,
                                                             const bf16_t* __restrict__ x, int P, int C,
                                                             const float* __restrict__ mean,
@@ -200,9 +213,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
   const int p0 = blockIdx.y * rpb, p1 = min(P, p0 + rpb);
-  auto acc8 = [&](bf16x8 gd, bf16x8 gx, bf16x8 go) {
+  auto acc8 = [&](bf16x8 gd, long off, bf16x8 gx, bf16x8 go) {
     float d[8], xv[8], ov[8];
-    unpack8(gd, d);
+    unpack8_sum(gd, dout2, off, d);
     unpack8(gx, xv);
     if (RELU) unpack8(go, ov);
 #pragma unroll
@@ -217,12 +230,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     const long o0 = (long)p * C + c0, o1 = o0 + 32L * C;
     const bf16x8 d0 = ld8(dout + o0), x0 = ld8(x + o0), d1 = ld8(dout + o1), x1 = ld8(x + o1);
     const bf16x8 r0 = RELU ? ld8(out + o0) : zero8(), r1 = RELU ? ld8(out + o1) : zero8();
-    acc8(d0, x0, r0);
-    acc8(d1, x1, r1);
+    acc8(d0, o0, x0, r0);
+    acc8(d1, o1, x1, r1);
   }
   for (; p < p1; p += 32) {
     const long o0 = (long)p * C + c0;
-    acc8(ld8(dout + o0), ld8(x + o0), RELU ? ld8(out + o0) : zero8());
+    acc8(ld8(dout + o0), o0, ld8(x + o0), RELU ? ld8(out + o0) : zero8());
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -280,6 +293,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 // fixed-channel-group grid stride as bn_apply.
 template <bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dout,
+                                                           const bf16_t* __restrict__ dout2,
                                                            const bf16_t* __restrict__ out,
                                                            const bf16_t* __restrict__ x, long n8,
                                                            int C, const float* __restrict__ mean,
@@ -301,7 +315,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   for (int j = 0; j < 8; ++j) k[j] = k[j] * is[j] / count;
   for (long i = t0; i < n8; i += stride) {
     float d[8], xv[8], ov[8], o[8];
-    unpack8(ld8(dout + i * 8), d);
+    unpack8_sum(ld8(dout + i * 8), dout2, i * 8, d);
     unpack8(ld8(x + i * 8), xv);
     if (RELU) unpack8(ld8(out + i * 8), ov);
 #pragma unroll
@@ -358,6 +372,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
 // (a per-pixel gather loads 9 per quad) and sums each pixel's matches in the window order
 // kh, kw = 0..2 (bitwise equal to the per-pixel form).
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ dy2,
                                                           const unsigned char* __restrict__ amax,
                                                           int N, int H, int W, int C, int OH, int OW,
                                                           bf16_t* __restrict__ dx) {
@@ -381,7 +396,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
       if (oh < OH && ow < OW) {
         const long o = (((long)n * OH + oh) * OW + ow) * C + g8;
         am[u][v] = *reinterpret_cast<const uint2*>(amax + o);
-        unpack8(ld8(dy + o), d[u][v]);
+        unpack8_sum(ld8(dy + o), dy2, o, d[u][v]);
       } else {
         am[u][v] = make_uint2(0xffffffffu, 0xffffffffu);  // matches no tap
 #pragma unroll
@@ -532,7 +547,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
                                                     long sam, long sak, const TB* __restrict__ B,
                                                     long sbk, long sbn, float* __restrict__ Cm,
                                                     long ldc, const float* __restrict__ bias,
-                                                    float alpha) {
+                                                    float alpha, int accum) {
   __shared__ float sA[16][17], sB[16][17];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int m = blockIdx.y * 16 + ty, n = blockIdx.x * 16 + tx;
@@ -550,7 +565,11 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
     for (int k = 0; k < 16; ++k) acc = fmaf(sA[ty][k], sB[k][tx], acc);
     __syncthreads();
   }
-  if (m < M && n < N) Cm[(long)m * ldc + n] = alpha * acc + (bias ? bias[n] : 0.f);
+  if (m < M && n < N) {
+    float v = alpha * acc + (bias ? bias[n] : 0.f);
+    if (accum) v += Cm[(long)m * ldc + n];  // direct gradient accumulation (C += A.B)
+    Cm[(long)m * ldc + n] = v;
+  }
 }
 
 // OHWI [Co][T][Ci] (fp32 master) -> bf16 [Ci][T][Co] (conv_gemm dgrad operand)
@@ -636,20 +655,21 @@ int bn_bwd_rows(long P, int C, int* rpb) {
 
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,
-            float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s) {
+            float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s,
+            const bf16_t* dout2) {
   int rpb = 0;
   const int R = bn_bwd_rows(P, C, &rpb);
   const dim3 grid(C / 64, R);
   int* tk = ticket_slots(C / 64);
   if (out)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), 0, s, dout, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), 0, s, dout, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
   const unsigned g = grid_for(P * C, 8);
   if (out)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(256), 0, s, dout, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(256), 0, s, dout, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
 }
 
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
@@ -660,10 +680,10 @@ void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf
 }
 
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
-                 int OW, bf16_t* dx, hipStream_t s) {
+                 int OW, bf16_t* dx, hipStream_t s, const bf16_t* dy2) {
   const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, dy,
-                     amax, N, H, W, C, OH, OW, dx);
+                     dy2, amax, N, H, W, C, OH, OW, dx);
 }
 
 void image_gather_nhwc4(const unsigned char* imgs, const long long* idx, int B, int HW, long N,
@@ -699,9 +719,9 @@ void avgpool_bwd(const float* dy, int N, int HW, int C, bf16_t* dx, hipStream_t 
 
 void sgemm(int M, int N, int K, const void* A, bool a_bf16, long sam, long sak, const void* B,
            bool b_bf16, long sbk, long sbn, float* C, long ldc, const float* bias, float alpha,
-           hipStream_t s) {
+           hipStream_t s, bool accum) {
   const dim3 grid((N + 15) / 16, (M + 15) / 16);
-#define SG(TA, TB) hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, s, M, N, K, (const TA*)A, sam, sak, (const TB*)B, sbk, sbn, C, ldc, bias, alpha)
+#define SG(TA, TB) hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, s, M, N, K, (const TA*)A, sam, sak, (const TB*)B, sbk, sbn, C, ldc, bias, alpha, (int)accum)
   if (a_bf16) { if (b_bf16) SG(bf16_t, bf16_t); else SG(bf16_t, float); }
   else { if (b_bf16) SG(float, bf16_t); else SG(float, float); }
 #undef SG

@@ -64,14 +64,16 @@ class BasicBlock(nn.Module):
         return self.relu(out + idt)
 
     def forward_hip(self, x):
-        from ..ops.resnet_fn import conv_bn_act
+        from ..ops.resnet_fn import attach_stash, conv_bn_act
 
+        # x feeds two branches: the residual one hands its gradient to x's producer, which
+        # adds it inside its own backward (no separate gradient-add kernel)
+        stash = attach_stash(x) if torch.is_grad_enabled() and x.requires_grad else None
         out = conv_bn_act(x, self.conv1, self.bn1, relu=True)
         if self.downsample is not None:
-            idt = conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False)
-        else:
-            idt = x
-        return conv_bn_act(out, self.conv2, self.bn2, res=idt, relu=True)
+            idt = conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, stash=stash)
+            return conv_bn_act(out, self.conv2, self.bn2, res=idt, relu=True)
+        return conv_bn_act(out, self.conv2, self.bn2, res=x, relu=True, stash=stash)
 
 
 class ResNet(nn.Module):

@@ -9,8 +9,15 @@ conv_bn_act         conv_gemm_fwd (+ BN sum/sumsq epilogue, or        bn_bwd (st
                     bn_apply (+ residual add + ReLU)                  grad, or slabs -> grad_reduce)
 maxpool3x3s2        maxpool_fwd (argmax saved)                        maxpool_bwd (deterministic gather)
 global_avgpool      avgpool_fwd                                       avgpool_bwd
-linear_head         library GEMM (hipBLASLt) + bias                   library GEMMs
+linear_head         sgemm (in-tree fp32 GEMM, + bias)                 sgemm x3 (dx; dW and db accumulated in place)
 ==================  ================================================  ===========================================
+
+Residual joins: a block's input x feeds its conv branch and its residual branch, so
+autograd would add the two gradients with a separate bf16 add kernel.  Instead the
+residual branch (``stash=``) parks its gradient in a :class:`GradStash` hung on x's
+producer node, returns none, and the producer's backward (BatchNorm backward or the
+maxpool backward) sums it into its upstream gradient while loading it - bitwise the same
+bf16 sum, one kernel and one full pass fewer per block.
 
 Weights: the MFMA operand is the model's flat bf16 parameter copy (``FlatSpace.bf16_params``,
 refreshed by FusedSGD inside its update kernel) when the model is flattened (DDP /
@@ -42,6 +49,42 @@ def to_nhwc4(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+class GradStash:
+    """A second upstream gradient of a tensor, handed from one consumer's backward to the
+    tensor producer's backward (see the module docstring)."""
+
+    def __init__(self):
+        self.grad = None
+
+    def put(self, g):
+        if g is None:
+            return
+        self.grad = g if self.grad is None else self.grad + g  # (never twice in a ResNet block)
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+def attach_stash(x: torch.Tensor):
+    """A GradStash on x's producer node (its ctx in backward), or None when x has no
+    producer that can consume one (then the residual branch returns its gradient)."""
+    fn = x.grad_fn
+    if fn is None or not isinstance(fn, (_ConvBNAct._backward_cls, _MaxPool._backward_cls)):
+        return None
+    st = getattr(fn, "_ddp_amd_stash", None)
+    if st is None:
+        st = GradStash()
+        fn._ddp_amd_stash = st
+    return st
+
+
+def _take_stash(ctx):
+    st = getattr(ctx, "_ddp_amd_stash", None)
+    g = st.take() if st is not None else None
+    return g.to(BF16).contiguous() if g is not None else None
+
+
 def _weight_bf16(w: torch.Tensor) -> torch.Tensor:
     fs = getattr(w, "_ddp_amd_fs", None)
     v = fs.bf16_view(w) if fs is not None else None
@@ -51,7 +94,7 @@ def _weight_bf16(w: torch.Tensor) -> torch.Tensor:
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, running_mean, running_var, nbt, res, stride, pad, relu,
-                training, momentum, eps):
+                training, momentum, eps, stash=None):
         N, H, W_, Cin = x.shape
         Cout, KH, KW, wcin = w.shape
         stem = Cin == 4 and wcin == 3
@@ -85,6 +128,9 @@ class _ConvBNAct(torch.autograd.Function):
         ctx.save_for_backward(x, wb, y, out, mean, invstd)
         ctx.params = (w, gamma, beta)
         ctx.cfg = (stride, pad, bool(relu), res is not None, stem, P)
+        # stash: this Function is the residual branch of a block; its gradient w.r.t. the
+        # block input (res's for a join, x's for a downsample conv) goes to the stash
+        ctx.stash = stash
         return out
 
     @staticmethod
@@ -108,7 +154,7 @@ class _ConvBNAct(torch.autograd.Function):
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if has_res else None
         C.bn_bwd(dout, out if relu else None, y, mean, invstd, gamma.detach(), float(P), ws, sums,
-                 dgamma, dbeta, direct_bn, dy, dres)
+                 dgamma, dbeta, direct_bn, dy, dres, _take_stash(ctx))
         # data gradient (the stem's input is the image: none)
         dx = None
         if ctx.needs_input_grad[0] and not stem:
@@ -130,7 +176,14 @@ class _ConvBNAct(torch.autograd.Function):
             C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, gw is not None)])
         rw = None if gw is not None else dw
         rg, rb = (None, None) if direct_bn else (dgamma, dbeta)
-        return dx, rw, rg, rb, None, None, None, dres, None, None, None, None, None, None
+        if ctx.stash is not None:  # residual branch: hand the block-input gradient over
+            if has_res:
+                ctx.stash.put(dres)
+                dres = None
+            else:
+                ctx.stash.put(dx)
+                dx = None
+        return dx, rw, rg, rb, None, None, None, dres, None, None, None, None, None, None, None
 
 
 class _MaxPool(torch.autograd.Function):
@@ -149,7 +202,7 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, dy):
         (am,) = ctx.saved_tensors
         dx = torch.empty(ctx.shape, dtype=BF16, device=dy.device)
-        _C().maxpool_bwd(dy.to(BF16).contiguous(), am, dx)
+        _C().maxpool_bwd(dy.to(BF16).contiguous(), am, dx, _take_stash(ctx))
         return dx
 
 
@@ -170,12 +223,18 @@ class _AvgPool(torch.autograd.Function):
 
 
 class _LinearHead(torch.autograd.Function):
-    """fp32 classifier head on library GEMMs (a plain [B,512]x[512,1000] GEMM)."""
+    """fp32 classifier head ([B,512] x [512,classes]) on the in-tree GEMM (``sgemm``): the
+    forward with the bias folded in; the backward as dx = dl.W, dW += dl^T.x and
+    db += 1^T.dl, the last two accumulated straight into the flat gradient views."""
 
     @staticmethod
     def forward(ctx, x, w, b):
         x = x.float().contiguous()
-        out = torch.addmm(b.detach(), x, w.detach().t()) if b is not None else x @ w.detach().t()
+        B, K = x.shape
+        N = w.shape[0]
+        out = torch.empty(B, N, device=x.device)
+        wd = w.detach()
+        _C().sgemm(B, N, K, x, K, 1, wd, 1, K, out, b.detach() if b is not None else None, 1.0)
         ctx.save_for_backward(x)
         ctx.params = (w, b)
         return out
@@ -184,30 +243,38 @@ class _LinearHead(torch.autograd.Function):
     def backward(ctx, dl):
         (x,) = ctx.saved_tensors
         w, b = ctx.params
+        C = _C()
         dl = dl.float().contiguous()
-        dx = dl @ w.detach()
+        B, K = x.shape
+        N = w.shape[0]
+        wd = w.detach()
+        dx = torch.empty(B, K, device=dl.device)
+        C.sgemm(B, K, N, dl, N, 1, wd, K, 1, dx, None, 1.0)                    # dl . W
         gw = direct_grad.grad_dst(w)
+        rw = None
         if gw is not None:
-            gw.addmm_(dl.t(), x)
-            rw = None
+            C.sgemm(N, K, B, dl, 1, N, x, K, 1, gw, None, 1.0, True)           # dW += dl^T . x
         else:
-            rw = dl.t() @ x
+            rw = torch.empty(N, K, device=dl.device)
+            C.sgemm(N, K, B, dl, 1, N, x, K, 1, rw, None, 1.0)
         rb = None
         if b is not None:
+            ones = torch.ones(B, device=dl.device)
             gb = direct_grad.grad_dst(b)
             if gb is not None:
-                gb.add_(dl.sum(0))
+                C.sgemm(1, N, B, ones, 0, 1, dl, N, 1, gb, None, 1.0, True)    # db += 1^T . dl
             else:
-                rb = dl.sum(0)
+                rb = torch.empty(N, device=dl.device)
+                C.sgemm(1, N, B, ones, 0, 1, dl, N, 1, rb, None, 1.0)
         return dx, rw, rb
 
 
-def conv_bn_act(x, conv, bn, res=None, relu=True):
+def conv_bn_act(x, conv, bn, res=None, relu=True, stash=None):
     training = bn.training
     nbt = bn.num_batches_tracked if (training and bn.track_running_stats) else None
     momentum = bn.momentum if bn.momentum is not None else 0.1
     return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                            nbt, res, conv.stride, conv.padding, relu, training, momentum, bn.eps)
+                            nbt, res, conv.stride, conv.padding, relu, training, momentum, bn.eps, stash)
 
 
 def maxpool3x3s2(x):
