@@ -572,6 +572,63 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
   }
 }
 
+// Small-M fp32 GEMM (M <= 32: the classifier head's batch rows) on v_mfma_f32_16x16x4_f32:
+// block = 16 waves over one 32 x 16 output tile, the K range split across the waves (each
+// wave: two 16x16 accumulators), partial tiles summed through LDS in fixed wave order
+// (deterministic).  Exact fp32 products; long K (512 / 1000) spreads over 16 waves
+// instead of one 16x16 VALU tile walking all of it.
+constexpr int SMM_WAVES = 16;
+template <typename TA, typename TB>
+__global__ __launch_bounds__(64 * SMM_WAVES) void gemm_small_m_kernel(
+    int M, int N, int K, const TA* __restrict__ A, long sam, long sak, const TB* __restrict__ B, long sbk,
+    long sbn, float* __restrict__ Cm, long ldc, const float* __restrict__ bias, float alpha, int accum) {
+  __shared__ float red[SMM_WAVES][32][17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 16;
+  auto ld = [](const auto* p, long i) -> float {
+    if constexpr (sizeof(*p) == 2) return bf2f(reinterpret_cast<const bf16_t*>(p)[i]);
+    else return reinterpret_cast<const float*>(p)[i];
+  };
+  const int kq = ((K + SMM_WAVES - 1) / SMM_WAVES + 3) & ~3;  // this wave's K range (multiple of 4)
+  const int kb = wave * kq, ke = min(K, kb + kq);
+  const int r = lane & 15, kl = lane >> 4;
+  const int n = n0 + r;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += 16) {
+    float a0[4], a1[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // 4 MFMA steps' operands in flight
+      const int k = k0 + 4 * u + kl;
+      const bool kok = k < ke;
+      a0[u] = (kok && r < M) ? ld(A, (long)r * sam + (long)k * sak) : 0.f;
+      a1[u] = (kok && r + 16 < M) ? ld(A, (long)(r + 16) * sam + (long)k * sak) : 0.f;
+      bv[u] = (kok && n < N) ? ld(B, (long)k * sbk + (long)n * sbn) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], bv[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], bv[u], acc1, 0, 0, 0);
+    }
+  }
+  // D[row = 4(l>>4) + j][col = l & 15]
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[wave][4 * kl + j][r] = acc0[j];
+    red[wave][16 + 4 * kl + j][r] = acc1[j];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 32 * 16; t += 64 * SMM_WAVES) {
+    const int m = t >> 4, c = t & 15, nn = n0 + c;
+    if (m >= M || nn >= N) continue;
+    float v = red[0][m][c];
+#pragma unroll
+    for (int w = 1; w < SMM_WAVES; ++w) v += red[w][m][c];
+    v = alpha * v + (bias ? bias[nn] : 0.f);
+    if (accum) v += Cm[(long)m * ldc + nn];
+    Cm[(long)m * ldc + nn] = v;
+  }
+}
+
 // OHWI [Co][T][Ci] (fp32 master) -> bf16 [Ci][T][Co] (conv_gemm dgrad operand)
 __global__ void transpose_w_kernel(const float* __restrict__ w, int Co, int T, int Ci,
                                    bf16_t* __restrict__ wt) {
@@ -720,6 +777,14 @@ void avgpool_bwd(const float* dy, int N, int HW, int C, bf16_t* dx, hipStream_t 
 void sgemm(int M, int N, int K, const void* A, bool a_bf16, long sam, long sak, const void* B,
            bool b_bf16, long sbk, long sbn, float* C, long ldc, const float* bias, float alpha,
            hipStream_t s, bool accum) {
+  if (M <= 32 && K >= 64) {  // long-K, few rows: the MFMA small-M kernel
+    const dim3 g2((N + 15) / 16);
+#define SM(TA, TB) hipLaunchKernelGGL((gemm_small_m_kernel<TA, TB>), g2, dim3(64 * SMM_WAVES), 0, s, M, N, K, (const TA*)A, sam, sak, (const TB*)B, sbk, sbn, C, ldc, bias, alpha, (int)accum)
+    if (a_bf16) { if (b_bf16) SM(bf16_t, bf16_t); else SM(bf16_t, float); }
+    else { if (b_bf16) SM(float, bf16_t); else SM(float, float); }
+#undef SM
+    return;
+  }
   const dim3 grid((N + 15) / 16, (M + 15) / 16);
 #define SG(TA, TB) hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, s, M, N, K, (const TA*)A, sam, sak, (const TB*)B, sbk, sbn, C, ldc, bias, alpha, (int)accum)
   if (a_bf16) { if (b_bf16) SG(bf16_t, bf16_t); else SG(bf16_t, float); }
