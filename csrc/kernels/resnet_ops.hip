@@ -594,10 +594,10 @@ __global__ __launch_bounds__(64 * SMM_WAVES) void gemm_small_m_kernel(
   const int r = lane & 15, kl = lane >> 4;
   const int n = n0 + r;
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kb; k0 < ke; k0 += 16) {
-    float a0[4], a1[4], bv[4];
+  for (int k0 = kb; k0 < ke; k0 += 32) {
+    float a0[8], a1[8], bv[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // 4 MFMA steps' operands in flight
+    for (int u = 0; u < 8; ++u) {  // 8 MFMA steps' operands in flight
       const int k = k0 + 4 * u + kl;
       const bool kok = k < ke;
       a0[u] = (kok && r < M) ? ld(A, (long)r * sam + (long)k * sak) : 0.f;
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(64 * SMM_WAVES) void gemm_small_m_kernel(
       bv[u] = (kok && n < N) ? ld(B, (long)k * sbk + (long)n * sbn) : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], bv[u], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], bv[u], acc1, 0, 0, 0);
     }
