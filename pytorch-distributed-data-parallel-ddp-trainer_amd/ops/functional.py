@@ -32,13 +32,16 @@ def _C():
 
 
 def wgrad_rows(H: int, B: int, dtype=BF16) -> int:
-    """Rows per wgrad block: the largest chunk that still gives >= 128 split-K blocks.
+    """Rows per wgrad block: the largest chunk that still gives >= 128 split-K blocks,
+    capped at 7 rows (bf16) / 4 rows (fp32).
 
-    Fewer, fatter blocks mean fewer fp32 slab rows to write and re-read; 128 blocks
-    keep half the CUs busy.  LDS bounds R at 14 for a 28x28x(32,64) layer in bf16 and at
-    7 in fp32 (twice the bytes per staged element).
+    Fewer, fatter blocks mean fewer fp32 slab rows to write and re-read, but the wgrad
+    role shares the conv-backward launch with the data gradient and a fat block becomes
+    its critical path.  Measured on MI355X (profiles/r2_perf/sweep.jsonl, 28x28x(32,64)):
+    bf16 B=32: R=7 41.9 us/step vs R=14 51.5, R=4 43.3; B=64: R=7 62.8 vs R=14 72.9;
+    fp32 B=32: R=4 83.4 vs R=7 92.3 (twice the LDS bytes per staged row).
     """
-    for R in ((14, 7, 4, 2, 1) if dtype == BF16 else (7, 4, 2, 1)):
+    for R in ((7, 4, 2, 1) if dtype == BF16 else (4, 2, 1)):
         if R <= H and B * ((H + R - 1) // R) >= 128:
             return R
     return 1
