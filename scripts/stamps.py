@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--fuse_level", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--graph", action="store_true", help="stamp the last step of a replayed graph")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -34,10 +35,10 @@ def main():
     C = native.require()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = SimpleCNN().to(dev)
+    model = SimpleCNN(compute_dtype=torch.float32 if a.dtype == "fp32" else torch.bfloat16).to(dev)
     opt = FusedSGD(model, lr=0.01)
     imgs, labels = synthetic_mnist()
-    eo = EngineOptions(use_graph=a.graph, graph_steps=10)
+    eo = EngineOptions(use_graph=a.graph, graph_steps=10, dtype=a.dtype)
     if a.fuse_level is not None:
         eo.fuse_level = a.fuse_level
     eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, dev, "synthetic"),
