@@ -279,16 +279,20 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       if (NOF > 0) {
 #pragma unroll
         for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
-          float wf[4];
+          float s = fcs[o];
           if constexpr (F32) {  // native [o][hw][c] fp32 weight: 4 consecutive channels
             const float4 w4 = *reinterpret_cast<const float4*>(wfc + ((long)o * HW + rem[pt]) * Cout + co);
-            wf[0] = w4.x; wf[1] = w4.y; wf[2] = w4.z; wf[3] = w4.w;
+            s = fmaf(q[0], w4.x, s); s = fmaf(q[1], w4.y, s);
+            s = fmaf(q[2], w4.z, s); s = fmaf(q[3], w4.w, s);
           } else {
-            unpack4(wv[pt][t][o], wf);
+            // the stored bf16 pairs against the bf16 weight pairs: v_dot2c_f32_bf16 (exact
+            // bf16 products, fp32 accumulate) - no unpacking of either operand
+            const uint2 pk = pack4(v0, v1, v2, v3);
+            s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, pk.x),
+                                                __builtin_bit_cast(bf16x2v, wv[pt][t][o].x), s, false);
+            s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, pk.y),
+                                                __builtin_bit_cast(bf16x2v, wv[pt][t][o].y), s, false);
           }
-          float s = fcs[o];
-          s = fmaf(q[0], wf[0], s); s = fmaf(q[1], wf[1], s);
-          s = fmaf(q[2], wf[2], s); s = fmaf(q[3], wf[3], s);
           fcs[o] = valid[pt] ? s : 0.f;
         }
       }
