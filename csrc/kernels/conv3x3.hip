@@ -229,6 +229,11 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[pt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // the epilogue's bias quads, requested before the MFMA loop (a dependent global load at
+  // the start of the epilogue cost ~1-2 us per block)
+  float4 bq[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bq[t] = *reinterpret_cast<const float4*>(bias + co0 + 16 * t + 4 * (lane >> 4));
 
   const T* wrow = sW + col * WS + kofs;
 #pragma unroll
@@ -266,7 +271,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int co = co0 + 16 * t + 4 * (lane >> 4);
-      const float4 bv = *reinterpret_cast<const float4*>(bias + co);
+      const float4 bv = bq[t];
       float v0 = acc[pt][t][0] + bv.x, v1 = acc[pt][t][1] + bv.y;
       float v2 = acc[pt][t][2] + bv.z, v3 = acc[pt][t][3] + bv.w;
       if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
