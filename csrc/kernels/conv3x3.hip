@@ -126,38 +126,6 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 
   const int wc = KW / CE;
   const int xc = Cin / CE;
-  const int kofs = P::kofs(lane);
-  const int col = lane & 15;
-  int h[PXT], w[PXT], rowc[PXT], rem[PXT];
-  bool valid[PXT];
-  long Pp[PXT];
-#pragma unroll
-  for (int pt = 0; pt < PXT; ++pt) {
-    const int lp = (wave * PXT + pt) * 16 + col;  // pixel within the block
-    Pp[pt] = P0 + lp;
-    valid[pt] = Pp[pt] < Ptot;
-    const long Pc = valid[pt] ? Pp[pt] : 0;
-    const int n = (int)(Pc / HW);
-    rem[pt] = (int)(Pc - (long)n * HW);
-    h[pt] = rem[pt] / W;
-    w[pt] = rem[pt] - h[pt] * W;
-    rowc[pt] = lp + W + 1;  // sX row of the pixel itself
-  }
-  // fc weight prefetch, issued first: its lines were written by the previous step's
-  // optimizer and come from HBM, so they need the whole staging + MFMA phase to land
-  // (issued after the staging they still stalled the epilogue ~2 us).  fp32 reads its
-  // native-layout weight in the epilogue instead (160 more VGPRs would not fit)
-  uint2 wv[NOF > 0 && !F32 ? PXT : 1][4][NOF > 0 && !F32 ? NOF : 1];
-  if (NOF > 0 && !F32) {
-#pragma unroll
-    for (int pt = 0; pt < PXT; ++pt)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o)
-          wv[pt][t][o] = *reinterpret_cast<const uint2*>(
-              wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
-  }
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave & 3);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
@@ -210,6 +178,37 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     DDP_STAMP(STAMP_K_CONV_FWD, 5);
   }
 
+  const int kofs = P::kofs(lane);
+  const int col = lane & 15;
+  int h[PXT], w[PXT], rowc[PXT], rem[PXT];
+  bool valid[PXT];
+  long Pp[PXT];
+#pragma unroll
+  for (int pt = 0; pt < PXT; ++pt) {
+    const int lp = (wave * PXT + pt) * 16 + col;  // pixel within the block
+    Pp[pt] = P0 + lp;
+    valid[pt] = Pp[pt] < Ptot;
+    const long Pc = valid[pt] ? Pp[pt] : 0;
+    const int n = (int)(Pc / HW);
+    rem[pt] = (int)(Pc - (long)n * HW);
+    h[pt] = rem[pt] / W;
+    w[pt] = rem[pt] - h[pt] * W;
+    rowc[pt] = lp + W + 1;  // sX row of the pixel itself
+  }
+  // fc weight prefetch (lands while the MFMAs run; issued before the staging it delayed
+  // it - in-order vmcnt - by more than it saved); fp32 reads its native-layout weight in
+  // the epilogue instead (160 more VGPRs would not fit next to the fp32 fragments)
+  uint2 wv[NOF > 0 && !F32 ? PXT : 1][4][NOF > 0 && !F32 ? NOF : 1];
+  if (NOF > 0 && !F32) {
+#pragma unroll
+    for (int pt = 0; pt < PXT; ++pt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o)
+          wv[pt][t][o] = *reinterpret_cast<const uint2*>(
+              wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
+  }
   __syncthreads();
   DDP_STAMP(STAMP_K_CONV_FWD, 2);
   if (A1X && !F32 && c1.a1_out) {
