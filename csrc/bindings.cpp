@@ -662,6 +662,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_dgrad", &op_conv3x3_dgrad);
   m.def("conv3x3_dgrad_fused_w1", &op_conv3x3_dgrad_fused_w1);
   m.def("conv3x3_dgrad_blocks", &conv3x3_dgrad_blocks);
+  m.def("fc_conv_bwd_fc_blocks", &fc_conv_bwd_fc_blocks);
   m.def("conv3x3_wgrad", &op_conv3x3_wgrad);
   m.def("conv3x3_wgrad_blocks", &conv3x3_wgrad_blocks);
   m.def("fc_partial", &op_fc_partial);
@@ -810,9 +811,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_opt = cfgd.contains("fuse_opt") ? (int)cfgd["fuse_opt"].cast<bool>() : 1;
              c.store_a1 = cfgd.contains("store_a1") ? cfgd["store_a1"].cast<int>() : 0;
              c.f32 = cfgd.contains("f32") ? (int)cfgd["f32"].cast<bool>() : 0;
+             c.fuse_reduce = cfgd.contains("fuse_reduce") ? (int)cfgd["fuse_reduce"].cast<bool>() : 1;
              const int es = c.f32 ? 4 : 2;
              TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");
-             TORCH_CHECK(c.fuse_level == 0 || c.fuse_level == 1, "engine: fuse_level must be 0 or 1");
+             TORCH_CHECK(c.fuse_level >= 0 && c.fuse_level <= 2, "engine: fuse_level must be 0, 1 or 2");
              TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0, es) <= 160 * 1024 &&
                              conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0, es) <= 160 * 1024 &&
                              conv3x3_dgrad_lds(c.W, c.C2, c.pxt_dgrad, true, es) <= 160 * 1024,
@@ -842,9 +844,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              TORCH_CHECK(b.off_wfc + (long)c.NO * HW * c.C2 <= b.n_params && b.off_w1 + 9L * c.C1 <= b.n_params &&
                          b.off_b2 + c.C2 <= b.n_params && b.off_w2 + 9L * c.C1 * c.C2 <= b.n_params,
                          "engine: parameter offsets out of range");
-             TORCH_CHECK(fc_bwd_lds(c.max_batch, c.NO, true) <= 160 * 1024, "engine: batch too large for fc_bwd LDS");
+             TORCH_CHECK(fc_bwd_lds(c.max_batch, c.NO, true, ((long)c.max_batch * HW + 64L * c.pxt_fwd - 1) / (64L * c.pxt_fwd) * 2 * c.NO) <= 160 * 1024,
+                         "engine: batch too large for fc_bwd LDS");
              if (c.f32) {  // exact fp32: fp32 activations + the conv2 weight's fp32 [tap][ci][co] copy
-               TORCH_CHECK(c.fuse_level == 1 && c.store_a1 == 0, "engine: fp32 needs fuse_level 1, store_a1 0");
+               TORCH_CHECK(c.fuse_level >= 1 && c.store_a1 == 0, "engine: fp32 needs fuse_level >= 1 (runs level 1), store_a1 0");
                b.a2_f32 = need("a2", at::kFloat, B * HW * c.C2).data_ptr<float>();
                b.dz2_f32 = need("dz2", at::kFloat, B * HW * c.C2).data_ptr<float>();
                b.w2t_f32 = need("w2t_f32", at::kFloat, 9L * c.C1 * c.C2).data_ptr<float>();
@@ -867,6 +870,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.step_ctr = need("step_ctr", at::kInt, 1).data_ptr<int>();
              b.xb = need("xb", at::kByte, B * HW).data_ptr<unsigned char>();
              b.yb = need("yb", at::kInt, B).data_ptr<int>();
+             if (t.contains("sync_flags")) {  // in-launch hand-offs (fused reduction, level 2)
+               const long nfl = SYNC_RED_INTS + fc_conv_bwd_fc_blocks(HW * c.C2) +
+                                conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_fwd);
+               b.sync_flags = need("sync_flags", at::kInt, nfl).data_ptr<int>();
+               b.sync_err = need("sync_err", at::kInt, 1).data_ptr<int>();
+             }
+             TORCH_CHECK(c.fuse_level < 2 || c.f32 || b.sync_flags, "engine: fuse_level 2 needs sync_flags");
              Tensor images = need("images", at::kByte, HW);
              b.images = images.data_ptr<unsigned char>();
              Tensor labels = need("labels", at::kInt, 1);
@@ -886,6 +896,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("replay", &SimpleCNNEngine::replay)
       .def("destroy_graph", &SimpleCNNEngine::destroy_graph)
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("level2_active", &SimpleCNNEngine::level2_active)
+      .def_property_readonly("last_fused_reduce", &SimpleCNNEngine::last_fused_reduce)
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
       .def("set_xgmi", &SimpleCNNEngine::set_xgmi, py::arg("xgmi"), py::arg("channels"))
       .def_property_readonly("num_buckets", &SimpleCNNEngine::num_buckets)

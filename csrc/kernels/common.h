@@ -33,17 +33,17 @@ constexpr int WAVE = 64;
 // so a stamp costs one scalar load + branch).  DDP_STAMP(kid, slot) makes lane 0 of the
 // block's first wave store the 100 MHz constant-rate clock (s_memrealtime, comparable
 // across CUs) at buf[kid][block][slot]; kid = kernel id (STAMP_K_*), 8 slots per block.
+// Blocks with blockIdx.y > 0 do not stamp: gridDim comes from the implicit kernel
+// arguments through a vector load, and its wait (vmcnt in order) would also wait for
+// every load the wave has in flight - a stamp must not change the schedule it measures.
 namespace {
 __constant__ unsigned long long* g_stamp_buf = nullptr;  // constant: a scalar load, no vmcnt wait
 }
 #define DDP_STAMP(kid, slot)                                                                 \
   do {                                                                                       \
     unsigned long long* _sb = g_stamp_buf;                                                   \
-    if (_sb && threadIdx.x == 0) {                                                           \
-      const unsigned _blk = blockIdx.x + blockIdx.y * gridDim.x;                             \
-      if (_blk < 4096)                                                                       \
-        _sb[(kid) * STAMP_KSTRIDE + _blk * STAMP_SLOTS + (slot)] = __builtin_amdgcn_s_memrealtime(); \
-    }                                                                                        \
+    if (_sb && threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4096)                    \
+      _sb[(kid) * STAMP_KSTRIDE + blockIdx.x * STAMP_SLOTS + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define DDP_STAMPS_SETTER(name)                                                              \
   void name(void* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &p, sizeof(p)); }
@@ -362,6 +362,95 @@ __device__ __forceinline__ float wave_max(float v) {
 // reading them.  Used by xent_rows (own kernel) and by the XENT prologue of fc_bwd, so
 // both produce bit-identical values.
 constexpr int XENT_MAX_BLK = 16;  // conv blocks per image: HW / CH + 2 <= 16
+// The fc_bwd prologue's variant: the whole partial array (nblk * 2 * NO floats, 15.7 KB
+// at B = 32) is copied to LDS with coalesced 16-byte loads issued FIRST in the kernel,
+// then every logit sums its partials from LDS in the same fixed order.  (Per-logit
+// global loads are 16 scattered 4-byte loads per thread: ~5k lane-addresses per block
+// through the texture addresser, measured ~2 us.)
+constexpr int XENT_PRE_Q = 4;  // float4 per thread held from the prefetch to the LDS write
+struct XentPre {
+  int lab0;
+  float bias_o;  // bias[threadIdx.x % NO]
+  float4 q[XENT_PRE_Q];
+};
+__device__ __forceinline__ void xent_prefetch(const float* __restrict__ part, int npart,
+                                              const float* __restrict__ bias, int NO, int B,
+                                              const int* __restrict__ labels32, const BatchIdx& bi,
+                                              XentPre& pre) {
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const int n4 = npart >> 2;
+#pragma unroll
+  for (int k = 0; k < XENT_PRE_Q; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    pre.q[k] = i < n4 ? p4[i] : make_float4(0.f, 0.f, 0.f, 0.f);  // fully defined: stays in VGPRs
+  }
+  pre.lab0 = (int)threadIdx.x < B ? labels32[bi.row(threadIdx.x, bi.base())] : 0;
+  pre.bias_o = (int)threadIdx.x < B * NO ? bias[threadIdx.x % NO] : 0.f;
+  DDP_STAMP(STAMP_K_XENT, 1);  // loads issued
+}
+// s_part: npart floats of LDS (may alias scratch the caller uses only afterwards).
+__device__ __forceinline__ void xent_finish(const XentPre& pre, const float* __restrict__ part, int npart,
+                                            int HW, int CH, const float* __restrict__ bias, int NO, int B,
+                                            const int* __restrict__ labels32, const BatchIdx& bi,
+                                            float gscale, float* dl, float* loss, float* s_lg, int* s_lab,
+                                            float* s_part) {
+  const int n4 = npart >> 2;
+  float4* s4 = reinterpret_cast<float4*>(s_part);
+#pragma unroll
+  for (int k = 0; k < XENT_PRE_Q; ++k) {
+    const int i = threadIdx.x + k * blockDim.x;
+    if (i < n4) s4[i] = pre.q[k];
+  }
+  for (int i = threadIdx.x + XENT_PRE_Q * blockDim.x; i < n4; i += blockDim.x)
+    s4[i] = reinterpret_cast<const float4*>(part)[i];
+  if ((int)threadIdx.x < B) s_lab[threadIdx.x] = pre.lab0;
+  __syncthreads();
+  DDP_STAMP(STAMP_K_XENT, 2);  // partials in LDS
+  // the thread's first logit uses only prefetched / LDS operands; later logits (B * NO >
+  // blockDim) run in a separate guarded loop - a global load the compiler may hoist into
+  // the first iteration would wait (vmcnt in order) for all of the caller's column loads
+  auto logit_sum = [&](int t) {
+    const int b = t / NO, o = t - (t / NO) * NO;
+    const int p0 = b * HW;
+    const int kb0 = p0 / CH, kb1 = (p0 + HW - 1) / CH;
+    const int slot0 = kb0 * CH == p0 ? 0 : 1;
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < XENT_MAX_BLK; ++j) {
+      const int kb = min(kb0 + j, kb1);
+      const float v = s_part[(kb * 2 + (j == 0 ? slot0 : 0)) * NO + o];
+      a += (kb0 + j <= kb1) ? v : 0.f;
+    }
+    return a;
+  };
+  if ((int)threadIdx.x < B * NO) s_lg[threadIdx.x] = pre.bias_o + logit_sum(threadIdx.x);
+  if (B * NO > (int)blockDim.x)
+    for (int t = threadIdx.x + blockDim.x; t < B * NO; t += blockDim.x) s_lg[t] = bias[t % NO] + logit_sum(t);
+  DDP_STAMP(STAMP_K_FC_BWD, 5);
+  __syncthreads();
+  DDP_STAMP(STAMP_K_FC_BWD, 6);
+  auto row_out = [&](int t, int label) {
+    const int b = t / NO, o = t - (t / NO) * NO;
+    label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
+    const float* x = s_lg + b * NO;
+    float mx = x[0];
+    for (int k = 1; k < NO; ++k) mx = fmaxf(mx, x[k]);
+    float se = 0.f;
+    for (int k = 0; k < NO; ++k) se += __expf(x[k] - mx);
+    const float inv = 1.f / se;
+    dl[t] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
+    if (o == 0) loss[b] = mx + __logf(se) - x[label];
+  };
+  // first logit: b = threadIdx.x / NO < blockDim, so its label is in s_lab (no pointer
+  // select: the compiler would merge LDS / global into one flat load counted in vmcnt)
+  if ((int)threadIdx.x < B * NO) row_out(threadIdx.x, s_lab[threadIdx.x / NO]);
+  if (B * NO > (int)blockDim.x)
+    for (int t = threadIdx.x + blockDim.x; t < B * NO; t += blockDim.x) {
+      const int b = t / NO;
+      row_out(t, b < (int)blockDim.x ? s_lab[b] : labels32[bi.row(b, bi.base())]);
+    }
+  DDP_STAMP(STAMP_K_FC_BWD, 7);
+}
 __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part, int HW, int CH,
                                                  const float* __restrict__ bias, int NO, int B,
                                                  const int* __restrict__ labels32, const BatchIdx& bi,
@@ -369,7 +458,6 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
                                                  int* s_lab) {
   const int base = bi.base();
   const int lab0 = (int)threadIdx.x < B ? labels32[bi.row(threadIdx.x, base)] : 0;
-  DDP_STAMP(STAMP_K_XENT, 1);  // label load issued
   for (int t = threadIdx.x; t < B * NO; t += blockDim.x) {
     // 32-bit index math only (B * HW < 2^31, checked on the host): 64-bit divisions
     // by runtime values are long software sequences.  Block kb0 is the only one that can
@@ -384,22 +472,18 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
       const int kb = min(kb0 + j, kb1);
       v[j] = part[(kb * 2 + (j == 0 ? slot0 : 0)) * NO + o];
     }
-    DDP_STAMP(STAMP_K_XENT, 2);  // partial loads issued
     float a = 0.f;
 #pragma unroll
     for (int j = 0; j < XENT_MAX_BLK; ++j) a += (kb0 + j <= kb1) ? v[j] : 0.f;
-    DDP_STAMP(STAMP_K_XENT, 3);  // partials arrived and summed
     s_lg[t] = bias[o] + a;
   }
-  DDP_STAMP(STAMP_K_FC_BWD, 5);
   if ((int)threadIdx.x < B) s_lab[threadIdx.x] = lab0;
   __syncthreads();
-  DDP_STAMP(STAMP_K_FC_BWD, 6);
   // Phase 2, one thread per logit again: every thread of row b evaluates the row's max
   // and sum-exp in the same serial order (bit-identical values), then its own class.
   for (int t = threadIdx.x; t < B * NO; t += blockDim.x) {
     const int b = t / NO, o = t - (t / NO) * NO;
-    int label = (int)threadIdx.x < B && b < (int)blockDim.x ? s_lab[b] : labels32[bi.row(b, base)];
+    int label = b < (int)blockDim.x ? s_lab[b] : labels32[bi.row(b, base)];
     label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
     const float* x = s_lg + b * NO;
     float mx = x[0];
@@ -410,7 +494,6 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
     dl[t] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
     if (o == 0) loss[b] = mx + __logf(se) - x[label];
   }
-  DDP_STAMP(STAMP_K_FC_BWD, 7);
 }
 
 }  // namespace ddp_amd

@@ -29,8 +29,12 @@
 //  * wgrad: split-K over image-row chunks, one fp32 slab row per block, bias
 //           gradient from an extra MFMA against a ones fragment; fixed-order
 //           reduction in grad_reduce (bitwise reproducible, no float atomics).
+#include <stdexcept>
+
 #include "kernels/common.h"
+#include "kernels/fc_bwd_body.h"
 #include "kernels/launchers.h"
+#include "kernels/slab_reduce.h"
 
 namespace ddp_amd {
 
@@ -60,6 +64,66 @@ __device__ __forceinline__ void stage2(int n1, S1 src1, D1 dst1, int n2, S2 src2
 template <typename SrcFn, typename DstFn>
 __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
   stage2<8>(n, src, dst, 0, src, dst);
+}
+
+// ---- in-launch dZ2 hand-off (fuse level 2: the fc role of the same launch produces dZ2)
+// fc-role block f publishes ready[f] = 1 once its COLS columns of dZ2 (all images) are
+// stored write-through and drained (fc_bwd_body.h); a conv-role block waits for the fc
+// blocks covering its staged pixel range, then reads dZ2 with sc1 loads (L1 bypass)
+// through a buffer resource - the MI355X_MICROARCH.md hand-off table's first row.
+struct DzWait {
+  const int* ready = nullptr;
+  int cols = 0;        // dZ2 columns (hw * C elements) per fc-role block
+  int* err = nullptr;  // set to 1 when a wait times out (the step's results are invalid)
+};
+constexpr unsigned long long DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 MHz clock
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dz_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
+}
+__device__ __forceinline__ bf16x8 ld16_sc1(__amdgpu_buffer_rsrc_t r, long byte_off) {
+  typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+  const i32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16 /* sc1 */);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Fused slab reduction of the conv backward (conv3x3_bwd_kernel<..., FRED>)
+struct BwdReduce {
+  SlabSet ss{};
+  long nchunks = 0;
+  int first_reducer = 0;  // blocks [first_reducer, grid) reduce after the arrival count
+  int* done = nullptr;  // 8 arrival counters, 32 ints apart (zeroed by the step's forward)
+  int* err = nullptr;   // set to 2 when the wait times out
+};
+
+// Block-wide wait until every fc-role block whose columns cover the flattened pixels
+// [p0, p1) (at most two images' hw ranges, p1 - p0 <= HW) has published.  Wave 0 polls
+// with sc1 loads (one flag per lane), sleeping between polls; then a block barrier.
+__device__ __noinline__ void wait_dz2(DzWait dw, long p0, long p1, int HW, int C) {
+  if ((threadIdx.x >> 6) == 0 && p0 < p1) {
+    const int lane = threadIdx.x & 63;
+    const long n0 = p0 / HW;
+    const long e0 = p1 < (n0 + 1) * HW ? p1 : (n0 + 1) * HW;
+    const int a0 = (int)(p0 - n0 * HW), a1 = (int)(e0 - n0 * HW);  // hw [a0, a1)
+    const int b1 = (int)(p1 - e0);                                  // next image: hw [0, b1)
+    const int fa0 = (int)((long)a0 * C / dw.cols), fa1 = (int)(((long)a1 * C - 1) / dw.cols);
+    const int fb1 = b1 > 0 ? (int)(((long)b1 * C - 1) / dw.cols) : -1;
+    int* rd = const_cast<int*>(dw.ready);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      int ok = 1;
+      for (int f = fa0 + lane; f <= fa1; f += 64) ok &= __hip_atomic_load(rd + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      for (int f = lane; f <= fb1; f += 64) ok &= __hip_atomic_load(rd + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      if (__all(ok)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > DZ_WAIT_TICKS) {
+        if (lane == 0 && dw.err) __hip_atomic_store(dw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
 }
 
 // Geometry specialisation: kernels take <GH, GW, GCI, GCO>; non-zero values replace
@@ -126,6 +190,8 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 
   const int wc = KW / CE;
   const int xc = Cin / CE;
+  if (A1X && c1.zero_i32)  // the step's level-2 hand-off flags (see C1Src)
+    for (int i = threadIdx.x; i < c1.zero_per_block; i += NT) c1.zero_i32[(long)blockIdx.x * c1.zero_per_block + i] = 0;
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave & 3);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
@@ -338,12 +404,16 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 // ---------------------------------------------------------------- data gradient
 // A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
 // being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
+// WAITDZ (fuse level 2): dY (= dZ2) is produced by the fc role of the same launch; the
+// block stages everything that does not depend on it first (weights, x0, the ReLU1 mask),
+// then waits for its pixel range (wait_dz2) and stages dY with sc1 loads.
 template <typename T, int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI,
-          int GCO>
+          int GCO, bool WAITDZ = false>
 __device__ __forceinline__ void dgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ WT,
     const T* __restrict__ Xact, T* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
-    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by) {
+    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by,
+    const DzWait& dzw = DzWait()) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int CE = P::CE;
@@ -387,7 +457,7 @@ __device__ __forceinline__ void dgrad_body(
             return ld16(WT + ((long)tap * Cin + ci_blk + r) * Cout + co);
           },
           [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * CE; st16(sWT + r * WS + c, v); },
-          XR * cpc,
+          WAITDZ ? 0 : XR * cpc,
           [&](int i) {
             const int r = i / cpc, c = (i - r * cpc) * CE;
             const long Pq = Pbase + r;
@@ -432,6 +502,19 @@ __device__ __forceinline__ void dgrad_body(
       s_m1[lp * 4 + g] = (unsigned char)m;
     }
     DDP_STAMP(STAMP_K_CONV1, 2);  // mask computed
+  }
+  if constexpr (WAITDZ) {
+    static_assert(!F32 && !MASK_DY, "the in-launch dZ2 hand-off is bf16, unmasked");
+    wait_dz2(dzw, Pbase > 0 ? Pbase : 0, Pbase + XR < Ptot ? Pbase + XR : Ptot, HW, Cout);
+    const __amdgpu_buffer_rsrc_t rs = dz_rsrc(dY, Ptot * Cout * (long)sizeof(T));
+    stage2<16>(XR * cpc,
+               [&](int i) {
+                 const int r = i / cpc, c = (i - r * cpc) * CE;
+                 const long Pq = Pbase + r;
+                 return (Pq >= 0 && Pq < Ptot) ? ld16_sc1(rs, (Pq * Cout + c) * (long)sizeof(T)) : zero8();
+               },
+               [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * CE; st16(sDY + r * DS + c, v); },
+               0, [&](int) { return zero8(); }, [&](int, bf16x8) {});
   }
 
   const int kofs = P::kofs(lane);
@@ -600,10 +683,17 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // so each lane reads single floats - MFMA j takes slot s0 + 4j + (lane >> 4) - with row
 // strides of 16 mod 32 dwords (Cout + 16, Cin + 16), conflict-free for ds_read_b32's two
 // 32-lane groups (lanes l and l + 16 read adjacent slots).
-template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO>
+// WAITDZ (fuse level 2): X staging / the conv1 recompute first, then wait_dz2 for the
+// block's rows and the dY staging with sc1 loads (see dgrad_body).
+// STAGE: the slab row goes through LDS (needs slab-row bytes of LDS, see conv3x3_bwd_lds)
+// and leaves as 16-byte write-through stores - from the MFMA layout each lane holds one
+// float per 64-byte run of the row, and 4-byte write-through stores took ~2.4 us per block.
+template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO, bool WAITDZ = false,
+          bool STAGE = false>
 __device__ __forceinline__ void wgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ X,
-    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by) {
+    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by,
+    const DzWait& dzw = DzWait()) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int CE = Prec<T>::CE;
   DDP_STAMP(STAMP_K_WGRAD, 0);
@@ -623,7 +713,7 @@ __device__ __forceinline__ void wgrad_body(
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
   // ---- stage dY rows (masked) and X rows with halo: one round of loads
   const int cpy_dy = Cout / CE, cpy_x = Cin / CE;
-  stage2<F32 ? 32 : 16>(nslot * cpy_dy,
+  stage2<F32 ? 32 : 16>(WAITDZ ? 0 : nslot * cpy_dy,
           [&](int i) {
             const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
             const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
@@ -676,6 +766,26 @@ __device__ __forceinline__ void wgrad_body(
           return sxx[(rr + k / 3) * XW2 + cc + k % 3];
         },
         [&](int pos, int g) { return sX + (long)pos * XS + 8 * g; });
+  }
+  if constexpr (WAITDZ) {
+    static_assert(!F32 && !MASK_DY, "the in-launch dZ2 hand-off is bf16, unmasked");
+    const long pimg = (long)n * H * W;
+    wait_dz2(dzw, pimg + (long)r0 * W, pimg + (long)(r0 + R < H ? r0 + R : H) * W, H * W, Cout);
+    const __amdgpu_buffer_rsrc_t rs = dz_rsrc(dY, (long)B * H * W * Cout * (long)sizeof(T));
+    stage2<16>(nslot * cpy_dy,
+               [&](int i) {
+                 const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
+                 const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
+                 const int hh = r0 + r;
+                 return (r < R && hh < H && c < W)
+                            ? ld16_sc1(rs, ((((long)n * H + hh) * W + c) * Cout + ch) * (long)sizeof(T))
+                            : zero8();
+               },
+               [&](int i, bf16x8 v) {
+                 const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
+                 st16(sdY + (long)slot * DS + ch, v);
+               },
+               0, [&](int) { return zero8(); }, [&](int, bf16x8) {});
   }
   __syncthreads();
   DDP_STAMP(STAMP_K_WGRAD, 2);
@@ -753,16 +863,47 @@ __device__ __forceinline__ void wgrad_body(
 
   DDP_STAMP(STAMP_K_WGRAD, 3);
   // ---- slab row: [Cout][3][3][Cin] (OHWI, the weight's native layout) then [Cout] bias
-  float* out = slab + (long)bx * ((long)Cout * 9 * Cin + Cout);
+  const long row = (long)Cout * 9 * Cin + Cout;
+  float* out = slab + (long)bx * row;
+  if constexpr (STAGE) {
+    __syncthreads();  // every wave is done with the staged tiles
+    float* srow = reinterpret_cast<float*>(smem);
+    // LDS position of row element e (output channel co): e + 16 * (co / 4), bias block
+    // + 16 * Cout / 4.  The 4 output rows of an MFMA lane group sit 4 * 9 * Cin floats
+    // apart (a multiple of the 64 banks); the skew spreads them over 4 bank quarters, and
+    // keeps runs of 4 elements contiguous and 16-byte aligned for the read-back.
+    const int wrow = 9 * Cin;
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = coT + 16 * c + 4 * g + r;
+      for (int r = 0; r < 4; ++r) {
+        const int co = coT + 16 * c + 4 * g + r;
+        const int sk = 16 * (co >> 2);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) st_wt(out + ((long)co * 9 + tap) * Cin + ciT + i16, acc[c][tap][r]);
-      if (ciT == 0 && i16 == 0) st_wt(out + (long)Cout * 9 * Cin + co, accb[c][r]);
+        for (int tap = 0; tap < 9; ++tap) srow[co * wrow + tap * Cin + ciT + i16 + sk] = acc[c][tap][r];
+        if (ciT == 0 && i16 == 0) srow[Cout * wrow + 4 * Cout + co] = accb[c][r];
+      }
+    __syncthreads();
+    // row % 4 == 0 and the slab rows are 16-byte aligned (checked by the launcher)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(row * 4), 0x00020000);
+    typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+    for (int i = threadIdx.x; i < row / 4; i += 256) {
+      const int e = 4 * i;
+      const int pos = e < Cout * wrow ? e + 16 * ((e / wrow) >> 2) : e + 4 * Cout;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, *reinterpret_cast<const float4*>(srow + pos)),
+                                             rs, i * 16, 0, 16 /* sc1: write-through */);
     }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = coT + 16 * c + 4 * g + r;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) st_wt(out + ((long)co * 9 + tap) * Cin + ciT + i16, acc[c][tap][r]);
+        if (ciT == 0 && i16 == 0) st_wt(out + (long)Cout * 9 * Cin + co, accb[c][r]);
+      }
+  }
   DDP_STAMP(STAMP_K_WGRAD, 4);
 }
 
@@ -788,19 +929,120 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // wgrad role needs full a1 tiles with halo and is as fast recomputing as loading.
 // bf16: 2 blocks per CU (<= 256 VGPR+AGPR per lane); fp32 tiles take ~135 KiB of LDS, so
 // one block per CU and the full register file
-template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO>
+// FRED (fused reduction): the last blocks of the grid also do grad_reduce's work
+// (slab_reduce.h).  Every block, once its slab rows are stored write-through and
+// drained, adds 1 to one of 8 per-XCD-sharded counters (red.done[32 * (blockIdx % 8)],
+// zeroed by the step's forward); the blocks from red.first_reducer on then wait until all
+// blocks have arrived and reduce the 64-output chunks w, w + nr, ... (sc1 loads, grad_
+// reduce's fixed order: bit-identical) with the fused SGD / shadows.  Deadlock-free: the
+// blocks below first_reducer never wait, a waiting block has already arrived, and the
+// host keeps the reducers within half the resident capacity (they are dispatched last,
+// each into a slot it can hold while the rest are dispatched).
+template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kernel(
     const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
-    int R, int nd, C1Src c1, const T* __restrict__ Xact) {
+    int R, int nd, C1Src c1, const T* __restrict__ Xact, BwdReduce red) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < nd)
     dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
         dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem,
         blockIdx.x, 0);
   else
-    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H, W, Cin,
-                                                 Cout, R, c1, smem, blockIdx.x - nd, 0);
+    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, false, true>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H, W,
+                                                              Cin, Cout, R, c1, smem, blockIdx.x - nd, 0);
+  if constexpr (FRED) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(red.done + 32 * (blockIdx.x & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)blockIdx.x < red.first_reducer) return;
+    // reducer w of nr: the LAST nr blocks of the grid (dispatched last; the host keeps nr
+    // within half the resident capacity, so they never starve a block they wait for)
+    const int w = blockIdx.x - red.first_reducer, nw = gridDim.x - red.first_reducer;
+    const int nblk = gridDim.x;
+    constexpr int J = 3;  // chunks per reducer pass (thread t < 64 * J finalises one output of chunk t >> 6)
+    SlabFusedPlan<J> pl;
+    slab_fused_plan<J>(red.ss, w, nw, red.nchunks, pl);  // index work + SGD operands before the wait
+    DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
+    if (threadIdx.x < 64) {  // wave 0 polls the 8 shards (sc1 loads), sleeping between polls
+      const int lane = threadIdx.x;
+      const int want = nblk;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {
+        const int v = lane < 8 ? __hip_atomic_load(red.done + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        int tot = 0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) tot += __builtin_amdgcn_readlane(v, l);
+        if (tot >= want) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > DZ_WAIT_TICKS) {
+          if (lane == 0 && red.err) __hip_atomic_store(red.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
+    float* part = reinterpret_cast<float*>(smem);
+    slab_fused_run<J>(red.ss, pl, part);
+    for (long q0 = w + (long)J * nw; q0 < red.nchunks; q0 += (long)J * nw) {  // few wgrad blocks: more passes
+      slab_fused_plan<J>(red.ss, q0, nw, red.nchunks, pl);
+      slab_fused_run<J>(red.ss, pl, part);
+    }
+    if (w == 0 && threadIdx.x == 0 && red.ss.step_ctr) red.ss.step_ctr[0] += 1;
+    DDP_STAMP(STAMP_K_GRAD_REDUCE, 2);
+  }
+}
+
+// ---------------------------------------------------------------- fused fc + conv backward
+// Fuse level 2 (bf16, single process): the fc backward and the whole conv backward in ONE
+// launch.  Blocks [0, nfc) are the fc role (fc_bwd_body.h: cross-entropy prologue, dZ2,
+// fc weight gradient + fused SGD; 4 waves x 2 virtual waves, bit-identical to the 8-wave
+// fc_bwd kernel) and publish their dZ2 columns; blocks [nfc, nfc + nd) the data gradient,
+// the rest the weight gradient.  The conv roles stage what does not depend on dZ2
+// (weights, uint8 images, the conv1 recompute / ReLU1 mask) while the fc role runs, then
+// wait for the fc blocks of their own pixel range (no kernel boundary between them).
+// Deadlock-free by dispatch order: the fc blocks have the lowest indices and never wait,
+// so every fc block is dispatched before any conv block can occupy a slot it needs.
+struct FcConvBwdArgs {
+  // fc role
+  const bf16_t* a2 = nullptr;
+  const bf16_t* wfc = nullptr;  // bf16 [NO][HW*C] shadow
+  bf16_t* dz2 = nullptr;
+  float* dW = nullptr;
+  float scale = 1.f;
+  long K = 0;
+  FcBwdExtras ex{};
+  int nfc = 0;
+  // conv roles
+  const bf16_t* w2t = nullptr;
+  float* w1slab = nullptr;
+  float* w2slab = nullptr;
+  int B = 0, H = 0, W = 0, Cin = 0, Cout = 0, R = 0, nd = 0;
+  C1Src c1{};
+  const bf16_t* Xact = nullptr;
+  DzWait dzw{};
+};
+constexpr int FCC_WPB = 4, FCC_VW = 8, FCC_CPL = 2;
+
+template <int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO>
+__global__ __launch_bounds__(256, 2) void fc_conv_bwd_kernel(FcConvBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bx = blockIdx.x;
+  if (bx < a.nfc) {
+    fc_bwd_body<bf16_t, true, true, 10, FCC_WPB, FCC_VW, FCC_CPL>(
+        nullptr, a.a2, a.wfc, a.dz2, a.dW, a.scale, a.B, a.K, 10, a.ex, reinterpret_cast<float*>(smem), bx,
+        const_cast<int*>(a.dzw.ready));
+  } else if (bx < a.nfc + a.nd) {
+    dgrad_body<bf16_t, PXT, false, true, true, DA1X, GH, GW, GCI, GCO, true>(
+        a.dz2, nullptr, a.w2t, DA1X ? nullptr : a.Xact, nullptr, a.B, a.H, a.W, a.Cin, a.Cout, a.c1.x, 1, a.c1.bi,
+        a.w1slab, a.c1, smem, bx - a.nfc, 0, a.dzw);
+  } else {
+    wgrad_body<bf16_t, false, WA1X, GH, GW, GCI, GCO, true>(a.dz2, nullptr, WA1X ? nullptr : a.Xact, a.w2slab, a.B,
+                                                          a.H, a.W, a.Cin, a.Cout, a.R, a.c1, smem,
+                                                          bx - a.nfc - a.nd, 0, a.dzw);
+  }
 }
 
 // ---------------------------------------------------------------- launchers
@@ -982,29 +1224,77 @@ void conv3x3_wgrad(const float* dY, const float* Yact, const float* X, float* sl
 
 size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es) {
   const size_t a = conv3x3_dgrad_lds(W, Cout, pxt, true, es), b = conv3x3_wgrad_lds(W, Cin, Cout, R, true, es);
-  return a > b ? a : b;
+  // the wgrad role's staged slab row (+ its bank skew, 4 floats per output channel)
+  const size_t row = sizeof(float) * ((size_t)Cout * 9 * Cin + Cout + 4 * (size_t)Cout);
+  const size_t m = a > b ? a : b;
+  return m > row ? m : row;
+}
+
+// Resident-block budget of the fused reduction: every waiting (reducer) block holds a
+// slot, so the reducers are at most HALF of the launch's resident capacity (occupancy API
+// x CUs; other kernels, e.g. a concurrent all-reduce, may take slots).  Returns the
+// number of reducers (the last blocks of the grid), 0 if the capacity is unknown.
+template <typename K>
+static int fused_reducers(K kernel, size_t lds, int nblocks) {
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), 256, lds) != hipSuccess)
+    return 0;
+  const int half = occ * cus / 2;
+  return nblocks < half ? nblocks : half;
 }
 
 template <typename T>
-static void bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
+static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
                        int Cin, int Cout, int pxt, int R, const C1Src& c1, const T* Xact,
-                       bool wgrad_load_a1, hipStream_t s) {
+                       bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err) {
   const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = conv3x3_wgrad_blocks(B, H, R);
   const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
   const bool g = simplecnn_geom(H, W, Cin, Cout);
+  if (((long)Cout * 9 * Cin + Cout) % 4 != 0 || (reinterpret_cast<uintptr_t>(slab) & 15) != 0)
+    throw std::runtime_error("conv3x3_bwd: slab rows must be 16-byte multiples on a 16-byte aligned buffer");
+  BwdReduce red;
+  if (fused) {
+    // the reducer's 16-byte row loads need n >= 4; its summation order is grad_reduce's
+    // 16-row-group one (deep slabs; shallow ones keep the separate kernel)
+    if (grad_reduce_groups(*fused) != 16) fused = nullptr;
+    for (int k = 0; fused && k < fused->count; ++k)
+      if (fused->s[k].n < 4) fused = nullptr;
+  }
+  if (fused) {
+    lds_optin(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds);
+    // reducers: the wgrad blocks (they finish last; extra early-finishing reducers measured
+    // slower - their polling shares the CUs of the still-running wgrad blocks)
+    const int nr = (g && red_done) ? fused_reducers(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds, nw) : 0;
+    if (nr <= 0) fused = nullptr;  // the caller reduces with grad_reduce
+    else red.first_reducer = nd + nw - nr;
+  }
+  if (fused) {
+    red.ss = *fused;
+    red.nchunks = slab_chunks(*fused);
+    red.done = red_done;
+    red.err = red_err;
+    if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");
+  }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
 #define LBW(PX, DA, WA)                                                                             \
   do {                                                                                              \
-    if (g) {                                                                                        \
-      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64>;                                   \
+    if (g && fused) {                                                                               \
+      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true>;                             \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
-                         Cout, R, nd, c1, Xact);                                                    \
+                         Cout, R, nd, c1, Xact, red);                                               \
+    } else if (g) {                                                                                 \
+      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false>;                            \
+      lds_optin(k, lds);                                                                            \
+      hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
+                         Cout, R, nd, c1, Xact, red);                                               \
     } else {                                                                                        \
-      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0>;                                       \
+      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0, false>;                                \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
-                         Cout, R, nd, c1, Xact);                                                    \
+                         Cout, R, nd, c1, Xact, red);                                               \
     }                                                                                               \
   } while (0)
   // Xact given: the dgrad role reads it; the wgrad role reads it only if wgrad_load_a1
@@ -1012,17 +1302,60 @@ static void bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   else if (wgrad_load_a1) { if (pxt == 2) LBW(2, false, false); else LBW(1, false, false); }
   else { if (pxt == 2) LBW(2, false, true); else LBW(1, false, true); }
 #undef LBW
+  return fused != nullptr;
 }
 
-void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
+bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
-                 bool wgrad_load_a1, hipStream_t s) {
-  bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s);
+                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err) {
+  return bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
+                     fused_reduce, red_done, red_err);
 }
-void conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
+bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
-                 bool wgrad_load_a1, hipStream_t s) {
-  bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s);
+                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err) {
+  return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
+                    fused_reduce, red_done, red_err);
+}
+
+int fc_conv_bwd_fc_blocks(long K) { return (int)((K + 64 * FCC_CPL - 1) / (64 * FCC_CPL)); }
+int fc_conv_bwd_cols() { return 64 * FCC_CPL; }
+
+void fc_conv_bwd(const bf16_t* a2, const bf16_t* wfc, bf16_t* dz2, float* dW, float scale, long K,
+                 const FcBwdExtras& ex, const bf16_t* w2t, float* w1slab, float* w2slab, int B, int H, int W,
+                 int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact, bool wgrad_load_a1,
+                 const int* ready, int* err, hipStream_t s) {
+  if (!ex.part || K != (long)H * W * Cout || (long)K % (64 * FCC_CPL) != 0)
+    throw std::runtime_error("fc_conv_bwd: needs the cross-entropy prologue and K = H*W*C, a multiple of the fc columns");
+  if (64L * pxt + 2 * W + 2 > (long)H * W || (long)(R < H ? R : H) * W > (long)H * W)
+    throw std::runtime_error("fc_conv_bwd: a conv block's pixel range must fit one image");
+  FcConvBwdArgs a;
+  a.a2 = a2; a.wfc = wfc; a.dz2 = dz2; a.dW = dW; a.scale = scale; a.K = K; a.ex = ex;
+  a.nfc = fc_conv_bwd_fc_blocks(K);
+  a.w2t = w2t; a.w1slab = w1slab; a.w2slab = w2slab;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.R = R;
+  a.nd = conv3x3_dgrad_blocks(B, H, W, pxt);
+  a.c1 = c1; a.Xact = Xact;
+  a.dzw.ready = ready; a.dzw.cols = 64 * FCC_CPL; a.dzw.err = err;
+  const int nw = conv3x3_wgrad_blocks(B, H, R);
+  const long npart = ((long)B * ex.HW + ex.CH - 1) / ex.CH * 2 * 10;
+  const size_t fc_lds = sizeof(float) * (size_t)fcb_lds_floats(B, 10, true, npart, fcb_red_floats<FCC_WPB, 10, FCC_CPL>());
+  const size_t cv_lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, 2);
+  const size_t lds = fc_lds > cv_lds ? fc_lds : cv_lds;
+  if (lds > 160 * 1024) throw std::runtime_error("fc_conv_bwd: LDS over 160 KiB");
+  if (!(H == 28 && W == 28 && Cin == 32 && Cout == 64))
+    throw std::runtime_error("fc_conv_bwd: built for SimpleCNN's conv2 (28x28, 32 -> 64)");
+  const dim3 grid((unsigned)(a.nfc + a.nd + nw));
+#define LFC(PX, DA, WA)                                                                               \
+  do {                                                                                                \
+    auto k = fc_conv_bwd_kernel<PX, DA, WA, 28, 28, 32, 64>;                                          \
+    lds_optin(k, lds);                                                                                \
+    hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);                                                \
+  } while (0)
+  if (!Xact) { if (pxt == 2) LFC(2, true, true); else LFC(1, true, true); }
+  else if (wgrad_load_a1) { if (pxt == 2) LFC(2, false, false); else LFC(1, false, false); }
+  else { if (pxt == 2) LFC(2, false, true); else LFC(1, false, true); }
+#undef LFC
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv3x3)

@@ -42,13 +42,23 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // fused level-1 conv backward (dgrad + conv1 wgrad slabs, and conv2 wgrad slabs) in one
 // launch; Cin == 32 (conv1's channels), (Cout / 32) * (Cin / 16) == 4
 // Xact != null: the dgrad role reads the forward's stored a1 (C1Src::a1_out) for its ReLU
-// mask instead of recomputing conv1; the wgrad role too when wgrad_load_a1
-void conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
+// mask instead of recomputing conv1; the wgrad role too when wgrad_load_a1.
+// fused_reduce != null: the same launch also does grad_reduce(*fused_reduce) (the wgrad
+// blocks reduce the slabs after an in-launch arrival count, red_done: 8 counters 32 ints
+// apart, zeroed beforehand - by the step's forward, C1Src::zero_i32); red_err[0] = 2 if
+// that wait timed out.  SimpleCNN geometry only, and only while the wgrad blocks fit in
+// half the launch's resident capacity; returns whether the reduction was fused (false:
+// the caller runs grad_reduce).
+struct SlabSet;
+constexpr int SYNC_RED_INTS = 256;  // ints of the 8 arrival counters (32 apart) of red_done
+bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
-                 bool wgrad_load_a1, hipStream_t s);
-void conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
+                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
+                 int* red_done = nullptr, int* red_err = nullptr);
+bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
-                 bool wgrad_load_a1, hipStream_t s);
+                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
+                 int* red_done = nullptr, int* red_err = nullptr);
 size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false, int es = 2);
@@ -159,12 +169,23 @@ struct FcBwdExtras {
   int frag_HW = 0, frag_C = 0;
   int sys_store = 0;  // dW / dbias with system-scope stores (read by peers over xGMI)
 };
-size_t fc_bwd_lds(int B, int NO, bool xent);
+size_t fc_bwd_lds(int B, int NO, bool xent, long npart = 0);  // npart: see linear.hip
 void noop(int blocks, int* sink, hipStream_t s);
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
 void fc_bwd(const float* dL, const float* X, const float* Wf, float* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
+
+// Fuse level 2 (bf16, single process): fc backward (cross-entropy prologue, dZ2, dW /
+// fused SGD, as fc_bwd with ex.part set) and the conv backward (as conv3x3_bwd) in ONE
+// launch, with an in-launch dZ2 hand-off through ready[fc_conv_bwd_fc_blocks(K)] flags
+// (zeroed by the step's conv3x3_fwd, C1Src::zero_i32); err[0] = 1 if a wait timed out.
+int fc_conv_bwd_fc_blocks(long K);
+int fc_conv_bwd_cols();
+void fc_conv_bwd(const bf16_t* a2, const bf16_t* wfc, bf16_t* dz2, float* dW, float scale, long K,
+                 const FcBwdExtras& ex, const bf16_t* w2t, float* w1slab, float* w2slab, int B, int H, int W,
+                 int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact, bool wgrad_load_a1,
+                 const int* ready, int* err, hipStream_t s);
 
 // ---- cross-entropy --------------------------------------------------------------------
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,
@@ -228,6 +249,8 @@ struct SlabSet {
 void sgd_step(float* p, const float* g, float* mbuf, long n, const SgdArgs& a, const ShadowSet& sh,
               int* step_ctr, hipStream_t s);
 void grad_reduce(const SlabSet& ss, hipStream_t s);
+// row groups (16 or 4) of the fixed summation order grad_reduce uses for this SlabSet
+int grad_reduce_groups(const SlabSet& ss);
 void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s);
 
 // ---- direct two-shot xGMI all-reduce (allreduce.hip) ----------------------------------

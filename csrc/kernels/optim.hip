@@ -12,6 +12,7 @@
 // gradient-bucket views, prescaled by 1/world_size (DDP averaging).
 #include "kernels/common.h"
 #include "kernels/launchers.h"
+#include "kernels/slab_reduce.h"
 
 namespace ddp_amd {
 
@@ -111,71 +112,17 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   DDP_STAMP(STAMP_K_SGD, 1);
 }
 
-// Block = 64 consecutive outputs x GR row groups (GR waves): thread (c, g) sums rows g,
-// g + GR, ... with up to 8 loads in flight, then the GR group sums are added in fixed
-// order via LDS (bitwise reproducible).  GR = 16 (1024 threads) puts a whole 128-row
-// slab column block in flight at once: the kernel reads ~9.5 MB of split-K slabs per
-// SimpleCNN step, and with 4 groups it was latency-bound at ~4.7 GB/s per CU.
+// Block = 64 consecutive outputs x GR row groups (GR waves, one group each): the
+// fixed-order chunk reduction of slab_reduce.h.  GR = 16 (1024 threads) puts a whole
+// 128-row slab column block in flight at once: the kernel reads ~9.5 MB of split-K slabs
+// per SimpleCNN step, and with 4 groups it was latency-bound at ~4.7 GB/s per CU.
 template <int GR>
 __global__ __launch_bounds__(64 * GR) void grad_reduce_kernel(SlabSet ss) {
-  __shared__ float part[GR][64];
+  __shared__ float part[GR * 64];
   DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
-  const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  // segments are laid out back to back, each padded to a multiple of 64 outputs, so
-  // a block (64 outputs) never straddles two segments
-  long i = (long)blockIdx.x * 64 + c;
-  int k = 0;
-  for (; k < ss.count; ++k) {
-    const long padded = (ss.s[k].n + 63) / 64 * 64;
-    if (i < padded) break;
-    i -= padded;
-  }
-  const bool live = k < ss.count && i < ss.s[k].n;
-  // fused-SGD operands first (same round trip as the slab loads)
-  float p0 = 0.f, m0 = 0.f;
-  if (ss.sgd.update && live && grp == 0 && ss.s[k].p) {
-    p0 = ss.s[k].p[i];
-    m0 = ss.s[k].m ? ss.s[k].m[i] : 0.f;
-  }
-  float acc = 0.f;
-  if (live) {
-    const SlabSeg& sg = ss.s[k];
-    const float* src = sg.slab + sg.src_off + i;
-    float a[8];
-    int r = grp;
-    for (; r + 7 * GR < sg.rows; r += 8 * GR) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] = src[(long)(r + GR * u) * sg.row_stride];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += a[u];
-    }
-    for (; r < sg.rows; r += GR) acc += src[(long)r * sg.row_stride];
-  }
-  part[grp][c] = acc;
-  __syncthreads();
-  if (grp == 0 && live) {
-    const SlabSeg& sg = ss.s[k];  // k is block-uniform
-    float g = part[0][c];
-#pragma unroll
-    for (int q = 1; q < GR; ++q) g += part[q][c];
-    g *= sg.scale;
-    if (sg.accum) g += sg.dst[i];
-    if (ss.sys_store) st_sys(sg.dst + i, g);
-    else sg.dst[i] = g;
-    if (ss.sgd.update && sg.p) {  // single-process step: the gradient is final -> fused SGD
-      float m = m0;
-      const float pn = sgd_one(p0, g, &m, ss.sgd);
-      sg.p[i] = pn;
-      if (sg.m) sg.m[i] = m;
-      if (sg.sh) sg.sh[i] = f2bf(pn);
-      if (sg.sh_t || sg.sh_t32) {  // OHWI [co][tap][ci] -> [tap][ci][co]
-        const long per = (long)sg.t_taps * sg.t_ci;
-        const long co = i / per;
-        if (sg.sh_t) sg.sh_t[(i - co * per) * sg.t_co + co] = f2bf(pn);
-        if (sg.sh_t32) sg.sh_t32[(i - co * per) * sg.t_co + co] = pn;
-      }
-    }
-  }
+  float p0, m0;
+  slab_sgd_prefetch(ss, blockIdx.x, p0, m0, threadIdx.x < 64);  // same round trip as the slab loads
+  slab_reduce_chunk<GR, 64 * GR, false>(ss, blockIdx.x, part, p0, m0);
   if (ss.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) ss.step_ctr[0] += 1;
   DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
 }
@@ -227,6 +174,12 @@ __global__ __launch_bounds__(256) void slab_reduce_rows_kernel(SlabSeg sg) {
   }
 }
 
+int grad_reduce_groups(const SlabSet& ss) {
+  int max_rows = 0;
+  for (int k = 0; k < ss.count; ++k) max_rows = ss.s[k].rows > max_rows ? ss.s[k].rows : max_rows;
+  return max_rows >= 64 ? 16 : 4;
+}
+
 void grad_reduce(const SlabSet& ss, hipStream_t s) {
   if (ss.count == 1 && !ss.sgd.update && !ss.sys_store && !ss.step_ctr && ss.s[0].rows <= 16 &&
       ss.s[0].n % 4 == 0 && ss.s[0].row_stride % 4 == 0 && ss.s[0].src_off % 4 == 0 &&
@@ -235,15 +188,10 @@ void grad_reduce(const SlabSet& ss, hipStream_t s) {
     hipLaunchKernelGGL(slab_reduce_rows_kernel, dim3((unsigned)(b < 4096 ? b : 4096)), dim3(256), 0, s, ss.s[0]);
     return;
   }
-  long blocks = 0;
-  int max_rows = 0;
-  for (int k = 0; k < ss.count; ++k) {
-    blocks += (ss.s[k].n + 63) / 64;
-    max_rows = ss.s[k].rows > max_rows ? ss.s[k].rows : max_rows;
-  }
+  const long blocks = slab_chunks(ss);
   if (blocks == 0) return;
   // deep slabs: 16 row groups per block (all rows in flight); shallow ones: 4
-  if (max_rows >= 64)
+  if (grad_reduce_groups(ss) == 16)
     hipLaunchKernelGGL(grad_reduce_kernel<16>, dim3((unsigned)blocks), dim3(1024), 0, s, ss);
   else
     hipLaunchKernelGGL(grad_reduce_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, s, ss);

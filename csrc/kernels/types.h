@@ -48,6 +48,10 @@ struct C1Src {
   // conv3x3_fwd only (optional): also store the recomputed a1 of the block's own pixels
   // (NHWC bf16, [B*H*W][Cin]) so the backward reads it instead of recomputing conv1
   bf16_t* a1_out = nullptr;
+  // conv3x3_fwd only (optional): block b zeroes zero_i32[b * zero_per_block ...] - the
+  // step's in-launch hand-off flags (fuse level 2), reset by the step's first kernel
+  int* zero_i32 = nullptr;
+  int zero_per_block = 0;
 };
 
 // torch.optim.SGD hyper-parameters of one step (first_step: momentum buffer init;

@@ -42,8 +42,8 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   if (cfg_.C2 % 64 != 0) throw std::runtime_error("engine: C2 must be a multiple of 64");
   if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
   if (cfg_.NO != 10) throw std::runtime_error("engine: the fused fc epilogue is built for 10 classes");
-  if (cfg_.f32 && (cfg_.fuse_level != 1 || cfg_.store_a1 != 0))
-    throw std::runtime_error("engine: fp32 mode needs fuse_level 1 and store_a1 0");
+  if (cfg_.f32 && (cfg_.fuse_level < 1 || cfg_.store_a1 != 0))
+    throw std::runtime_error("engine: fp32 mode needs fuse_level >= 1 (runs the level-1 chain) and store_a1 0");
   if (cfg_.f32 && !(b_.a2_f32 && b_.dz2_f32 && b_.w2t_f32))
     throw std::runtime_error("engine: fp32 mode needs the a2 / dz2 / w2t fp32 buffers");
   // bucket plan: in-range, ordered, non-overlapping; stage by the first conv gradient
@@ -83,7 +83,21 @@ void SimpleCNNEngine::destroy_graph() {
   graph_steps_ = 0;
 }
 
-void SimpleCNNEngine::synchronize() { DDP_HIP_CHECK(hipStreamSynchronize(cs_)); }
+void SimpleCNNEngine::synchronize() {
+  DDP_HIP_CHECK(hipStreamSynchronize(cs_));
+  if (b_.sync_err) {
+    int e = 0;
+    DDP_HIP_CHECK(hipMemcpy(&e, b_.sync_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) throw std::runtime_error(std::string("engine: an in-launch hand-off wait timed out (") +
+                                    (e == 1 ? "level-2 dZ2" : "fused slab reduction") + "); results invalid");
+  }
+}
+
+bool SimpleCNNEngine::level2_active() const {
+  const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
+  const bool dist = use_x || (comm_ && (comm_->world() > 1 || cfg_.force_allreduce));
+  return cfg_.fuse_level >= 2 && !cfg_.f32 && !dist && cfg_.fuse_opt && b_.sync_flags && b_.sync_err;
+}
 
 void SimpleCNNEngine::refresh_shadows() {
   SgdArgs a{0.f, 0.f, 0.f, 0.f, 0, 0, 0, /*update=*/0};
@@ -136,6 +150,15 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   c1.yb_out = b_.yb;
   c1.labels = b_.labels;
   if (cfg_.store_a1) c1.a1_out = b_.a1;
+  const bool l2 = level2_active();
+  const bool fred = f1 && !l2 && cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
+  const long n_fc = (long)NO * HW * C2;
+  if (l2 || fred) {  // the forward resets the step's hand-off counters / flags
+    const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
+    const int nsync = SYNC_RED_INTS + (l2 ? fc_conv_bwd_fc_blocks((long)HW * C2) : 0);
+    c1.zero_i32 = b_.sync_flags;
+    c1.zero_per_block = (nsync + nfwd - 1) / nfwd;
+  }
   const C1Src* pc1 = f1 ? &c1 : nullptr;
   BatchIdx bid{nullptr, nullptr, 0, 0};
   bid.n_rows = B;
@@ -173,7 +196,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // optimizer runs in the epilogues of the kernels that finish each gradient (fc weight:
   // fc_bwd; convs + fc bias: grad_reduce) and the separate SGD pass disappears
   const bool fopt = !dist && cfg_.fuse_opt;
-  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2, n_fc = (long)NO * HW * C2;
+  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
   const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
                    cfg_.maximize, first_momentum_step ? 1 : 0, 1};
   float* M = b_.momentum;  // null when momentum == 0
@@ -188,8 +211,15 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ex.frag_C = C2;
   }
   // (fused optimizer: the fc weight gradient is consumed in registers and not stored)
-  fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
-         (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+  if (l2) {
+    // level 2: fc backward + conv backward in one launch (dZ2 handed off inside it)
+    fc_conv_bwd(b_.a2, b_.wfc_bf16, b_.dz2, nullptr, inv_ws, (long)HW * C2, ex, b_.w2t_bf16, b_.w1slab,
+                b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b,
+                cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, b_.sync_flags + SYNC_RED_INTS, b_.sync_err, cs_);
+  } else {
+    fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
+           (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+  }
   // every bf16 shadow; a bucket's fused SGD refreshes the ones inside its range
   ShadowSet sh_all{};
   sh_all.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
@@ -199,16 +229,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   sh_all.count = 4;
   // fc-only buckets: all-reduce (and, over xGMI, the fused SGD) overlaps the conv backward
   if (dist) launch_buckets(0, use_x, sa, M, sh_all);
-  // ---- conv backward (bucket 1)
-  if (f1) {
-    // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
-    conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
-                cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_);
-  } else {
-    conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
-                  b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
-    conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
-  }
+  // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
   SlabSet ss{};
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
   ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, n_w2, wblk, G + b_.off_w2, inv_ws};
@@ -237,7 +258,21 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ss.step_ctr = b_.step_ctr;  // the step's last kernel advances the batch window
   }
   ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
-  grad_reduce(ss, cs_);
+  bool reduced = false;  // the conv backward launch also did grad_reduce's work
+  if (l2) {
+    // (inside fc_conv_bwd)
+  } else if (f1) {
+    // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
+    reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
+                          cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
+                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err);
+  } else {
+    conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
+                  b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
+    conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
+  }
+  if (!reduced) grad_reduce(ss, cs_);
+  last_fused_reduce_ = reduced;
   if (fopt) return;
   if (dist) {
     launch_buckets(1, use_x, sa, M, sh_all);
@@ -299,6 +334,12 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   c1b.bi = bid;
   c1b.w = c1.w;
   c1b.b = c1.b;
+  const bool fred = cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
+  if (fred) {
+    const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
+    c1.zero_i32 = b_.sync_flags;
+    c1.zero_per_block = (SYNC_RED_INTS + nfwd - 1) / nfwd;
+  }
   const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
   const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
                    cfg_.maximize, first_momentum_step ? 1 : 0, 1};
@@ -332,9 +373,7 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
   sh1.count = 1;
   if (dist) launch_buckets(0, use_x, sa, M, sh1);
-  // ---- conv backward (bucket 1)
-  conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
-              cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr), false, cs_);
+  // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
   SlabSet ss{};
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
   ss.s[0] = SlabSeg{b_.w2slab, w2row, 0, n_w2, wblk, G + b_.off_w2, inv_ws};
@@ -361,7 +400,11 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     ss.step_ctr = b_.step_ctr;
   }
   ss.sys_store = use_x ? 1 : 0;
-  grad_reduce(ss, cs_);
+  const bool reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2,
+                                   cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr),
+                                   false, cs_, fred ? &ss : nullptr, b_.sync_flags, b_.sync_err);
+  if (!reduced) grad_reduce(ss, cs_);
+  last_fused_reduce_ = reduced;
   if (fopt) return;
   if (dist) {
     launch_buckets(1, use_x, sa, M, sh1);

@@ -170,6 +170,11 @@ struct EngineBuffers {
   int* step_ctr;
   unsigned char* xb;  // the step's batch, compact: u8 [max_batch][H*W] (fuse level 1)
   int* yb;            // its labels [max_batch]
+  // in-launch hand-offs, zeroed by each step's forward (C1Src::zero_i32): [0, 256) the
+  // fused conv backward's 8 arrival counters (32 ints apart), [256, 256 + fc blocks) the
+  // level-2 dZ2 flags; sync_err: wait-timeout word (0 = ok, 1 = dZ2 wait, 2 = reduction)
+  int* sync_flags = nullptr;
+  int* sync_err = nullptr;
   // data
   const unsigned char* images;  // u8 [N][H*W]
   const int* labels;            // i32 [N]
@@ -187,6 +192,10 @@ struct EngineConfig {
   // 0: 8 kernels (a1 materialised, separate cross-entropy kernel)
   // 1: 6 kernels - conv1 recomputed inside conv2 fwd/dgrad/wgrad from the uint8
   //    images (a1 never touches HBM) and cross-entropy folded into fc_bwd
+  //    (4 per step with the fused optimizer: conv fwd, fc_bwd, conv bwd, grad_reduce)
+  // 2: level 1 with fc_bwd and the conv backward in ONE launch (in-launch dZ2 hand-off,
+  //    fc_conv_bwd) where it applies - bf16, single process, fused optimizer: 3 kernels
+  //    per step; otherwise (world > 1, fp32, fuse_opt 0) the level-1 chain
   int fuse_level = 0;
   // 1: single-process steps apply SGD in the epilogues of fc_bwd / grad_reduce (no
   //    separate optimizer kernel); 0: always the flat SGD kernel (equivalence tests)
@@ -198,6 +207,9 @@ struct EngineConfig {
   // 1: exact fp32 operands everywhere (v_mfma_f32_16x16x4_f32 conv2, fp32 fc, fp32
   //    activations), the reference's precision; needs fuse_level 1 and store_a1 0
   int f32 = 0;
+  // 1: the conv backward launch also reduces the split-K slabs + fused SGD (no separate
+  //    grad_reduce kernel; level >= 1, needs sync_flags); 0: grad_reduce kernel
+  int fuse_reduce = 1;
 };
 
 // Gradient bucket of the engine's data plane: a [off, off + n) range of the flat gradient
@@ -224,7 +236,11 @@ class SimpleCNNEngine {
   int graph_steps() const { return graph_steps_; }
   void destroy_graph();
   hipStream_t stream() const { return cs_; }
-  void synchronize();
+  void synchronize();  // throws if a level-2 hand-off wait timed out
+  bool level2_active() const;
+  // whether the last launched step reduced its weight-gradient slabs inside the conv
+  // backward launch (false: separate grad_reduce kernel)
+  bool last_fused_reduce() const { return last_fused_reduce_; }
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
   // bucket b; set before capturing a graph
@@ -257,6 +273,7 @@ class SimpleCNNEngine {
   hipGraphExec_t graph_exec_ = nullptr;
   int graph_steps_ = 0;
   bool momentum_started_ = false;
+  bool last_fused_reduce_ = false;
 };
 
 }  // namespace ddp_amd

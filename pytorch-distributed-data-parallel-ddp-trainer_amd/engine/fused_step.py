@@ -45,10 +45,16 @@ class EngineOptions:
     first_bucket_mb: float = 1.0   # torch DDP's first-bucket cap (the rest use bucket_cap_mb)
     force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
-    # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd)
+    # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd; 4 with
+    # the fused optimizer); 2: level 1 with fc_bwd and the conv backward in ONE launch
+    # (in-launch dZ2 hand-off) where it applies - bf16, world size 1, fused optimizer: 3
+    # kernels per step; elsewhere the level-1 chain runs
     fuse_level: int = 1
     # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
     fuse_opt: bool = True
+    # level >= 1: the conv backward launch also reduces the split-K weight-gradient slabs
+    # (+ fused SGD) after an in-launch arrival count - no separate grad_reduce kernel
+    fuse_reduce: bool = True
     # level 1: 0 = the conv backward recomputes conv1 from the compact uint8 batch;
     # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
     # wgrad role reads a1 tiles too
@@ -91,8 +97,8 @@ class FusedSimpleCNNEngine:
         if self.opts.dtype not in ("bf16", "fp32"):
             raise ValueError(f"engine dtype must be bf16 or fp32, got {self.opts.dtype!r}")
         f32 = self.opts.dtype == "fp32"
-        if f32 and (self.opts.fuse_level != 1 or self.opts.store_a1 != 0):
-            raise ValueError("the fp32 engine runs the level-1 chain (fuse_level 1, store_a1 0)")
+        if f32 and (self.opts.fuse_level < 1 or self.opts.store_a1 != 0):
+            raise ValueError("the fp32 engine runs the level-1 chain (fuse_level >= 1, store_a1 0)")
         R = self.wgrad_rows = self.opts.wgrad_rows or wgrad_rows(28, B, torch.float32 if f32 else BF16)
         g = self.opt.param_groups[0]
         if g["momentum"] != 0 and self.opt.momentum_buffer is None:
@@ -121,6 +127,11 @@ class FusedSimpleCNNEngine:
             images=data.images_u8.view(-1), labels=data.labels_i32,
             idx=torch.zeros(n_rank, dtype=torch.int32, device=dev),
         )
+        # in-launch hand-offs (fused slab reduction, level-2 dZ2 flags), zeroed by each
+        # step's forward, and their wait-timeout word
+        nfl = 256 + self.C.fc_conv_bwd_fc_blocks(HW * 64) + self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_fwd)
+        self.t["sync_flags"] = torch.zeros(nfl, dtype=torch.int32, device=dev)
+        self.t["sync_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
         cfg = dict(max_batch=B, H=28, W=28, C1=32, C2=64, NO=10, pxt_fwd=self.opts.pxt_fwd,
                    pxt_dgrad=self.opts.pxt_dgrad, wgrad_rows=R, world=world_size, rank=rank,
                    lr=float(g["lr"]), momentum=float(g["momentum"]),
@@ -128,7 +139,7 @@ class FusedSimpleCNNEngine:
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
-                   store_a1=int(self.opts.store_a1), f32=f32)
+                   store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=bool(self.opts.fuse_reduce))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
@@ -171,6 +182,8 @@ class FusedSimpleCNNEngine:
         if self.opt.momentum_buffer is not None and self.opt.steps > 0:
             self.eng.set_momentum_started(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)
+        # kernels per step of the chain that actually runs (engine.cpp / EngineConfig)
+        self.level2 = bool(self.eng.level2_active)
         self._captured = 0
         self.steps_done = 0
 

@@ -9,7 +9,7 @@ dev = "cuda"
 
 
 def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentum=0.0,
-           fuse_level=0, fuse_opt=True, weight_decay=0.0, store_a1=True):
+           fuse_level=0, fuse_opt=True, weight_decay=0.0, store_a1=True, **eo):
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
     from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
     from ddp_amd.models import SimpleCNN
@@ -23,7 +23,7 @@ def _setup(n=2048, B=32, graph_steps=5, use_graph=True, seed=0, lr=0.01, momentu
     eng = FusedSimpleCNNEngine(model, opt, data, B, 1, 0,
                                opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph,
                                                   fuse_level=fuse_level, fuse_opt=fuse_opt,
-                                                  store_a1=store_a1))
+                                                  store_a1=store_a1, **eo))
     eng.refresh()
     return model, opt, data, eng, imgs, labels
 
@@ -71,6 +71,68 @@ def test_fuse_level1_bitwise_equals_level0(B):
     for (n, a), (_, b) in zip(m0.named_parameters(), m1.named_parameters()):
         assert torch.equal(a, b), n
     assert torch.equal(e0.t["loss_hist"][:7], e1.t["loss_hist"][:7])
+
+
+@pytest.mark.parametrize("B", [32, 20, 64])
+def test_fuse_level2_bitwise_equals_level1(B):
+    """Level 2 runs fc_bwd and the conv backward as ONE launch with an in-launch dZ2
+    hand-off (fc role: 4 waves x 2 virtual waves); params, momentum and losses must equal
+    the level-1 chain bit for bit, graph-captured, and no hand-off wait may time out."""
+    m1, o1, _, e1, _, _ = _setup(B=B, use_graph=True, momentum=0.9, fuse_level=1)
+    m2, o2, _, e2, _, _ = _setup(B=B, use_graph=True, momentum=0.9, fuse_level=2)
+    assert not e1.level2 and e2.level2
+    e1.run_steps(12)
+    e2.run_steps(12)
+    e1.synchronize(); e2.synchronize()
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
+    assert torch.equal(o1.momentum_buffer, o2.momentum_buffer)
+    assert torch.equal(e1.t["loss_hist"][:12], e2.t["loss_hist"][:12])
+    for k in ("w2_bf16", "w2t_bf16", "wfc_bf16", "wfc_frag"):
+        assert torch.equal(e1.t[k], e2.t[k]), k
+    assert int(e2.t["sync_err"].item()) == 0
+
+
+@pytest.mark.parametrize("dtype,B,opt", [("bf16", 32, True), ("bf16", 20, True), ("bf16", 64, False),
+                                         ("fp32", 32, True), ("fp32", 20, False)])
+def test_fused_reduce_bitwise_equals_grad_reduce(dtype, B, opt):
+    """The conv backward launch that also reduces the split-K slabs (wgrad blocks, after an
+    in-launch arrival count, sc1 loads, grad_reduce's fixed order) must equal the separate
+    grad_reduce kernel bit for bit - with the fused optimizer (opt) and without it (flat
+    SGD kernel after the reduction)."""
+    kw = dict(B=B, use_graph=True, momentum=0.9, weight_decay=1e-4, fuse_level=1, fuse_opt=opt,
+              store_a1=0, dtype=dtype)
+    m1, o1, _, e1, _, _ = _setup(fuse_reduce=False, **kw)
+    m2, o2, _, e2, _, _ = _setup(fuse_reduce=True, **kw)
+    e1.run_steps(11)
+    e2.run_steps(11)
+    e1.synchronize(); e2.synchronize()
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
+    assert torch.equal(o1.momentum_buffer, o2.momentum_buffer)
+    assert torch.equal(e1.fs.grads, e2.fs.grads)
+    assert torch.equal(e1.t["loss_hist"][:11], e2.t["loss_hist"][:11])
+    assert torch.equal(e1.t["step_ctr"], e2.t["step_ctr"])
+    assert int(e2.t["sync_err"].item()) == 0
+    assert not e1.eng.last_fused_reduce
+    # bf16 tiles (2 blocks per CU) always leave the wgrad blocks room to wait; fp32 tiles
+    # (1 per CU) fuse only while they fit half the resident capacity - bitwise either way
+    if dtype == "bf16":
+        assert e2.eng.last_fused_reduce
+    print(f"fused reduce {dtype} B={B}: {e2.eng.last_fused_reduce}")
+
+
+def test_fuse_level2_ragged_epoch_matches_level1():
+    """A whole epoch with a ragged last batch (eager steps at B < max_batch re-zero fewer
+    flags per forward block) - still bit-identical to level 1."""
+    m1, _, _, e1, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=1)
+    m2, _, _, e2, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=2)
+    for e in (e1, e2):
+        e.run_epoch(0)
+        e.run_epoch(1)
+        e.synchronize()
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
 
 
 @pytest.mark.parametrize("momentum,wd", [(0.0, 0.0), (0.9, 1e-4)])
@@ -121,7 +183,7 @@ def test_fuse_level1_one_step_matches_bf16_reference():
     assert abs(eng.t["loss_hist"][0].item() - loss.item()) < 1e-4
 
 
-@pytest.mark.parametrize("fuse_level", [0, 1])
+@pytest.mark.parametrize("fuse_level", [0, 1, 2])
 @pytest.mark.parametrize("B", [1, 12, 16, 24, 48, 64])
 def test_engine_batch_sweep_nan_poisoned(B, fuse_level):
     """SURVEY §4.1 batch sizes; every intermediate buffer starts as NaN so a kernel that
