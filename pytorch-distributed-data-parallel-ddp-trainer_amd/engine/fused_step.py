@@ -139,7 +139,7 @@ class FusedSimpleCNNEngine:
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
-                   store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=bool(self.opts.fuse_reduce))
+                   store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
@@ -188,6 +188,14 @@ class FusedSimpleCNNEngine:
         self.steps_done = 0
 
     # ------------------------------------------------------------------ helpers
+    def _fuse_reduce_ok(self, world_size: int) -> bool:
+        """The fused reduction's waiting blocks are sized against ONE launch's share of the
+        GPU; ranks that share a device (same-GPU rehearsals: more ranks than devices) each
+        hold waiting blocks at once, so they keep the separate grad_reduce kernel."""
+        if not self.opts.fuse_reduce:
+            return False
+        return world_size <= 1 or torch.cuda.device_count() >= world_size
+
     def sync_from_torch(self):
         """Order the engine stream after work queued on torch's current stream."""
         ev = torch.cuda.Event()
