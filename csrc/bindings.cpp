@@ -885,6 +885,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.idx = idx.data_ptr<int>();
              b.n_idx = (int)idx.numel();
              b.n_rows = (int)std::min<long>(images.numel() / HW, labels.numel());
+             // images / labels already permuted into the epoch's order: no index lookup
+             if (cfgd.contains("epoch_order") && cfgd["epoch_order"].cast<bool>()) b.idx = nullptr;
              TORCH_CHECK(conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, true, es) <= 160 * 1024, "wgrad rows too large");
              return std::make_shared<SimpleCNNEngine>(c, b, comm, buckets);
            }),

@@ -12,8 +12,10 @@ typedef unsigned short bf16_t;  // bf16 storage word
 // step_ctr != nullptr (graph-replayable), else `offset` is used as is.
 // Both lookups are clamped (n_idx = length of the index list, n_rows = dataset
 // rows): a mis-sized replay must never become an out-of-bounds gather.
+// idx == nullptr: the rows are already in epoch order (the fused engine permutes the
+// dataset once per epoch), row = base + b - one dependent load fewer per step.
 struct BatchIdx {
-  const int* idx;       // epoch index list (int32), nullptr -> identity (row b)
+  const int* idx;       // epoch index list (int32), nullptr -> rows base + b
   const int* step_ctr;  // device step counter or nullptr
   int batch_stride;
   int offset;
@@ -23,7 +25,10 @@ struct BatchIdx {
     return step_ctr ? (*step_ctr) * batch_stride : offset;
   }
   __device__ __forceinline__ int row(int b, int base_) const {
-    if (!idx) return b;
+    if (!idx) {
+      const int r = base_ + b;
+      return r < 0 ? 0 : (r >= n_rows ? n_rows - 1 : r);
+    }
     int i = base_ + b;
     i = i < 0 ? 0 : (i >= n_idx ? n_idx - 1 : i);
     int r = idx[i];

@@ -178,7 +178,7 @@ struct EngineBuffers {
   // data
   const unsigned char* images;  // u8 [N][H*W]
   const int* labels;            // i32 [N]
-  const int* idx;               // i32 epoch index list
+  const int* idx;               // i32 epoch index list (nullptr: images / labels already in epoch order)
   int n_idx, n_rows;            // bounds for the clamped batch gather
 };
 

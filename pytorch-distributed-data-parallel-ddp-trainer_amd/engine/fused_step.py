@@ -65,6 +65,10 @@ class EngineOptions:
     # reduce in the same order); "tune" = time two-shot, two-shot + one-shot and RCCL on
     # the node and keep the fastest; "xgmi2" / "xgmi1" = that plan, forced; "rccl" = RCCL
     comm: str = "auto"
+    # copy the rank's samples into epoch order once per epoch (images + labels, one
+    # index_select each): the step's batch is then rows [step * B, step * B + B) - one
+    # dependent load fewer at the head of every forward (no index-list lookup)
+    epoch_order: bool = True
     # compute precision: "bf16" (bf16 MFMA operands, fp32 master weights / gradients /
     # optimizer) or "fp32" (exact fp32 operands on v_mfma_f32_16x16x4_f32 - the
     # reference's precision; always the level-1 kernel chain)
@@ -124,7 +128,10 @@ class FusedSimpleCNNEngine:
             step_ctr=torch.zeros(1, dtype=torch.int32, device=dev),
             xb=torch.empty(B * HW, dtype=torch.uint8, device=dev),   # the step's batch (compact)
             yb=torch.empty(B, dtype=torch.int32, device=dev),
-            images=data.images_u8.view(-1), labels=data.labels_i32,
+            images=(torch.empty(n_rank * HW, dtype=torch.uint8, device=dev) if self.opts.epoch_order
+                    else data.images_u8.view(-1)),
+            labels=(torch.empty(n_rank, dtype=torch.int32, device=dev) if self.opts.epoch_order
+                    else data.labels_i32),
             idx=torch.zeros(n_rank, dtype=torch.int32, device=dev),
         )
         # in-launch hand-offs (fused slab reduction, level-2 dZ2 flags), zeroed by each
@@ -139,7 +146,8 @@ class FusedSimpleCNNEngine:
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
-                   store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size))
+                   store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
+                   epoch_order=bool(self.opts.epoch_order))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
@@ -253,6 +261,11 @@ class FusedSimpleCNNEngine:
         idx = self.sampler.indices().to(torch.int32)
         with torch.cuda.stream(self.stream):
             self.t["idx"].copy_(idx)
+            if self.opts.epoch_order:  # the rank's samples in this epoch's order
+                n, HW = self.t["idx"].numel(), 28 * 28
+                torch.index_select(self.data.images_u8.view(-1, HW), 0, self.t["idx"],
+                                   out=self.t["images"].view(n, HW))
+                torch.index_select(self.data.labels_i32, 0, self.t["idx"], out=self.t["labels"])
             self.t["step_ctr"].zero_()
             self.t["loss_hist"].zero_()
 
