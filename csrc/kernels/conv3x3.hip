@@ -1231,9 +1231,13 @@ size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es) {
 }
 
 // Resident-block budget of the fused reduction: every waiting (reducer) block holds a
-// slot, so the reducers are at most HALF of the launch's resident capacity (occupancy API
-// x CUs; other kernels, e.g. a concurrent all-reduce, may take slots).  Returns the
-// number of reducers (the last blocks of the grid), 0 if the capacity is unknown.
+// slot, so the reducers are at most a QUARTER of the launch's resident capacity as the
+// occupancy API reports it (other kernels, e.g. a concurrent all-reduce, may take slots,
+// and the API was measured to overstate the fp32 variant's residency: with the wgrad
+// blocks dispatched first, 128 waiting fp32 reducers starved the rest of the grid).
+// Returns the number of reducers (the last blocks of the grid: all the wgrad blocks), 0
+// when they do not fit that budget (fewer reducers, two passes each, measured slower than
+// the separate grad_reduce kernel: fp32 364k vs 383k img/s) or the capacity is unknown.
 template <typename K>
 static int fused_reducers(K kernel, size_t lds, int nblocks) {
   int dev = 0, cus = 0, occ = 0;
@@ -1241,8 +1245,8 @@ static int fused_reducers(K kernel, size_t lds, int nblocks) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), 256, lds) != hipSuccess)
     return 0;
-  const int half = occ * cus / 2;
-  return nblocks < half ? nblocks : half;
+  const int quarter = occ * cus / 4;
+  return nblocks <= quarter ? nblocks : 0;
 }
 
 template <typename T>
