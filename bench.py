@@ -152,6 +152,8 @@ def main():
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
+    ap.add_argument("--wgrad_split", type=int, default=None, choices=[1, 2],
+                    help="fused conv backward: wgrad blocks per slab row (input-channel halves)")
     ap.add_argument("--store_a1", type=int, default=None, choices=[0, 1, 2],
                     help="fused engine: conv1 output for the backward recomputed (0) / stored for dgrad (1) / for both (2)")
     ap.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
@@ -237,7 +239,7 @@ def main():
     eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=args.dtype,
                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
     eo.comm = args.comm
-    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1"):
+    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split"):
         if getattr(args, f) is not None:
             setattr(eo, f, getattr(args, f))
     eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
@@ -301,7 +303,8 @@ def main():
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
                        "graph_steps": k, "fuse_level": eo.fuse_level,
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
-                                  "wgrad_rows": eng.wgrad_rows, "store_a1": eo.store_a1},
+                                  "wgrad_rows": eng.wgrad_rows, "store_a1": eo.store_a1,
+                                  "wgrad_split": eo.wgrad_split},
                        "params_finite": finite,
                        "bucket_allreduce": eng.comm_kind, "bucket_allreduce_us": bucket_us,
                        "buckets_elems": [n for _, n in eng.ranges],

@@ -812,6 +812,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.store_a1 = cfgd.contains("store_a1") ? cfgd["store_a1"].cast<int>() : 0;
              c.f32 = cfgd.contains("f32") ? (int)cfgd["f32"].cast<bool>() : 0;
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? (int)cfgd["fuse_reduce"].cast<bool>() : 1;
+             c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
+             TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;
              TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");
              TORCH_CHECK(c.fuse_level >= 0 && c.fuse_level <= 2, "engine: fuse_level must be 0, 1 or 2");

@@ -688,20 +688,40 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // STAGE: the slab row goes through LDS (needs slab-row bytes of LDS, see conv3x3_bwd_lds)
 // and leaves as 16-byte write-through stores - from the MFMA layout each lane holds one
 // float per 64-byte run of the row, and 4-byte write-through stores took ~2.4 us per block.
+// CS == 2 (bf16, STAGE, SimpleCNN geometry Cin 32 / Cout 64): the input channels are
+// split over TWO blocks per (image, row chunk) - half h stages / recomputes only channels
+// 16h .. 16h+15 of X (half the conv1 recompute) and each wave runs one 16x16 (co, ci)
+// tile (half the MFMAs), so the wgrad role's critical path roughly halves.  Each output's
+// MFMA chain over the K slots is unchanged: the slab row is bit-identical to CS == 1's,
+// half 0 writes the ci < 16 columns and the bias, half 1 the rest.  The two halves of a
+// row chunk are 8 blocks apart (same XCD: blocks go round-robin over the 8 XCDs), so the
+// second one's dY tile reads hit the same L2.
 template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO, bool WAITDZ = false,
-          bool STAGE = false>
+          bool STAGE = false, int CS = 1>
 __device__ __forceinline__ void wgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ X,
     float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by,
     const DzWait& dzw = DzWait()) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int CE = Prec<T>::CE;
+  static_assert(CS == 1 || (CS == 2 && STAGE && !F32 && !WAITDZ && GCI == 32 && GCO == 64),
+                "the channel-split wgrad role is the bf16 staged-slab SimpleCNN variant");
   DDP_STAMP(STAMP_K_WGRAD, 0);
   DDP_GEOM_OVERRIDE();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nRC = (H + R - 1) / R;
-  const int n = bx / nRC;
-  const int r0 = (bx - n * nRC) * R;
+  int rb = bx, half = 0;  // slab row (image, row chunk) and channel half of this block
+  if constexpr (CS == 2) {
+    if (((B * nRC) & 7) == 0) {
+      half = (bx >> 3) & 1;
+      rb = ((bx >> 4) << 3) | (bx & 7);
+    } else {
+      half = bx & 1;
+      rb = bx >> 1;
+    }
+  }
+  const int n = rb / nRC;
+  const int r0 = (rb - n * nRC) * R;
   const int Wp = (W + 7) & ~7;
   const int DS = Cout + 16, XS = Cin + 16;  // LDS row strides (elements)
   const int nslot = ((R * Wp + 31) / 32) * 32;
@@ -709,10 +729,13 @@ __device__ __forceinline__ void wgrad_body(
   T* sX = sdY + (long)nslot * DS;
   const int XW = Wp + 2;
 
+  // conv1 channel group of this wave (CS == 2: waves 2k, 2k+1 share the half's groups)
+  const int c1g = CS == 2 ? 2 * half + (wave & 1) : wave;
   Conv1Group cg;
-  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
+  if (A1X) cg = conv1_group_load(c1.w, c1.b, c1g);  // lands during the staging round
   // ---- stage dY rows (masked) and X rows with halo: one round of loads
-  const int cpy_dy = Cout / CE, cpy_x = Cin / CE;
+  const int cxn = CS == 2 ? Cin / 2 : Cin, cx0 = half * cxn;  // staged X channels
+  const int cpy_dy = Cout / CE, cpy_x = cxn / CE;
   stage2<F32 ? 32 : 16>(WAITDZ ? 0 : nslot * cpy_dy,
           [&](int i) {
             const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
@@ -732,14 +755,14 @@ __device__ __forceinline__ void wgrad_body(
           },
           A1X ? 0 : (R + 2) * XW * cpy_x,
           [&](int i) {
-            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * CE;
+            const int pos = i / cpy_x, ch = cx0 + (i - pos * cpy_x) * CE;
             const int rr = pos / XW, cc = pos - (pos / XW) * XW;
             const int hh = r0 - 1 + rr, ww = cc - 1;
             return ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
                        ? ld16(X + (((long)n * H + hh) * W + ww) * Cin + ch) : zero8();
           },
           [&](int i, bf16x8 v) {
-            const int pos = i / cpy_x, ch = (i - pos * cpy_x) * CE;
+            const int pos = i / cpy_x, ch = cx0 + (i - pos * cpy_x) * CE;
             st16(sX + (long)pos * XS + ch, v);
           });
   if (A1X) {
@@ -756,7 +779,7 @@ __device__ __forceinline__ void wgrad_body(
     __syncthreads();
     DDP_STAMP(STAMP_K_WGRAD, 1);
     conv1_recompute_tile<T>(
-        (R + 2) * XW, cg, wave, 0, 64,
+        (R + 2) * XW, cg, c1g, CS == 2 ? 64 * (wave >> 1) : 0, CS == 2 ? 128 : 64,
         [&](int pos) {
           const int rr = pos / XW, cc = pos - (pos / XW) * XW;
           return (unsigned)(r0 - 1 + rr) < (unsigned)H && (unsigned)(cc - 1) < (unsigned)W;
@@ -790,16 +813,18 @@ __device__ __forceinline__ void wgrad_body(
   __syncthreads();
   DDP_STAMP(STAMP_K_WGRAD, 2);
 
-  // ---- wave assignment: (pair of 16-wide co tiles) x (16-wide ci tile)
+  // ---- wave assignment: (pair of 16-wide co tiles) x (16-wide ci tile); CS == 2: one
+  // 16-wide co tile per wave x the block's ci half
+  constexpr int NCT = CS == 2 ? 1 : 2;  // 16-wide co tiles per wave
   const int nct = Cin / 16;
   const int asg = by * 4 + wave;
-  const int coT = (asg / nct) * 32;
-  const int ciT = (asg - (asg / nct) * nct) * 16;
+  const int coT = CS == 2 ? 16 * wave : (asg / nct) * 32;
+  const int ciT = CS == 2 ? 16 * half : (asg - (asg / nct) * nct) * 16;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
 
-  f32x4 acc[2][9], accb[2];
+  f32x4 acc[NCT][9], accb[NCT];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < NCT; ++c) {
     accb[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc[c][k] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -832,9 +857,9 @@ __device__ __forceinline__ void wgrad_body(
 
     for (int s0 = 0; s0 < nslot; s0 += 32) {
       const int sA = s0 + 4 * g + q, sB = s0 + 16 + 4 * g + q;  // this lane's tr-read rows
-      bf16x8 a[2];
+      bf16x8 a[NCT];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NCT; ++c) {
         const bf16_t* pA = sdY + (long)sA * DS + coT + 16 * c + 4 * p;
         const bf16_t* pB = sdY + (long)sB * DS + coT + 16 * c + 4 * p;
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
@@ -853,18 +878,20 @@ __device__ __forceinline__ void wgrad_body(
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
         const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
         const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc[0][tap] = mfma16(a[0], b, acc[0][tap]);
-        acc[1][tap] = mfma16(a[1], b, acc[1][tap]);
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) acc[c][tap] = mfma16(a[c], b, acc[c][tap]);
       }
-      accb[0] = mfma16(a[0], ones, accb[0]);
-      accb[1] = mfma16(a[1], ones, accb[1]);
+      if (CS == 1 || ciT == 0) {  // CS == 2: only half 0 stores the bias (block-uniform)
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) accb[c] = mfma16(a[c], ones, accb[c]);
+      }
     }
   }
 
   DDP_STAMP(STAMP_K_WGRAD, 3);
   // ---- slab row: [Cout][3][3][Cin] (OHWI, the weight's native layout) then [Cout] bias
   const long row = (long)Cout * 9 * Cin + Cout;
-  float* out = slab + (long)bx * row;
+  float* out = slab + (long)rb * row;
   if constexpr (STAGE) {
     __syncthreads();  // every wave is done with the staged tiles
     float* srow = reinterpret_cast<float*>(smem);
@@ -874,7 +901,7 @@ __device__ __forceinline__ void wgrad_body(
     // keeps runs of 4 elements contiguous and 16-byte aligned for the read-back.
     const int wrow = 9 * Cin;
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < NCT; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = coT + 16 * c + 4 * g + r;
@@ -887,15 +914,28 @@ __device__ __forceinline__ void wgrad_body(
     // row % 4 == 0 and the slab rows are 16-byte aligned (checked by the launcher)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(row * 4), 0x00020000);
     typedef __attribute__((ext_vector_type(4))) int i32x4_t;
-    for (int i = threadIdx.x; i < row / 4; i += 256) {
-      const int e = 4 * i;
-      const int pos = e < Cout * wrow ? e + 16 * ((e / wrow) >> 2) : e + 4 * Cout;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, *reinterpret_cast<const float4*>(srow + pos)),
-                                             rs, i * 16, 0, 16 /* sc1: write-through */);
+    if constexpr (CS == 2) {
+      // this half's 4-float runs: (co, tap) row ct, columns 16 * half + 4 * cq; half 0 also
+      // the bias quads
+      const int nq = Cout * 9 * 4;
+      const int nst = nq + (half == 0 ? Cout / 4 : 0);
+      for (int i = threadIdx.x; i < nst; i += 256) {
+        const int e = i < nq ? (i >> 2) * Cin + 16 * half + 4 * (i & 3) : Cout * wrow + 4 * (i - nq);
+        const int pos = e < Cout * wrow ? e + 16 * ((e / wrow) >> 2) : e + 4 * Cout;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, *reinterpret_cast<const float4*>(srow + pos)),
+                                               rs, e * 4, 0, 16 /* sc1: write-through */);
+      }
+    } else {
+      for (int i = threadIdx.x; i < row / 4; i += 256) {
+        const int e = 4 * i;
+        const int pos = e < Cout * wrow ? e + 16 * ((e / wrow) >> 2) : e + 4 * Cout;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4_t, *reinterpret_cast<const float4*>(srow + pos)),
+                                               rs, i * 16, 0, 16 /* sc1: write-through */);
+      }
     }
   } else {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < NCT; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = coT + 16 * c + 4 * g + r;
@@ -938,7 +978,9 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // blocks below first_reducer never wait, a waiting block has already arrived, and the
 // host keeps the reducers within half the resident capacity (they are dispatched last,
 // each into a slot it can hold while the rest are dispatched).
-template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED>
+// CS: wgrad role channel split (see wgrad_body); the grid then has CS wgrad blocks per
+// slab row.
+template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kernel(
     const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
@@ -949,8 +991,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
         dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem,
         blockIdx.x, 0);
   else
-    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, false, true>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H, W,
-                                                              Cin, Cout, R, c1, smem, blockIdx.x - nd, 0);
+    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, false, true, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
+                                                                  W, Cin, Cout, R, c1, smem, blockIdx.x - nd, 0);
   if constexpr (FRED) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
     __syncthreads();
@@ -1252,10 +1294,14 @@ static int fused_reducers(K kernel, size_t lds, int nblocks) {
 template <typename T>
 static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
                        int Cin, int Cout, int pxt, int R, const C1Src& c1, const T* Xact,
-                       bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err) {
-  const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = conv3x3_wgrad_blocks(B, H, R);
-  const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
+                       bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err,
+                       int csplit) {
   const bool g = simplecnn_geom(H, W, Cin, Cout);
+  // the channel split is the bf16 SimpleCNN variant (wgrad_body); otherwise one block per row
+  const int cs = (csplit == 2 && g && sizeof(T) == 2) ? 2 : 1;
+  const int nrows = conv3x3_wgrad_blocks(B, H, R);
+  const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = nrows * cs;
+  const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
   if (((long)Cout * 9 * Cin + Cout) % 4 != 0 || (reinterpret_cast<uintptr_t>(slab) & 15) != 0)
     throw std::runtime_error("conv3x3_bwd: slab rows must be 16-byte multiples on a 16-byte aligned buffer");
   BwdReduce red;
@@ -1270,7 +1316,8 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     lds_optin(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds);
     // reducers: the wgrad blocks (they finish last; extra early-finishing reducers measured
     // slower - their polling shares the CUs of the still-running wgrad blocks)
-    const int nr = (g && red_done) ? fused_reducers(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds, nw) : 0;
+    // (channel split: the last nrows blocks - as many reducers as without the split)
+    const int nr = (g && red_done) ? fused_reducers(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds, nrows) : 0;
     if (nr <= 0) fused = nullptr;  // the caller reduces with grad_reduce
     else red.first_reducer = nd + nw - nr;
   }
@@ -1284,7 +1331,15 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
 #define LBW(PX, DA, WA)                                                                             \
   do {                                                                                              \
-    if (g && fused) {                                                                               \
+    if (cs == 2) {                                                                                  \
+      if constexpr (sizeof(T) == 2) {                                                               \
+        auto k = fused ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2>                 \
+                       : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2>;               \
+        lds_optin(k, lds);                                                                          \
+        hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
+                           Cout, R, nd, c1, Xact, red);                                             \
+      }                                                                                             \
+    } else if (g && fused) {                                                                        \
       auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true>;                             \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
@@ -1311,15 +1366,17 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
 
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
-                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err) {
+                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
+                 int wgrad_split) {
   return bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                     fused_reduce, red_done, red_err);
+                     fused_reduce, red_done, red_err, wgrad_split);
 }
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
-                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err) {
+                 bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
+                 int wgrad_split) {
   return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                    fused_reduce, red_done, red_err);
+                    fused_reduce, red_done, red_err, wgrad_split);
 }
 
 int fc_conv_bwd_fc_blocks(long K) { return (int)((K + 64 * FCC_CPL - 1) / (64 * FCC_CPL)); }

@@ -48,17 +48,18 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // apart, zeroed beforehand - by the step's forward, C1Src::zero_i32); red_err[0] = 2 if
 // that wait timed out.  SimpleCNN geometry only, and only while the wgrad blocks fit in
 // half the launch's resident capacity; returns whether the reduction was fused (false:
-// the caller runs grad_reduce).
+// the caller runs grad_reduce).  wgrad_split == 2 (bf16, SimpleCNN geometry): two wgrad
+// blocks per slab row, one per half of the input channels (bit-identical slabs).
 struct SlabSet;
 constexpr int SYNC_RED_INTS = 256;  // ints of the 8 arrival counters (32 apart) of red_done
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
-                 int* red_done = nullptr, int* red_err = nullptr);
+                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1);
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
-                 int* red_done = nullptr, int* red_err = nullptr);
+                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1);
 size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false, int es = 2);

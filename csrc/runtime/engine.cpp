@@ -265,7 +265,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
     reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                           cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
-                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err);
+                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split);
   } else {
     conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
                   b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);

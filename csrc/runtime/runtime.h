@@ -210,6 +210,9 @@ struct EngineConfig {
   // 1: the conv backward launch also reduces the split-K slabs + fused SGD (no separate
   //    grad_reduce kernel; level >= 1, needs sync_flags); 0: grad_reduce kernel
   int fuse_reduce = 1;
+  // 2: the fused conv backward's wgrad role runs two blocks per slab row, one per half of
+  //    conv2's input channels (bf16; bit-identical slabs); 1: one block per row
+  int wgrad_split = 1;
 };
 
 // Gradient bucket of the engine's data plane: a [off, off + n) range of the flat gradient

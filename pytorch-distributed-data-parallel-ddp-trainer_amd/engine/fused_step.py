@@ -73,6 +73,11 @@ class EngineOptions:
     # optimizer) or "fp32" (exact fp32 operands on v_mfma_f32_16x16x4_f32 - the
     # reference's precision; always the level-1 kernel chain)
     dtype: str = "bf16"
+    # fused conv backward (bf16): 2 = two wgrad blocks per slab row, one per half of conv2's
+    # input channels (half the conv1 recompute and MFMAs on the role's critical path;
+    # bit-identical slabs - measured 801k -> 811k img/s at B = 32, 1.04M -> 1.06M at B = 64,
+    # profiles/r2_split); 1 = one block per row.  fp32 always runs 1.
+    wgrad_split: int = 2
 
 
 class FusedSimpleCNNEngine:
@@ -147,7 +152,7 @@ class FusedSimpleCNNEngine:
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
                    store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
-                   epoch_order=bool(self.opts.epoch_order))
+                   epoch_order=bool(self.opts.epoch_order), wgrad_split=int(self.opts.wgrad_split))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None

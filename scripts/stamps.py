@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--graph", action="store_true", help="stamp the last step of a replayed graph")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--wgrad_split", type=int, default=None)
+    ap.add_argument("--wgrad_rows", type=int, default=None)
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -41,6 +43,9 @@ def main():
     eo = EngineOptions(use_graph=a.graph, graph_steps=10, dtype=a.dtype)
     if a.fuse_level is not None:
         eo.fuse_level = a.fuse_level
+    for f in ("wgrad_split", "wgrad_rows"):
+        if getattr(a, f) is not None:
+            setattr(eo, f, getattr(a, f))
     eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, dev, "synthetic"),
                                a.batch_size, 1, 0, None, eo)
     eng.refresh()

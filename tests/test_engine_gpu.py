@@ -123,6 +123,30 @@ def test_fused_reduce_bitwise_equals_grad_reduce(dtype, B, opt):
     print(f"fused reduce {dtype} B={B}: {e2.eng.last_fused_reduce}")
 
 
+@pytest.mark.parametrize("B,fred,store_a1", [(32, True, 0), (32, False, 0), (20, True, 0), (64, True, 0),
+                                             (32, True, 2)])
+def test_wgrad_channel_split_bitwise(B, fred, store_a1):
+    """Two wgrad blocks per slab row (input-channel halves, XCD-paired block order; B=20
+    gives a row count that is not a multiple of 8 - the adjacent-pair order) must write
+    the same slab rows as one block per row: parameters, momentum, gradients and losses
+    bit-identical after 11 steps, with the fused in-launch reduction and without it,
+    recomputing a1 (store_a1 0) or loading it (2)."""
+    kw = dict(B=B, use_graph=True, momentum=0.9, weight_decay=1e-4, fuse_level=1, store_a1=store_a1,
+              fuse_reduce=fred)
+    m1, o1, _, e1, _, _ = _setup(wgrad_split=1, **kw)
+    m2, o2, _, e2, _, _ = _setup(wgrad_split=2, **kw)
+    e1.run_steps(11)
+    e2.run_steps(11)
+    e1.synchronize(); e2.synchronize()
+    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), n
+    assert torch.equal(o1.momentum_buffer, o2.momentum_buffer)
+    assert torch.equal(e1.fs.grads, e2.fs.grads)
+    assert torch.equal(e1.t["loss_hist"][:11], e2.t["loss_hist"][:11])
+    assert int(e2.t["sync_err"].item()) == 0
+    assert e1.eng.last_fused_reduce == e2.eng.last_fused_reduce
+
+
 def test_fuse_level2_ragged_epoch_matches_level1():
     """A whole epoch with a ragged last batch (eager steps at B < max_batch re-zero fewer
     flags per forward block) - still bit-identical to level 1."""
