@@ -24,6 +24,11 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) char lds_char;
+// LDS pointer to bf16 element elem_off of an LDS byte base (32-bit address arithmetic)
+__device__ __forceinline__ lds_bf16x4* lds_ptr4(lds_char* base, int elem_off) {
+  return (lds_bf16x4*)(base + 2 * elem_off);
+}
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;  // v_dot2c_f32_bf16 operand
 
 constexpr int WAVE = 64;

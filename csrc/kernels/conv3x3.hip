@@ -736,23 +736,47 @@ __device__ __forceinline__ void wgrad_body(
   // ---- stage dY rows (masked) and X rows with halo: one round of loads
   const int cxn = CS == 2 ? Cin / 2 : Cin, cx0 = half * cxn;  // staged X channels
   const int cpy_dy = Cout / CE, cpy_x = cxn / CE;
-  stage2<F32 ? 32 : 16>(WAITDZ ? 0 : nslot * cpy_dy,
-          [&](int i) {
-            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
-            const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
-            const int hh = r0 + r;
-            bf16x8 v = zero8();
-            if (r < R && hh < H && c < W) {
-              const long off = (((long)n * H + hh) * W + c) * Cout + ch;
-              v = ld16(dY + off);
-              if (MASK_DY) v = mask16<T>(v, ld16(Yact + off));
-            }
-            return v;
-          },
-          [&](int i, bf16x8 v) {
-            const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
-            st16(sdY + (long)slot * DS + ch, v);
-          },
+  auto dy_src = [&](int i) {
+    const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
+    const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
+    const int hh = r0 + r;
+    bf16x8 v = zero8();
+    if (r < R && hh < H && c < W) {
+      const long off = (((long)n * H + hh) * W + c) * Cout + ch;
+      v = ld16(dY + off);
+      if (MASK_DY) v = mask16<T>(v, ld16(Yact + off));
+    }
+    return v;
+  };
+  auto dy_dst = [&](int i, bf16x8 v) {
+    const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
+    st16(sdY + (long)slot * DS + ch, v);
+  };
+  // A1X: uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, then a1 (conv1 recompute)
+  const int XW2 = Wp + 4, XR2 = R + 4, NXX = XR2 * XW2;
+  float* sxx = reinterpret_cast<float*>(sX + (long)(R + 2) * XW * XS);
+  const long img = A1X ? (long)c1.bi.row(n, c1.bi.base()) * H * W : 0;
+  auto x_inside = [&](int i, int& off) {
+    const int rr = i / XW2, cc = i - (i / XW2) * XW2;
+    const int hh = r0 - 2 + rr, ww = cc - 2;
+    off = hh * W + ww;
+    return (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+  };
+  auto recompute = [&]() {
+    conv1_recompute_tile<T>(
+        (R + 2) * XW, cg, c1g, CS == 2 ? 64 * (wave >> 1) : 0, CS == 2 ? 128 : 64,
+        [&](int pos) {
+          const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+          return (unsigned)(r0 - 1 + rr) < (unsigned)H && (unsigned)(cc - 1) < (unsigned)W;
+        },
+        [&](int pos, int k) {
+          const int rr = pos / XW, cc = pos - (pos / XW) * XW;
+          return sxx[(rr + k / 3) * XW2 + cc + k % 3];
+        },
+        [&](int pos, int g) { return sX + (long)pos * XS + 8 * g; });
+  };
+  const int ndy = WAITDZ ? 0 : nslot * cpy_dy;
+  stage2<F32 ? 32 : 16>(ndy, dy_src, dy_dst,
           A1X ? 0 : (R + 2) * XW * cpy_x,
           [&](int i) {
             const int pos = i / cpy_x, ch = cx0 + (i - pos * cpy_x) * CE;
@@ -766,29 +790,13 @@ __device__ __forceinline__ void wgrad_body(
             st16(sX + (long)pos * XS + ch, v);
           });
   if (A1X) {
-    // uint8 x rows r0-2 .. r0+R+1, cols -2 .. Wp+1 -> LDS floats, then a1 (conv1 recompute)
-    const int XW2 = Wp + 4, XR2 = R + 4;
-    float* sxx = reinterpret_cast<float*>(sX + (long)(R + 2) * XW * XS);
-    const long img = (long)c1.bi.row(n, c1.bi.base()) * H * W;
-    for (int i = threadIdx.x; i < XR2 * XW2; i += 256) {
-      const int rr = i / XW2, cc = i - (i / XW2) * XW2;
-      const int hh = r0 - 2 + rr, ww = cc - 2;
-      sxx[i] = ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                   ? (float)c1.x[img + hh * W + ww] / 255.0f : 0.f;
+    for (int i = threadIdx.x; i < NXX; i += 256) {
+      int off = 0;
+      sxx[i] = x_inside(i, off) ? (float)c1.x[img + off] / 255.0f : 0.f;
     }
     __syncthreads();
     DDP_STAMP(STAMP_K_WGRAD, 1);
-    conv1_recompute_tile<T>(
-        (R + 2) * XW, cg, c1g, CS == 2 ? 64 * (wave >> 1) : 0, CS == 2 ? 128 : 64,
-        [&](int pos) {
-          const int rr = pos / XW, cc = pos - (pos / XW) * XW;
-          return (unsigned)(r0 - 1 + rr) < (unsigned)H && (unsigned)(cc - 1) < (unsigned)W;
-        },
-        [&](int pos, int k) {
-          const int rr = pos / XW, cc = pos - (pos / XW) * XW;
-          return sxx[(rr + k / 3) * XW2 + cc + k % 3];
-        },
-        [&](int pos, int g) { return sX + (long)pos * XS + 8 * g; });
+    recompute();
   }
   if constexpr (WAITDZ) {
     static_assert(!F32 && !MASK_DY, "the in-launch dZ2 hand-off is bf16, unmasked");
@@ -855,28 +863,32 @@ __device__ __forceinline__ void wgrad_body(
 #pragma unroll
     for (int j = 0; j < 8; ++j) ones[j] = (short)0x3F80;
 
+    // 32-bit LDS element offsets (64-bit generic-pointer math per read cost a
+    // v_mad_u64_u32 each); a tap adds the constant (kh * XW + kw) * XS, which folds into
+    // the ds_read offset field under the geometry specialisation
+    const int ldsX = nslot * DS;  // sX = sdY + nslot * DS
+    lds_char* lsm = (lds_char*)smem;
     for (int s0 = 0; s0 < nslot; s0 += 32) {
       const int sA = s0 + 4 * g + q, sB = s0 + 16 + 4 * g + q;  // this lane's tr-read rows
       bf16x8 a[NCT];
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
-        const bf16_t* pA = sdY + (long)sA * DS + coT + 16 * c + 4 * p;
-        const bf16_t* pB = sdY + (long)sB * DS + coT + 16 * c + 4 * p;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
+        const int oA = sA * DS + coT + 16 * c + 4 * p, oB = sB * DS + coT + 16 * c + 4 * p;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, oA));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, oB));
         a[c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
       // X position of slot s for tap (kh,kw): sX row (r+kh), col (c+kw).  Padding slots
       // (r >= R) carry dY == 0; clamp their row so the read stays inside initialised LDS.
       const int rA0 = sA / Wp, cA = sA - rA0 * Wp, rB0 = sB / Wp, cB = sB - rB0 * Wp;
       const int rA = min(rA0, R - 1), rB = min(rB0, R - 1);
+      const int xA = ldsX + (rA * XW + cA) * XS + ciT + 4 * p, xB = ldsX + (rB * XW + cB) * XS + ciT + 4 * p;
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int kh = tap / 3, kw = tap % 3;
-        const bf16_t* pA = sX + (long)((rA + kh) * XW + cA + kw) * XS + ciT + 4 * p;
-        const bf16_t* pB = sX + (long)((rB + kh) * XW + cB + kw) * XS + ciT + 4 * p;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pA);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)pB);
+        const int to = (kh * XW + kw) * XS;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xA + to));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xB + to));
         const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int c = 0; c < NCT; ++c) acc[c][tap] = mfma16(a[c], b, acc[c][tap]);

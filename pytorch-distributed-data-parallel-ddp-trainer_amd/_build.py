@@ -58,11 +58,27 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
-def _needs(obj: str, src: str, hdr_mtime: float) -> bool:
+def _needs(obj: str, src: str, hdr_mtime: float, cmd=None) -> bool:
+    """Rebuild when the object is missing, older than its source or any header, or was
+    built by a different command line (flags change: the ``.cmd`` sidecar differs)."""
     if not os.path.exists(obj):
         return True
+    if cmd is not None:
+        try:
+            with open(obj + ".cmd") as f:
+                if f.read() != " ".join(cmd):
+                    return True
+        except OSError:
+            return True
     t = os.path.getmtime(obj)
     return os.path.getmtime(src) > t or hdr_mtime > t
+
+
+# per-TU device flags.  conv3x3.hip: no SLP vectorizer - it packed the 16-lane DPP
+# reductions' adds into v_pk_add_f32, which cannot take a DPP operand, so every step became
+# v_mov 0 + v_mov_dpp + add (the conv1 weight-gradient reduction of the dgrad role: 750 ->
+# 400 VALU instructions with the adds folded into v_add_f32_dpp)
+KERNEL_FLAGS = {"conv3x3.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile_cmds():
@@ -73,7 +89,7 @@ def _compile_cmds():
     cmds = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(BUILD_DIR, "k_" + os.path.basename(src) + ".o")
-        cmds.append((src, obj, [hipcc, f"--offload-arch={ARCH}", *common,
+        cmds.append((src, obj, [hipcc, f"--offload-arch={ARCH}", *common, *KERNEL_FLAGS.get(os.path.basename(src), []),
                                 "-munsafe-fp-atomics", "-c", src, "-o", obj]))
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD_DIR, "r_" + os.path.basename(src) + ".o")
@@ -105,7 +121,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     os.makedirs(BUILD_DIR, exist_ok=True)
     hdr = _headers_mtime()
     cmds = _compile_cmds()
-    todo = [(s, o, c) for (s, o, c) in cmds if force or _needs(o, s, hdr)]
+    todo = [(s, o, c) for (s, o, c) in cmds if force or _needs(o, s, hdr, c)]
     jobs = jobs or min(8, int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), max(1, len(todo)))
 
     def run(item):
@@ -115,6 +131,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if p.returncode != 0:
             raise RuntimeError(f"compile failed: {src}\n{p.stdout}")
+        with open(obj + ".cmd", "w") as f:
+            f.write(" ".join(cmd))
         return src
 
     if todo:

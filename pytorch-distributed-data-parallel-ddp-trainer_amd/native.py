@@ -25,7 +25,17 @@ def _try_import():
         try:
             import torch  # noqa: F401  (loads torch's HIP runtime + RCCL first)
 
-            _mod = importlib.import_module(__package__ + "._C")
+            variant = os.environ.get("DDP_AMD_NATIVE_SO")
+            if variant:  # A/B experiments: another build of the same extension
+                import sys
+                from importlib import util as _ilu
+
+                spec = _ilu.spec_from_file_location(__package__ + "._C", variant)
+                _mod = _ilu.module_from_spec(spec)
+                spec.loader.exec_module(_mod)
+                sys.modules[__package__ + "._C"] = _mod
+            else:
+                _mod = importlib.import_module(__package__ + "._C")
             import atexit
 
             atexit.register(_mod._mark_exiting)  # no HIP/RCCL teardown during interpreter exit
