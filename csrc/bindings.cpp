@@ -902,6 +902,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("level2_active", &SimpleCNNEngine::level2_active)
       .def_property_readonly("last_fused_reduce", &SimpleCNNEngine::last_fused_reduce)
+      .def_property_readonly("sync_error", &SimpleCNNEngine::sync_error)
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
       .def("set_xgmi", &SimpleCNNEngine::set_xgmi, py::arg("xgmi"), py::arg("channels"))
       .def_property_readonly("num_buckets", &SimpleCNNEngine::num_buckets)

@@ -240,6 +240,8 @@ class SimpleCNNEngine {
   void destroy_graph();
   hipStream_t stream() const { return cs_; }
   void synchronize();  // throws if a level-2 hand-off wait timed out
+  // in-launch wait-timeout word (0 = ok, 1 = level-2 dZ2 wait, 2 = fused reduction); sticky
+  int sync_error() const { return err_host_ ? __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) : 0; }
   bool level2_active() const;
   // whether the last launched step reduced its weight-gradient slabs inside the conv
   // backward launch (false: separate grad_reduce kernel)
@@ -277,6 +279,7 @@ class SimpleCNNEngine {
   int graph_steps_ = 0;
   bool momentum_started_ = false;
   bool last_fused_reduce_ = false;
+  int* err_host_ = nullptr;  // coherent host word behind b_.sync_err
 };
 
 }  // namespace ddp_amd

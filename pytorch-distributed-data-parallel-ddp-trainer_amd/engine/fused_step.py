@@ -143,6 +143,7 @@ class FusedSimpleCNNEngine:
         # step's forward, and their wait-timeout word
         nfl = 256 + self.C.fc_conv_bwd_fc_blocks(HW * 64) + self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_fwd)
         self.t["sync_flags"] = torch.zeros(nfl, dtype=torch.int32, device=dev)
+        # (the engine replaces it by a coherent host word: eng.sync_error)
         self.t["sync_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
         cfg = dict(max_batch=B, H=28, W=28, C1=32, C2=64, NO=10, pxt_fwd=self.opts.pxt_fwd,
                    pxt_dgrad=self.opts.pxt_dgrad, wgrad_rows=R, world=world_size, rank=rank,
