@@ -22,9 +22,9 @@ Metric/config are BASELINE.json's: images/sec of the reference's SimpleCNN
 random-init weights (no network for the real dataset), bf16 compute with fp32
 master weights / gradients / optimizer.  A timed step is the complete training
 step of the reference's loop: batch gather + forward + loss + backward + DDP
-bucket all-reduce (RCCL, N>1) + SGD update - executed by the native fused
-engine (4-5 HIP kernels + 2 bucket all-reduces - the direct xGMI kernel, RCCL as the
-fallback - replayed from a hipGraph).
+bucket all-reduce (N>1) + SGD update - executed by the native fused engine (3 HIP
+kernels per step, + one all-reduce per gradient bucket at N>1 - the direct xGMI kernel,
+RCCL as the fallback - replayed from a hipGraph).
 
 W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
 ``torch.cuda.synchronize()`` on both sides; the step time is the MAX over ranks;
@@ -148,7 +148,8 @@ def main():
     ap.add_argument("--graph_steps", type=int, default=None)
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--fuse_level", type=int, default=None,
-                    help="engine fusion level (0: 8 kernels/step, 1: 6 kernels/step); default = engine default")
+                    help="engine fusion level (0: 8 kernels/step, 1: 3 kernels/step, 2: fc + conv backward "
+                         "in one launch); default = engine default (1)")
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")

@@ -53,7 +53,7 @@ def parse_args(argv=None):
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
     p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1, 2],
                    help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
-                        "1 = 4 kernels/step (default)")
+                        "1 = 3 kernels/step (default); 2 = fc + conv backward in one launch (opt-in)")
     p.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
                    help="fused engine bucket all-reduce at world size > 1: auto = the direct xGMI kernels "
                         "(one-shot for the small bucket; RCCL if their self-test fails) - deterministic, so "
