@@ -174,6 +174,10 @@ def main():
     ap.add_argument("--model", choices=["simplecnn", "resnet18"], default="simplecnn",
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
     ap.add_argument("--image_size", type=int, default=224, help="resnet18 input size")
+    ap.add_argument("--wgrad_halo", type=int, default=1, choices=[0, 1, 2],
+                    help="resnet18: tap-fused halo weight gradient for the stride-1 3x3 layers where "
+                         "the per-tap GEMM would use 64x64 tiles (1), every eligible layer (2), never (0)")
+    ap.add_argument("--wgrad_halo_target", type=int, default=256, help="resnet18: halo wgrad blocks per launch")
     ap.add_argument("--dry_launch", action="store_true",
                     help="self-launch test hook: workers report their launcher env and exit (no GPU)")
     ap.add_argument("--no_scaling_ref", action="store_true",
@@ -327,7 +331,7 @@ def bench_resnet(args):
     from ddp_amd.ops.resnet_fn import to_nhwc4
     from ddp_amd.parallel import DistributedDataParallel, setup
 
-    native.require()
+    native.require().conv_gemm_wgrad_set_halo(args.wgrad_halo, args.wgrad_halo_target)
     if args.dtype != "bf16":
         raise SystemExit("--model resnet18 runs the bf16 MFMA kernels only")
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -410,6 +414,7 @@ def bench_resnet(args):
                        "per_rank_batch": B, "seq_len": None, "parallelism": f"dp{ws}",
                        "engine": "module path (HIP autograd + native reducer)"
                                  + (", whole step in one hipGraph" if use_graph else ", eager"),
+                       "wgrad_halo": args.wgrad_halo, "wgrad_halo_target": args.wgrad_halo_target,
                        "bucket_allreduce": ddp.comm_kind if ws > 1 else "none",
                        "buckets": len(ddp.buckets), "ranks_seen": dist.get_world_size(),
                        "loss": round(float(loss.item()), 4)},

@@ -402,7 +402,8 @@ void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& out, int KH, 
   check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(out, "out", at::kFloat);
   const ConvGeom g = geom_of(X, dY, KH, KW, stride, pad);
   TORCH_CHECK((g.Cin % 64 == 0 || g.Cin == 4) && g.Cout % 64 == 0, "conv_gemm_wgrad: Cin % 64 (or 4), Cout % 64");
-  TORCH_CHECK(ppc % 32 == 0 && ppc > 0, "pixels per chunk must be a multiple of 32");
+  TORCH_CHECK(conv_gemm_wgrad_ppc_ok(g, ppc), "pixels per chunk must be a multiple of 32 (or whole rows "
+              "for the halo kernel)");
   const long row = (long)g.Cout * KH * KW * (g.Cin == 4 ? 3 : g.Cin);
   TORCH_CHECK(out.numel() >= (long)conv_gemm_wgrad_chunks(g, ppc) * row, "wgrad output too small");
   TORCH_CHECK(ks == 0 || ks == 32 || ks == 64, "conv_gemm_wgrad: ks 0 (auto), 32 or 64");
@@ -685,6 +686,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1,
         py::arg("halo") = -1);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
+  m.def("conv_gemm_wgrad_set_halo", &conv_gemm_wgrad_set_halo, py::arg("halo"), py::arg("target") = 256,
+        "weight-gradient plan override: halo 0 = the per-tap GEMM kernel only, 1 = tap-fused halo "
+        "kernel for the stride-1 3x3 layers where the GEMM would use 64 x 64 tiles (default), 2 = "
+        "halo wherever eligible; target = blocks per launch");
   m.def("conv_gemm_wgrad_force_tile", &conv_gemm_wgrad_force_tile);
   m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
     return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));

@@ -858,6 +858,36 @@ static void wgrad_tile(const ConvGeom& g, int* bm, int* bn) {
   }
 }
 
+// tap-fused halo weight gradient (conv_halo.hip) for stride-1 3x3 layers: plan = chunks of
+// whole output rows so that the launch has ~g_wgrad_halo_target blocks of 64 co x 32 ci
+static int g_wgrad_halo = 1, g_wgrad_halo_target = 256;  // halo: 0 off, 1 auto, 2 wherever eligible
+void conv_gemm_wgrad_set_halo(int halo, int target) {
+  g_wgrad_halo = halo < 0 ? 0 : (halo > 2 ? 2 : halo);
+  g_wgrad_halo_target = target > 0 ? target : 256;
+}
+static void wgrad_tile(const ConvGeom& g, int* bm, int* bn);
+// only where the per-tap GEMM would run its 64 x 64 tile (ResNet-18/224: the 56-wide
+// layer1 and 7-wide layer4 3x3 convs, 32.7 -> 23.6 and 37.3 -> 23.6 us); the 128 x 128 GEMM
+// tile of the 28- and 14-wide layers measured faster than the halo kernel (22.2 / 20.9 vs
+// 23.6 us, profiles/r2_halo_wgrad)
+static bool wgrad_use_halo(const ConvGeom& g) {
+  if (!g_wgrad_halo || !conv_halo_wgrad_ok(g)) return false;
+  if (g_wgrad_halo == 2) return true;  // forced (tests, sweeps)
+  int bm, bn;
+  wgrad_tile(g, &bm, &bn);
+  return bm == 64 && bn == 64;
+}
+static int wgrad_halo_ppc(const ConvGeom& g) {
+  const int bpc = (g.Cout / 64) * (g.Cin / 32);
+  int chunks = g_wgrad_halo_target / bpc;
+  if (chunks < 1) chunks = 1;
+  const int rows = g.N * g.H;
+  int rpc = (rows + chunks - 1) / chunks;
+  const int q = conv_halo_wgrad_row_quantum(g);  // whole images when groups stack images
+  rpc = (rpc + q - 1) / q * q;
+  return rpc * g.W;
+}
+
 int conv_gemm_wgrad_tiles(const ConvGeom& g) {
   int bm, bn;
   wgrad_tile(g, &bm, &bn);
@@ -867,7 +897,14 @@ int conv_gemm_wgrad_tiles(const ConvGeom& g) {
 
 // pixels per chunk: split K until the grid has ~target blocks (1x1: 256 - a tiny GEMM
 // whose slab reduction dominates; 128-wide tiles: 512; 64 x 64: 1024)
+bool conv_gemm_wgrad_ppc_ok(const ConvGeom& g, int ppc) {
+  if (ppc <= 0) return false;
+  if (ppc % 32 == 0) return true;
+  return wgrad_use_halo(g) && ppc % (g.W * conv_halo_wgrad_row_quantum(g)) == 0;
+}
+
 int conv_gemm_wgrad_ppc(const ConvGeom& g) {
+  if (wgrad_use_halo(g)) return wgrad_halo_ppc(g);
   int bm, bn;
   wgrad_tile(g, &bm, &bn);
   const int T = g.KH * g.KW;
@@ -889,6 +926,10 @@ void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float
                      int px_per_chunk, bool accum, hipStream_t s, int ks) {
   const int ch = conv_gemm_wgrad_chunks(g, px_per_chunk);
   const int acc = (accum && ch == 1) ? 1 : 0;
+  if (wgrad_use_halo(g) && px_per_chunk % (g.W * conv_halo_wgrad_row_quantum(g)) == 0) {  // whole rows
+    conv_halo_wgrad(g, dY, X, out, px_per_chunk / g.W, acc != 0, s);
+    return;
+  }
   int bm, bn;
   wgrad_tile(g, &bm, &bn);
   if (ks != 32 && ks != 64) ks = 32;

@@ -423,4 +423,182 @@ void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* 
 #undef HLF
 }
 
+
+// ---------------------------------------------------------------- weight gradient
+// Tap-fused stride-1 3x3 weight gradient (ResNet-18's 56/28/14/7-wide 3x3 layers).
+//   D[co][tap][ci] = sum_p dY[p][co] * X[p @ tap][ci]
+// conv_gemm_wgrad_kernel makes one block per (co tile, tap, ci tile) and re-gathers X per
+// tap - dY and X are fetched from L2 nine times.  Here a block owns (64 co) x (32 ci) x
+// all 9 taps: it walks its chunk of output rows in groups of R rows of one image
+// (R * Wp = 224 K slots, Wp = W rounded up to 8), stages the group's dY rows and the
+// (R+2) x (Wp+2) input halo into LDS once, and every wave runs its 2 co tiles x 9 taps
+// (18 MFMAs per 32-slot K-step, operands via ds_read_b64_tr_b16 at 32-bit LDS offsets,
+// the tap offsets folded into the instruction).  The next group's tiles are loaded into
+// registers while the current one computes.  One fp32 slab row per chunk (grid.z) in the
+// weight's OHWI layout, reduced by grad_reduce in fixed order - the same output contract
+// as conv_gemm_wgrad (a single chunk writes / accumulates the gradient directly).
+// Padding slots (rows past the group, columns >= W) carry dY == 0.  Images shorter than
+// a group (the 7x7 layers: R = 28) are stacked: a group is R / H whole images, each with
+// its own 2 halo rows (chunks then hold whole images).
+constexpr int HWG_SLOTS = 224;              // K slots per row group
+constexpr int HWG_DS = 64 + 16;             // sdY row stride: 40 dwords (odd multiple of 8)
+constexpr int HWG_XS = 32 + 16;             // sX row stride: 24 dwords (odd multiple of 8)
+constexpr int HWG_MAXPOS = 360;             // largest halo: 4 x (7 + 2) x (8 + 2) (W = 56: 6 x 58)
+constexpr int HWG_DYC = HWG_SLOTS * 8 / 256;         // 16-byte dY chunks per thread (7)
+constexpr int HWG_XC = (HWG_MAXPOS * 4 + 255) / 256;  // 16-byte X chunks per thread (6)
+
+__host__ __device__ inline int hwg_wp(int W) { return (W + 7) & ~7; }
+size_t conv_halo_wgrad_lds() {
+  return sizeof(bf16_t) * ((size_t)HWG_SLOTS * HWG_DS + (size_t)HWG_MAXPOS * HWG_XS);
+}
+
+__global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
+                                                                      const bf16_t* __restrict__ X,
+                                                                      float* __restrict__ out, int rows_per_chunk,
+                                                                      int accum) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = g.H, W = g.W, Cin = g.Cin, Cout = g.Cout;
+  const int Wp = hwg_wp(W), R = HWG_SLOTS / Wp, XW = Wp + 2;
+  // segment = rows sharing one halo: a group of R rows of one image, or nimg stacked images
+  const int Hs = H < R ? H : R, nimg = R / Hs, live = nimg * Hs;
+  const int nxc = nimg * (Hs + 2) * XW * 4;  // 16-byte X chunks of the halo(s) (32 channels = 4 chunks)
+  bf16_t* sdY = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* sX = sdY + HWG_SLOTS * HWG_DS;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
+  const int rows = g.N * H;
+  const int rbeg = blockIdx.z * rows_per_chunk;
+  const int rend = min(rows, rbeg + rows_per_chunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // rows of the group starting at flattened row r: at most R, never past the image (or,
+  // stacked, the last whole image) or the chunk
+  auto group_rows = [&](int r) { return min(H < R ? live : min(R, H - r % H), rend - r); };
+  bf16x8 vd[HWG_DYC], vx[HWG_XC];
+  auto load = [&](int r, int cnt) {
+#pragma unroll
+    for (int u = 0; u < HWG_DYC; ++u) {
+      const int c = tid + 256 * u;
+      const int slot = c >> 3, ch = (c & 7) * 8;
+      const int rr = slot / Wp, col = slot - rr * Wp;
+      vd[u] = (rr < cnt && col < W) ? ld8(dY + ((long)(r + rr) * W + col) * Cout + co0 + ch) : zero8();
+    }
+#pragma unroll
+    for (int u = 0; u < HWG_XC; ++u) {
+      const int c = tid + 256 * u;
+      const int pos = c >> 2, ch = (c & 3) * 8;
+      const int hr = pos / XW, cc = pos - hr * XW;
+      const int k = hr / (Hs + 2), loc = hr - k * (Hs + 2);  // segment k, halo row loc
+      const int fr = r + k * Hs;                            // first row of segment k
+      const int n = fr / H, hh = fr - n * H - 1 + loc, ww = cc - 1;
+      // segments past the group's rows (a partial stacked group at the end of a chunk:
+      // their images may not exist) stay zero, like the halo outside the image
+      vx[u] = (c < nxc && k * Hs < cnt && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+                  ? ld8(X + ((long)(n * H + hh) * W + ww) * Cin + ci0 + ch) : zero8();
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < HWG_DYC; ++u) {
+      const int c = tid + 256 * u;
+      *reinterpret_cast<bf16x8*>(sdY + (c >> 3) * HWG_DS + (c & 7) * 8) = vd[u];
+    }
+#pragma unroll
+    for (int u = 0; u < HWG_XC; ++u) {
+      const int c = tid + 256 * u;
+      if (c < nxc) *reinterpret_cast<bf16x8*>(sX + (c >> 2) * HWG_XS + (c & 3) * 8) = vx[u];
+    }
+  };
+  // wave tile: co pair (wave >> 1: 2 x 16 co) x ci half (wave & 1: 16 ci), all 9 taps
+  const int coT = (wave >> 1) * 32, ciT = (wave & 1) * 16;
+  const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[c][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  lds_char* lsm = (lds_char*)smem;
+  const int ldsX = HWG_SLOTS * HWG_DS;  // element offset of sX
+  int r0 = rbeg, cnt = r0 < rend ? group_rows(r0) : 0;
+  if (cnt > 0) load(r0, cnt);
+  while (cnt > 0) {
+    store();
+    __syncthreads();
+    const int r1 = r0 + cnt;
+    const int cnt1 = r1 < rend ? group_rows(r1) : 0;
+    if (cnt1 > 0) load(r1, cnt1);  // lands while this group's MFMAs run
+#pragma unroll 1
+    for (int s0 = 0; s0 < HWG_SLOTS; s0 += 32) {
+      const int sA = s0 + 4 * gq + q, sB = s0 + 16 + 4 * gq + q;  // this lane's K rows
+      bf16x8 a[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, sA * HWG_DS + coT + 16 * c + 4 * p));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, sB * HWG_DS + coT + 16 * c + 4 * p));
+        a[c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      // halo row of slot row r: r + 2 per preceding segment; rows past the live ones (dY 0)
+      // are clamped onto staged halo rows
+      const int rA0 = min(sA / Wp, live - 1), cA = sA - (sA / Wp) * Wp;
+      const int rB0 = min(sB / Wp, live - 1), cB = sB - (sB / Wp) * Wp;
+      const int rA = rA0 + 2 * (rA0 / Hs), rB = rB0 + 2 * (rB0 / Hs);
+      const int xA = ldsX + (rA * XW + cA) * HWG_XS + ciT + 4 * p;
+      const int xB = ldsX + (rB * XW + cB) * HWG_XS + ciT + 4 * p;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int to = ((tap / 3) * XW + tap % 3) * HWG_XS;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xA + to));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xB + to));
+        const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[0][tap] = mfma16(a[0], b, acc[0][tap]);
+        acc[1][tap] = mfma16(a[1], b, acc[1][tap]);
+      }
+    }
+    __syncthreads();  // every wave is done with this group's tiles
+    r0 = r1;
+    cnt = cnt1;
+  }
+  // slab row of this chunk: [co][tap][ci] (OHWI); 16 lanes hold 16 consecutive ci
+  float* o = out + (long)blockIdx.z * Cout * 9 * Cin;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + coT + 16 * c + 4 * gq + r;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const long idx = ((long)co * 9 + tap) * Cin + ci0 + ciT + i16;
+        o[idx] = accum ? o[idx] + acc[c][tap][r] : acc[c][tap][r];
+      }
+    }
+}
+
+bool conv_halo_wgrad_ok(const ConvGeom& g) {
+  if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad != 1) return false;
+  if (g.OH != g.H || g.OW != g.W || g.Cin % 32 != 0 || g.Cout % 64 != 0) return false;
+  const int Wp = hwg_wp(g.W), R = HWG_SLOTS / Wp;
+  if (HWG_SLOTS % Wp != 0) return false;
+  const int Hs = g.H < R ? g.H : R;
+  return (R / Hs) * (Hs + 2) * (Wp + 2) <= HWG_MAXPOS;
+}
+
+// rows per chunk must keep stacked groups on image starts: a multiple of H when H < R
+int conv_halo_wgrad_row_quantum(const ConvGeom& g) {
+  const int R = HWG_SLOTS / hwg_wp(g.W);
+  return g.H < R ? g.H : 1;
+}
+
+void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out, int rows_per_chunk,
+                     bool accum, hipStream_t s) {
+  const int chunks = (g.N * g.H + rows_per_chunk - 1) / rows_per_chunk;
+  const dim3 grid(g.Cout / 64, g.Cin / 32, chunks);
+  const size_t lds = conv_halo_wgrad_lds();
+  static bool opted = false;
+  if (!opted) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    opted = true;
+  }
+  hipLaunchKernelGGL(conv3x3s1_halo_wgrad_kernel, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk,
+                     accum && chunks == 1 ? 1 : 0);
+}
+
 }  // namespace ddp_amd

@@ -85,6 +85,17 @@ ConvPlan conv_gemm_plan(const ConvGeom& g, bool dgrad, int bp, int bc, int split
                         int halo = -1);
 bool conv_halo_fits(const ConvGeom& g, int bp);
 int conv_halo_rows(const ConvGeom& g, int bp);
+// tap-fused stride-1 3x3 weight gradient (conv_halo.hip): chunks of whole output rows
+bool conv_halo_wgrad_ok(const ConvGeom& g);
+int conv_halo_wgrad_row_quantum(const ConvGeom& g);  // rows per chunk must be a multiple
+void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out, int rows_per_chunk,
+                     bool accum, hipStream_t s);
+// wgrad plan overrides for sweeps / A-B: halo 0 = never, 1 = auto (where the per-tap GEMM
+// would use 64 x 64 tiles), 2 = wherever eligible; target = blocks per launch
+void conv_gemm_wgrad_set_halo(int halo, int target);
+// pixels per chunk the weight-gradient launcher accepts: multiples of 32 (per-tap GEMM), or
+// whole-row chunks for the halo kernel
+bool conv_gemm_wgrad_ppc_ok(const ConvGeom& g, int ppc);
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
                    bf16_t* Y, float* stats, float* part, hipStream_t s);
 void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* dY, const bf16_t* Wt,

@@ -139,6 +139,50 @@ def test_conv_gemm_wgrad(C, N, H, Cin, Cout, K, s, p):
     assert relerr((d2 - prior).view(Cout, K, K, Cin), rdw) < 2e-3
 
 
+@pytest.mark.parametrize("N,H,Cin,Cout,rpc", [
+    (2, 56, 64, 64, 4), (2, 56, 64, 64, 12),      # W = 56: 4-row groups, chunks inside an image
+    (3, 28, 128, 64, 8), (3, 28, 64, 128, 24),    # W = 28 (Wp 32, 7-row groups), chunks across images
+    (2, 14, 256, 64, 16),                         # W = 14: padded columns, chunks across images
+    (4, 7, 64, 512, 14), (8, 7, 64, 64, 21),      # W = 7: images stacked 4 per group (2 / 3 per chunk)
+])
+def test_conv_halo_wgrad(C, N, H, Cin, Cout, rpc):
+    """Tap-fused stride-1 3x3 weight gradient (conv_halo.hip): whole-row chunks (row groups
+    split at image boundaries), slabs + fixed-order reduce, a single chunk written /
+    accumulated directly, and the planner's own chunking - against fp32 PyTorch and the
+    per-tap GEMM kernel."""
+    x = rnd(N, H, H, Cin, relu=True, seed=11)
+    dy = rnd(N, H, H, Cout, scale=0.5, seed=13)
+    rdw = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (Cout, Cin, 3, 3),
+                                      dy.float().permute(0, 3, 1, 2), stride=1,
+                                      padding=1).permute(0, 2, 3, 1)
+    row = Cout * 9 * Cin
+    C.conv_gemm_wgrad_set_halo(2)  # the halo kernel wherever eligible (auto skips 128-tile layers)
+    try:
+        for ppc in (rpc * H, C.conv_gemm_wgrad_ppc(x, dy, 3, 3, 1, 1)):
+            assert ppc % H == 0
+            ch = C.conv_gemm_wgrad_chunks(x, dy, 3, 3, 1, 1, ppc)
+            slab = torch.full((ch, row), float("nan"), device=dev)  # every slab element is written
+            C.conv_gemm_wgrad(dy, x, slab, 3, 3, 1, 1, ppc, False)
+            dw = torch.zeros(row, device=dev)
+            C.grad_reduce([(slab, row, 0, row, ch, dw, 1.0, False)])
+            assert relerr(dw.view(Cout, 3, 3, Cin), rdw) < 2e-3, ppc
+        P = N * H * H  # one chunk: overwrite, then accumulate
+        d1 = torch.full((row,), 7.0, device=dev)
+        C.conv_gemm_wgrad(dy, x, d1, 3, 3, 1, 1, P, False)
+        assert relerr(d1.view(Cout, 3, 3, Cin), rdw) < 2e-3
+        prior = torch.randn(row, device=dev)
+        d2 = prior.clone()
+        C.conv_gemm_wgrad(dy, x, d2, 3, 3, 1, 1, P, True)
+        assert relerr((d2 - prior).view(Cout, 3, 3, Cin), rdw) < 2e-3
+        if P % 32 == 0:
+            C.conv_gemm_wgrad_set_halo(0)  # the per-tap GEMM kernel on the same chunking
+            d3 = torch.full((row,), 7.0, device=dev)
+            C.conv_gemm_wgrad(dy, x, d3, 3, 3, 1, 1, P, False)
+            assert relerr(d1, d3) < 1e-4
+    finally:
+        C.conv_gemm_wgrad_set_halo(1)
+
+
 def test_stem_conv_7x7_s2():
     from ddp_amd import native
     from ddp_amd.ops.resnet_fn import to_nhwc4
