@@ -1,3 +1,6 @@
+# Host-side replay of conv3x3s1_halo_wgrad_kernel's index math (csrc/kernels/conv_halo.hip):
+# for every ResNet-18 stride-1 3x3 shape and chunk plan, asserts that every dY / X load and
+# every LDS halo read stays in bounds.  Run: python scripts/halo_wgrad_bounds.py
 # host-side bounds check of conv3x3s1_halo_wgrad_kernel's index math
 SLOTS, MAXPOS = 224, 360
 def wp(W): return (W + 7) & ~7
