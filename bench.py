@@ -308,7 +308,7 @@ def main():
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
                        "graph_steps": k, "fuse_level": eo.fuse_level,
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
-                                  "wgrad_rows": eng.wgrad_rows, "store_a1": eo.store_a1,
+                                  "wgrad_rows": eng.wgrad_rows, "store_a1": eng.store_a1,
                                   "wgrad_split": eo.wgrad_split},
                        "params_finite": finite,
                        "bucket_allreduce": eng.comm_kind, "bucket_allreduce_us": bucket_us,

@@ -57,8 +57,10 @@ class EngineOptions:
     fuse_reduce: bool = True
     # level 1: 0 = the conv backward recomputes conv1 from the compact uint8 batch;
     # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
-    # wgrad role reads a1 tiles too
-    store_a1: int = 0
+    # wgrad role reads a1 tiles too.  None = 1 for bf16 (with the wgrad role split over
+    # channel halves the dgrad role is the conv backward's critical path: 808k -> 825k
+    # img/s at B = 32, 1.08M -> 1.11M at B = 64, profiles/r2_split), 0 for fp32
+    store_a1: int | None = None
     # bucket all-reduce data plane at world size > 1 (the direct kernels fall back to RCCL
     # when their self-test fails): "auto"/"xgmi" = the direct xGMI kernels, one-shot for
     # buckets <= ONESHOT_MAX_ELEMS (deterministic: same plane on every start, so resumes
@@ -106,7 +108,8 @@ class FusedSimpleCNNEngine:
         if self.opts.dtype not in ("bf16", "fp32"):
             raise ValueError(f"engine dtype must be bf16 or fp32, got {self.opts.dtype!r}")
         f32 = self.opts.dtype == "fp32"
-        if f32 and (self.opts.fuse_level < 1 or self.opts.store_a1 != 0):
+        self.store_a1 = self.opts.store_a1 if self.opts.store_a1 is not None else (0 if f32 else 1)
+        if f32 and (self.opts.fuse_level < 1 or self.store_a1 != 0):
             raise ValueError("the fp32 engine runs the level-1 chain (fuse_level >= 1, store_a1 0)")
         R = self.wgrad_rows = self.opts.wgrad_rows or wgrad_rows(28, B, torch.float32 if f32 else BF16)
         g = self.opt.param_groups[0]
@@ -152,7 +155,7 @@ class FusedSimpleCNNEngine:
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
                    fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
-                   store_a1=int(self.opts.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
+                   store_a1=int(self.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
                    epoch_order=bool(self.opts.epoch_order), wgrad_split=int(self.opts.wgrad_split))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce

@@ -123,7 +123,7 @@ def test_fused_reduce_bitwise_equals_grad_reduce(dtype, B, opt):
     print(f"fused reduce {dtype} B={B}: {e2.eng.last_fused_reduce}")
 
 
-@pytest.mark.parametrize("B,fred,store_a1", [(32, True, 0), (32, False, 0), (20, True, 0), (64, True, 0),
+@pytest.mark.parametrize("B,fred,store_a1", [(32, True, 0), (32, False, 0), (20, True, 0), (64, True, 0), (32, True, 1),
                                              (32, True, 2)])
 def test_wgrad_channel_split_bitwise(B, fred, store_a1):
     """Two wgrad blocks per slab row (input-channel halves, XCD-paired block order; B=20
