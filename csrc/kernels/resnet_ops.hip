@@ -226,6 +226,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     }
   };
   int p = p0 + tp;
+  // four pixels' loads in flight (a block streams ~150 KB at layer1; with two in flight
+  // the pass was latency-bound at ~2.2 TB/s), then two, then one - the per-thread
+  // summation order is still pixel order
+  for (; p + 96 < p1; p += 128) {
+    bf16x8 d[4], xx[4], r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long o = (long)(p + 32 * u) * C + c0;
+      d[u] = ld8(dout + o);
+      xx[u] = ld8(x + o);
+      r[u] = RELU ? ld8(out + o) : zero8();
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc8(d[u], (long)(p + 32 * u) * C + c0, xx[u], r[u]);
+  }
   for (; p + 32 < p1; p += 64) {  // two pixels' loads in flight
     const long o0 = (long)p * C + c0, o1 = o0 + 32L * C;
     const bf16x8 d0 = ld8(dout + o0), x0 = ld8(x + o0), d1 = ld8(dout + o1), x1 = ld8(x + o1);

@@ -7,5 +7,5 @@ mkdir -p $out
 for r in $(seq $reps); do
   DDP_AMD_NATIVE_SO=$a timeout -k 10 120 python -u bench.py $args > $out/a_$r.json 2>> $out/err.log || exit $?
   timeout -k 10 120 python -u bench.py $args > $out/b_$r.json 2>> $out/err.log || exit $?
-  python -c "import json; a=json.load(open('$out/a_$r.json')); b=json.load(open('$out/b_$r.json')); print('A', a['value'], a['ms_per_step'], ' B', b['value'], b['ms_per_step'])"
+  python -c "import json; j=lambda f: json.loads([l for l in open(f) if l.startswith('{')][-1]); a=j('$out/a_$r.json'); b=j('$out/b_$r.json'); print('A', a['value'], a['ms_per_step'], ' B', b['value'], b['ms_per_step'])"
 done
