@@ -175,8 +175,8 @@ def main():
                     help="simplecnn = the headline metric; resnet18 = BASELINE config 5 (synthetic 3x224x224)")
     ap.add_argument("--image_size", type=int, default=224, help="resnet18 input size")
     ap.add_argument("--wgrad_halo", type=int, default=1, choices=[0, 1, 2],
-                    help="resnet18: tap-fused halo weight gradient for the stride-1 3x3 layers where "
-                         "the per-tap GEMM would use 64x64 tiles (1), every eligible layer (2), never (0)")
+                    help="resnet18: tap-fused halo weight gradient for every eligible stride-1 3x3 "
+                         "layer (1, 2) or the per-tap GEMM kernel only (0)")
     ap.add_argument("--wgrad_halo_target", type=int, default=256, help="resnet18: halo wgrad blocks per launch")
     ap.add_argument("--dry_launch", action="store_true",
                     help="self-launch test hook: workers report their launcher env and exit (no GPU)")

@@ -687,9 +687,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("halo") = -1);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
   m.def("conv_gemm_wgrad_set_halo", &conv_gemm_wgrad_set_halo, py::arg("halo"), py::arg("target") = 256,
-        "weight-gradient plan override: halo 0 = the per-tap GEMM kernel only, 1 = tap-fused halo "
-        "kernel for the stride-1 3x3 layers where the GEMM would use 64 x 64 tiles (default), 2 = "
-        "halo wherever eligible; target = blocks per launch");
+        "weight-gradient plan override: halo 0 = the per-tap GEMM kernel only, 1 (default) / 2 = "
+        "tap-fused halo kernel for every eligible stride-1 3x3 layer; target = blocks per launch");
   m.def("conv_gemm_wgrad_force_tile", &conv_gemm_wgrad_force_tile);
   m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
     return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));

@@ -865,17 +865,14 @@ void conv_gemm_wgrad_set_halo(int halo, int target) {
   g_wgrad_halo = halo < 0 ? 0 : (halo > 2 ? 2 : halo);
   g_wgrad_halo_target = target > 0 ? target : 256;
 }
-static void wgrad_tile(const ConvGeom& g, int* bm, int* bn);
-// only where the per-tap GEMM would run its 64 x 64 tile (ResNet-18/224: the 56-wide
-// layer1 and 7-wide layer4 3x3 convs, 32.7 -> 23.6 and 37.3 -> 23.6 us); the 128 x 128 GEMM
-// tile of the 28- and 14-wide layers measured faster than the halo kernel (22.2 / 20.9 vs
-// 23.6 us, profiles/r2_halo_wgrad)
+// auto (1): every eligible layer.  Per launch the halo kernel beats the per-tap GEMM's
+// 64 x 64 tile (ResNet-18/224 layer1: 32.7 -> 23.6 us, layer4: 37.3 -> 23.6 us) and loses a
+// little to its 128 x 128 tile (layer2 / layer3: 22.2 / 20.9 vs 23.6 us), but its smaller
+// slabs make the whole step faster on every layer (14.29-14.31k -> 14.36-14.40k img/s over
+// "64 x 64 layers only", profiles/r2_halo_wgrad); 2 = the same, kept for the sweeps
 static bool wgrad_use_halo(const ConvGeom& g) {
   if (!g_wgrad_halo || !conv_halo_wgrad_ok(g)) return false;
-  if (g_wgrad_halo == 2) return true;  // forced (tests, sweeps)
-  int bm, bn;
-  wgrad_tile(g, &bm, &bn);
-  return bm == 64 && bn == 64;
+  return true;
 }
 static int wgrad_halo_ppc(const ConvGeom& g) {
   const int bpc = (g.Cout / 64) * (g.Cin / 32);

@@ -54,7 +54,7 @@ def test_plans_are_valid(layer):
     ppc = C.conv_gemm_wgrad_ppc(x, y, K, K, s, p)
     # per-tap GEMM chunks: multiples of its 32-pixel K-step; halo wgrad (stride-1 3x3 layers
     # where the GEMM would run 64x64 tiles): whole output rows (whole images when stacked)
-    halo_w = K == 3 and s == 1 and Cout == 64 or (K == 3 and s == 1 and OH == 7)
+    halo_w = K == 3 and s == 1
     assert ppc >= 32 and (ppc % (OH * OH if OH < 28 else OH) == 0 if halo_w else ppc % 32 == 0)
     chunks = C.conv_gemm_wgrad_chunks(x, y, K, K, s, p, ppc)
     assert chunks * ppc >= P and (chunks - 1) * ppc < P
@@ -75,13 +75,13 @@ def test_plans_match_sweep_winners():
     assert plan("l3.1x1s2", False)[:3] == (64, 64, 1)
     assert plan("l2.3x3s2", True)[:3] == (128, 64, 1) and plan("l2.3x3s2", True)[4] == 1
     assert plan("l4.1x1s2", True)[:3] == (64, 64, 1)
-    # weight gradient: tap-fused halo kernel on layer1 / layer4 (profiles/r2_halo_wgrad):
+    # weight gradient: tap-fused halo kernel on every stride-1 3x3 layer (profiles/r2_halo_wgrad):
     # whole-row chunks, ~256 blocks of 64 co x 32 ci
-    for name, ppc in (("l1.3x3", 14 * 56), ("l4.3x3", 112 * 7), ("l2.3x3", None), ("l3.3x3", None)):
+    for name, ppc in (("l1.3x3", 14 * 56), ("l2.3x3", 28 * 28), ("l3.3x3", 56 * 14), ("l4.3x3", 112 * 7)):
         _, N, H, Cin, Cout, K, s, p = layers[name]
         x, y, _ = _shapes(N, H, Cin, Cout, K, s, p)
         got = C.conv_gemm_wgrad_ppc(x, y, K, K, s, p)
-        assert (got == ppc) if ppc else (got % 32 == 0), (name, got)
+        assert got == ppc, (name, got)
 
 
 def test_explicit_plan_overrides_and_bad_tiles():
