@@ -178,6 +178,8 @@ def main():
                     help="resnet18: tap-fused halo weight gradient for every eligible stride-1 3x3 "
                          "layer (1, 2) or the per-tap GEMM kernel only (0)")
     ap.add_argument("--wgrad_halo_target", type=int, default=256, help="resnet18: halo wgrad blocks per launch")
+    ap.add_argument("--wgrad_halo_cit", type=int, default=0, choices=[0, 16, 32],
+                    help="resnet18: input channels per halo wgrad block (0 = planner default)")
     ap.add_argument("--dry_launch", action="store_true",
                     help="self-launch test hook: workers report their launcher env and exit (no GPU)")
     ap.add_argument("--no_scaling_ref", action="store_true",
@@ -331,7 +333,7 @@ def bench_resnet(args):
     from ddp_amd.ops.resnet_fn import to_nhwc4
     from ddp_amd.parallel import DistributedDataParallel, setup
 
-    native.require().conv_gemm_wgrad_set_halo(args.wgrad_halo, args.wgrad_halo_target)
+    native.require().conv_gemm_wgrad_set_halo(args.wgrad_halo, args.wgrad_halo_target, args.wgrad_halo_cit)
     if args.dtype != "bf16":
         raise SystemExit("--model resnet18 runs the bf16 MFMA kernels only")
     ws = int(os.environ.get("WORLD_SIZE", "1"))

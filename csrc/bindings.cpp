@@ -687,8 +687,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("halo") = -1);
   m.def("conv_gemm_wgrad_chunks", &op_conv_gemm_wgrad_chunks);
   m.def("conv_gemm_wgrad_set_halo", &conv_gemm_wgrad_set_halo, py::arg("halo"), py::arg("target") = 256,
+        py::arg("cit") = 0,
         "weight-gradient plan override: halo 0 = the per-tap GEMM kernel only, 1 (default) / 2 = "
-        "tap-fused halo kernel for every eligible stride-1 3x3 layer; target = blocks per launch");
+        "tap-fused halo kernel for every eligible stride-1 3x3 layer; target = blocks per launch; cit = "
+        "input channels per halo block (0 auto, 16, 32)");
   m.def("conv_gemm_wgrad_force_tile", &conv_gemm_wgrad_force_tile);
   m.def("conv_gemm_wgrad_tiles", [](const Tensor& X, const Tensor& dY, int KH, int KW, int st, int pd) {
     return conv_gemm_wgrad_tiles(geom_of(X, dY, KH, KW, st, pd));

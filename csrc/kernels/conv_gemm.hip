@@ -861,10 +861,13 @@ static void wgrad_tile(const ConvGeom& g, int* bm, int* bn) {
 // tap-fused halo weight gradient (conv_halo.hip) for stride-1 3x3 layers: plan = chunks of
 // whole output rows so that the launch has ~g_wgrad_halo_target blocks of 64 co x 32 ci
 static int g_wgrad_halo = 1, g_wgrad_halo_target = 256;  // halo: 0 off, 1 auto, 2 wherever eligible
-void conv_gemm_wgrad_set_halo(int halo, int target) {
+static int g_wgrad_halo_cit = 0;                             // input channels per block (0 = auto)
+void conv_gemm_wgrad_set_halo(int halo, int target, int cit) {
   g_wgrad_halo = halo < 0 ? 0 : (halo > 2 ? 2 : halo);
   g_wgrad_halo_target = target > 0 ? target : 256;
+  g_wgrad_halo_cit = (cit == 16 || cit == 32) ? cit : 0;
 }
+static int wgrad_halo_cit(const ConvGeom& g) { return g_wgrad_halo_cit ? g_wgrad_halo_cit : 32; }
 // auto (1): every eligible layer.  Per launch the halo kernel beats the per-tap GEMM's
 // 64 x 64 tile (ResNet-18/224 layer1: 32.7 -> 23.6 us, layer4: 37.3 -> 23.6 us) and loses a
 // little to its 128 x 128 tile (layer2 / layer3: 22.2 / 20.9 vs 23.6 us), but its smaller
@@ -875,7 +878,7 @@ static bool wgrad_use_halo(const ConvGeom& g) {
   return true;
 }
 static int wgrad_halo_ppc(const ConvGeom& g) {
-  const int bpc = (g.Cout / 64) * (g.Cin / 32);
+  const int bpc = (g.Cout / 64) * (g.Cin / wgrad_halo_cit(g));
   int chunks = g_wgrad_halo_target / bpc;
   if (chunks < 1) chunks = 1;
   const int rows = g.N * g.H;
@@ -924,7 +927,7 @@ void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float
   const int ch = conv_gemm_wgrad_chunks(g, px_per_chunk);
   const int acc = (accum && ch == 1) ? 1 : 0;
   if (wgrad_use_halo(g) && px_per_chunk % (g.W * conv_halo_wgrad_row_quantum(g)) == 0) {  // whole rows
-    conv_halo_wgrad(g, dY, X, out, px_per_chunk / g.W, acc != 0, s);
+    conv_halo_wgrad(g, dY, X, out, px_per_chunk / g.W, acc != 0, s, wgrad_halo_cit(g));
     return;
   }
   int bm, bn;

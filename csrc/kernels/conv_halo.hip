@@ -445,13 +445,19 @@ constexpr int HWG_DS = 64 + 16;             // sdY row stride: 40 dwords (odd mu
 constexpr int HWG_XS = 32 + 16;             // sX row stride: 24 dwords (odd multiple of 8)
 constexpr int HWG_MAXPOS = 360;             // largest halo: 4 x (7 + 2) x (8 + 2) (W = 56: 6 x 58)
 constexpr int HWG_DYC = HWG_SLOTS * 8 / 256;         // 16-byte dY chunks per thread (7)
-constexpr int HWG_XC = (HWG_MAXPOS * 4 + 255) / 256;  // 16-byte X chunks per thread (6)
+// 16-byte X chunks per thread: CIT / 8 chunks per halo position (32 ci: 6, 16 ci: 3)
+template <int CIT>
+constexpr int hwg_xc() { return (HWG_MAXPOS * (CIT / 8) + 255) / 256; }
 
 __host__ __device__ inline int hwg_wp(int W) { return (W + 7) & ~7; }
 size_t conv_halo_wgrad_lds() {
   return sizeof(bf16_t) * ((size_t)HWG_SLOTS * HWG_DS + (size_t)HWG_MAXPOS * HWG_XS);
 }
 
+// CIT: input channels per block (32: 4 waves = 2 co pairs x 2 ci halves; 16: 4 waves x one
+// 16-wide co tile - twice the blocks per chunk, so half the chunks and slab bytes for the
+// same launch size, at twice the dY re-reads)
+template <int CIT>
 __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                                       const bf16_t* __restrict__ X,
                                                                       float* __restrict__ out, int rows_per_chunk,
@@ -461,10 +467,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
   const int Wp = hwg_wp(W), R = HWG_SLOTS / Wp, XW = Wp + 2;
   // segment = rows sharing one halo: a group of R rows of one image, or nimg stacked images
   const int Hs = H < R ? H : R, nimg = R / Hs, live = nimg * Hs;
-  const int nxc = nimg * (Hs + 2) * XW * 4;  // 16-byte X chunks of the halo(s) (32 channels = 4 chunks)
+  constexpr int XCP = CIT / 8, HWG_XC = hwg_xc<CIT>();        // 16-byte chunks per position / thread
+  const int nxc = nimg * (Hs + 2) * XW * XCP;  // 16-byte X chunks of the halo(s)
   bf16_t* sdY = reinterpret_cast<bf16_t*>(smem);
   bf16_t* sX = sdY + HWG_SLOTS * HWG_DS;
-  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * 32;
+  const int co0 = blockIdx.x * 64, ci0 = blockIdx.y * CIT;
   const int rows = g.N * H;
   const int rbeg = blockIdx.z * rows_per_chunk;
   const int rend = min(rows, rbeg + rows_per_chunk);
@@ -484,7 +491,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
 #pragma unroll
     for (int u = 0; u < HWG_XC; ++u) {
       const int c = tid + 256 * u;
-      const int pos = c >> 2, ch = (c & 3) * 8;
+      const int pos = c / XCP, ch = (c - pos * XCP) * 8;
       const int hr = pos / XW, cc = pos - hr * XW;
       const int k = hr / (Hs + 2), loc = hr - k * (Hs + 2);  // segment k, halo row loc
       const int fr = r + k * Hs;                            // first row of segment k
@@ -504,15 +511,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
 #pragma unroll
     for (int u = 0; u < HWG_XC; ++u) {
       const int c = tid + 256 * u;
-      if (c < nxc) *reinterpret_cast<bf16x8*>(sX + (c >> 2) * HWG_XS + (c & 3) * 8) = vx[u];
+      if (c < nxc) *reinterpret_cast<bf16x8*>(sX + (c / XCP) * HWG_XS + (c % XCP) * 8) = vx[u];
     }
   };
   // wave tile: co pair (wave >> 1: 2 x 16 co) x ci half (wave & 1: 16 ci), all 9 taps
-  const int coT = (wave >> 1) * 32, ciT = (wave & 1) * 16;
+  constexpr int NCT = CIT == 32 ? 2 : 1;  // 16-wide co tiles per wave
+  const int coT = CIT == 32 ? (wave >> 1) * 32 : wave * 16, ciT = CIT == 32 ? (wave & 1) * 16 : 0;
   const int gq = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
-  f32x4 acc[2][9];
+  f32x4 acc[NCT][9];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < NCT; ++c)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[c][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   lds_char* lsm = (lds_char*)smem;
@@ -528,9 +536,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
 #pragma unroll 1
     for (int s0 = 0; s0 < HWG_SLOTS; s0 += 32) {
       const int sA = s0 + 4 * gq + q, sB = s0 + 16 + 4 * gq + q;  // this lane's K rows
-      bf16x8 a[2];
+      bf16x8 a[NCT];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NCT; ++c) {
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, sA * HWG_DS + coT + 16 * c + 4 * p));
         const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, sB * HWG_DS + coT + 16 * c + 4 * p));
         a[c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -548,8 +556,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xA + to));
         const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xB + to));
         const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc[0][tap] = mfma16(a[0], b, acc[0][tap]);
-        acc[1][tap] = mfma16(a[1], b, acc[1][tap]);
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) acc[c][tap] = mfma16(a[c], b, acc[c][tap]);
       }
     }
     __syncthreads();  // every wave is done with this group's tiles
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
   // slab row of this chunk: [co][tap][ci] (OHWI); 16 lanes hold 16 consecutive ci
   float* o = out + (long)blockIdx.z * Cout * 9 * Cin;
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c < NCT; ++c)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = co0 + coT + 16 * c + 4 * gq + r;
@@ -587,18 +595,22 @@ int conv_halo_wgrad_row_quantum(const ConvGeom& g) {
 }
 
 void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out, int rows_per_chunk,
-                     bool accum, hipStream_t s) {
+                     bool accum, hipStream_t s, int cit) {
   const int chunks = (g.N * g.H + rows_per_chunk - 1) / rows_per_chunk;
-  const dim3 grid(g.Cout / 64, g.Cin / 32, chunks);
+  const dim3 grid(g.Cout / 64, g.Cin / cit, chunks);
   const size_t lds = conv_halo_wgrad_lds();
   static bool opted = false;
   if (!opted) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (const void* k : {reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<32>),
+                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<16>)})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     opted = true;
   }
-  hipLaunchKernelGGL(conv3x3s1_halo_wgrad_kernel, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk,
-                     accum && chunks == 1 ? 1 : 0);
+  const int acc = accum && chunks == 1 ? 1 : 0;
+  if (cit == 16)
+    hipLaunchKernelGGL(conv3x3s1_halo_wgrad_kernel<16>, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc);
+  else
+    hipLaunchKernelGGL(conv3x3s1_halo_wgrad_kernel<32>, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc);
 }
 
 }  // namespace ddp_amd

@@ -89,10 +89,10 @@ int conv_halo_rows(const ConvGeom& g, int bp);
 bool conv_halo_wgrad_ok(const ConvGeom& g);
 int conv_halo_wgrad_row_quantum(const ConvGeom& g);  // rows per chunk must be a multiple
 void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out, int rows_per_chunk,
-                     bool accum, hipStream_t s);
+                     bool accum, hipStream_t s, int cit = 32);  // cit: input channels per block (16 | 32)
 // wgrad plan overrides for sweeps / A-B: halo 0 = never, 1 / 2 = every eligible stride-1
 // 3x3 layer (default 1); target = blocks per launch
-void conv_gemm_wgrad_set_halo(int halo, int target);
+void conv_gemm_wgrad_set_halo(int halo, int target, int cit = 0);  // cit 0 = auto, 16, 32
 // pixels per chunk the weight-gradient launcher accepts: multiples of 32 (per-tap GEMM), or
 // whole-row chunks for the halo kernel
 bool conv_gemm_wgrad_ppc_ok(const ConvGeom& g, int ppc);

@@ -145,7 +145,8 @@ def test_conv_gemm_wgrad(C, N, H, Cin, Cout, K, s, p):
     (2, 14, 256, 64, 16),                         # W = 14: padded columns, chunks across images
     (4, 7, 64, 512, 14), (8, 7, 64, 64, 21),      # W = 7: images stacked 4 per group (2 / 3 per chunk)
 ])
-def test_conv_halo_wgrad(C, N, H, Cin, Cout, rpc):
+@pytest.mark.parametrize("cit", [32, 16])
+def test_conv_halo_wgrad(C, N, H, Cin, Cout, rpc, cit):
     """Tap-fused stride-1 3x3 weight gradient (conv_halo.hip): whole-row chunks (row groups
     split at image boundaries), slabs + fixed-order reduce, a single chunk written /
     accumulated directly, and the planner's own chunking - against fp32 PyTorch and the
@@ -156,7 +157,7 @@ def test_conv_halo_wgrad(C, N, H, Cin, Cout, rpc):
                                       dy.float().permute(0, 3, 1, 2), stride=1,
                                       padding=1).permute(0, 2, 3, 1)
     row = Cout * 9 * Cin
-    C.conv_gemm_wgrad_set_halo(2)  # the halo kernel wherever eligible (auto skips 128-tile layers)
+    C.conv_gemm_wgrad_set_halo(2, 256, cit)  # the halo kernel, cit input channels per block
     try:
         for ppc in (rpc * H, C.conv_gemm_wgrad_ppc(x, dy, 3, 3, 1, 1)):
             assert ppc % H == 0
