@@ -269,9 +269,9 @@ def main():
     barrier()
     t0 = time.perf_counter()
     eng.run_steps(args.steps)
-    eng.synchronize()
-    barrier()
+    barrier()  # torch.cuda.synchronize() waits for the engine's streams too
     dt = time.perf_counter() - t0
+    eng.synchronize()  # (idle by now) raises if an in-launch / cross-GPU wait timed out
     if ws > 1:
         t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
