@@ -480,25 +480,42 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
   // stacked, the last whole image) or the chunk
   auto group_rows = [&](int r) { return min(H < R ? live : min(R, H - r % H), rend - r); };
   bf16x8 vd[HWG_DYC], vx[HWG_XC];
+  // per-thread staging geometry, the same for every row group (the divisions by the
+  // runtime Wp / XW / Hs + 2 were ~1.5k VALU instructions per group when done in load()):
+  // dY chunk u -> packed (slot row rr | column col << 8); X chunk u -> packed (segment k |
+  // halo row loc << 8 | halo column cc << 16 | channel chunk << 24), 0xff in k = past the halo
+  unsigned dgeo[HWG_DYC], xgeo[HWG_XC];
+#pragma unroll
+  for (int u = 0; u < HWG_DYC; ++u) {
+    const int slot = (tid + 256 * u) >> 3;
+    const int rr = slot / Wp;
+    dgeo[u] = (unsigned)rr | (unsigned)(slot - rr * Wp) << 8;
+  }
+#pragma unroll
+  for (int u = 0; u < HWG_XC; ++u) {
+    const int c = tid + 256 * u;
+    const int pos = c / XCP, chk = c - pos * XCP;
+    const int hr = pos / XW, cc = pos - hr * XW;
+    const int k = hr / (Hs + 2), loc = hr - k * (Hs + 2);
+    xgeo[u] = c < nxc ? ((unsigned)k | (unsigned)loc << 8 | (unsigned)cc << 16 | (unsigned)chk << 24) : 0xffu;
+  }
   auto load = [&](int r, int cnt) {
+    // group start: image n0, row h0 (stacked groups start on an image: h0 = 0, segment k
+    // is image n0 + k; a single-image group has k = 0 only)
+    const int n0 = r / H, h0 = r - n0 * H;
 #pragma unroll
     for (int u = 0; u < HWG_DYC; ++u) {
-      const int c = tid + 256 * u;
-      const int slot = c >> 3, ch = (c & 7) * 8;
-      const int rr = slot / Wp, col = slot - rr * Wp;
+      const int rr = dgeo[u] & 0xff, col = dgeo[u] >> 8, ch = ((tid + 256 * u) & 7) * 8;
       vd[u] = (rr < cnt && col < W) ? ld8(dY + ((long)(r + rr) * W + col) * Cout + co0 + ch) : zero8();
     }
 #pragma unroll
     for (int u = 0; u < HWG_XC; ++u) {
-      const int c = tid + 256 * u;
-      const int pos = c / XCP, ch = (c - pos * XCP) * 8;
-      const int hr = pos / XW, cc = pos - hr * XW;
-      const int k = hr / (Hs + 2), loc = hr - k * (Hs + 2);  // segment k, halo row loc
-      const int fr = r + k * Hs;                            // first row of segment k
-      const int n = fr / H, hh = fr - n * H - 1 + loc, ww = cc - 1;
+      const unsigned gq8 = xgeo[u];
+      const int k = gq8 & 0xff, loc = (gq8 >> 8) & 0xff, cc = (gq8 >> 16) & 0xff, ch = (int)(gq8 >> 24) * 8;
+      const int n = n0 + k, hh = h0 - 1 + loc, ww = cc - 1;
       // segments past the group's rows (a partial stacked group at the end of a chunk:
       // their images may not exist) stay zero, like the halo outside the image
-      vx[u] = (c < nxc && k * Hs < cnt && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
+      vx[u] = (k != 0xff && k * Hs < cnt && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
                   ? ld8(X + ((long)(n * H + hh) * W + ww) * Cin + ci0 + ch) : zero8();
     }
   };
