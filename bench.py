@@ -149,7 +149,12 @@ def main():
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--fuse_level", type=int, default=None,
                     help="engine fusion level (0: 8 kernels/step, 1: 3 kernels/step, 2: fc + conv backward "
-                         "in one launch); default = engine default (1)")
+                         "in one launch, 3: dZ2 in the forward, fc weight gradient inside the conv "
+                         "backward - 2 kernels/step); default = engine default (3)")
+    ap.add_argument("--l3_fc_role", type=int, default=None, choices=[0, 1, 2],
+                    help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch, right "
+                         "after the dgrad blocks (1) or after every conv block (2), or as its own kernel "
+                         "between forward and conv backward (0)")
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
@@ -246,7 +251,7 @@ def main():
     eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=args.dtype,
                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
     eo.comm = args.comm
-    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split"):
+    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role"):
         if getattr(args, f) is not None:
             setattr(eo, f, getattr(args, f))
     eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)

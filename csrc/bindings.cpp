@@ -819,10 +819,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.f32 = cfgd.contains("f32") ? (int)cfgd["f32"].cast<bool>() : 0;
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? (int)cfgd["fuse_reduce"].cast<bool>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
+             c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
+             TORCH_CHECK(c.l3_fc_role >= 0 && c.l3_fc_role <= 2, "engine: l3_fc_role must be 0, 1 or 2");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;
              TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");
-             TORCH_CHECK(c.fuse_level >= 0 && c.fuse_level <= 2, "engine: fuse_level must be 0, 1 or 2");
+             TORCH_CHECK(c.fuse_level >= 0 && c.fuse_level <= 3, "engine: fuse_level must be 0, 1, 2 or 3");
              TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0, es) <= 160 * 1024 &&
                              conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0, es) <= 160 * 1024 &&
                              conv3x3_dgrad_lds(c.W, c.C2, c.pxt_dgrad, true, es) <= 160 * 1024,
@@ -908,6 +910,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("level2_active", &SimpleCNNEngine::level2_active)
       .def_property_readonly("last_fused_reduce", &SimpleCNNEngine::last_fused_reduce)
+      .def_property_readonly("last_level3", &SimpleCNNEngine::last_level3)
+      .def_property_readonly("last_fc_role", &SimpleCNNEngine::last_fc_role)
+      .def("level3_active", &SimpleCNNEngine::level3_active, py::arg("batch"))
       .def_property_readonly("sync_error", &SimpleCNNEngine::sync_error)
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)
       .def("set_xgmi", &SimpleCNNEngine::set_xgmi, py::arg("xgmi"), py::arg("channels"))

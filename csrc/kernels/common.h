@@ -373,6 +373,38 @@ constexpr int XENT_MAX_BLK = 16;  // conv blocks per image: HW / CH + 2 <= 16
 // global loads are 16 scattered 4-byte loads per thread: ~5k lane-addresses per block
 // through the texture addresser, measured ~2 us.)
 constexpr int XENT_PRE_Q = 4;  // float4 per thread held from the prefetch to the LDS write
+// The two fixed-order pieces every producer of dL shares (xent_finish below, the fc_bwd
+// prologue, and the level-3 conv forward that computes dZ2 itself): one inlined body each,
+// so every caller evaluates the same float operations in the same order (bit-identical).
+// Image b's raw logit o (before the bias): sum over the conv blocks kb0..kb1 touching it of
+// part[kb][slot][o] (slot 1 only for a first block that started in the previous image).
+template <typename Ld>
+__device__ __forceinline__ float xent_logit_acc(int b, int o, int HW, int CH, int NO, Ld ld) {
+  const int p0 = b * HW;
+  const int kb0 = p0 / CH, kb1 = (p0 + HW - 1) / CH;
+  const int slot0 = kb0 * CH == p0 ? 0 : 1;
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < XENT_MAX_BLK; ++j) {
+    const int kb = min(kb0 + j, kb1);
+    const float v = ld((kb * 2 + (j == 0 ? slot0 : 0)) * NO + o);
+    a += (kb0 + j <= kb1) ? v : 0.f;
+  }
+  return a;
+}
+// dL[o] of one row x[0..NO) (softmax - onehot, times gscale); *loss (if o == 0 and loss)
+// = logsumexp - x[label].  label is clamped to [0, NO).
+__device__ __forceinline__ float xent_row_dl(const float* x, int NO, int o, int label, float gscale,
+                                             float* loss) {
+  label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
+  float mx = x[0];
+  for (int k = 1; k < NO; ++k) mx = fmaxf(mx, x[k]);
+  float se = 0.f;
+  for (int k = 0; k < NO; ++k) se += __expf(x[k] - mx);
+  const float inv = 1.f / se;
+  if (o == 0 && loss) *loss = mx + __logf(se) - x[label];
+  return (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
+}
 struct XentPre {
   int lab0;
   float bias_o;  // bias[threadIdx.x % NO]
@@ -416,17 +448,7 @@ __device__ __forceinline__ void xent_finish(const XentPre& pre, const float* __r
   // the first iteration would wait (vmcnt in order) for all of the caller's column loads
   auto logit_sum = [&](int t) {
     const int b = t / NO, o = t - (t / NO) * NO;
-    const int p0 = b * HW;
-    const int kb0 = p0 / CH, kb1 = (p0 + HW - 1) / CH;
-    const int slot0 = kb0 * CH == p0 ? 0 : 1;
-    float a = 0.f;
-#pragma unroll
-    for (int j = 0; j < XENT_MAX_BLK; ++j) {
-      const int kb = min(kb0 + j, kb1);
-      const float v = s_part[(kb * 2 + (j == 0 ? slot0 : 0)) * NO + o];
-      a += (kb0 + j <= kb1) ? v : 0.f;
-    }
-    return a;
+    return xent_logit_acc(b, o, HW, CH, NO, [&](int i) { return s_part[i]; });
   };
   if ((int)threadIdx.x < B * NO) s_lg[threadIdx.x] = pre.bias_o + logit_sum(threadIdx.x);
   if (B * NO > (int)blockDim.x)
@@ -436,15 +458,7 @@ __device__ __forceinline__ void xent_finish(const XentPre& pre, const float* __r
   DDP_STAMP(STAMP_K_FC_BWD, 6);
   auto row_out = [&](int t, int label) {
     const int b = t / NO, o = t - (t / NO) * NO;
-    label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
-    const float* x = s_lg + b * NO;
-    float mx = x[0];
-    for (int k = 1; k < NO; ++k) mx = fmaxf(mx, x[k]);
-    float se = 0.f;
-    for (int k = 0; k < NO; ++k) se += __expf(x[k] - mx);
-    const float inv = 1.f / se;
-    dl[t] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
-    if (o == 0) loss[b] = mx + __logf(se) - x[label];
+    dl[t] = xent_row_dl(s_lg + b * NO, NO, o, label, gscale, loss + b);
   };
   // first logit: b = threadIdx.x / NO < blockDim, so its label is in s_lab (no pointer
   // select: the compiler would merge LDS / global into one flat load counted in vmcnt)
@@ -468,19 +482,7 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
     // by runtime values are long software sequences.  Block kb0 is the only one that can
     // start in the previous image (slot 1); every later block starts inside image b.
     const int b = t / NO, o = t - (t / NO) * NO;
-    const int p0 = b * HW;
-    const int kb0 = p0 / CH, kb1 = (p0 + HW - 1) / CH;
-    const int slot0 = kb0 * CH == p0 ? 0 : 1;
-    float v[XENT_MAX_BLK];
-#pragma unroll
-    for (int j = 0; j < XENT_MAX_BLK; ++j) {
-      const int kb = min(kb0 + j, kb1);
-      v[j] = part[(kb * 2 + (j == 0 ? slot0 : 0)) * NO + o];
-    }
-    float a = 0.f;
-#pragma unroll
-    for (int j = 0; j < XENT_MAX_BLK; ++j) a += (kb0 + j <= kb1) ? v[j] : 0.f;
-    s_lg[t] = bias[o] + a;
+    s_lg[t] = bias[o] + xent_logit_acc(b, o, HW, CH, NO, [&](int i) { return part[i]; });
   }
   if ((int)threadIdx.x < B) s_lab[threadIdx.x] = lab0;
   __syncthreads();
@@ -488,16 +490,8 @@ __device__ __forceinline__ void xent_batch_block(const float* __restrict__ part,
   // and sum-exp in the same serial order (bit-identical values), then its own class.
   for (int t = threadIdx.x; t < B * NO; t += blockDim.x) {
     const int b = t / NO, o = t - (t / NO) * NO;
-    int label = b < (int)blockDim.x ? s_lab[b] : labels32[bi.row(b, base)];
-    label = label < 0 ? 0 : (label >= NO ? NO - 1 : label);
-    const float* x = s_lg + b * NO;
-    float mx = x[0];
-    for (int k = 1; k < NO; ++k) mx = fmaxf(mx, x[k]);
-    float se = 0.f;
-    for (int k = 0; k < NO; ++k) se += __expf(x[k] - mx);
-    const float inv = 1.f / se;
-    dl[t] = (__expf(x[o] - mx) * inv - (o == label ? 1.f : 0.f)) * gscale;
-    if (o == 0) loss[b] = mx + __logf(se) - x[label];
+    const int label = b < (int)blockDim.x ? s_lab[b] : labels32[bi.row(b, base)];
+    dl[t] = xent_row_dl(s_lg + b * NO, NO, o, label, gscale, loss + b);
   }
 }
 

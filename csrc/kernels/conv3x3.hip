@@ -92,7 +92,8 @@ __device__ __forceinline__ bf16x8 ld16_sc1(__amdgpu_buffer_rsrc_t r, long byte_o
 struct BwdReduce {
   SlabSet ss{};
   long nchunks = 0;
-  int first_reducer = 0;  // blocks [first_reducer, grid) reduce after the arrival count
+  int first_reducer = 0;  // blocks [first_reducer, nconv) reduce after the arrival count
+  int nconv = 0;          // conv-role blocks (the arrivals the reducers wait for); fc-role blocks follow
   int* done = nullptr;  // 8 arrival counters, 32 ints apart (zeroed by the step's forward)
   int* err = nullptr;   // set to 2 when the wait times out
 };
@@ -164,13 +165,19 @@ __host__ __device__ inline size_t fc_epi_lds(int pxt, int nof) { return sizeof(f
 // NW waves per block, PXT 16-pixel tiles per wave: a block covers CH = 16 * NW * PXT
 // pixels (64 * pxt in launcher terms).  With NW = 8 two waves share each SIMD, which
 // doubles the VALU issue rate of the conv1 recompute and the fc epilogue.
-template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO>
+// DZ (fuse level 3, launchers.h FwdDz): after the fc partials, wait for every block of the
+// block's image(s), evaluate dL and write dZ2 for the block's own pixels (see FwdDz).
+constexpr unsigned long long FWD_DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 MHz clock
+
+template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
+          bool DZ = false>
 __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     const T* __restrict__ X, const T* __restrict__ Wt, const float* __restrict__ bias,
     T* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
-    const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1) {
+    const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1, FwdDz dzo) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
+  static_assert(!DZ || (!F32 && NOF == 10 && A1X), "level-3 dZ2 needs the bf16 fc epilogue and the conv1 recompute");
   constexpr int CE = P::CE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DDP_STAMP(STAMP_K_CONV_FWD, 0);
@@ -191,7 +198,10 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   const int wc = KW / CE;
   const int xc = Cin / CE;
   if (A1X && c1.zero_i32)  // the step's level-2 hand-off flags (see C1Src)
-    for (int i = threadIdx.x; i < c1.zero_per_block; i += NT) c1.zero_i32[(long)blockIdx.x * c1.zero_per_block + i] = 0;
+    for (int i = threadIdx.x; i < c1.zero_per_block; i += NT) {
+      const long z = (long)blockIdx.x * c1.zero_per_block + i;
+      if (z < c1.zero_total) c1.zero_i32[z] = 0;
+    }
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave & 3);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
@@ -328,6 +338,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
   float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X, (int)sizeof(T)));
+  uint2 a2pk[DZ ? PXT : 1][4];  // DZ: the stored bf16 a2 quads (dZ2's ReLU mask)
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -347,6 +358,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
         const uint2 pk = pack4(v0, v1, v2, v3);
         if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
         unpack4(pk, q);
+        if constexpr (DZ) a2pk[pt][t] = pk;
       }
       if (NOF > 0) {
 #pragma unroll
@@ -395,10 +407,111 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
           for (int g = 0; g < 4; ++g) acc_o += s_fc[(tile * 4 + g) * NOF + o];
         }
       }
-      fc_part[((long)blockIdx.x * 2 + slot) * NOF + o] = acc_o;
+      float* dst = fc_part + ((long)blockIdx.x * 2 + slot) * NOF + o;
+      if constexpr (DZ) st_wt(dst, acc_o);  // read by the other blocks of the image in-launch
+      else *dst = acc_o;
     }
   }
   DDP_STAMP(STAMP_K_CONV_FWD, 4);
+  if constexpr (DZ) {
+    // ---- level 3: dL of the block's image(s), then dZ2 of its own pixels.
+    // Hand-off (MI355X_MICROARCH.md, hand-off table row 1): the partials were stored sc1 by
+    // wave 0 (threads < 2 * NOF), which drains them and then adds 1 to each touched image's
+    // counter (one lane per counter); the same wave polls the counters with sc1 loads and
+    // reads the partials with sc1 loads; the other waves only read LDS after a barrier.
+    const int HWi = H * W;
+    const int img0 = (int)(P0 / HWi);
+    const long plast = (P0 + CH < Ptot ? P0 + CH : Ptot) - 1;
+    const int nimg = (int)(plast / HWi) - img0 + 1;  // 1 or 2 (CH <= HW)
+    float* s_lg = s_fc + NW * PXT * 4 * NOF;          // [2][NOF] logits
+    float* s_dl = s_lg + 2 * NOF;                     // [2][NOF] dL
+    DDP_STAMP(STAMP_K_FWD_DZ, 0);
+    if (wave == 0) {
+      int label = 0;
+      if (lane < 2 * NOF) {  // the label of this thread's row, requested before the wait
+        const int im = img0 + (lane >= NOF ? 1 : 0);
+        if (im < B) label = c1.labels[c1.bi.row(im, c1.bi.base())];
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial-logit stores are out
+      DDP_STAMP(STAMP_K_FWD_DZ, 1);
+      if (lane < nimg)
+        __hip_atomic_fetch_add(dzo.img_cnt + (img0 + lane) * FWD_DZ_CNT_STRIDE, 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      {
+        const int im = img0 + (lane < nimg ? lane : 0);
+        const int kb0 = im * HWi / CH, kb1 = (im * HWi + HWi - 1) / CH;
+        const int want = kb1 - kb0 + 1;  // blocks touching image im
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (true) {
+          const int v = lane < nimg ? __hip_atomic_load(dzo.img_cnt + im * FWD_DZ_CNT_STRIDE, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                                    : want;
+          if (__all(v >= want)) break;
+          if (__builtin_amdgcn_s_memrealtime() - t0 > FWD_DZ_WAIT_TICKS) {
+            if (lane == 0 && dzo.err) __hip_atomic_store(dzo.err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      DDP_STAMP(STAMP_K_FWD_DZ, 2);
+      if (lane < 2 * NOF) {
+        const int slot = lane >= NOF ? 1 : 0, o = lane - slot * NOF;
+        if (slot < nimg) {
+          const float a = xent_logit_acc(img0 + slot, o, HWi, CH, NOF, [&](int i) {
+            return __hip_atomic_load(fc_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          });
+          s_lg[lane] = dzo.fc_bias[o] + a;
+        }
+      }
+      DDP_STAMP(STAMP_K_FWD_DZ, 4);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row's logits (other lanes) are in LDS
+      if (lane < 2 * NOF) {
+        const int slot = lane >= NOF ? 1 : 0, o = lane - slot * NOF;
+        if (slot < nimg) {
+          float lossv = 0.f;
+          const float d = xent_row_dl(s_lg + slot * NOF, NOF, o, label, dzo.gscale, &lossv);
+          s_dl[lane] = d;
+          // the block holding the image's first pixel publishes its dL row and loss
+          if (dzo.dl_out && (slot == 1 || P0 == (long)img0 * HWi)) {
+            const int im = img0 + slot;
+            dzo.dl_out[im * NOF + o] = d;
+            if (o == 0) dzo.loss_rows[im] = lossv;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    DDP_STAMP(STAMP_K_FWD_DZ, 3);
+    // dZ2 = relu2'(a2) * sum_o dL[o] W[o][p][c], in fc_bwd's order (o = 0..9, fma from 0)
+#pragma unroll
+    for (int pt = 0; pt < PXT; ++pt) {
+      const long tp = P0 + (wave * PXT + pt) * 16;  // a 16-pixel tile never straddles images (HW % 16 == 0)
+      const float* dl = s_dl + (tp / HWi != img0 ? NOF : 0);
+      float d[NOF];
+#pragma unroll
+      for (int o = 0; o < NOF; ++o) d[o] = dl[o];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float dz[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int o = 0; o < NOF; ++o) {
+          float w4[4];
+          unpack4(wv[pt][t][o], w4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dz[j] = fmaf(d[o], w4[j], dz[j]);
+        }
+        float q[4];
+        unpack4(a2pk[pt][t], q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dz[j] = q[j] > 0.f ? dz[j] : 0.f;
+        const int co = co0 + 16 * t + 4 * (lane >> 4);
+        if (valid[pt]) st_wt(reinterpret_cast<uint2*>(dzo.dz2 + Pp[pt] * Cout + co), pack4(dz[0], dz[1], dz[2], dz[3]));
+      }
+    }
+    DDP_STAMP(STAMP_K_CONV_FWD, 7);
+    DDP_STAMP(STAMP_K_FWD_DZ, 5);
+  }
 }
 
 // ---------------------------------------------------------------- data gradient
@@ -992,29 +1105,50 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // each into a slot it can hold while the rest are dispatched).
 // CS: wgrad role channel split (see wgrad_body); the grid then has CS wgrad blocks per
 // slab row.
-template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1>
+// FCR (fuse level 3, single process): the fc weight gradient + fused SGD (fc_bwd_body
+// without dX, dL given by the level-3 forward) as a third role: blocks [nconv, grid) after
+// the conv roles.  They never wait and are not counted by the fused reduction, so the
+// dispatch-order argument above is unchanged (every block a reducer waits for has a lower
+// index than the reducer); the fc role's own last block (FcBwdExtras::last_ctr) finishes the
+// fc bias, the loss and the step counter (launchers.h BwdFc).
+// 4 waves x 2 virtual waves, 4 columns per lane: == the 8-wave fc_bwd (same VW, fc_bwd_body.h)
+constexpr int BFC_WPB = 4, BFC_VW = 8, BFC_CPL = 4;
+
+template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
+          bool FCR = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kernel(
     const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
-    int R, int nd, C1Src c1, const T* __restrict__ Xact, BwdReduce red) {
+    int R, int nd, C1Src c1, const T* __restrict__ Xact, BwdReduce red, BwdFc fcr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if ((int)blockIdx.x < nd)
+  // conv-role index: the fc-role blocks [fc0, fc0 + nfc) are cut out of the grid order
+  int cb = (int)blockIdx.x;
+  if constexpr (FCR) {
+    const int f = cb - fcr.fc0;
+    if (f >= 0 && f < fcr.nfc) {
+      fc_bwd_body<bf16_t, false, false, 10, BFC_WPB, BFC_VW, BFC_CPL, false>(
+          fcr.dl, fcr.a2, nullptr, nullptr, fcr.dW, fcr.scale, B, fcr.K, 10, fcr.ex, reinterpret_cast<float*>(smem),
+          f, nullptr);
+      return;
+    }
+    if (f >= 0) cb -= fcr.nfc;
+  }
+  if (cb < nd)
     dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
-        dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem,
-        blockIdx.x, 0);
+        dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, cb, 0);
   else
     wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, false, true, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
-                                                                  W, Cin, Cout, R, c1, smem, blockIdx.x - nd, 0);
+                                                                  W, Cin, Cout, R, c1, smem, cb - nd, 0);
   if constexpr (FRED) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
     __syncthreads();
     if (threadIdx.x == 0)
       __hip_atomic_fetch_add(red.done + 32 * (blockIdx.x & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((int)blockIdx.x < red.first_reducer) return;
-    // reducer w of nr: the LAST nr blocks of the grid (dispatched last; the host keeps nr
-    // within half the resident capacity, so they never starve a block they wait for)
-    const int w = blockIdx.x - red.first_reducer, nw = gridDim.x - red.first_reducer;
-    const int nblk = gridDim.x;
+    if (cb < red.first_reducer) return;
+    // reducer w of nr: the LAST nr conv blocks of the grid (dispatched after every block they
+    // wait for; the host keeps nr within a quarter of the resident capacity)
+    const int nblk = red.nconv > 0 ? red.nconv : (int)gridDim.x;
+    const int w = cb - red.first_reducer, nw = nblk - red.first_reducer;
     constexpr int J = 3;  // chunks per reducer pass (thread t < 64 * J finalises one output of chunk t >> 6)
     SlabFusedPlan<J> pl;
     slab_fused_plan<J>(red.ss, w, nw, red.nchunks, pl);  // index work + SGD operands before the wait
@@ -1124,10 +1258,34 @@ static void lds_optin(K kernel, size_t bytes) {
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// the level-3 forward of SimpleCNN's conv2 (bf16, fc epilogue, conv1 recompute, pxt 1 / 2)
+template <int PX>
+static auto fwd_dz_kernel() {
+  return conv3x3_fwd_kernel<bf16_t, 1, 4 * PX, true, 10, true, 28, 28, 32, 64, true>;
+}
+
+bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt) {
+  if (H != 28 || W != 28 || (pxt != 1 && pxt != 2) || B <= 0) return false;
+  const long P = (long)B * H * W;
+  const int per_blk = 64 * pxt;
+  if (per_blk > H * W || P >= (1L << 31)) return false;
+  const long grid = (P + per_blk - 1) / per_blk;
+  const size_t lds = conv3x3_fwd_lds(W, 32, pxt, true, 2);
+  const void* k = pxt == 2 ? reinterpret_cast<const void*>(fwd_dz_kernel<2>())
+                           : reinterpret_cast<const void*>(fwd_dz_kernel<1>());
+  lds_optin(pxt == 2 ? fwd_dz_kernel<2>() : fwd_dz_kernel<1>(), lds);
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256 * pxt, lds) != hipSuccess) return false;
+  // every block of the grid spins on its image's other blocks: all of them must be resident
+  return grid <= (long)occ * cus;
+}
+
 template <typename T>
 static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, int H, int W, int Cin,
                        int Cout, bool relu, const T* wfc, float* fc_part, int pxt, hipStream_t s,
-                       const C1Src* c1) {
+                       const C1Src* c1, const FwdDz* dz) {
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
   const dim3 grid((unsigned)((P + per_blk - 1) / per_blk), Cout / 64);
@@ -1136,6 +1294,19 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
   const bool fc = wfc != nullptr;  // host guarantees NO == 10 when fused
   const C1Src cs = a1x ? *c1 : C1Src();
   const bool g = simplecnn_geom(H, W, Cin, Cout);
+  const FwdDz dzo = dz ? *dz : FwdDz();
+  if (dz) {
+    if (sizeof(T) != 2 || !g || !fc || !a1x || !(pxt == 1 || pxt == 2) || !dz->dz2 || !dz->img_cnt || !dz->fc_bias)
+      throw std::runtime_error("conv3x3_fwd: the level-3 dZ2 epilogue is the bf16 SimpleCNN forward with the fc "
+                               "epilogue and the conv1 recompute");
+    if constexpr (sizeof(T) == 2) {
+      auto k = pxt == 2 ? fwd_dz_kernel<2>() : fwd_dz_kernel<1>();
+      lds_optin(k, lds);
+      hipLaunchKernelGGL(k, grid, dim3(256 * pxt), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs,
+                         dzo);
+    }
+    return;
+  }
   // one 16-pixel tile per wave: pxt 2 -> 8 waves (2 per SIMD), pxt 1 -> 4 waves
 #define LF(PX, RL, NF, AX)                                                                          \
   do {                                                                                              \
@@ -1143,12 +1314,12 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
       auto k = conv3x3_fwd_kernel<T, 1, 4 * PX, RL, NF, AX, 28, 28, 32, 64>;                        \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, grid, dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,  \
-                         fc_part, cs);                                                              \
+                         fc_part, cs, dzo);                                                         \
     } else {                                                                                        \
       auto k = conv3x3_fwd_kernel<T, 1, 4 * PX, RL, NF, AX, 0, 0, 0, 0>;                            \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, grid, dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,  \
-                         fc_part, cs);                                                              \
+                         fc_part, cs, dzo);                                                         \
     }                                                                                               \
   } while (0)
   if (pxt == 2) {
@@ -1163,15 +1334,15 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
 
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s, const C1Src* c1) {
-  (void)NO;
-  fwd_launch<bf16_t>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1);
+                 int pxt, hipStream_t s, const C1Src* c1, const FwdDz* dz) {
+  if (dz && NO != 10) throw std::runtime_error("conv3x3_fwd: the level-3 dZ2 epilogue is built for 10 classes");
+  fwd_launch<bf16_t>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1, dz);
 }
 void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
                  int pxt, hipStream_t s, const C1Src* c1) {
   (void)NO;
-  fwd_launch<float>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1);
+  fwd_launch<float>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1, nullptr);
 }
 
 template <typename T>
@@ -1304,19 +1475,76 @@ static int fused_reducers(K kernel, size_t lds, int nblocks) {
 }
 
 template <typename T>
+using BwdKFn = void (*)(const T*, const T*, T*, float*, float*, int, int, int, int, int, int, int, C1Src, const T*,
+                        BwdReduce, BwdFc);
+
+// The conv backward instantiation a launch runs (chosen BEFORE the fused reduction's residency
+// query, so that query sees the exact kernel - its registers decide its residency).
+// cs == 2 and FCR: the bf16 SimpleCNN variants only (FCR: pxt 2, channel split).
+template <typename T, int PX, bool DA, bool WA>
+static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr) {
+  if (!g) return conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0, false>;
+  if constexpr (sizeof(T) == 2) {
+    if (cs == 2) {
+      if constexpr (PX == 2) {
+        if (fcr)
+          return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true>
+                      : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, true>;
+      }
+      return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2>
+                  : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2>;
+    }
+  }
+  return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true>
+              : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false>;
+}
+template <typename T>
+static BwdKFn<T> pick_bwd(int pxt, bool da, bool wa, bool g, bool fred, int cs, bool fcr) {
+  if (pxt == 2) {
+    if (da) return pick_bwd3<T, 2, true, true>(g, fred, cs, fcr);
+    return wa ? pick_bwd3<T, 2, false, true>(g, fred, cs, fcr) : pick_bwd3<T, 2, false, false>(g, fred, cs, fcr);
+  }
+  if (da) return pick_bwd3<T, 1, true, true>(g, fred, cs, fcr);
+  return wa ? pick_bwd3<T, 1, false, true>(g, fred, cs, fcr) : pick_bwd3<T, 1, false, false>(g, fred, cs, fcr);
+}
+
+bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split) {
+  return simplecnn_geom(H, W, Cin, Cout) && pxt == 2 && wgrad_split == 2;
+}
+
+template <typename T>
 static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
                        int Cin, int Cout, int pxt, int R, const C1Src& c1, const T* Xact,
                        bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err,
-                       int csplit) {
+                       int csplit, const BwdFc* fc) {
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   // the channel split is the bf16 SimpleCNN variant (wgrad_body); otherwise one block per row
   const int cs = (csplit == 2 && g && sizeof(T) == 2) ? 2 : 1;
   const int nrows = conv3x3_wgrad_blocks(B, H, R);
   const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = nrows * cs;
-  const size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
+  size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
   if (((long)Cout * 9 * Cin + Cout) % 4 != 0 || (reinterpret_cast<uintptr_t>(slab) & 15) != 0)
     throw std::runtime_error("conv3x3_bwd: slab rows must be 16-byte multiples on a 16-byte aligned buffer");
+  BwdFc fcr;
+  int nfc = 0;
+  if (fc) {
+    if (sizeof(T) != 2 || !conv3x3_bwd_fc_role_ok(H, W, Cin, Cout, pxt, cs) || !fc->dl || !fc->a2 ||
+        fc->K % (64 * BFC_CPL) != 0)
+      throw std::runtime_error("conv3x3_bwd: the fc role is the bf16 SimpleCNN variant (pxt 2, channel split, dL given)");
+    fcr = *fc;
+    fcr.nconv = nd + nw;
+    nfc = (int)(fc->K / (64 * BFC_CPL));
+    fcr.nfc = nfc;
+    // fc blocks right after the dgrad role (fc_pos 1: they run while the first wgrad blocks
+    // do, on the slots the dgrad blocks free first) or after every conv block (fc_pos 0)
+    fcr.fc0 = fc->fc_pos == 1 ? nd : nd + nw;
+    if (fcr.ex.last_ctr) fcr.ex.last_n = nfc;
+    const size_t fl = sizeof(float) * (size_t)fcb_lds_floats(B, 10, false, 0, fcb_red_floats<BFC_WPB, 10, BFC_CPL>());
+    lds = lds > fl ? lds : fl;
+  }
+  const bool da = !Xact, wa = !Xact || !wgrad_load_a1;
   BwdReduce red;
+  red.nconv = nd + nw;
   if (fused) {
     // the reducer's 16-byte row loads need n >= 4; its summation order is grad_reduce's
     // 16-row-group one (deep slabs; shallow ones keep the separate kernel)
@@ -1325,11 +1553,13 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
       if (fused->s[k].n < 4) fused = nullptr;
   }
   if (fused) {
-    lds_optin(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds);
     // reducers: the wgrad blocks (they finish last; extra early-finishing reducers measured
     // slower - their polling shares the CUs of the still-running wgrad blocks)
-    // (channel split: the last nrows blocks - as many reducers as without the split)
-    const int nr = (g && red_done) ? fused_reducers(conv3x3_bwd_kernel<T, 2, true, true, 28, 28, 32, 64, true>, lds, nrows) : 0;
+    // (channel split: the last nrows blocks - as many reducers as without the split).
+    // Residency of the exact instantiation that will run.
+    const BwdKFn<T> kf = pick_bwd<T>(pxt, da, wa, g, true, cs, fc != nullptr);
+    lds_optin(kf, lds);
+    const int nr = (g && red_done) ? fused_reducers(kf, lds, nrows) : 0;
     if (nr <= 0) fused = nullptr;  // the caller reduces with grad_reduce
     else red.first_reducer = nd + nw - nr;
   }
@@ -1341,54 +1571,26 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");
   }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
-#define LBW(PX, DA, WA)                                                                             \
-  do {                                                                                              \
-    if (cs == 2) {                                                                                  \
-      if constexpr (sizeof(T) == 2) {                                                               \
-        auto k = fused ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2>                 \
-                       : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2>;               \
-        lds_optin(k, lds);                                                                          \
-        hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
-                           Cout, R, nd, c1, Xact, red);                                             \
-      }                                                                                             \
-    } else if (g && fused) {                                                                        \
-      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true>;                             \
-      lds_optin(k, lds);                                                                            \
-      hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
-                         Cout, R, nd, c1, Xact, red);                                               \
-    } else if (g) {                                                                                 \
-      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false>;                            \
-      lds_optin(k, lds);                                                                            \
-      hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
-                         Cout, R, nd, c1, Xact, red);                                               \
-    } else {                                                                                        \
-      auto k = conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0, false>;                                \
-      lds_optin(k, lds);                                                                            \
-      hipLaunchKernelGGL(k, dim3(nd + nw), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, \
-                         Cout, R, nd, c1, Xact, red);                                               \
-    }                                                                                               \
-  } while (0)
-  // Xact given: the dgrad role reads it; the wgrad role reads it only if wgrad_load_a1
-  if (!Xact) { if (pxt == 2) LBW(2, true, true); else LBW(1, true, true); }
-  else if (wgrad_load_a1) { if (pxt == 2) LBW(2, false, false); else LBW(1, false, false); }
-  else { if (pxt == 2) LBW(2, false, true); else LBW(1, false, true); }
-#undef LBW
+  const BwdKFn<T> k = pick_bwd<T>(pxt, da, wa, g, fused != nullptr, cs, fc != nullptr);
+  lds_optin(k, lds);
+  hipLaunchKernelGGL(k, dim3(nd + nw + nfc), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R,
+                     nd, c1, Xact, red, fcr);
   return fused != nullptr;
 }
 
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
-                 int wgrad_split) {
+                 int wgrad_split, const BwdFc* fc) {
   return bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                     fused_reduce, red_done, red_err, wgrad_split);
+                     fused_reduce, red_done, red_err, wgrad_split, fc);
 }
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
                  int wgrad_split) {
   return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                    fused_reduce, red_done, red_err, wgrad_split);
+                    fused_reduce, red_done, red_err, wgrad_split, nullptr);
 }
 
 int fc_conv_bwd_fc_blocks(long K) { return (int)((K + 64 * FCC_CPL - 1) / (64 * FCC_CPL)); }

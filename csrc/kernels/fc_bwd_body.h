@@ -90,7 +90,40 @@ __host__ __device__ inline long fcb_lds_floats(int B, int NO, bool xent, long np
   return head + (red > npart ? red : npart);
 }
 
-template <typename T, bool MASK, bool XENT, int NOT, int WPB, int VW, int CPL>
+// The fc bias gradient (fixed batch order), the fused SGD of the bias and the batch-mean
+// loss from the block's LDS dL / per-row losses - wave 0 of block 0, or of the last block to
+// arrive (FcBwdExtras::last_ctr).
+template <bool XENT>
+__device__ __forceinline__ void fc_bwd_bias_loss(const FcBwdExtras& ex, const float* s_dl, const float* s_loss,
+                                                 int B, int NO, bool last) {
+  const int lane = threadIdx.x & 63;
+  if (ex.dbias && lane < NO) {
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += s_dl[b * NO + lane];
+    const float g = acc * ex.dbias_scale;
+    if (ex.sys_store) st_sys(ex.dbias + lane, g);
+    else ex.dbias[lane] = g;
+    if (last && ex.p_b && ex.sgd.update) {
+      // == the 1-row in-place slab the fused slab reduction used to apply it from (0 + g)
+      float m = ex.m_b ? ex.m_b[lane] : 0.f;
+      const float pn = sgd_one(ex.p_b[lane], 0.f + g, &m, ex.sgd);
+      ex.p_b[lane] = pn;
+      if (ex.m_b) ex.m_b[lane] = m;
+    }
+  }
+  if ((XENT || ex.loss_rows) && ex.loss_out && lane == 63) {
+    const float* lr = XENT ? s_loss : ex.loss_rows;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += lr[b];
+    const int at = ex.step_ctr ? *ex.step_ctr : 0;
+    ex.loss_out[at] = acc / (float)B;
+    if (last && ex.step_inc) *ex.step_inc = at + 1;  // ex.step_inc == ex.step_ctr (read just above)
+  }
+  if (ex.zero_i32 && (last || !ex.last_ctr))  // (block 0 when there is no last-block count)
+    for (int i = lane; i < ex.n_zero; i += 64) ex.zero_i32[(long)i * ex.zero_stride] = 0;
+}
+
+template <typename T, bool MASK, bool XENT, int NOT, int WPB, int VW, int CPL, bool DXO = true>
 __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const T* __restrict__ X,
                                             const T* __restrict__ Wf, T* __restrict__ dX,
                                             float* __restrict__ dW, float scale, int B, long K, int NO_rt,
@@ -110,13 +143,15 @@ __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const 
   const bool active = col < K;  // host guarantees K % CPL == 0
   const long cc = active ? col : 0;
   // ---- this block's column loads first (independent of the prologue)
-  ColF<CPL> wr[NOT];
+  ColF<CPL> wr[DXO ? NOT : 1];
+  if constexpr (DXO) {
 #pragma unroll
-  for (int o = 0; o < NOT; ++o) {
-    if (o < NO) wr[o] = ldc<CPL>(Wf + (long)o * K + cc);
-    else
+    for (int o = 0; o < NOT; ++o) {
+      if (o < NO) wr[o] = ldc<CPL>(Wf + (long)o * K + cc);
+      else
 #pragma unroll
-      for (int j = 0; j < CPL; ++j) wr[o].v[j] = 0.f;
+        for (int j = 0; j < CPL; ++j) wr[o].v[j] = 0.f;
+    }
   }
   // rows of virtual wave v = wave + WPB * kv (uniform)
   int nr[KV];
@@ -166,21 +201,8 @@ __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const 
   }
   __syncthreads();
   DDP_STAMP(STAMP_K_FC_BWD, 1);
-  if (bx == 0) {
-    // fc bias gradient (sum over the batch, fixed order) and the batch-mean loss
-    if (ex.dbias && threadIdx.x < NO) {
-      float acc = 0.f;
-      for (int b = 0; b < B; ++b) acc += s_dl[b * NO + threadIdx.x];
-      if (ex.sys_store) st_sys(ex.dbias + threadIdx.x, acc * ex.dbias_scale);
-      else ex.dbias[threadIdx.x] = acc * ex.dbias_scale;
-    }
-    if ((XENT || ex.loss_rows) && ex.loss_out && threadIdx.x == 64) {
-      const float* lr = XENT ? s_loss : ex.loss_rows;
-      float acc = 0.f;
-      for (int b = 0; b < B; ++b) acc += lr[b];
-      ex.loss_out[ex.step_ctr ? *ex.step_ctr : 0] = acc / (float)B;
-    }
-  }
+  // fc bias gradient (sum over the batch, fixed order) and the batch-mean loss
+  if (bx == 0 && !ex.last_ctr && wave == 0) fc_bwd_bias_loss<XENT>(ex, s_dl, s_loss, B, NO, false);
   float dw[KV][NOT][CPL];
 #pragma unroll
   for (int kv = 0; kv < KV; ++kv)
@@ -213,15 +235,17 @@ __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const 
               const float d = dl[o];
 #pragma unroll
               for (int j = 0; j < CPL; ++j) {
-                dz[j] = fmaf(d, wr[o].v[j], dz[j]);
+                if constexpr (DXO) dz[j] = fmaf(d, wr[o].v[j], dz[j]);
                 dw[kv][o][j] = fmaf(d, xr[kv][u].v[j], dw[kv][o][j]);
               }
             }
-          if (MASK) {
+          if constexpr (DXO) {
+            if (MASK) {
 #pragma unroll
-            for (int j = 0; j < CPL; ++j) dz[j] = xr[kv][u].v[j] > 0.f ? dz[j] : 0.f;
+              for (int j = 0; j < CPL; ++j) dz[j] = xr[kv][u].v[j] > 0.f ? dz[j] : 0.f;
+            }
+            if (active) stc_wt<CPL>(dX + (long)b * K + col, dz);  // dZ2: write-through
           }
-          if (active) stc_wt<CPL>(dX + (long)b * K + col, dz);  // dZ2: write-through
         }
       }
     }
@@ -279,6 +303,14 @@ __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const 
         if (ex.sh_frag) st_wt(ex.sh_frag + fcfrag_index((int)idx, ex.frag_HW, ex.frag_C), pb);
       }
     }
+  }
+  if (ex.last_ctr && wave == 0) {
+    // arrival after the block's whole body: every read of the fc bias (prologue) is done.
+    // Only wave 0 of the last block goes on; its LDS dL / losses are the block's own.
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(ex.last_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old == (ex.last_n > 0 ? ex.last_n : (int)gridDim.x) - 1) fc_bwd_bias_loss<XENT>(ex, s_dl, s_loss, B, NO, true);
   }
   DDP_STAMP(STAMP_K_FC_BWD, 4);
 }

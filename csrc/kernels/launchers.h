@@ -23,11 +23,35 @@ void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const float* dy, cons
                  float* slab, int B, int H, int W, int Cout, int chunk, hipStream_t s);
 
 // ---- 3x3 / s1 / p1 NHWC conv (MFMA) --------------------------------------------------
+// Fuse level 3 (bf16 SimpleCNN forward with the fc epilogue and the conv1 recompute): the
+// forward also produces dZ2 = relu2'(a2) * (dL . W_fc) for its own pixels, so the fc
+// backward leaves the critical path.  Every block publishes its partial logits
+// (write-through) and adds 1 to the arrival counter of each image it touches, waits until
+// every block of its image(s) has arrived, sums the image's logits in the fc_bwd prologue's
+// fixed order, evaluates the softmax cross-entropy gradient dL of its image(s) and then dZ2
+// from the bf16 fc weight fragments it already holds for the fc partials (fc_bwd's FMA
+// order: bit-identical dZ2).  All blocks must be co-resident (conv3x3_fwd_dz_fits).
+constexpr int FWD_DZ_CNT_STRIDE = 64;  // ints between two images' counters (256 B: no shared line)
+struct FwdDz {
+  bf16_t* dz2 = nullptr;          // [B*H*W][Cout] out (write-through)
+  int* img_cnt = nullptr;         // [B][FWD_DZ_CNT_STRIDE] arrival counters (first int of each
+                                  // row), zero on entry (re-zeroed by the step's fc backward:
+                                  // FcBwdExtras::zero_i32)
+  const float* fc_bias = nullptr;
+  float gscale = 1.f;             // 1 / B (mean cross-entropy)
+  int* err = nullptr;             // set to 3 when the wait times out (results invalid)
+  // optional: dL [B][10] and the per-row losses [B] (the block holding an image's first
+  // pixel writes its row) - the fc backward then needs no cross-entropy prologue
+  float* dl_out = nullptr;
+  float* loss_rows = nullptr;
+};
+// whether a level-3 forward of this shape keeps every block resident at once
+bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt);
 // bf16 operands (v_mfma_f32_16x16x32_bf16) or exact fp32 operands (v_mfma_f32_16x16x4_f32,
 // the float overloads); `es` = element size of the LDS-size helpers (2 or 4).
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s, const C1Src* c1 = nullptr);
+                 int pxt, hipStream_t s, const C1Src* c1 = nullptr, const FwdDz* dz = nullptr);
 // fp32: wfc (fused fc epilogue) is the fc weight in its native [NO][H*W][C] layout
 void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
@@ -51,11 +75,15 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // the caller runs grad_reduce).  wgrad_split == 2 (bf16, SimpleCNN geometry): two wgrad
 // blocks per slab row, one per half of the input channels (bit-identical slabs).
 struct SlabSet;
+struct BwdFc;
 constexpr int SYNC_RED_INTS = 256;  // ints of the 8 arrival counters (32 apart) of red_done
+// fc != null (fuse level 3, single process): the same launch also runs the fc weight
+// gradient + fused SGD as a third role (conv3x3_bwd_fc_role_ok shapes only; BwdFc below)
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
-                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1);
+                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr);
+bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split);
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
@@ -180,9 +208,39 @@ struct FcBwdExtras {
   bf16_t* sh_frag = nullptr;   // FCFRAG shadow (conv3x3_fwd epilogue order)
   int frag_HW = 0, frag_C = 0;
   int sys_store = 0;  // dW / dbias with system-scope stores (read by peers over xGMI)
+  // Last-block epilogue (fuse level 3: this kernel runs BESIDE the conv backward, so nothing
+  // after it in the step can own the fc bias): instead of block 0 writing dbias / the loss,
+  // every block adds 1 to *last_ctr (zero on entry) when it is done - after its prologue read
+  // the fc bias - and the block that arrives last writes dbias and the loss, applies the
+  // fused SGD to the fc bias (p_b / m_b, when sgd.update), advances *step_inc (after reading
+  // the loss index from step_ctr) and zeroes zero_i32[0, n_zero) (the forward's per-image
+  // arrival counters, FwdDz::img_cnt).
+  int* last_ctr = nullptr;
+  float* p_b = nullptr;
+  float* m_b = nullptr;
+  int* step_inc = nullptr;
+  int* zero_i32 = nullptr;      // zero_i32[i * zero_stride] = 0 for i < n_zero
+  int n_zero = 0, zero_stride = 1;
+  int last_n = 0;               // arrivals of the last-block count (0: the grid size)
+};
+// The fc role of the level-3 conv backward launch (conv3x3_bwd, fc != null): fc_bwd_body
+// without dX, dL given (the forward's FwdDz::dl_out), blocks [nconv, grid) after the conv
+// roles; they never wait and are not counted by the fused reduction.  The fc role's own last
+// block (ex.last_ctr) finishes the fc bias, the loss and the step counter.
+struct BwdFc {
+  const bf16_t* a2 = nullptr;  // ReLU2 output [B][K]
+  const float* dl = nullptr;   // dL [B][10]
+  float* dW = nullptr;         // null: fused optimizer only
+  float scale = 1.f;
+  long K = 0;
+  int fc_pos = 1;              // 1: fc blocks right after the dgrad blocks, 0: after every conv block
+  int nconv = 0, fc0 = 0, nfc = 0;  // (set by the launcher)
+  FcBwdExtras ex{};
 };
 size_t fc_bwd_lds(int B, int NO, bool xent, long npart = 0);  // npart: see linear.hip
 void noop(int blocks, int* sink, hipStream_t s);
+// dX == nullptr: no data gradient (fuse level 3: the conv forward produced dZ2); the weight
+// columns are then not read at all
 void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
 void fc_bwd(const float* dL, const float* X, const float* Wf, float* dX, float* dW, float scale,

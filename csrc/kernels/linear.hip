@@ -89,7 +89,7 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __
 // and gets bit-identical results).
 constexpr int FCB_WPB = 8, FCB_CPL = 2, FCB_COLS = 64 * FCB_CPL;
 
-template <typename T, bool MASK, bool XENT, int NOT, int WPB>
+template <typename T, bool MASK, bool XENT, int NOT, int WPB, bool DXO = true>
 __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restrict__ dL,
                                                           const T* __restrict__ X,
                                                           const T* __restrict__ Wf,
@@ -98,8 +98,8 @@ __global__ __launch_bounds__(WPB * 64) void fc_bwd_kernel(const float* __restric
                                                           int B, long K, int NO_rt,
                                                           FcBwdExtras ex) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  fc_bwd_body<T, MASK, XENT, NOT, WPB, WPB, FCB_CPL>(dL, X, Wf, dX, dW, scale, B, K, NO_rt, ex, smem,
-                                                     blockIdx.x, nullptr);
+  fc_bwd_body<T, MASK, XENT, NOT, WPB, WPB, FCB_CPL, DXO>(dL, X, Wf, dX, dW, scale, B, K, NO_rt, ex, smem,
+                                                          blockIdx.x, nullptr);
 }
 
 void fc_partial(const bf16_t* X, const bf16_t* Wf, float* part, int B, int HW, int C, int NO,
@@ -140,9 +140,23 @@ static void fc_bwd_launch(const float* dL, const T* X, const T* Wf, T* dX, float
 #define OPT(M, XE, N) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fc_bwd_kernel<T, M, XE, N, FCB_WPB>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
     OPT(true, true, 10); OPT(false, true, 10); OPT(true, true, FC_MAXO); OPT(false, true, FC_MAXO);
 #undef OPT
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fc_bwd_kernel<T, false, true, 10, FCB_WPB, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fc_bwd_kernel<T, false, false, 10, FCB_WPB, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   }
+  if (ex.last_ctr && (NO != 10 || dX))
+    throw std::runtime_error("fc_bwd: the last-block epilogue is the level-3 variant (10 classes, no dX)");
 #define LB(M, XE, N) hipLaunchKernelGGL((fc_bwd_kernel<T, M, XE, N, FCB_WPB>), grid, dim3(FCB_WPB * 64), lds, s, dL, X, Wf, dX, dW, scale, B, K, NO, ex)
-  if (NO == 10) {
+  if (!dX) {  // level 3: no data gradient (the conv forward produced dZ2); dL from the prologue or given
+    if (NO != 10 || (!xe && !dL)) throw std::runtime_error("fc_bwd: dX == nullptr needs 10 classes and dL (or its prologue)");
+    if (xe)
+      hipLaunchKernelGGL((fc_bwd_kernel<T, false, true, 10, FCB_WPB, false>), grid, dim3(FCB_WPB * 64), lds, s, dL, X,
+                         Wf, dX, dW, scale, B, K, NO, ex);
+    else
+      hipLaunchKernelGGL((fc_bwd_kernel<T, false, false, 10, FCB_WPB, false>), grid, dim3(FCB_WPB * 64), lds, s, dL,
+                         X, Wf, dX, dW, scale, B, K, NO, ex);
+  } else if (NO == 10) {
     if (xe) { if (mask) LB(true, true, 10); else LB(false, true, 10); }
     else { if (mask) LB(true, false, 10); else LB(false, false, 10); }
   } else {

@@ -57,6 +57,7 @@ struct C1Src {
   // step's in-launch hand-off flags (fuse level 2), reset by the step's first kernel
   int* zero_i32 = nullptr;
   int zero_per_block = 0;
+  int zero_total = 0x7fffffff;  // ints [0, zero_total) only (the words past it belong to others)
 };
 
 // torch.optim.SGD hyper-parameters of one step (first_step: momentum buffer init;
@@ -69,7 +70,7 @@ struct SgdArgs {
 // diagnostic phase-stamp kernel ids / buffer geometry (common.h DDP_STAMP)
 enum { STAMP_K_CONV_FWD = 0, STAMP_K_FC_BWD = 1, STAMP_K_DGRAD = 2, STAMP_K_WGRAD = 3,
        STAMP_K_GRAD_REDUCE = 4, STAMP_K_SGD = 5, STAMP_K_XENT = 6, STAMP_K_CONV1 = 7,
-       STAMP_K_COUNT = 8 };
+       STAMP_K_FWD_DZ = 8, STAMP_K_COUNT = 9 };
 constexpr int STAMP_SLOTS = 8, STAMP_KSTRIDE = 4096 * STAMP_SLOTS;
 
 }  // namespace ddp_amd

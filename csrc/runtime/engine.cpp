@@ -64,6 +64,7 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
   for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
     DDP_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  l3_fits_.assign(cfg_.max_batch + 1, -1);
   // the in-launch wait-timeout word lives in coherent host memory: a kernel that times out
   // stores to it over the fabric and synchronize() reads it with a plain load - no
   // device-to-host copy (~10-20 us) after every synchronize
@@ -99,14 +100,23 @@ void SimpleCNNEngine::synchronize() {
   DDP_HIP_CHECK(hipStreamSynchronize(cs_));
   if (const int e = sync_error()) {
     throw std::runtime_error(std::string("engine: an in-launch hand-off wait timed out (") +
-                                    (e == 1 ? "level-2 dZ2" : "fused slab reduction") + "); results invalid");
+                             (e == 1 ? "level-2 dZ2" : e == 2 ? "fused slab reduction" : "level-3 forward dZ2") +
+                             "); results invalid");
   }
 }
 
 bool SimpleCNNEngine::level2_active() const {
   const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
   const bool dist = use_x || (comm_ && (comm_->world() > 1 || cfg_.force_allreduce));
-  return cfg_.fuse_level >= 2 && !cfg_.f32 && !dist && cfg_.fuse_opt && b_.sync_flags && b_.sync_err;
+  return cfg_.fuse_level == 2 && !cfg_.f32 && !dist && cfg_.fuse_opt && b_.sync_flags && b_.sync_err;
+}
+
+bool SimpleCNNEngine::level3_active(int batch) {
+  if (cfg_.fuse_level < 3 || cfg_.f32 || !b_.sync_flags || !b_.sync_err || level2_active()) return false;
+  if (batch <= 0 || batch > cfg_.max_batch) return false;
+  signed char& f = l3_fits_[batch];
+  if (f < 0) f = conv3x3_fwd_dz_fits(batch, cfg_.H, cfg_.W, cfg_.pxt_fwd) && cfg_.C1 == 32 && cfg_.C2 == 64 ? 1 : 0;
+  return f == 1;
 }
 
 void SimpleCNNEngine::refresh_shadows() {
@@ -161,14 +171,38 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   c1.labels = b_.labels;
   if (cfg_.store_a1) c1.a1_out = b_.a1;
   const bool l2 = level2_active();
+  const bool l3 = level3_active(B);
   const bool fred = f1 && !l2 && cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
   const long n_fc = (long)NO * HW * C2;
-  if (l2 || fred) {  // the forward resets the step's hand-off counters / flags
+  if (l2 || fred || l3) {  // the forward resets the step's hand-off counters / flags
     const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
-    const int nsync = SYNC_RED_INTS + (l2 ? fc_conv_bwd_fc_blocks((long)HW * C2) : 0);
+    const int nsync = SYNC_RED_INTS + (l2 ? fc_conv_bwd_fc_blocks((long)HW * C2) : 0) + (l3 ? L3_FC_INTS : 0);
     c1.zero_i32 = b_.sync_flags;
     c1.zero_per_block = (nsync + nfwd - 1) / nfwd;
+    c1.zero_total = nsync;  // level 3: the per-image counters follow (L3_IMG_OFF)
   }
+  if (!l3 && plain_stale_) {
+    // the plain bf16 fc shadow (read by the level-1/2 fc backward) was not refreshed by the
+    // level-3 steps before this one: re-derive every shadow from the fp32 master first
+    refresh_shadows();
+    plain_stale_ = false;
+  }
+  // level 3: the forward also writes dZ2 (per-image in-launch wait for the logits)
+  FwdDz dzo;
+  if (l3) {
+    dzo.dz2 = b_.dz2;
+    dzo.img_cnt = b_.sync_flags + L3_IMG_OFF;
+    dzo.fc_bias = P + b_.off_bfc;
+    dzo.gscale = 1.f / (float)B;
+    dzo.err = b_.sync_err;
+    dzo.dl_out = b_.dlogits;     // dL rows + per-row losses: the fc backward reads them
+    dzo.loss_rows = b_.loss_rows;
+  }
+  // level 3, single process: the fc weight gradient runs as a third role of the conv
+  // backward launch (2 kernels per step); at world size > 1 it runs as its own light kernel
+  // before it (the fc bucket's all-reduce then overlaps the conv backward)
+  const bool fc_role = l3 && !dist && cfg_.l3_fc_role &&
+                       conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
   const C1Src* pc1 = f1 ? &c1 : nullptr;
   BatchIdx bid{nullptr, nullptr, 0, 0};
   bid.n_rows = B;
@@ -181,7 +215,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // ---- forward
   if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
   conv3x3_fwd(f1 ? nullptr : b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true,
-              b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1);
+              b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1, l3 ? &dzo : nullptr);
   // ---- loss + fc backward (bucket 0)
   if (!f1)
     xent_rows(b_.fc_part, HW, 64 * cfg_.pxt_fwd, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits,
@@ -221,7 +255,38 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ex.frag_C = C2;
   }
   // (fused optimizer: the fc weight gradient is consumed in registers and not stored)
-  if (l2) {
+  BwdFc fcr;  // the conv backward's fc role (fc_role)
+  if (l3) {
+    // level 3: no dZ2 and no cross-entropy prologue here (the forward wrote dZ2, dL, losses)
+    ex.part = nullptr;
+    ex.loss_rows = b_.loss_rows;
+    ex.zero_i32 = dzo.img_cnt;  // re-arm the forward's per-image counters for the next step
+    ex.n_zero = B;
+    ex.zero_stride = FWD_DZ_CNT_STRIDE;
+    if (fc_role) {
+      // inside the conv backward launch: the fc role's last block owns the fc bias, the loss
+      // and the step counter (nothing after it in the launch may read them)
+      ex.last_ctr = b_.sync_flags + SYNC_RED_INTS;
+      if (fopt) {
+        ex.p_b = P + b_.off_bfc;
+        ex.m_b = M ? M + b_.off_bfc : nullptr;
+        ex.step_inc = b_.step_ctr;
+      }
+      ex.sh_plain = nullptr;  // level 3 never reads the plain bf16 fc shadow (stale until refreshed)
+      fcr.a2 = b_.a2;
+      fcr.dl = b_.dlogits;
+      fcr.fc_pos = cfg_.l3_fc_role == 2 ? 0 : 1;
+      fcr.dW = fopt ? nullptr : G + b_.off_wfc;
+      fcr.scale = inv_ws;
+      fcr.K = (long)HW * C2;
+      fcr.ex = ex;
+    } else {
+      ex.sh_plain = nullptr;
+      fc_bwd(b_.dlogits, b_.a2, nullptr, nullptr, fopt ? nullptr : G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
+             /*mask=*/true, cs_, ex);
+    }
+    plain_stale_ = true;
+  } else if (l2) {
     // level 2: fc backward + conv backward in one launch (dZ2 handed off inside it)
     fc_conv_bwd(b_.a2, b_.wfc_bf16, b_.dz2, nullptr, inv_ws, (long)HW * C2, ex, b_.w2t_bf16, b_.w1slab,
                 b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b,
@@ -260,12 +325,16 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     opt(ss.s[1], b_.off_b2);
     opt(ss.s[2], b_.off_w1);
     opt(ss.s[3], b_.off_b1);
-    // fc bias: its gradient (fc_bwd block 0) is already final; a 1-row "slab" in place
-    ss.s[4] = SlabSeg{G + b_.off_bfc, (long)NO, 0, (long)NO, 1, G + b_.off_bfc, 1.f};
-    opt(ss.s[4], b_.off_bfc);
-    ss.count = 5;
+    ss.count = 4;
     ss.sgd = sa;
-    ss.step_ctr = b_.step_ctr;  // the step's last kernel advances the batch window
+    if (!fc_role) {
+      // fc bias: its gradient (fc_bwd block 0) is already final; a 1-row "slab" in place
+      // (level-3 fc role: its last block applies it - that role runs inside this launch)
+      ss.s[4] = SlabSeg{G + b_.off_bfc, (long)NO, 0, (long)NO, 1, G + b_.off_bfc, 1.f};
+      opt(ss.s[4], b_.off_bfc);
+      ss.count = 5;
+      ss.step_ctr = b_.step_ctr;  // the step's last kernel advances the batch window
+    }
   }
   ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
   bool reduced = false;  // the conv backward launch also did grad_reduce's work
@@ -275,7 +344,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
     reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                           cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
-                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split);
+                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
+                          fc_role ? &fcr : nullptr);
   } else {
     conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
                   b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
@@ -283,6 +353,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   }
   if (!reduced) grad_reduce(ss, cs_);
   last_fused_reduce_ = reduced;
+  last_level3_ = l3;
+  last_fc_role_ = fc_role;
   if (fopt) return;
   if (dist) {
     launch_buckets(1, use_x, sa, M, sh_all);

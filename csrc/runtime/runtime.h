@@ -172,7 +172,10 @@ struct EngineBuffers {
   int* yb;            // its labels [max_batch]
   // in-launch hand-offs, zeroed by each step's forward (C1Src::zero_i32): [0, 256) the
   // fused conv backward's 8 arrival counters (32 ints apart), [256, 256 + fc blocks) the
-  // level-2 dZ2 flags; sync_err: wait-timeout word (0 = ok, 1 = dZ2 wait, 2 = reduction)
+  // level-2 dZ2 flags; level 3: [256] the fc backward's last-block counter (zeroed by the
+  // forward too) and [L3_IMG_OFF, + max_batch) the forward's per-image arrival counters
+  // (zeroed by the fc backward's last block); sync_err: wait-timeout word (0 = ok, 1 = dZ2
+  // wait, 2 = reduction, 3 = level-3 forward wait)
   int* sync_flags = nullptr;
   int* sync_err = nullptr;
   // data
@@ -181,6 +184,9 @@ struct EngineBuffers {
   const int* idx;               // i32 epoch index list (nullptr: images / labels already in epoch order)
   int n_idx, n_rows;            // bounds for the clamped batch gather
 };
+
+constexpr int L3_FC_INTS = 32;                          // [SYNC_RED_INTS, + 32): fc last-block counter
+constexpr int L3_IMG_OFF = SYNC_RED_INTS + L3_FC_INTS;  // per-image arrival counters
 
 struct EngineConfig {
   int max_batch, H, W, C1, C2, NO;
@@ -196,7 +202,17 @@ struct EngineConfig {
   // 2: level 1 with fc_bwd and the conv backward in ONE launch (in-launch dZ2 hand-off,
   //    fc_conv_bwd) where it applies - bf16, single process, fused optimizer: 3 kernels
   //    per step; otherwise (world > 1, fp32, fuse_opt 0) the level-1 chain
+  // 3: the fc backward leaves the critical path - the conv forward computes dZ2 itself
+  //    (FwdDz: per-image in-launch wait, then dL and dZ2 from the fc weight fragments it
+  //    holds) and the fc weight gradient + fused SGD (fc_bwd without dX, dL given) runs as
+  //    a third role of the conv backward launch (single process, l3_fc_role: 2 kernels per
+  //    step), or as a light kernel between the two (world size > 1: the fc bucket's
+  //    all-reduce overlaps the conv backward).  bf16, where every forward block fits on the
+  //    GPU at once (conv3x3_fwd_dz_fits); otherwise the level-1 chain
   int fuse_level = 0;
+  // level 3, single process: 1 = fc role right after the dgrad blocks, 2 = after every conv
+  // block, 0 = the fc weight gradient as its own kernel (what world size > 1 runs)
+  int l3_fc_role = 1;
   // 1: single-process steps apply SGD in the epilogues of fc_bwd / grad_reduce (no
   //    separate optimizer kernel); 0: always the flat SGD kernel (equivalence tests)
   int fuse_opt = 1;
@@ -240,12 +256,19 @@ class SimpleCNNEngine {
   void destroy_graph();
   hipStream_t stream() const { return cs_; }
   void synchronize();  // throws if a level-2 hand-off wait timed out
-  // in-launch wait-timeout word (0 = ok, 1 = level-2 dZ2 wait, 2 = fused reduction); sticky
+  // in-launch wait-timeout word (0 = ok, 1 = level-2 dZ2 wait, 2 = fused reduction,
+  // 3 = level-3 forward's per-image wait); sticky
   int sync_error() const { return err_host_ ? __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) : 0; }
   bool level2_active() const;
+  // whether a step of `batch` images runs the level-3 chain (fuse_level 3 and it applies)
+  bool level3_active(int batch);
   // whether the last launched step reduced its weight-gradient slabs inside the conv
   // backward launch (false: separate grad_reduce kernel)
   bool last_fused_reduce() const { return last_fused_reduce_; }
+  // whether the last launched step ran the level-3 chain (dZ2 in the forward, fc beside)
+  bool last_level3() const { return last_level3_; }
+  // ... and whether its fc weight gradient ran as a role of the conv backward launch
+  bool last_fc_role() const { return last_fc_role_; }
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
   // bucket b; set before capturing a graph
@@ -274,11 +297,15 @@ class SimpleCNNEngine {
   bool stage_used_[2] = {false, false};
   hipStream_t cs_ = nullptr, ms_ = nullptr;
   hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_;
+  std::vector<signed char> l3_fits_;  // per batch size: -1 unknown, 0 / 1
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
   int graph_steps_ = 0;
   bool momentum_started_ = false;
   bool last_fused_reduce_ = false;
+  bool last_level3_ = false;
+  bool last_fc_role_ = false;
+  bool plain_stale_ = false;  // level-3 steps skipped the plain bf16 fc shadow
   int* err_host_ = nullptr;  // coherent host word behind b_.sync_err
 };
 

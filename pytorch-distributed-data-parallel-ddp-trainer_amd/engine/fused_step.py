@@ -2,8 +2,12 @@
 
 The engine trains the SAME parameters as the ``SimpleCNN`` module (its flat fp32
 buffer is the engine's parameter buffer), so ``state_dict()`` / checkpoints /
-resume work unchanged; only the step itself is replaced by 8 fused HIP kernels
-+ 2 RCCL bucket all-reduces, captured into one hipGraph per ``graph_steps``
+resume work unchanged; only the step itself is replaced by 2 fused HIP kernels
+(default fuse level 3: the conv forward, which also produces dZ2 and dL; then the conv
+backward with the fused slab reduction + SGD, whose launch also runs the fc weight
+gradient + SGD as a third role) - at world size > 1 the fc weight gradient is a light
+kernel of its own between the two, so that its bucket's all-reduce (direct xGMI kernels,
+or RCCL) overlaps the conv backward - captured into one hipGraph per ``graph_steps``
 steps.
 
 Per epoch: the rank's ``DistributedSampler``-exact index list is uploaded once
@@ -45,11 +49,21 @@ class EngineOptions:
     first_bucket_mb: float = 1.0   # torch DDP's first-bucket cap (the rest use bucket_cap_mb)
     force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
-    # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd; 4 with
-    # the fused optimizer); 2: level 1 with fc_bwd and the conv backward in ONE launch
-    # (in-launch dZ2 hand-off) where it applies - bf16, world size 1, fused optimizer: 3
-    # kernels per step; elsewhere the level-1 chain runs
-    fuse_level: int = 1
+    # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd; 3 with
+    # the fused optimizer and the fused slab reduction: forward -> fc_bwd -> conv backward);
+    # 2: level 1 with fc_bwd and the conv backward in ONE launch (in-launch dZ2 hand-off)
+    # where it applies - bf16, world size 1, fused optimizer (slower: kept for reference);
+    # 3: the fc backward off the critical path - the forward computes dZ2 itself (per-image
+    # in-launch wait for the logits) and the fc weight gradient + SGD runs on a side stream
+    # beside the conv backward (critical path: forward -> conv backward).  bf16 where every
+    # forward block is resident at once (B <= 40 on MI355X) and the GPU is not shared by
+    # several ranks; elsewhere the level-1 chain runs.  Bit-identical to level 1.
+    fuse_level: int = 3
+    # level 3, single process: the fc weight gradient as a third role of the conv backward
+    # launch (2 kernels per step) - 1: its blocks right after the dgrad blocks, 2: after every
+    # conv block; 0: its own light kernel between forward and conv backward (what world
+    # size > 1 always runs, so the fc bucket's all-reduce overlaps the conv backward)
+    l3_fc_role: int = 1
     # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
     fuse_opt: bool = True
     # level >= 1: the conv backward launch also reduces the split-K weight-gradient slabs
@@ -144,7 +158,10 @@ class FusedSimpleCNNEngine:
         )
         # in-launch hand-offs (fused slab reduction, level-2 dZ2 flags), zeroed by each
         # step's forward, and their wait-timeout word
+        # (level 3: [256] the fc side kernel's last-block counter, [288, 288 + B) the
+        # forward's per-image arrival counters - engine.cpp L3_IMG_OFF)
         nfl = 256 + self.C.fc_conv_bwd_fc_blocks(HW * 64) + self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_fwd)
+        nfl = max(nfl, 256 + 32 + 64 * B)  # (counters 64 ints apart: FWD_DZ_CNT_STRIDE)
         self.t["sync_flags"] = torch.zeros(nfl, dtype=torch.int32, device=dev)
         # (the engine replaces it by a coherent host word: eng.sync_error)
         self.t["sync_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -154,9 +171,10 @@ class FusedSimpleCNNEngine:
                    dampening=float(g["dampening"]), weight_decay=float(g["weight_decay"]),
                    nesterov=bool(g["nesterov"]), maximize=bool(g["maximize"]),
                    force_allreduce=bool(self.opts.force_allreduce),
-                   fuse_level=int(self.opts.fuse_level), fuse_opt=bool(self.opts.fuse_opt),
+                   fuse_level=self._fuse_level_ok(world_size), fuse_opt=bool(self.opts.fuse_opt),
                    store_a1=int(self.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
-                   epoch_order=bool(self.opts.epoch_order), wgrad_split=int(self.opts.wgrad_split))
+                   epoch_order=bool(self.opts.epoch_order), wgrad_split=int(self.opts.wgrad_split),
+                   l3_fc_role=int(self.opts.l3_fc_role))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
@@ -201,10 +219,20 @@ class FusedSimpleCNNEngine:
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)
         # kernels per step of the chain that actually runs (engine.cpp / EngineConfig)
         self.level2 = bool(self.eng.level2_active)
+        self.level3 = bool(self.eng.level3_active(B))
         self._captured = 0
         self.steps_done = 0
 
     # ------------------------------------------------------------------ helpers
+    def _fuse_level_ok(self, world_size: int) -> int:
+        """Level 3's forward spins on the other blocks of its images, which must all be
+        resident: ranks that share a device (same-GPU rehearsals) would split the GPU
+        between two such forwards, so they run the level-1 chain instead."""
+        lvl = int(self.opts.fuse_level)
+        if lvl >= 3 and world_size > 1 and torch.cuda.device_count() < world_size:
+            return 1
+        return lvl
+
     def _fuse_reduce_ok(self, world_size: int) -> bool:
         """The fused reduction's waiting blocks are sized against ONE launch's share of the
         GPU; ranks that share a device (same-GPU rehearsals: more ranks than devices) each

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 NAMES = {0: "conv3x3_fwd", 1: "fc_bwd", 2: "conv3x3_dgrad", 3: "conv3x3_wgrad",
-         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging"}
+         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging", 8: "fwd-dZ2"}
 
 
 def main():
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--wgrad_split", type=int, default=None)
     ap.add_argument("--wgrad_rows", type=int, default=None)
+    ap.add_argument("--store_a1", type=int, default=None)
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -43,7 +44,7 @@ def main():
     eo = EngineOptions(use_graph=a.graph, graph_steps=10, dtype=a.dtype)
     if a.fuse_level is not None:
         eo.fuse_level = a.fuse_level
-    for f in ("wgrad_split", "wgrad_rows"):
+    for f in ("wgrad_split", "wgrad_rows", "store_a1"):
         if getattr(a, f) is not None:
             setattr(eo, f, getattr(a, f))
     eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, dev, "synthetic"),

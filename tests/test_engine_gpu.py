@@ -93,6 +93,63 @@ def test_fuse_level2_bitwise_equals_level1(B):
     assert e2.eng.sync_error == 0
 
 
+@pytest.mark.parametrize("B,opt,momentum,role", [(32, True, 0.9, 1), (32, False, 0.9, 1), (20, True, 0.0, 1),
+                                                  (1, True, 0.9, 1), (40, True, 0.9, 1), (32, True, 0.9, 2),
+                                                  (32, True, 0.9, 0), (20, False, 0.9, 0)])
+def test_fuse_level3_bitwise_equals_level1(B, opt, momentum, role):
+    """Level 3: the forward computes dZ2 itself (per-image in-launch wait, then dL and
+    dZ2 from its fc weight fragments) and the fc weight gradient + SGD runs as a third role
+    of the conv backward launch (role) or as its own light kernel (not role).  Parameters,
+    momentum, gradients, shadows, losses and the step counter after 10+ graph-captured
+    steps must equal the level-1 chain bit for bit, and no in-launch wait
+    may time out."""
+    kw = dict(B=B, use_graph=True, graph_steps=5, momentum=momentum, weight_decay=1e-4, fuse_opt=opt, store_a1=1)
+    m1, o1, _, e1, _, _ = _setup(fuse_level=1, **kw)
+    m3, o3, _, e3, _, _ = _setup(fuse_level=3, l3_fc_role=role, **kw)
+    assert e3.level3 and not e1.level3
+    # one engine at a time: level 3's forward spins on the other blocks of its images, which
+    # must all be resident - not shared with another engine's spinning reducers
+    e1.run_steps(12)
+    e1.synchronize()
+    e3.run_steps(12)
+    e3.synchronize()
+    assert e3.eng.last_level3 and e3.eng.last_fc_role == (role > 0)
+    for (n, a), (_, b) in zip(m1.named_parameters(), m3.named_parameters()):
+        assert torch.equal(a, b), n
+    if momentum:
+        assert torch.equal(o1.momentum_buffer, o3.momentum_buffer)
+    assert torch.equal(e1.t["loss_hist"][:12], e3.t["loss_hist"][:12])
+    assert torch.equal(e1.t["step_ctr"], e3.t["step_ctr"])
+    assert torch.equal(e1.t["dz2"], e3.t["dz2"])
+    for k in ("w2_bf16", "w2t_bf16", "wfc_frag"):  # (level 3 never reads / refreshes wfc_bf16)
+        assert torch.equal(e1.t[k], e3.t[k]), k
+    if not opt:  # the flat SGD kernel reads the reduced gradients
+        assert torch.equal(e1.fs.grads, e3.fs.grads)
+    assert e3.eng.sync_error == 0
+
+
+def test_fuse_level3_ragged_epoch_and_fallback():
+    """A whole epoch with a ragged last batch (eager level-3 step at B = 8, counters of
+    fewer images), bit-identical to level 1; at B = 64 the forward grid (392 blocks) does
+    not fit the GPU at once, so level 3 falls back to the level-1 chain."""
+    m1, _, _, e1, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=1, momentum=0.9)
+    m3, _, _, e3, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=3, momentum=0.9)
+    losses = ([], [])
+    for e, ls in ((e1, losses[0]), (e3, losses[1])):  # one engine at a time (see above)
+        e.run_epoch(0, on_loss=lambda b, l, ls=ls: ls.append(l), log_every=5)
+        e.run_epoch(1)
+        e.synchronize()
+    assert e3.eng.level3_active(8) and e3.eng.last_level3
+    for (n, a), (_, b) in zip(m1.named_parameters(), m3.named_parameters()):
+        assert torch.equal(a, b), n
+    assert losses[0] == losses[1]
+    _, _, _, e64, _, _ = _setup(B=64, fuse_level=3)
+    assert not e64.level3  # capacity check: 392 blocks > resident capacity
+    e64.run_steps(2)
+    e64.synchronize()
+    assert not e64.eng.last_level3 and e64.eng.sync_error == 0
+
+
 @pytest.mark.parametrize("dtype,B,opt", [("bf16", 32, True), ("bf16", 20, True), ("bf16", 64, False),
                                          ("fp32", 32, True), ("fp32", 20, False)])
 def test_fused_reduce_bitwise_equals_grad_reduce(dtype, B, opt):
@@ -208,7 +265,7 @@ def test_fuse_level1_one_step_matches_bf16_reference():
     assert abs(eng.t["loss_hist"][0].item() - loss.item()) < 1e-4
 
 
-@pytest.mark.parametrize("fuse_level", [0, 1, 2])
+@pytest.mark.parametrize("fuse_level", [0, 1, 2, 3])
 @pytest.mark.parametrize("B", [1, 12, 16, 24, 48, 64])
 def test_engine_batch_sweep_nan_poisoned(B, fuse_level):
     """SURVEY §4.1 batch sizes; every intermediate buffer starts as NaN so a kernel that
@@ -286,9 +343,12 @@ def test_module_ddp_world1_rccl(tmp_path):
         dist.destroy_process_group()
 
 
-def test_engine_rccl_allreduce_inside_graph_world1():
-    """Bucket all-reduces on the comm stream, captured in the hipGraph with their events
-    (RCCL at world size 1 is the identity): bitwise equal to the comm-free run."""
+@pytest.mark.parametrize("fuse_level", [1, 3])
+def test_engine_rccl_allreduce_inside_graph_world1(fuse_level):
+    """Bucket all-reduces over RCCL on the comm stream, captured in the hipGraph with their
+    events (RCCL at world size 1 is the identity): bitwise equal to the comm-free run.
+    comm="rccl" forces the RCCL data plane (the default "auto" would pick the xGMI kernels
+    even at world size 1) - the plane the 8-GPU run falls back to."""
     import torch.distributed as dist
 
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -309,10 +369,53 @@ def test_engine_rccl_allreduce_inside_graph_world1():
             torch.manual_seed(0)
             m = SimpleCNN().to(dev)
             e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01), data, 32, 1, 0, comm,
-                                     EngineOptions(graph_steps=5, force_allreduce=force))
+                                     EngineOptions(graph_steps=5, force_allreduce=force, comm="rccl",
+                                                   fuse_level=fuse_level))
+            assert e.comm_kind == ("rccl" if force else "none")
+            assert e.level3 == (fuse_level == 3)
             e.refresh()
             e.run_steps(10)
             e.synchronize()
+            assert e.eng.sync_error == 0
+            out.append(e.fs.params.clone())
+        assert torch.equal(out[0], out[1])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fuse_level", [1, 3])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_engine_xgmi_world1_beside_fused_reduce(fuse_level, use_graph):
+    """The direct xGMI all-reduce kernels at world size 1 (forced) on the comm stream, next
+    to the conv backward's fused in-launch slab reduction (its reducers spin beside the
+    all-reduce kernel of the fc bucket): eager and graph-captured runs equal the comm-free
+    run bit for bit, and the reduction really was fused."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import free_port
+
+    dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}")
+    try:
+        imgs, labels = synthetic_mnist(2048)
+        data = DeviceMNIST(imgs, labels, dev)
+        out = []
+        for force in (False, True):
+            torch.manual_seed(0)
+            m = SimpleCNN().to(dev)
+            e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, None,
+                                     EngineOptions(graph_steps=5, use_graph=use_graph, force_allreduce=force,
+                                                   comm="xgmi", fuse_level=fuse_level))
+            if force:
+                assert e.comm_kind.startswith("xgmi"), e.comm_kind
+            e.refresh()
+            e.run_steps(10)
+            e.synchronize()
+            assert e.eng.last_fused_reduce
+            assert e.eng.sync_error == 0
             out.append(e.fs.params.clone())
         assert torch.equal(out[0], out[1])
     finally:

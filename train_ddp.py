@@ -51,7 +51,7 @@ def parse_args(argv=None):
     p.add_argument("--num_workers", type=int, default=2, help="CPU DataLoader workers")
     p.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch (module/CPU path)")
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
-    p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1, 2],
+    p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1, 2, 3],
                    help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
                         "1 = 3 kernels/step (default); 2 = fc + conv backward in one launch (opt-in)")
     p.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
