@@ -206,7 +206,8 @@ def _verify_and_broadcast(fs, model, world_size):
         dist.broadcast(fs.params, src=0)  # one flat collective (SimpleCNN has no buffers)
         bs = buffer_space(model)
         if bs is not None:
-            dist.broadcast(bs.bytes, src=0)
+            for t in bs.flat_list():  # one flat collective per dtype
+                dist.broadcast(t, src=0)
 
 
 def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_steps,

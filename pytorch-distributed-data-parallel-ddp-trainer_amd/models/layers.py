@@ -318,30 +318,37 @@ class FlatSpace:
 
 class BufferSpace:
     """Every buffer of a module (BatchNorm running stats, ``num_batches_tracked``, ...) as a
-    typed view into ONE contiguous byte buffer, so DDP's ``broadcast_buffers`` is a single
-    collective per forward instead of one per tensor (torch DDP coalesces the same way,
+    view into one contiguous flat tensor PER DTYPE, so DDP's ``broadcast_buffers`` is one
+    collective per dtype per forward (2 for BatchNorm models: float32 stats, int64 counters)
+    instead of one per tensor (torch DDP coalesces the same way,
     ``torch/nn/parallel/distributed.py:1557-1558``; ResNet-18 has 60 buffers).
 
-    Each buffer starts on a 64-byte boundary; the module's ``_buffers`` entries are
-    replaced by views, so in-place kernel updates land in the flat bytes.
-    :meth:`rehome` copies back any buffer that was REPLACED by a new tensor since
-    (``module.buf = t``) and re-points it at its view."""
+    Each flat tensor has the dtype of its buffers, so ``torch.save(module.state_dict())``
+    sees only same-typed views of each storage (one byte buffer shared by float32 and int64
+    views made it refuse: "Cannot save multiple tensors or storages that view the same data
+    as different types" - ADVICE r2).  Each buffer starts on a 64-byte boundary; the
+    module's ``_buffers`` entries are replaced by views, so in-place kernel updates land in
+    the flat tensors.  :meth:`rehome` copies back any buffer that was REPLACED by a new
+    tensor of the same dtype / shape / device (``module.buf = t``); :func:`buffer_space`
+    rebuilds the space when a buffer changed dtype, shape or device (``model.to(...)``,
+    ``.double()``) instead of silently copying it back."""
 
     def __init__(self, module: nn.Module, align: int = 64):
         self.module = module
         self.names = [n for n, _ in module.named_buffers()]
         named = dict(module.named_buffers())
-        self.offsets, self.nbytes, self.meta = {}, {}, {}
-        off = 0
+        self.offsets, self.meta = {}, {}
+        totals = {}  # dtype -> elements
         for n in self.names:
             b = named[n]
-            nb = b.numel() * b.element_size()
-            self.offsets[n], self.nbytes[n] = off, nb
-            self.meta[n] = (b.dtype, tuple(b.shape))
-            off += (nb + align - 1) // align * align
-        self.total = off
+            es = b.element_size()
+            q = max(1, align // es)  # elements per alignment quantum
+            off = totals.get(b.dtype, 0)
+            self.offsets[n] = off
+            self.meta[n] = (b.dtype, tuple(b.shape), b.device)
+            totals[b.dtype] = off + (b.numel() + q - 1) // q * q
         dev = named[self.names[0]].device if self.names else torch.device("cpu")
-        self.bytes = torch.zeros(max(off, 1), dtype=torch.uint8, device=dev)
+        self.flats = {dt: torch.zeros(max(n, 1), dtype=dt, device=dev) for dt, n in totals.items()}
         self._views = {}
         for n in self.names:
             v = self.view(n)
@@ -352,25 +359,41 @@ class BufferSpace:
             mod._buffers[attr] = v
         module._ddp_amd_bufs = self
 
+    def flat_list(self) -> list:
+        """The flat tensors, in first-appearance order of their dtypes (one collective each)."""
+        return list(self.flats.values())
+
     def view(self, name: str) -> torch.Tensor:
-        """Alias of the buffer's bytes with its OWN version counter (``set_`` on the
+        """Alias of the buffer's elements with its OWN version counter (``set_`` on the
         storage, not an autograd view): BatchNorm saves running stats for backward, and
         a version counter shared by all 60 buffers would make every later layer's
         in-place stat update look like a modification of the saved tensor."""
-        dt, shape = self.meta[name]
-        es = torch.empty(0, dtype=dt).element_size()
-        t = torch.empty(0, dtype=dt, device=self.bytes.device)
-        t.set_(self.bytes.untyped_storage(), self.offsets[name] // es, shape)
+        dt, shape, _ = self.meta[name]
+        flat = self.flats[dt]
+        t = torch.empty(0, dtype=dt, device=flat.device)
+        t.set_(flat.untyped_storage(), self.offsets[name], shape)
         return t
 
+    def matches(self) -> bool:
+        """Whether every current buffer still has the dtype / shape / device it was laid
+        out with (and no buffer was added or removed)."""
+        cur = dict(self.module.named_buffers())
+        if list(cur) != self.names:
+            return False
+        return all((b.dtype, tuple(b.shape), b.device) == self.meta[n] for n, b in cur.items())
+
     def rehome(self) -> int:
-        """Pull replaced buffers back into the flat bytes; returns how many moved."""
+        """Pull replaced buffers back into the flat tensors; returns how many moved.
+        Raises if a replacement changed dtype / shape / device (use :func:`buffer_space`,
+        which rebuilds the space in that case)."""
         moved = 0
         for n in self.names:
             mod, attr = _resolve(self.module, n)
             cur, v = mod._buffers.get(attr), self._views[n]
             if cur is None or cur.data_ptr() == v.data_ptr():
                 continue
+            if (cur.dtype, tuple(cur.shape), cur.device) != self.meta[n]:
+                raise RuntimeError(f"buffer {n} changed dtype/shape/device: rebuild the BufferSpace")
             with torch.no_grad():
                 v.copy_(cur)
             mod._buffers[attr] = v
@@ -379,9 +402,10 @@ class BufferSpace:
 
 
 def buffer_space(module: nn.Module) -> BufferSpace | None:
-    """The module's BufferSpace (created on first use); ``None`` if it has no buffers."""
+    """The module's BufferSpace (created on first use, rebuilt when a buffer changed dtype,
+    shape or device); ``None`` if it has no buffers."""
     bs = getattr(module, "_ddp_amd_bufs", None)
-    if bs is None:
+    if bs is None or not bs.matches():
         if not any(True for _ in module.buffers()):
             return None
         bs = BufferSpace(module)

@@ -193,7 +193,8 @@ class DistributedDataParallel(nn.Module):
             return
         self._broadcast(self.fs.params)
         if self.bufs is not None:
-            self._broadcast(self.bufs.bytes)
+            for t in self.bufs.flat_list():  # one per dtype
+                self._broadcast(t)
 
     def _broadcast(self, t: torch.Tensor):
         """One broadcast of a flat buffer from the group's rank 0: our native RCCL
@@ -261,9 +262,10 @@ class DistributedDataParallel(nn.Module):
             # the step's compute stream: the bucket all-reduces order after it (see the hooks)
             self._stream = torch.cuda.current_stream(self.fs.params.device)
         if self.broadcast_buffers and self.world_size > 1 and self.bufs is not None:
-            self.bufs.rehome()
+            self.bufs = buffer_space(self.module)  # rehomed (or rebuilt after a .to())
             with torch.no_grad():
-                self._broadcast(self.bufs.bytes)
+                for t in self.bufs.flat_list():  # one per dtype
+                    self._broadcast(t)
             self.buffer_broadcasts += 1
         return self.module(*args, **kwargs)
 

@@ -53,9 +53,16 @@ def default_backend() -> str:
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
+_VISIBILITY_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
 def _gpu_host() -> bool:
-    """The host exposes an AMD GPU (the KFD device node) - a GPU run is the expected one."""
-    return os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != ""
+    """The host exposes an AMD GPU (the KFD device node) and the user did not hide every
+    device (an empty HIP_ / ROCR_ / CUDA_VISIBLE_DEVICES means "no GPU requested") - a GPU
+    run is the expected one."""
+    if any(os.environ.get(v, "x") == "" for v in _VISIBILITY_VARS):
+        return False
+    return os.path.exists("/dev/kfd")
 
 
 def resolve_backend(backend: str | None = None, device: str | None = None) -> str:

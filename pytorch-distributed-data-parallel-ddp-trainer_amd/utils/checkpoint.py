@@ -129,9 +129,10 @@ def resume(model, optimizer, ckpt_dir="./checkpoints", rank: int = 0, world_size
                     dist.broadcast(p.data, src=0)
             from ..models.layers import buffer_space
 
-            bs = buffer_space(model)  # every buffer in one flat byte broadcast
+            bs = buffer_space(model)  # every buffer: one flat broadcast per dtype
             if bs is not None:
-                dist.broadcast(bs.bytes, src=0)
+                for t in bs.flat_list():
+                    dist.broadcast(t, src=0)
         hp = [optimizer.param_groups[0] if rank == 0 else None]
         dist.broadcast_object_list(hp, src=0)
         optimizer.param_groups[0].update(hp[0])

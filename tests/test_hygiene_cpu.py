@@ -68,3 +68,17 @@ def test_loaded_momentum_state_means_started():
     opt3 = FusedSGD(SimpleCNN(), lr=0.01, momentum=0.9)
     opt3.load_state_dict(FusedSGD(SimpleCNN(), lr=0.01, momentum=0.9).state_dict())
     assert opt3.steps == 0 and opt3.momentum_buffer is None
+
+
+@pytest.mark.parametrize("var", ["HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"])
+def test_hidden_devices_mean_cpu_run(monkeypatch, var):
+    """hiding every GPU through ANY of the visibility variables (empty value) is
+    an explicit "no GPU" request - auto mode then trains over gloo instead of raising."""
+    from ddp_amd.parallel import process_group as pg
+
+    for v in pg._VISIBILITY_VARS:
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv(var, "")
+    monkeypatch.setattr(pg.torch.cuda, "is_available", lambda: False)
+    assert not pg._gpu_host()
+    assert pg.resolve_backend(None, "auto") == "gloo"
