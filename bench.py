@@ -354,8 +354,10 @@ def bench_resnet(args):
     torch.manual_seed(0)
     model = resnet18().to(dev)
     # gloo rehearsal: no buffer broadcast (a c10d gloo call is not graph-capturable)
+    from ddp_amd.engine.trainer import module_comm
+
     ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb,
-                                  broadcast_buffers=args.backend == "nccl")
+                                  broadcast_buffers=args.backend == "nccl", comm=module_comm(args.comm))
     opt = FusedSGD(model, lr=args.lr, momentum=0.9)
     lossf = CrossEntropyLoss()
     B, S = args.batch_size, args.image_size

@@ -70,7 +70,9 @@ __device__ __forceinline__ void shadow_one(const ShadowSet& sh, long j, float v)
 
 // Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
 // has signalled `target` to us.  Caller guarantees every wave drained its stores.
-__device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target, unsigned* s_fail) {
+// On a timeout the FIRST stalled wait is recorded in the error word (xgmi_error_code:
+// block, peer, barrier); the word stays non-zero (sticky) for every later call.
+__device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target, unsigned* s_fail, int phase) {
   __syncthreads();
   const int t = threadIdx.x;
   if (t < a.world && !*s_fail) {
@@ -81,7 +83,10 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
     while ((int)(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-        __hip_atomic_store(a.sig[a.rank] + XGMI_ERR_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        unsigned expected = 0u;
+        __hip_atomic_compare_exchange_strong(a.sig[a.rank] + XGMI_ERR_OFF, &expected,
+                                             xgmi_error_code((int)blockIdx.x, t, phase), __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         *s_fail = 1u;
         break;
       }
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
     const long par1 = (long)(e & 1u) * a.n;
     for (long i = i0; i < a.n; i += G) st_sys(a.stage[r] + par1 + i, a.data[r][a.off + i]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    xgmi_barrier(a, 2u * e, &s_fail);
+    xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_ONESHOT);
     if (!s_fail) {
       float* src[XGMI_MAX_RANKS];
 #pragma unroll
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  xgmi_barrier(a, 2u * e, &s_fail);  // B0
+  xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_B0);  // B0
   if (!s_fail) {
     // ---- RS: elements of my slice, fixed-order sum over ranks 0..N-1
     float* src[XGMI_MAX_RANKS];
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
     if (i < lim) st_sys(a.stage[r] + par + i, rank_sum(a, src, i, N));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  xgmi_barrier(a, 2u * e + 1u, &s_fail);  // B1
+  xgmi_barrier(a, 2u * e + 1u, &s_fail, XGMI_PHASE_B1);  // B1
   if (!s_fail) {
     // ---- AG: element i of every rank's reduced slice into my gradient buffer
     for (long i = i0; i < slice; i += G) {

@@ -331,6 +331,14 @@ constexpr int XGMI_FLAG_OFF = 0;
 constexpr int XGMI_SEQ_OFF = XGMI_MAX_BLOCKS * XGMI_MAX_RANKS;
 constexpr int XGMI_ERR_OFF = XGMI_SEQ_OFF + XGMI_MAX_BLOCKS;
 constexpr int XGMI_SIG_WORDS = XGMI_ERR_OFF + 64;
+// error word of a channel: 0 = ok, else the first barrier wait that timed out (sticky):
+// bit 31 | block << 12 | peer rank << 4 | phase (0: entry barrier B0, 1: after the
+// reduce-scatter B1, 2: the one-shot barrier)
+enum { XGMI_PHASE_B0 = 0, XGMI_PHASE_B1 = 1, XGMI_PHASE_ONESHOT = 2 };
+__host__ __device__ constexpr unsigned xgmi_error_code(int block, int peer, int phase) {
+  return 0x80000000u | ((unsigned)block << 12) | ((unsigned)(peer & 0xff) << 4) | (unsigned)(phase & 0xf);
+}
+constexpr double XGMI_DEFAULT_TIMEOUT_S = 30.0;  // per barrier spin (a slow peer is not an error)
 struct XgmiArgs {
   float* data[XGMI_MAX_RANKS];    // every rank's gradient buffer (peer-mapped; [rank] = own)
   float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats (one-shot: 2 x n)

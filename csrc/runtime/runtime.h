@@ -82,7 +82,9 @@ class XgmiComm {
   // the same, with SGD fused into the all-gather (see XgmiArgs)
   void all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
                       const ShadowSet& sh, int* step_ctr, float scale = 1.f, bool publish = false);
-  unsigned error_flags() const;  // != 0: a barrier timed out (result invalid)
+  // != 0: a barrier timed out (result invalid) - the first failed channel's error word
+  // (xgmi_error_code: block, peer, barrier)
+  unsigned error_flags() const;
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -106,7 +108,7 @@ class XgmiComm {
   std::vector<Channel> ch_;
   std::vector<void*> opened_;
   bool imported_ = false;
-  double timeout_s_ = 2.0;
+  double timeout_s_ = XGMI_DEFAULT_TIMEOUT_S;
 };
 
 // ---------------------------------------------------------------- gradient reducer

@@ -32,7 +32,7 @@ XgmiComm::XgmiComm(int rank, int world, int device) : rank_(rank), world_(world)
     throw std::runtime_error("xgmi: world size must be 1.." + std::to_string(XGMI_MAX_RANKS));
   if (rank < 0 || rank >= world) throw std::runtime_error("xgmi: bad rank");
   DDP_HIP_CHECK(hipSetDevice(device));
-  // rehearsal knobs (several ranks sharing one GPU): a longer barrier bound
+  // per-barrier spin bound (default XGMI_DEFAULT_TIMEOUT_S; set_timeout / this override)
   if (const char* e = std::getenv("DDP_AMD_XGMI_TIMEOUT_S")) timeout_s_ = std::atof(e);
 }
 
@@ -167,13 +167,12 @@ void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, fl
 }
 
 unsigned XgmiComm::error_flags() const {
-  unsigned e = 0;
   for (const auto& c : ch_) {
     unsigned v = 0;
     DDP_HIP_CHECK(hipMemcpy(&v, c.sig_local + XGMI_ERR_OFF, sizeof(v), hipMemcpyDeviceToHost));
-    e |= v;
+    if (v) return v;  // the first failed channel's code (codes must not be OR-ed together)
   }
-  return e;
+  return 0;
 }
 
 }  // namespace ddp_amd

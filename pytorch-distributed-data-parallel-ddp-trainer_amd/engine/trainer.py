@@ -3,10 +3,14 @@
 Same phases, same log lines, same checkpoint/resume contract,
 with the reference's bugs fixed and the hot loop replaced:
 
-* GPU (default): the native fused step engine - 8 HIP kernels + 2 RCCL bucket
-  all-reduces per step, hipGraph-replayed, dataset resident in HBM;
+* GPU (default): the native fused step engine - 2 HIP kernels per step on one GPU
+  (fuse level 3), plus the light fc weight-gradient kernel and one direct-xGMI (or RCCL)
+  all-reduce per gradient bucket on several, hipGraph-replayed, dataset resident in HBM;
 * GPU ``--engine module``: the module path (HIP autograd Functions + our DDP with
   the native C++ reducer) - the reference's loop shape, kernel-for-kernel on HIP;
+* GPU with ``--backend gloo --device gpu``: the same GPU paths with a gloo control plane
+  and the direct xGMI data plane - several ranks may share one GPU, which rehearses the
+  multi-GPU trainer (checkpoint / resume, bucket all-reduces) on a single device;
 * CPU: gloo + the reference's loop over a DataLoader (BASELINE config 1).
 
 ``model="resnet18"`` (BASELINE config 5) trains torchvision-layout ResNet-18 on
@@ -64,6 +68,8 @@ class TrainOptions:
     dataset_size: int = 2048          # resnet18: synthetic images resident per rank
     graph_module: bool = False        # module path on GPU: capture each step in a hipGraph
     dtype: str = "bf16"               # GPU compute precision: bf16 | fp32 (exact fp32 MFMA, reference precision)
+    verify_replicas: bool = False     # after every epoch: all ranks' parameters (+ momentum) bitwise equal, or raise
+    stall: tuple | None = None        # (epoch, rank, seconds): that rank sleeps before the epoch's first step
 
 
 def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
@@ -71,8 +77,13 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
     opts = opts or TrainOptions()
     backend = setup(rank=rank, world_size=world_size, backend=opts.backend,
                     timeout_s=opts.pg_timeout_s, device=opts.device)
-    on_gpu = backend == "nccl"
+    # RCCL means the GPU; gloo means the GPU only when it was asked for explicitly (a gloo
+    # control plane over GPU tensors + the direct xGMI data plane: same-GPU rehearsals)
+    want = (opts.device or os.environ.get("DDP_AMD_DEVICE") or "auto").lower()
+    on_gpu = backend == "nccl" or (want == "gpu" and torch.cuda.is_available())
     device = torch.device("cuda", local_rank(rank)) if on_gpu else torch.device("cpu")
+    if on_gpu:
+        torch.cuda.set_device(device)
     print(f"Rank {rank} initialized", flush=True)
     if opts.grad_accum < 1:
         raise ValueError("--grad_accum must be >= 1")
@@ -101,7 +112,7 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
         _verify_and_broadcast(fs, model, world_size)
         ddp_model = model
     else:
-        ddp_model = DDP(model, bucket_cap_mb=opts.bucket_cap_mb)
+        ddp_model = DDP(model, bucket_cap_mb=opts.bucket_cap_mb, comm=module_comm(opts.comm))
         fs = ddp_model.fs
     print(f"Rank {rank} model wrapped in DDP", flush=True)
 
@@ -152,6 +163,9 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
                 print(f"Epoch {epoch} | Batch {batch_idx} | Loss: {loss_value:.4f}", flush=True)
 
         fault_step = _fault_step(opts.fault, epoch, rank)
+        if opts.stall and int(opts.stall[0]) == epoch and int(opts.stall[1]) == rank:
+            print(f"Rank {rank}: injected stall of {float(opts.stall[2]):g} s before epoch {epoch}", flush=True)
+            time.sleep(float(opts.stall[2]))  # a slow rank: the peers' all-reduces wait for it
         if fused:
             nsteps = engine.run_epoch(epoch, on_loss=log, log_every=opts.log_every,
                                       max_steps=fault_step if fault_step is not None else opts.max_steps)
@@ -170,12 +184,48 @@ def ddp_train(rank: int, world_size: int, epochs: int, batch_size: int,
         _record_metrics(opts, rank, world_size, epoch, nsteps, batch_size, dt,
                         samples_processed(nsteps, batch_size, len(sampler)))
 
+        if opts.verify_replicas and world_size > 1:
+            verify_replicas(fs, opt, rank, world_size, epoch)
         if rank == 0 and opts.save:
             save_checkpoint(opts.checkpoint_dir, epoch, model, opt)
         if world_size > 1:
             dist.barrier()  # B13: nobody races past a half-written checkpoint
     cleanup()
     return model
+
+
+def module_comm(comm: str) -> str:
+    """The module path's data plane for the trainer's ``--comm`` (the engine's plan names):
+    rccl -> RCCL, xgmi / xgmi1 / xgmi2 / tune -> the direct xGMI kernels, auto -> DDP's own
+    choice (RCCL under nccl, xGMI under a gloo control plane)."""
+    if comm in ("auto", "rccl"):
+        return comm
+    if comm in ("xgmi", "xgmi1", "xgmi2", "tune"):
+        return "xgmi"
+    raise ValueError(f"unknown comm {comm!r}")
+
+
+def replica_digest(fs, opt) -> str:
+    """SHA-1 of this rank's flat parameters (+ momentum): bitwise replica identity."""
+    import hashlib
+
+    h = hashlib.sha1(fs.params.detach().cpu().numpy().tobytes())
+    mb = getattr(opt, "momentum_buffer", None)
+    if mb is not None:
+        h.update(mb.detach().cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
+def verify_replicas(fs, opt, rank: int, world_size: int, epoch: int):
+    """DDP's invariant, checked: every rank holds bitwise the same parameters and optimizer
+    state (a divergence would mean a broken all-reduce or a non-deterministic kernel)."""
+    d = replica_digest(fs, opt)
+    allg = [None] * world_size
+    dist.all_gather_object(allg, d)
+    if any(x != allg[0] for x in allg):
+        raise RuntimeError(f"epoch {epoch}: replicas diverged across ranks: {allg}")
+    if rank == 0:
+        print(f"Rank 0: replicas bitwise identical after epoch {epoch} ({d[:12]})", flush=True)
 
 
 def _fault_step(fault, epoch, rank):
@@ -261,7 +311,19 @@ def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_s
     return n
 
 
-_graphed = {}
+class _GraphCache(dict):
+    """{input shape: GraphedStep} of one model (a dict subclass so it is weak-referenceable)."""
+
+
+def _graph_cache(model) -> dict:
+    """The model's captured training-step graphs, keyed by input shape.  Kept ON the model
+    object (not in a module global keyed by ``id(model)``): it dies with the model, and a
+    recycled id can never replay another model's graph."""
+    cache = getattr(model, "_ddp_amd_step_graphs", None)
+    if cache is None:
+        cache = _GraphCache()
+        object.__setattr__(model, "_ddp_amd_step_graphs", cache)
+    return cache
 
 
 def _run_graphed_epoch(model, loader, loss_fn, opt, log, log_every, max_steps):
@@ -274,17 +336,19 @@ def _run_graphed_epoch(model, loader, loss_fn, opt, log, log_every, max_steps):
         opt.step()
         return loss
 
+    graphs = _graph_cache(model)
+    full = getattr(loader, "batch_size", None)  # the full batch: only that shape is captured
     n = 0
     for batch_idx, (images, labels) in enumerate(loader):
-        key = (id(model), tuple(images.shape))
-        if key not in _graphed:
-            if _graphed and images.shape[0] < next(iter(_graphed))[1][0]:
+        key = tuple(images.shape)
+        if key not in graphs:
+            if full is not None and images.shape[0] != full:
                 loss = step(images, labels)  # ragged tail: eager, no new capture
             else:
-                _graphed[key] = GraphedStep(step, (images, labels), warmup=1)  # = this batch's step
-                loss = _graphed[key].warmup_out
+                graphs[key] = GraphedStep(step, (images, labels), warmup=1)  # = this batch's step
+                loss = graphs[key].warmup_out
         else:
-            loss = _graphed[key](images, labels)
+            loss = graphs[key](images, labels)
         if batch_idx % log_every == 0:
             log(batch_idx, loss.item())
         n += 1

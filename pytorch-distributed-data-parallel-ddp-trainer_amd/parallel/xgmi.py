@@ -81,6 +81,22 @@ def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
     return x
 
 
+_PHASES = {0: "B0 (entry: gradients final)", 1: "B1 (reduce-scatter done)", 2: "one-shot publish"}
+
+
+def describe_xgmi_error(code: int) -> str:
+    """Readable form of an XgmiComm error word (launchers.h ``xgmi_error_code``): which
+    block of this rank waited for which peer at which barrier until the spin bound."""
+    code = int(code)
+    if code == 0:
+        return "ok"
+    if code & 0x80000000:
+        blk, peer, phase = (code >> 12) & 0x7FFFF, (code >> 4) & 0xFF, code & 0xF
+        return (f"block {blk} timed out waiting for peer rank {peer} at barrier "
+                f"{_PHASES.get(phase, phase)}")
+    return f"error word {code:#x}"
+
+
 def channel_plan(nbuckets: int, oneshot=()) -> dict:
     """``{(bucket, oneshot): channel}`` for a comm built by ``create_xgmi(..., oneshot=...)``."""
     plan = {(b, False): b for b in range(nbuckets)}
@@ -100,7 +116,8 @@ def _self_test(x, grads, chans, rank, world) -> bool:
                 x.all_reduce(ch)
                 stream.synchronize()
                 if x.error_flags():
-                    print(f"[ddp_amd] rank {rank}: xGMI barrier timeout in self-test", file=sys.stderr)
+                    print(f"[ddp_amd] rank {rank}: xGMI self-test: {describe_xgmi_error(x.error_flags())}",
+                          file=sys.stderr)
                     return False
                 want = sum(_pattern(n, r + rounds, grads.device) for r in range(world))
                 if not torch.equal(grads[off:off + n], want):

@@ -1,0 +1,112 @@
+"""The multi-rank GPU trainer, rehearsed on ONE MI355X (VERDICT r2 "missing" #1, BASELINE config
+4 at world size 2): ``train_ddp.py --world_size 2 --backend gloo --device gpu`` spawns two
+ranks that share the GPU - a gloo control plane (RCCL refuses two ranks on one device) and
+the direct xGMI data plane for the bucket all-reduces (same-GPU IPC mappings).  Every run
+is a fresh ``train_ddp.py`` process tree, as on a real node.
+
+Reference behaviour pinned here: the world-size spawn (/root/reference/train_ddp.py:221-224),
+rank-0 discovery + broadcast resume (:45-185), rank-0 save (:204-209), DDP's replicated
+parameters (:34) - checked bitwise after every epoch (``--verify_replicas``) - and a crash +
+re-run reproducing the uninterrupted run's checkpoint byte for byte (all zip records but the
+random serialization_id)."""
+import os
+import subprocess
+import sys
+import zipfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _train(cwd, *args, expect_rc=0, timeout=300):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, "-u", os.path.join(REPO, "train_ddp.py"), "--world_size", "2", "--backend", "gloo",
+           "--device", "gpu", "--data", "synthetic", "--verify_replicas", *args]
+    p = subprocess.run(cmd, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    if expect_rc == 0:
+        assert p.returncode == 0, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    else:
+        assert p.returncode != 0, f"expected a failure\n{p.stdout[-3000:]}"
+    return p.stdout + p.stderr
+
+
+def _zip_diff(a, b):
+    za, zb = zipfile.ZipFile(a), zipfile.ZipFile(b)
+    assert [i.filename for i in za.infolist()] == [i.filename for i in zb.infolist()]
+    return {i.filename for i in za.infolist() if za.read(i.filename) != zb.read(i.filename)}
+
+
+@pytest.mark.parametrize("engine", ["fused", "module"])
+def test_two_rank_train_save_resume(tmp_path, engine):
+    """2 ranks: every reference log line from both ranks, epoch_0.pt written once by rank 0,
+    replicas bitwise identical, and a re-run with more epochs resumes at epoch 1 on both
+    ranks (broadcast from rank 0)."""
+    common = ["--batch_size", "32", "--max_steps", "30", "--log_every", "10", "--engine", engine]
+    out = _train(tmp_path, "--epochs", "1", *common)
+    for r in (0, 1):
+        for line in [f"Rank: {r} has initialized its process group with world size 2", f"Rank {r} initialized",
+                     f"Rank {r} model wrapped in DDP", f"Rank {r}: Dataloader ready",
+                     f"Rank {r}: Loss and Optimizer ready", f"Rank {r}: No checkpoint found, starting from scratch.",
+                     f"Rank {r}: Starting epoch 0", f"Rank {r} cleaned up."]:
+            assert line in out, (line, out[-2000:])
+    assert "Epoch 0 | Batch 0 | Loss:" in out and "Epoch 0 | Batch 20 | Loss:" in out
+    assert "Rank 0: replicas bitwise identical after epoch 0" in out
+    ck_dir = tmp_path / "checkpoints"
+    assert sorted(os.listdir(ck_dir)) == ["epoch_0.pt"]
+    ck = torch.load(ck_dir / "epoch_0.pt", weights_only=True)
+    assert ck["epoch"] == 0 and list(ck) == ["epoch", "model", "optimizer"]
+    out2 = _train(tmp_path, "--epochs", "2", *common)
+    for r in (0, 1):
+        assert f"Rank {r}: Starting epoch 1" in out2 and f"Rank {r}: Starting epoch 0" not in out2
+    assert "No checkpoint found" not in out2
+    assert "Rank 0: replicas bitwise identical after epoch 1" in out2
+    assert sorted(os.listdir(ck_dir)) == ["epoch_0.pt", "epoch_1.pt"]
+
+
+@pytest.mark.parametrize("momentum", ["0", "0.9"])
+def test_two_rank_fault_resume_byte_identical(tmp_path, momentum):
+    """BASELINE config 4 at world size 2: rank 1 crashes at epoch 1 step 20 (the launcher
+    tears the job down), the re-run resumes from epoch_0.pt and its epoch_2.pt equals the
+    uninterrupted 2-rank run's byte for byte - plain SGD and momentum (its buffer is part
+    of the checkpoint and of the resume broadcast)."""
+    common = ["--epochs", "3", "--batch_size", "32", "--max_steps", "40", "--graph_steps", "16",
+              "--momentum", momentum, "--log_every", "1000"]
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    out_a = _train(a, *common)
+    assert out_a.count("replicas bitwise identical") == 3
+    out = _train(b, *common, "--fault_at", "1:20:1", expect_rc=17)
+    assert "Rank 1: injected fault at epoch 1 step 20" in out
+    assert sorted(os.listdir(b / "checkpoints")) == ["epoch_0.pt"]
+    out = _train(b, *common)
+    assert "Rank 0: Starting epoch 1" in out and "Rank 1: Starting epoch 1" in out and "Starting epoch 0" not in out
+    for e in (1, 2):
+        diff = _zip_diff(a / "checkpoints" / f"epoch_{e}.pt", b / "checkpoints" / f"epoch_{e}.pt")
+        assert diff <= {f"epoch_{e}/.data/serialization_id"}, (e, diff)
+    ck = torch.load(a / "checkpoints" / "epoch_2.pt", weights_only=True)
+    assert bool(ck["optimizer"]["state"]) == (momentum != "0")
+
+
+def test_two_rank_slow_rank_survives(tmp_path):
+    """Rank 1 sleeps 3 s before epoch 1 (after the epoch-0 barrier, so rank 0 is already
+    inside epoch 1's first all-reduce, spinning on its device-side barrier): the xGMI
+    barrier's spin bound (30 s) must absorb a slow peer - the run finishes with bitwise
+    identical replicas and the same checkpoint as an undisturbed run."""
+    common = ["--epochs", "2", "--batch_size", "32", "--max_steps", "30", "--graph_steps", "10",
+              "--momentum", "0.9", "--log_every", "1000"]
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    _train(a, *common)
+    out = _train(b, *common, "--stall_at", "1:1:3")
+    assert "Rank 1: injected stall of 3 s before epoch 1" in out
+    assert "Rank 0: replicas bitwise identical after epoch 1" in out
+    diff = _zip_diff(a / "checkpoints" / "epoch_1.pt", b / "checkpoints" / "epoch_1.pt")
+    assert diff <= {"epoch_1/.data/serialization_id"}, diff

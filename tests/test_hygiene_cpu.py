@@ -82,3 +82,49 @@ def test_hidden_devices_mean_cpu_run(monkeypatch, var):
     monkeypatch.setattr(pg.torch.cuda, "is_available", lambda: False)
     assert not pg._gpu_host()
     assert pg.resolve_backend(None, "auto") == "gloo"
+
+
+def test_module_comm_mapping():
+    """--comm reaches the module path: the engine's plan names map onto the
+    module reducer's planes."""
+    from ddp_amd.engine.trainer import module_comm
+
+    assert module_comm("auto") == "auto" and module_comm("rccl") == "rccl"
+    for c in ("xgmi", "xgmi1", "xgmi2", "tune"):
+        assert module_comm(c) == "xgmi"
+    with pytest.raises(ValueError):
+        module_comm("nope")
+
+
+def test_graph_cache_scoped_to_model():
+    """The captured-step cache lives on the model: two models never share
+    entries, and it goes away with the model instead of pinning graphs in a global."""
+    import gc
+    import weakref
+
+    from ddp_amd.engine.trainer import _graph_cache
+
+    a, b = torch.nn.Linear(2, 2), torch.nn.Linear(2, 2)
+    ca, cb = _graph_cache(a), _graph_cache(b)
+    ca[(4, 2)] = "graph-a"
+    assert _graph_cache(a) is ca and cb == {} and ca is not cb
+    ref = weakref.ref(ca)
+    del a, ca
+    gc.collect()
+    assert ref() is None
+
+
+def test_replica_digest_detects_divergence():
+    from ddp_amd.engine.trainer import replica_digest
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.models.layers import flat_space
+    from ddp_amd.ops import FusedSGD
+
+    torch.manual_seed(0)
+    m = SimpleCNN()
+    fs, opt = flat_space(m), FusedSGD(m, lr=0.01, momentum=0.9)
+    d0 = replica_digest(fs, opt)
+    assert replica_digest(fs, opt) == d0
+    with torch.no_grad():
+        fs.params[123] = torch.nextafter(fs.params[123], torch.tensor(1e9))  # one ulp
+    assert replica_digest(fs, opt) != d0

@@ -53,11 +53,14 @@ def parse_args(argv=None):
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
     p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1, 2, 3],
                    help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
-                        "1 = 3 kernels/step (default); 2 = fc + conv backward in one launch (opt-in)")
+                        "1 = 3 kernels/step; 2 = fc + conv backward in one launch (opt-in); 3 = dZ2 in the "
+                        "forward, fc weight gradient inside the conv backward: 2 kernels/step (default)")
     p.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
-                   help="fused engine bucket all-reduce at world size > 1: auto = the direct xGMI kernels "
-                        "(one-shot for the small bucket; RCCL if their self-test fails) - deterministic, so "
-                        "resumes reduce in the same order; tune = fastest of xgmi2 / xgmi1 / RCCL on the node")
+                   help="bucket all-reduce data plane at world size > 1. Fused engine: auto = the direct xGMI "
+                        "kernels (one-shot for the small bucket; RCCL if their self-test fails) - deterministic, "
+                        "so resumes reduce in the same order; tune = fastest of xgmi2 / xgmi1 / RCCL on the "
+                        "node. Module path (--engine module, resnet18): rccl, or xgmi for any xgmi* / tune; "
+                        "auto = RCCL under the rccl backend, xGMI under gloo")
     p.add_argument("--grad_accum", type=int, default=1,
                    help="micro-batches per optimizer step (module/CPU path; DDP no_sync)")
     p.add_argument("--global_loss", action="store_true",
@@ -73,6 +76,10 @@ def parse_args(argv=None):
                    help="module path on GPU: replay each training step as one captured hipGraph")
     p.add_argument("--fault_at", default=None, metavar="EPOCH:STEP[:RANK]",
                    help="simulate a crash (os._exit) at that step; re-run to auto-resume")
+    p.add_argument("--stall_at", default=None, metavar="EPOCH:RANK:SECONDS",
+                   help="simulate a slow rank: it sleeps before that epoch's first step")
+    p.add_argument("--verify_replicas", action="store_true",
+                   help="after every epoch check that all ranks' parameters and momentum are bitwise equal")
     return p.parse_args(argv)
 
 
@@ -88,7 +95,8 @@ def main(argv=None):
                         global_loss=a.global_loss, pg_timeout_s=a.pg_timeout_min * 60.0,
                         comm=a.comm, model=a.model, image_size=a.image_size,
                         num_classes=a.num_classes, dataset_size=a.dataset_size,
-                        graph_module=a.graph_module,
+                        graph_module=a.graph_module, verify_replicas=a.verify_replicas,
+                        stall=tuple(float(v) for v in a.stall_at.split(":")) if a.stall_at else None,
                         fault=tuple(int(v) for v in a.fault_at.split(":")) if a.fault_at else None)
     launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
 
