@@ -22,9 +22,11 @@ Metric/config are BASELINE.json's: images/sec of the reference's SimpleCNN
 random-init weights (no network for the real dataset), bf16 compute with fp32
 master weights / gradients / optimizer.  A timed step is the complete training
 step of the reference's loop: batch gather + forward + loss + backward + DDP
-bucket all-reduce (N>1) + SGD update - executed by the native fused engine (3 HIP
-kernels per step, + one all-reduce per gradient bucket at N>1 - the direct xGMI kernel,
-RCCL as the fallback - replayed from a hipGraph).
+bucket all-reduce (N>1) + SGD update - executed by the native fused engine (2 HIP
+kernels per step on one GPU; at N>1 3 kernels + one all-reduce per gradient bucket - the
+direct xGMI kernel, RCCL as the fallback - replayed from a hipGraph).  After the bf16
+headline the same process times the exact-fp32 engine (the reference's precision) the same
+way and reports it as ``config.fp32_images_per_sec`` (``--no_fp32`` skips it).
 
 W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
 ``torch.cuda.synchronize()`` on both sides; the step time is the MAX over ranks;
@@ -173,6 +175,9 @@ def main():
     ap.add_argument("--bucket_cap_mb", type=float, default=25.0,
                     help="DDP bucket cap (torch rule: first bucket 1 MiB, then this cap)")
     ap.add_argument("--first_bucket_mb", type=float, default=1.0)
+    ap.add_argument("--bucket_plan", choices=["model", "torch"], default="model",
+                    help="gradient buckets: model = the xGMI cost model's plan (parallel/bucket_model.py), "
+                         "torch = torch DDP's size rule with --bucket_cap_mb / --first_bucket_mb")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
                     help="compute precision: bf16 MFMA operands (default) or exact fp32 MFMA (the "
                          "reference's precision)")
@@ -185,6 +190,8 @@ def main():
     ap.add_argument("--wgrad_halo_target", type=int, default=256, help="resnet18: halo wgrad blocks per launch")
     ap.add_argument("--wgrad_halo_cit", type=int, default=0, choices=[0, 16, 32],
                     help="resnet18: input channels per halo wgrad block (0 = planner default)")
+    ap.add_argument("--no_fp32", action="store_true",
+                    help="skip the exact-fp32 (reference precision) run after the bf16 headline")
     ap.add_argument("--dry_launch", action="store_true",
                     help="self-launch test hook: workers report their launcher env and exit (no GPU)")
     ap.add_argument("--no_scaling_ref", action="store_true",
@@ -234,34 +241,8 @@ def main():
         elif args.comm == "rccl":
             raise SystemExit("--backend gloo has no RCCL data plane: use --comm xgmi")
 
-    torch.manual_seed(0)
-    model = SimpleCNN().to(dev)
-    fs = flat_space(model)
-    if ws > 1:
-        if args.backend == "nccl":
-            dist.broadcast(fs.params, src=0)  # DDP construction semantics (rank-0 init)
-        else:
-            t = fs.params.detach().cpu()
-            dist.broadcast(t, src=0)
-            fs.params.data.copy_(t)
-    opt = FusedSGD(model, lr=args.lr)
     imgs, labels = synthetic_mnist()
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
-    k = args.graph_steps or graph_chunk(args.steps)
-    eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=args.dtype,
-                       bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
-    eo.comm = args.comm
-    for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role"):
-        if getattr(args, f) is not None:
-            setattr(eo, f, getattr(args, f))
-    eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
-    eng.refresh()
-    if not args.no_graph:
-        eng.run_steps(0)           # uploads epoch 0's indices
-        eng._ensure_graph()        # capture outside the timed region
-    if args.warmup:
-        eng.run_steps(args.warmup)
-    eng.synchronize()
 
     def barrier():
         if ws > 1:
@@ -271,20 +252,61 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    eng.run_steps(args.steps)
-    barrier()  # torch.cuda.synchronize() waits for the engine's streams too
-    dt = time.perf_counter() - t0
-    eng.synchronize()  # (idle by now) raises if an in-launch / cross-GPU wait timed out
-    if ws > 1:
-        t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    def timed_run(dtype):
+        """Build the engine for ``dtype`` (fresh seeded model, rank-0 init broadcast), warm up,
+        time exactly ``args.steps`` steps between barrier + synchronize brackets; returns
+        (seconds = MAX over ranks, engine, flat space, model, graph chunk)."""
+        torch.manual_seed(0)
+        model = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
+        fs = flat_space(model)
+        if ws > 1:
+            if args.backend == "nccl":
+                dist.broadcast(fs.params, src=0)  # DDP construction semantics (rank-0 init)
+            else:
+                t = fs.params.detach().cpu()
+                dist.broadcast(t, src=0)
+                fs.params.data.copy_(t)
+        opt = FusedSGD(model, lr=args.lr)
+        k = args.graph_steps or graph_chunk(args.steps)
+        eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=dtype,
+                           bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
+                           bucket_plan=args.bucket_plan)
+        eo.comm = args.comm
+        for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role"):
+            if getattr(args, f) is not None and not (dtype == "fp32" and f in ("fuse_level", "store_a1")):
+                setattr(eo, f, getattr(args, f))
+        if dtype == "fp32":
+            eo.fuse_level, eo.store_a1 = 1, 0  # the exact-fp32 chain (engine.cpp launch_step_f32)
+        eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
+        eng.refresh()
+        if not args.no_graph:
+            eng.run_steps(0)           # uploads epoch 0's indices
+            eng._ensure_graph()        # capture outside the timed region
+        if args.warmup:
+            eng.run_steps(args.warmup)
+        eng.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        eng.run_steps(args.steps)
+        barrier()  # torch.cuda.synchronize() waits for the engine's streams too
+        dt = time.perf_counter() - t0
+        eng.synchronize()  # (idle by now) raises if an in-launch / cross-GPU wait timed out
+        if ws > 1:
+            t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, eng, fs, model, k, eo
+
+    dt, eng, fs, model, k, eo = timed_run(args.dtype)
     ms = dt * 1000.0 / args.steps
     img_s = ws * args.batch_size * args.steps / dt
     bucket_us = eng.measure_bucket_allreduce() if ws > 1 else None  # after the timed region
+    from ddp_amd.parallel.bucket_model import describe
+
+    plan = describe(eng.buckets, fs, eng.cost) if ws > 1 else None
     finite = bool(torch.isfinite(fs.params).all().item())
+    level3 = bool(eng.eng.last_level3)
+    kps = (2 if eng.eng.last_fc_role else 3) if level3 else None
     same = True
     if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
         pd = dev if args.backend == "nccl" else "cpu"
@@ -294,6 +316,15 @@ def main():
         diff = torch.tensor([0 if torch.equal(ref, mine) else 1], device=pd)
         dist.all_reduce(diff)
         same = int(diff.item()) == 0
+    # the reference's own precision (fp32 nn.Conv2d / nn.Linear, /root/reference/model.py:8-16):
+    # the exact-fp32 engine timed the same way, after the headline
+    fp32 = None
+    if args.dtype == "bf16" and not args.no_fp32:
+        dt32, eng32, _, _, _, _ = timed_run("fp32")
+        fp32 = {"images_per_sec": round(ws * args.batch_size * args.steps / dt32, 1),
+                "ms_per_step": round(dt32 * 1000.0 / args.steps, 5),
+                "kernels": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32), level-1 chain"}
+        del eng32
     if rank == 0:
         base = BASELINE_IMG_S.get(ws)
         print(json.dumps({
@@ -313,7 +344,8 @@ def main():
                        "global_batch": ws * args.batch_size, "per_rank_batch": args.batch_size,
                        "seq_len": None, "image": "1x28x28", "parallelism": f"dp{ws}",
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
-                       "graph_steps": k, "fuse_level": eo.fuse_level,
+                       "graph_steps": k, "fuse_level": eo.fuse_level, "level3": level3,
+                       "kernels_per_step": kps,
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
                                   "wgrad_rows": eng.wgrad_rows, "store_a1": eng.store_a1,
                                   "wgrad_split": eo.wgrad_split},
@@ -322,7 +354,12 @@ def main():
                        "buckets_elems": [n for _, n in eng.ranges],
                        "params_identical_across_ranks": same, "ranks_seen": ranks_seen,
                        "rccl_nranks": rccl_nranks, "backend": args.backend if ws > 1 else None,
-                       "scaling_efficiency": None, "tuned_planes_us": eng.allreduce_us},
+                       "scaling_efficiency": None, "tuned_planes_us": eng.allreduce_us,
+                       "bucket_plan": {"rule": args.bucket_plan, "buckets": plan,
+                                       "pred_last_allreduce_done_us": (round(eng.pred_comm_us, 2)
+                                                                       if ws > 1 and eng.pred_comm_us else None)},
+                       "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
+                       "fp32_ms_per_step": fp32["ms_per_step"] if fp32 else None},
         }), flush=True)
     if ws > 1:
         barrier()
@@ -353,11 +390,21 @@ def bench_resnet(args):
     setup(rank, ws, backend=args.backend, verbose=False)
     torch.manual_seed(0)
     model = resnet18().to(dev)
+    S0 = args.image_size
     # gloo rehearsal: no buffer broadcast (a c10d gloo call is not graph-capturable)
     from ddp_amd.engine.trainer import module_comm
 
+    plan = None
+    if args.bucket_plan == "model" and ws > 1:
+        from ddp_amd.models.layers import flat_space
+        from ddp_amd.parallel.bucket_model import module_plan
+
+        # cost-model plan from the CPU twin's layer shapes (same module tree, per-rank batch)
+        cpu_twin = resnet18()
+        plan, _ = module_plan(flat_space(cpu_twin), cpu_twin, torch.randn(args.batch_size, 3, S0, S0), ws)
     ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb,
-                                  broadcast_buffers=args.backend == "nccl", comm=module_comm(args.comm))
+                                  broadcast_buffers=args.backend == "nccl", comm=module_comm(args.comm),
+                                  buckets=plan)
     opt = FusedSGD(model, lr=args.lr, momentum=0.9)
     lossf = CrossEntropyLoss()
     B, S = args.batch_size, args.image_size

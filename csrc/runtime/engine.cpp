@@ -1,34 +1,38 @@
 // Fused SimpleCNN DDP training step (the MI355X-native replacement of the
 // reference's hot loop, train_ddp.py:195-200).
 //
-// One step = 8 kernels on the compute stream + 2 bucket all-reduces on the comm
-// stream, all stream-ordered so that a whole run of steps can be captured in a
-// single hipGraph and replayed (no per-step host launches):
+// Every kernel of a step is stream-ordered on the engine's compute stream (bucket
+// all-reduces on a comm stream, joined by events), so a whole run of steps is captured
+// in ONE hipGraph and replayed (no per-step host launches).  The default chain
+// (EngineConfig::fuse_level 3, bf16, one GPU) is 2 kernels per step:
 //
-//   conv1_fwd      u8 dataset gather (epoch index list) + /255 + conv1 + bias + ReLU -> a1
-//   conv3x3_fwd    conv2 (MFMA) + bias + ReLU -> a2, fused fc partial logits
-//   xent           split-K logits reduce + bias + softmax-xent fwd/bwd, fc bias grad
-//   fc_bwd         dZ2 = relu2'(a2) * dL.Wfc ; dWfc -> bucket 0 (prescaled 1/ws)
-//       -> event -> comm stream: all-reduce(bucket 0)  [overlaps the conv backward]
-//   conv3x3_dgrad  dZ1 = relu1'(a1) * conv2^T(dZ2) + fused conv1 wgrad slabs
-//   conv3x3_wgrad  conv2 weight/bias grad slabs (MFMA, split-K over image rows)
-//   grad_reduce    fixed-order slab sums -> bucket 1 (prescaled)
-//       -> event -> comm stream: all-reduce(bucket 1)
-//   sgd            wait both buckets; p -= lr*g over the flat buffer, bf16 shadows,
-//                  step counter += 1 (the next step's batch window)
+//   conv3x3_fwd   uint8 batch gather + /255 + conv1 (recomputed in the LDS staging pass)
+//                 + conv2 (MFMA) + bias + ReLU -> a2, the fc partial logits; then a
+//                 per-image in-launch wait for the image's other blocks, the softmax
+//                 cross-entropy dL and dZ2 = relu2'(a2) * (dL . W_fc) for its own pixels
+//   conv3x3_bwd   dgrad role (dZ1 + conv1 weight gradient), wgrad role (conv2 weight /
+//                 bias gradient slabs, two blocks per slab row), the fc role (fc weight
+//                 gradient + SGD of the fc weight and bias, the loss, the step counter)
+//                 and the in-launch fixed-order slab reduction + SGD of the conv weights
 //
-// fuse_level 1 drops conv1_fwd and xent: conv3x3_fwd / dgrad / wgrad recompute
-// a1 = relu(conv1(x)) from the uint8 images in their LDS staging pass (C1Src) and
-// fc_bwd runs the softmax cross-entropy in its prologue -> 6 kernels per step,
-// bit-identical to level 0 (same FMA orders, same fixed-order reductions).
+// At world size > 1 the fc weight gradient is its own light kernel between the two
+// (fc_bwd without dX, dL given), so the fc bucket's all-reduce - the direct xGMI kernels
+// with SGD fused into their all-gather, or RCCL + one SGD pass - overlaps the conv
+// backward on the comm stream; the conv bucket's all-reduce follows the conv backward.
 //
-// f32 = 1 (--dtype fp32) runs the same level-1 chain with exact fp32 operands
-// (launch_step_f32): fp32 a2 / dZ2, the fp32 master weights read directly by the conv
-// forward and fc kernels, and one fp32 [tap][ci][co] copy of the conv2 weight (kept by
-// the optimizer pass, like the bf16 shadows) for the data gradient.
+// Older chains stay selectable (tests pin them bit for bit against each other):
+//   level 0: 8 kernels (conv1_fwd, conv3x3_fwd, xent, fc_bwd, dgrad, wgrad, grad_reduce,
+//            sgd) with a1 materialised;
+//   level 1: conv1 recomputed inside conv2 fwd / dgrad / wgrad, cross-entropy in the
+//            fc_bwd prologue, optimizer in the epilogues, the slab reduction inside the
+//            conv backward: 3 kernels (forward -> fc_bwd -> conv backward);
+//   level 2: level 1 with fc_bwd and the conv backward in one launch (dZ2 handed off
+//            inside it; slower - its blocks are not co-resident);
+//   f32 = 1 (--dtype fp32): the level-1 chain with exact fp32 operands (launch_step_f32).
 //
-// Buckets follow the reference DDP's rebuilt layout:
-// bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB).
+// Buckets follow the reference DDP's rebuilt layout by default:
+// bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB); any
+// bucket plan works (stage 0 = fc-only buckets, stage 1 = the rest).
 #include <algorithm>
 
 #include "runtime/runtime.h"

@@ -31,9 +31,11 @@ from ..models.layers import flat_space
 from ..ops.functional import wgrad_rows
 from ..parallel.ddp import bucket_plan, bucket_ranges
 
-# buckets up to this many fp32 elements also get a one-shot xGMI channel (SimpleCNN's
-# conv bucket: 18,816 = 75 KB); the bucket must fit one kernel grid (1024 x 256)
-ONESHOT_MAX_ELEMS = 65536
+# buckets up to this many fp32 elements may get a one-shot xGMI channel: the bucket must
+# fit one kernel grid (1024 x 256); below it the cost model's crossover decides
+# (parallel/bucket_model.py: SimpleCNN's 75 KB conv bucket is one-shot at every N, the
+# 2 MB fc bucket one-shot at N = 2 and two-shot at N >= 4)
+ONESHOT_MAX_ELEMS = 1024 * 256
 
 BF16 = torch.bfloat16
 
@@ -47,6 +49,10 @@ class EngineOptions:
     wgrad_rows: int | None = None
     bucket_cap_mb: float = 25.0
     first_bucket_mb: float = 1.0   # torch DDP's first-bucket cap (the rest use bucket_cap_mb)
+    # "model": the xGMI cost model's plan (parallel/bucket_model.engine_plan: one bucket per
+    # stage - [fc] then [conv] - which is also the reference DDP's rebuilt layout);
+    # "torch": torch's size rule with bucket_cap_mb / first_bucket_mb
+    bucket_plan: str = "model"
     force_allreduce: bool = False  # bucket all-reduces even at world size 1 (plumbing tests)
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
     # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd; 3 with
@@ -112,7 +118,15 @@ class FusedSimpleCNNEngine:
                  "b2": "net.2.bias", "wfc": "fl.weight", "bfc": "fl.bias"}
         # any DDP bucket plan: each bucket's all-reduce starts as soon as its gradients are
         # final (fc-only buckets right after fc_bwd, overlapping the conv backward)
-        self.buckets = bucket_plan(fs, self.opts.bucket_cap_mb, self.opts.first_bucket_mb)
+        from ..parallel.bucket_model import XgmiCost, engine_plan
+
+        self.cost = XgmiCost(world_size)
+        if self.opts.bucket_plan == "model":
+            self.buckets, self.pred_comm_us = engine_plan(fs, world_size, self.cost)
+        elif self.opts.bucket_plan == "torch":
+            self.buckets, self.pred_comm_us = bucket_plan(fs, self.opts.bucket_cap_mb, self.opts.first_bucket_mb), None
+        else:
+            raise ValueError(f"bucket_plan must be model|torch, got {self.opts.bucket_plan!r}")
         ranges = bucket_ranges(fs, self.buckets)
         offs = {k: fs.offsets[v] for k, v in names.items()}
         offs["buckets"] = [(int(o), int(n)) for o, n in ranges]
@@ -185,7 +199,8 @@ class FusedSimpleCNNEngine:
             from ..parallel.xgmi import channel_plan, create_xgmi, pick_data_plane
 
             # small buckets also get a one-shot channel (one cross-GPU barrier instead of two)
-            oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= ONESHOT_MAX_ELEMS)
+            lim = min(ONESHOT_MAX_ELEMS, self.cost.oneshot_max_elems())
+            oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
             self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size, oneshot=oneshot)
             if self.xgmi is not None and self.opts.comm in ("xgmi1", "xgmi2"):
                 plan = "xgmi1" if self.opts.comm == "xgmi1" else "xgmi"  # forced (tests, sweeps)

@@ -50,6 +50,15 @@ def bucket_plan(fs: FlatSpace, bucket_cap_mb: float = 25.0, first_bucket_mb: flo
     return buckets
 
 
+def check_plan(fs: FlatSpace, buckets):
+    """An explicit bucket plan must cover every parameter once, in gradient-ready order."""
+    flat = [n for b in buckets for n in b]
+    if flat != list(fs.names) or any(not b for b in buckets):
+        raise ValueError("bucket plan must split the gradient-ready parameter order into non-empty "
+                         f"contiguous buckets: got {[len(b) for b in buckets]} over {len(fs.names)} params")
+    return [list(b) for b in buckets]
+
+
 def bucket_ranges(fs: FlatSpace, buckets):
     """(offset, numel) of each bucket in the flat buffer (contiguous by construction)."""
     out = []
@@ -86,8 +95,6 @@ class _NativeReducer:
     RCCL, or the direct xGMI kernels (``comm="xgmi"``: fixed rank-order sums, bitwise
     identical on every rank; the only data plane when the ranks bootstrapped over gloo)."""
 
-    ONESHOT_MAX_ELEMS = 65536  # small buckets: one-shot kernel (one cross-GPU barrier)
-
     def __init__(self, fs: FlatSpace, buckets, ranges, comm: str = "rccl"):
         from .. import native
         from .process_group import native_comm
@@ -101,7 +108,12 @@ class _NativeReducer:
         if comm == "xgmi":
             from .xgmi import channel_plan, create_xgmi
 
-            oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= self.ONESHOT_MAX_ELEMS)
+            from .bucket_model import XgmiCost
+
+            # small buckets: the one-shot kernel (one cross-GPU barrier), below the cost
+            # model's crossover for this world size
+            lim = XgmiCost(dist.get_world_size()).oneshot_max_elems()
+            oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
             self.xgmi = create_xgmi(fs.grads, ranges, dist.get_rank(), dist.get_world_size(),
                                     oneshot=oneshot)
             if self.xgmi is None and not rccl:
@@ -128,10 +140,13 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None,
                  broadcast_buffers: bool = True, bucket_cap_mb: float = 25.0,
                  find_unused_parameters: bool = False, process_group=None,
-                 first_bucket_mb: float = 1.0, native: bool | None = None, comm: str = "auto"):
+                 first_bucket_mb: float = 1.0, native: bool | None = None, comm: str = "auto",
+                 buckets: list | None = None):
         """``comm`` (GPU, default group): ``"rccl"``, ``"xgmi"`` (the direct kernels) or
         ``"auto"`` - RCCL under the nccl backend, xGMI when the ranks bootstrapped over gloo
-        (several ranks on one GPU rehearse the multi-GPU path that way)."""
+        (several ranks on one GPU rehearse the multi-GPU path that way).  ``buckets``: an
+        explicit plan (lists of parameter names covering the gradient-ready order, e.g.
+        ``bucket_model.module_plan``) instead of torch's size rule."""
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -146,7 +161,8 @@ class DistributedDataParallel(nn.Module):
         self.buffer_broadcasts = 0
         self._verify_params()
         self._sync_module_states()
-        self.buckets = bucket_plan(self.fs, bucket_cap_mb, first_bucket_mb)
+        self.buckets = (check_plan(self.fs, buckets) if buckets is not None
+                        else bucket_plan(self.fs, bucket_cap_mb, first_bucket_mb))
         self.ranges = bucket_ranges(self.fs, self.buckets)
         self._bucket_of = {n: i for i, b in enumerate(self.buckets) for n in b}
         self._pending = [len(b) for b in self.buckets]

@@ -175,7 +175,7 @@ def _plan_worker(rank, world, port, q, cap_mb, first_mb, dtype):
         opt = FusedSGD(model, lr=0.05, momentum=0.9)
         imgs, labels = synthetic_mnist(4096)
         eo = EngineOptions(graph_steps=4, comm="xgmi", bucket_cap_mb=cap_mb, first_bucket_mb=first_mb,
-                           dtype=dtype)
+                           dtype=dtype, bucket_plan="torch")
         eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, torch.device("cuda", 0)),
                                    16, world, rank, None, eo)
         assert eng.comm_kind in ("xgmi", "xgmi1"), eng.comm_kind
