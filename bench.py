@@ -154,9 +154,9 @@ def main():
                          "in one launch, 3: dZ2 in the forward, fc weight gradient inside the conv "
                          "backward - 2 kernels/step); default = engine default (3)")
     ap.add_argument("--l3_fc_role", type=int, default=None, choices=[0, 1, 2],
-                    help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch, right "
-                         "after the dgrad blocks (1) or after every conv block (2), or as its own kernel "
-                         "between forward and conv backward (0)")
+                    help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch on "
+                         "persistent blocks after every conv block (1) or right after the dgrad blocks (2), "
+                         "or as its own kernel between forward and conv backward (0)")
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")

@@ -1111,8 +1111,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // dispatch-order argument above is unchanged (every block a reducer waits for has a lower
 // index than the reducer); the fc role's own last block (FcBwdExtras::last_ctr) finishes the
 // fc bias, the loss and the step counter (launchers.h BwdFc).
-// 4 waves x 2 virtual waves, 4 columns per lane: == the 8-wave fc_bwd (same VW, fc_bwd_body.h)
-constexpr int BFC_WPB = 4, BFC_VW = 8, BFC_CPL = 4;
+constexpr int BFC_MAXB = 48;  // batch capacity of the fc role (level 3 needs B <= 41 anyway)
 
 template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
           bool FCR = false>
@@ -1126,9 +1125,26 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
   if constexpr (FCR) {
     const int f = cb - fcr.fc0;
     if (f >= 0 && f < fcr.nfc) {
-      fc_bwd_body<bf16_t, false, false, 10, BFC_WPB, BFC_VW, BFC_CPL, false>(
-          fcr.dl, fcr.a2, nullptr, nullptr, fcr.dW, fcr.scale, B, fcr.K, 10, fcr.ex, reinterpret_cast<float*>(smem),
-          f, nullptr);
+      // fc role (persistent): dL of the batch into LDS once, block 0 finishes the fc bias,
+      // the loss and the step counter (nothing else in this launch reads them), then every
+      // wave takes 128-column chunks f * 4 + wave, + 4 * nfc, ... (fc_dw_wave_chunk)
+      DDP_STAMP(STAMP_K_FC_BWD, 0);
+      float* s_dl = reinterpret_cast<float*>(smem);  // [B][FCDW_LD] (padded rows)
+      for (int i = threadIdx.x; i < B * 10; i += 256) s_dl[(i / 10) * FCDW_LD + i % 10] = fcr.dl[i];
+      __syncthreads();
+      if (f == 0 && threadIdx.x < 64) {  // fc_bwd_bias_loss reads dense [B][10] rows
+        float* s_dd = s_dl + B * FCDW_LD;
+        for (int i = threadIdx.x; i < B * 10; i += 64) s_dd[i] = s_dl[(i / 10) * FCDW_LD + i % 10];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (same wave: the copy is in LDS)
+        fc_bwd_bias_loss<false>(fcr.ex, s_dd, nullptr, B, 10, true);
+      }
+      DDP_STAMP(STAMP_K_FC_BWD, 1);
+      // one 128-column chunk per wave, straight-line (a chunk loop let the compiler hoist
+      // every row offset / guard of the unrolled body out of it: 300 spilled registers)
+      const int nch = (int)((fcr.K + 127) / 128);
+      const int q = f * 4 + (threadIdx.x >> 6);
+      if (q < nch) fc_dw_wave_chunk<BFC_MAXB>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, (long)q * 128);
+      DDP_STAMP(STAMP_K_FC_BWD, 4);
       return;
     }
     if (f >= 0) cb -= fcr.nfc;
@@ -1527,22 +1543,24 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     throw std::runtime_error("conv3x3_bwd: slab rows must be 16-byte multiples on a 16-byte aligned buffer");
   BwdFc fcr;
   int nfc = 0;
+  const bool da = !Xact, wa = !Xact || !wgrad_load_a1;
   if (fc) {
     if (sizeof(T) != 2 || !conv3x3_bwd_fc_role_ok(H, W, Cin, Cout, pxt, cs) || !fc->dl || !fc->a2 ||
-        fc->K % (64 * BFC_CPL) != 0)
-      throw std::runtime_error("conv3x3_bwd: the fc role is the bf16 SimpleCNN variant (pxt 2, channel split, dL given)");
+        fc->K % 2 != 0 || B > BFC_MAXB || fc->ex.last_ctr)
+      throw std::runtime_error("conv3x3_bwd: the fc role is the bf16 SimpleCNN variant (pxt 2, channel split, dL "
+                               "given, B <= 48, no last-block count)");
     fcr = *fc;
     fcr.nconv = nd + nw;
-    nfc = (int)(fc->K / (64 * BFC_CPL));
+    // one 128-column chunk per wave (4 per block): the first blocks take the resident slots
+    // the conv blocks leave free, the rest those the dgrad blocks free first
+    nfc = (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
-    // fc blocks right after the dgrad role (fc_pos 1: they run while the first wgrad blocks
-    // do, on the slots the dgrad blocks free first) or after every conv block (fc_pos 0)
+    // fc blocks after every conv block (fc_pos 0: dispatched into the slots the conv blocks
+    // leave free) or right after the dgrad role (fc_pos 1)
     fcr.fc0 = fc->fc_pos == 1 ? nd : nd + nw;
-    if (fcr.ex.last_ctr) fcr.ex.last_n = nfc;
-    const size_t fl = sizeof(float) * (size_t)fcb_lds_floats(B, 10, false, 0, fcb_red_floats<BFC_WPB, 10, BFC_CPL>());
-    lds = lds > fl ? lds : fl;
+    if ((size_t)B * (FCDW_LD + 10) * sizeof(float) > lds)
+      throw std::runtime_error("conv3x3_bwd: LDS too small for the fc role");
   }
-  const bool da = !Xact, wa = !Xact || !wgrad_load_a1;
   BwdReduce red;
   red.nconv = nd + nw;
   if (fused) {

@@ -123,6 +123,108 @@ __device__ __forceinline__ void fc_bwd_bias_loss(const FcBwdExtras& ex, const fl
     for (int i = lane; i < ex.n_zero; i += 64) ex.zero_i32[(long)i * ex.zero_stride] = 0;
 }
 
+// Wave-independent fc weight gradient (+ fused SGD) of 128 consecutive columns [col0,
+// col0 + 128): lane l owns columns col0 + 2l, +1 and sums their dW over the whole batch
+// itself, in fc_bwd_body's virtual-wave order for VW = 8 (virtual wave v: rows v, v + 8,
+// ..., an fma chain from 0; partials combined v = 0, 1, ..., 7) - bit-identical to the
+// block-wide body, with no LDS reduction and no block barrier per chunk.  dL comes from
+// LDS, rows padded to FCDW_LD floats (s_dl [B][FCDW_LD], filled by the caller; read as
+// broadcast 16-byte loads).  B <= MAXB.  Every global load of the chunk (the SGD operands,
+// then all B rows) is issued up front; a scheduling barrier per virtual wave keeps only
+// that wave's dL values live.  The level-3 conv backward's fc role runs it on the launch's
+// otherwise idle resident slots (conv3x3.hip FCR).
+constexpr int FCDW_LD = 12;
+template <int MAXB>
+__device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const bf16_t* __restrict__ X,
+                                                 float* __restrict__ dW, float scale, int B, long K,
+                                                 const FcBwdExtras& ex, long col0) {
+  constexpr int NO = 10, VW = 8, RPV = (MAXB + VW - 1) / VW;
+  const int lane = threadIdx.x & 63;
+  const long col = col0 + 2 * lane;
+  const bool active = col < K;  // host guarantees K % 2 == 0
+  const long cc = active ? col : 0;
+  // buffer loads: one scalar base per tensor, the row / class offset in the scalar offset
+  // field, the lane's column offset in ONE VGPR shared by every load (no per-load 64-bit
+  // addresses; the fc tensors are < 2 GiB)
+  typedef __attribute__((ext_vector_type(2))) int i32x2_t;
+  const int vo4 = (int)cc * 4, vo2 = (int)cc * 2;
+  float2 pp[NO], mm[NO];
+  if (ex.sgd.update) {
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(ex.p_w, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm =
+        __builtin_amdgcn_make_buffer_rsrc(ex.m_w ? ex.m_w : ex.p_w, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      pp[o] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rp, vo4, (int)(o * K * 4), 0));
+      mm[o] = ex.m_w ? __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rm, vo4, (int)(o * K * 4), 0))
+                     : make_float2(0.f, 0.f);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), (short)0, 0x7fffffff,
+                                                                      0x00020000);
+  unsigned xw[MAXB];
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b)
+    xw[b] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rx, vo2, (int)((long)min(b, B - 1) * K * 2), 0);
+  float acc[NO][2];
+#pragma unroll
+  for (int v = 0; v < VW; ++v) {
+    __builtin_amdgcn_sched_barrier(0);
+    float p[NO][2];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) p[o][0] = p[o][1] = 0.f;
+#pragma unroll
+    for (int u = 0; u < RPV; ++u) {
+      const int b = v + VW * u;
+      if (b < MAXB && b < B) {  // wave-uniform
+        const float x0 = __builtin_bit_cast(float, xw[b] << 16);
+        const float x1 = __builtin_bit_cast(float, xw[b] & 0xffff0000u);
+        const float4 d0 = *reinterpret_cast<const float4*>(s_dl + b * FCDW_LD);
+        const float4 d1 = *reinterpret_cast<const float4*>(s_dl + b * FCDW_LD + 4);
+        const float2 d2 = *reinterpret_cast<const float2*>(s_dl + b * FCDW_LD + 8);
+        const float d[NO] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w, d2.x, d2.y};
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          p[o][0] = fmaf(d[o], x0, p[o][0]);
+          p[o][1] = fmaf(d[o], x1, p[o][1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      acc[o][0] = v == 0 ? p[o][0] : acc[o][0] + p[o][0];
+      acc[o][1] = v == 0 ? p[o][1] : acc[o][1] + p[o][1];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  if (!active) return;
+  const long frag0 = ex.sh_frag ? fcfrag_index((int)col, ex.frag_HW, ex.frag_C) : 0;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    const float g0 = acc[o][0] * scale, g1 = acc[o][1] * scale;
+    const long idx = (long)o * K + col;
+    if (dW) {
+      if (ex.sys_store) {
+        st_sys(dW + idx, g0);
+        st_sys(dW + idx + 1, g1);
+      } else {
+        *reinterpret_cast<float2*>(dW + idx) = make_float2(g0, g1);
+      }
+    }
+    if (ex.sgd.update) {
+      float m0 = mm[o].x, m1 = mm[o].y;
+      const float p0 = sgd_one(pp[o].x, g0, &m0, ex.sgd), p1 = sgd_one(pp[o].y, g1, &m1, ex.sgd);
+      st_wt(reinterpret_cast<float2*>(ex.p_w + idx), make_float2(p0, p1));
+      if (ex.m_w) *reinterpret_cast<float2*>(ex.m_w + idx) = make_float2(m0, m1);
+      const unsigned pb = (unsigned)f2bf(p0) | ((unsigned)f2bf(p1) << 16);
+      if (ex.sh_plain) st_wt(reinterpret_cast<unsigned*>(ex.sh_plain + idx), pb);
+      // FCFRAG keeps channel pairs (c, c + 1), c even, adjacent: one 4-byte store; the class
+      // is its outermost dimension, so class o's index is class 0's + o * K
+      if (ex.sh_frag) st_wt(reinterpret_cast<unsigned*>(ex.sh_frag + frag0 + (long)o * K), pb);
+    }
+  }
+}
+
 template <typename T, bool MASK, bool XENT, int NOT, int WPB, int VW, int CPL, bool DXO = true>
 __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const T* __restrict__ X,
                                             const T* __restrict__ Wf, T* __restrict__ dX,

@@ -223,18 +223,20 @@ struct FcBwdExtras {
   int n_zero = 0, zero_stride = 1;
   int last_n = 0;               // arrivals of the last-block count (0: the grid size)
 };
-// The fc role of the level-3 conv backward launch (conv3x3_bwd, fc != null): fc_bwd_body
-// without dX, dL given (the forward's FwdDz::dl_out), blocks [nconv, grid) after the conv
-// roles; they never wait and are not counted by the fused reduction.  The fc role's own last
-// block (ex.last_ctr) finishes the fc bias, the loss and the step counter.
+// The fc role of the level-3 conv backward launch (conv3x3_bwd, fc != null): the fc weight
+// gradient + fused SGD without dX, dL given (the forward's FwdDz::dl_out), on blocks
+// [fc0, fc0 + nfc) whose waves each own one 128-column chunk (fc_dw_wave_chunk,
+// bit-identical to fc_bwd); they never wait and are not counted by the fused reduction.
+// Block 0 of the role finishes the fc bias (gradient + SGD), the loss and the step counter -
+// nothing else in the launch reads them (ex.last_ctr must be null).
 struct BwdFc {
   const bf16_t* a2 = nullptr;  // ReLU2 output [B][K]
   const float* dl = nullptr;   // dL [B][10]
   float* dW = nullptr;         // null: fused optimizer only
   float scale = 1.f;
   long K = 0;
-  int fc_pos = 1;              // 1: fc blocks right after the dgrad blocks, 0: after every conv block
-  int nconv = 0, fc0 = 0, nfc = 0;  // (set by the launcher)
+  int fc_pos = 0;              // 0: fc blocks after every conv block, 1: right after the dgrad blocks
+  int nconv = 0, fc0 = 0, nfc = 0;  // (set by the launcher: nfc = one 128-column chunk per wave)
   FcBwdExtras ex{};
 };
 size_t fc_bwd_lds(int B, int NO, bool xent, long npart = 0);  // npart: see linear.hip

@@ -34,6 +34,7 @@
 // bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB); any
 // bucket plan works (stage 0 = fc-only buckets, stage 1 = the rest).
 #include <algorithm>
+#include <cstdlib>
 
 #include "runtime/runtime.h"
 
@@ -268,9 +269,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ex.n_zero = B;
     ex.zero_stride = FWD_DZ_CNT_STRIDE;
     if (fc_role) {
-      // inside the conv backward launch: the fc role's last block owns the fc bias, the loss
-      // and the step counter (nothing after it in the launch may read them)
-      ex.last_ctr = b_.sync_flags + SYNC_RED_INTS;
+      // inside the conv backward launch: block 0 of the fc role owns the fc bias, the loss
+      // and the step counter (nothing else in the launch reads them)
       if (fopt) {
         ex.p_b = P + b_.off_bfc;
         ex.m_b = M ? M + b_.off_bfc : nullptr;
@@ -279,7 +279,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       ex.sh_plain = nullptr;  // level 3 never reads the plain bf16 fc shadow (stale until refreshed)
       fcr.a2 = b_.a2;
       fcr.dl = b_.dlogits;
-      fcr.fc_pos = cfg_.l3_fc_role == 2 ? 0 : 1;
+      fcr.fc_pos = cfg_.l3_fc_role == 2 ? 1 : 0;
       fcr.dW = fopt ? nullptr : G + b_.off_wfc;
       fcr.scale = inv_ws;
       fcr.K = (long)HW * C2;

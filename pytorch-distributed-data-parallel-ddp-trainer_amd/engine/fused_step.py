@@ -66,9 +66,10 @@ class EngineOptions:
     # several ranks; elsewhere the level-1 chain runs.  Bit-identical to level 1.
     fuse_level: int = 3
     # level 3, single process: the fc weight gradient as a third role of the conv backward
-    # launch (2 kernels per step) - 1: its blocks right after the dgrad blocks, 2: after every
-    # conv block; 0: its own light kernel between forward and conv backward (what world
-    # size > 1 always runs, so the fc bucket's all-reduce overlaps the conv backward)
+    # launch (2 kernels per step) - 1: its blocks (one 128-column chunk per wave) after every
+    # conv block, on the resident slots the conv blocks leave free; 2: the same blocks right
+    # after the dgrad blocks; 0: its own light kernel between forward and conv backward (what
+    # world size > 1 always runs, so the fc bucket's all-reduce overlaps the conv backward)
     l3_fc_role: int = 1
     # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
     fuse_opt: bool = True
