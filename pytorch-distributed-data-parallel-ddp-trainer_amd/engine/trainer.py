@@ -254,6 +254,7 @@ def _verify_and_broadcast(fs, model, world_size):
         raise RuntimeError(f"parameter shapes differ across ranks: {allm}")
     with torch.no_grad():
         dist.broadcast(fs.params, src=0)  # one flat collective (SimpleCNN has no buffers)
+        fs.params_written()
         bs = buffer_space(model)
         if bs is not None:
             for t in bs.flat_list():  # one flat collective per dtype

@@ -286,6 +286,12 @@ class FlatSpace:
             return None
         return self.bf16_params()[off:off + p.numel()].view(p.shape)
 
+    def params_written(self):
+        """The fp32 parameters were rewritten outside torch's in-place tracking (a c10d /
+        RCCL broadcast writes the storage without bumping the version counter): rebuild the
+        bf16 copies on next use."""
+        self._bf16_version = -1
+
     def mark_bf16_fresh(self):
         """Called by the optimizer after a step that rewrote the bf16 copy."""
         if self._bf16 is not None:

@@ -208,6 +208,7 @@ class DistributedDataParallel(nn.Module):
         if self.world_size == 1:
             return
         self._broadcast(self.fs.params)
+        self.fs.params_written()  # stale bf16 weight copies otherwise (no version bump)
         if self.bufs is not None:
             for t in self.bufs.flat_list():  # one per dtype
                 self._broadcast(t)

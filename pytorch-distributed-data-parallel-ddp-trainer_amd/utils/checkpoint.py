@@ -124,6 +124,7 @@ def resume(model, optimizer, ckpt_dir="./checkpoints", rank: int = 0, world_size
         with torch.no_grad():
             if flat is not None:
                 dist.broadcast(flat.params, src=0)
+                flat.params_written()  # (the broadcast does not bump the version counter)
             else:
                 for p in model.parameters():
                     dist.broadcast(p.data, src=0)

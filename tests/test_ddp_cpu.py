@@ -183,3 +183,49 @@ def test_grad_accum_matches_large_batch(tmp_path):
     m2 = run(16, 2, "b")
     for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-6), n
+
+
+def _worker_bf16_copy_after_broadcast(rank, ws, port, q):
+    """A c10d broadcast into the flat parameters does not bump their version counter: the
+    bf16 weight copy the MFMA kernels read must still be rebuilt (the r3 multi-rank GPU
+    rehearsal found a resumed rank 1 training on its own stale init through that copy)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import DistributedDataParallel
+    from ddp_amd.utils.checkpoint import resume
+
+    torch.manual_seed(100 + rank)  # different init per rank
+    m = SimpleCNN()
+    fs = flat_space(m)
+    stale = fs.bf16_params().clone()  # built from this rank's own init
+    DistributedDataParallel(m)        # construction: rank 0's parameters broadcast
+    ok_ctor = torch.equal(fs.bf16_params(), fs.params.to(torch.bfloat16))
+    # resume() broadcasts the flat buffer the same way
+    ck = os.environ["DDP_AMD_TEST_CKDIR"]
+    opt = FusedSGD(m, lr=0.1)
+    fs.bf16_params()
+    resume(m, opt, ck, rank, ws, flat=fs)
+    ok_resume = torch.equal(fs.bf16_params(), fs.params.to(torch.bfloat16))
+    q.put((rank, ok_ctor, ok_resume, rank == 0 or not torch.equal(stale, fs.bf16_params())))
+    dist.destroy_process_group()
+
+
+def test_bf16_copy_rebuilt_after_broadcasts(tmp_path):
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.utils.checkpoint import save_checkpoint
+
+    torch.manual_seed(5)
+    m = SimpleCNN()
+    save_checkpoint(str(tmp_path), 0, m, FusedSGD(m, lr=0.1))
+    os.environ["DDP_AMD_TEST_CKDIR"] = str(tmp_path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=_worker_bf16_copy_after_broadcast, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] and r[2] and r[3] for r in res), res
