@@ -1471,13 +1471,15 @@ size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es) {
   return m > row ? m : row;
 }
 
-// Resident-block budget of the fused reduction: every waiting (reducer) block holds a
-// slot, so the reducers are at most a QUARTER of the launch's resident capacity as the
-// occupancy API reports it (other kernels, e.g. a concurrent all-reduce, may take slots,
-// and the API was measured to overstate the fp32 variant's residency: with the wgrad
-// blocks dispatched first, 128 waiting fp32 reducers starved the rest of the grid).
-// Returns the number of reducers (the last blocks of the grid: all the wgrad blocks), 0
-// when they do not fit that budget (fewer reducers, two passes each, measured slower than
+// Resident-block budget of the fused reduction.  The reducers are the LAST conv blocks of
+// the grid and wait only for blocks with lower indices, so with in-order dispatch every
+// block a waiting reducer needs already holds a slot (or finished): no capacity makes it
+// deadlock.  The budget - at most HALF of the launch's resident capacity as the occupancy
+// API reports it for the exact instantiation - keeps room for what may share the GPU (a
+// concurrent all-reduce kernel; ranks sharing a device never fuse, fused_step.py).  (A
+// quarter was the rule while the wgrad blocks were dispatched FIRST: 128 waiting fp32
+// reducers starved the rest of that grid.)  Returns the number of reducers (all the wgrad
+// blocks), 0 when they do not fit (fewer reducers, two passes each, measured slower than
 // the separate grad_reduce kernel: fp32 364k vs 383k img/s) or the capacity is unknown.
 template <typename K>
 static int fused_reducers(K kernel, size_t lds, int nblocks) {
@@ -1486,8 +1488,8 @@ static int fused_reducers(K kernel, size_t lds, int nblocks) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), 256, lds) != hipSuccess)
     return 0;
-  const int quarter = occ * cus / 4;
-  return nblocks <= quarter ? nblocks : 0;
+  const int half = occ * cus / 2;
+  return nblocks <= half ? nblocks : 0;
 }
 
 template <typename T>

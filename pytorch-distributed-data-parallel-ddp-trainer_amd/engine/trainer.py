@@ -219,11 +219,23 @@ def replica_digest(fs, opt) -> str:
 def verify_replicas(fs, opt, rank: int, world_size: int, epoch: int):
     """DDP's invariant, checked: every rank holds bitwise the same parameters and optimizer
     state (a divergence would mean a broken all-reduce or a non-deterministic kernel)."""
+    import hashlib
+
     d = replica_digest(fs, opt)
     allg = [None] * world_size
     dist.all_gather_object(allg, d)
     if any(x != allg[0] for x in allg):
-        raise RuntimeError(f"epoch {epoch}: replicas diverged across ranks: {allg}")
+        # which tensors differ (and by how much), for the error message
+        per = {n: hashlib.sha1(fs.view(fs.params, n).detach().cpu().numpy().tobytes()).hexdigest()
+               for n in fs.names}
+        mine = fs.params.detach().cpu()
+        allp, allpar = [None] * world_size, [None] * world_size
+        dist.all_gather_object(allp, per)
+        dist.all_gather_object(allpar, mine)
+        bad = [n for n in fs.names if any(p[n] != allp[0][n] for p in allp)]
+        worst = max(float((t - allpar[0]).abs().max()) for t in allpar)
+        raise RuntimeError(f"epoch {epoch}: replicas diverged across ranks ({allg}); differing tensors "
+                           f"{bad}, max |diff| {worst:.3e}")
     if rank == 0:
         print(f"Rank 0: replicas bitwise identical after epoch {epoch} ({d[:12]})", flush=True)
 
@@ -259,6 +271,27 @@ def _verify_and_broadcast(fs, model, world_size):
         if bs is not None:
             for t in bs.flat_list():  # one flat collective per dtype
                 dist.broadcast(t, src=0)
+
+
+_SYNC_EACH_STEP = os.environ.get("DDP_AMD_SYNC_EACH_STEP") == "1"
+_VERIFY_EACH_STEP = os.environ.get("DDP_AMD_VERIFY_EACH_STEP") == "1"
+
+
+def _verify_step(model, opt, step):
+    """Diagnostic (DDP_AMD_VERIFY_EACH_STEP=1): compare the reduced gradients and the
+    parameters across ranks after every step; raise at the first difference."""
+    import hashlib
+
+    fs = model.fs if hasattr(model, "fs") else flat_space(model)
+    torch.cuda.synchronize()
+    h = lambda t: hashlib.sha1(t.detach().cpu().numpy().tobytes()).hexdigest()[:10]  # noqa: E731
+    mine = {"grads": {n: h(fs.view(fs.grads, n)) for n in fs.names}, "params": h(fs.params)}
+    allm = [None] * dist.get_world_size()
+    dist.all_gather_object(allm, mine)
+    bad = [n for n in fs.names if any(m["grads"][n] != allm[0]["grads"][n] for m in allm)]
+    if bad or any(m["params"] != allm[0]["params"] for m in allm):
+        raise RuntimeError(f"step {step}: replicas differ - reduced gradients {bad}, params "
+                           f"{[m['params'] for m in allm]}")
 
 
 def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_steps,
@@ -299,6 +332,10 @@ def _run_module_epoch(model, loader, loss_fn, opt, device, log, log_every, max_s
             opt.step()
             if grad_accum > 1:
                 opt.zero_grad()
+        if _SYNC_EACH_STEP:  # diagnostic: device-synchronise every step
+            torch.cuda.synchronize()
+        if _VERIFY_EACH_STEP and dist.is_initialized() and dist.get_world_size() > 1:
+            _verify_step(model, opt, batch_idx)
         if batch_idx % log_every == 0:
             lv = loss.detach()
             if global_loss and dist.is_initialized() and dist.get_world_size() > 1:

@@ -60,7 +60,12 @@ class XgmiCost:
 
     def oneshot_max_elems(self) -> int:
         """Largest fp32 bucket for which the one-shot kernel is predicted faster: one barrier
-        saved against (N - 2) / N of the bucket's bytes more per link."""
+        saved against (N - 2) / N of the bucket's bytes more per link.
+        ``DDP_AMD_XGMI_ONESHOT_MAX`` overrides it (sweeps, A/B)."""
+        import os
+
+        if os.environ.get("DDP_AMD_XGMI_ONESHOT_MAX"):
+            return int(os.environ["DDP_AMD_XGMI_ONESHOT_MAX"])
         if self.world <= 2:
             return 1 << 30  # N <= 2: one-shot moves no more bytes per link than two-shot
         per_byte = self._link_us(1.0) * (1.0 - 2.0 / self.world)
