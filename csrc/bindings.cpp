@@ -755,7 +755,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
       .def(py::init<int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("device"))
-      .def("add_channel", &XgmiComm::add_channel, py::arg("off"), py::arg("n"), py::arg("oneshot") = false)
+      .def("add_channel", &XgmiComm::add_channel, py::arg("off"), py::arg("n"), py::arg("oneshot") = false,
+           py::arg("grid_cap") = 0)
+      .def("blocks", &XgmiComm::blocks)
+      .def("bus_id", &XgmiComm::bus_id)
       .def("oneshot", &XgmiComm::oneshot)
       .def_property_readonly("channels", &XgmiComm::channels)
       .def("set_data", [](XgmiComm& x, Tensor& t) {

@@ -77,6 +77,9 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
   const int t = threadIdx.x;
   if (t < a.world && !*s_fail) {
     unsigned* dst = a.sig[t] + XGMI_FLAG_OFF + blockIdx.x * XGMI_MAX_RANKS + a.rank;
+    // release at system scope: everything this block stored (the caller drained its
+    // waves) is visible to the peers before they can see the flag
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(dst, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned* src = a.sig[a.rank] + XGMI_FLAG_OFF + blockIdx.x * XGMI_MAX_RANKS + t;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -91,37 +94,103 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
         break;
       }
     }
+    // acquire at system scope: no later load of this block may hit a cache line older
+    // than the peer's release (invalidates this CU's L1 and the non-coherent L2 lines)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
 }
 
-// Element i of the slice per thread and rank, blocks striding over 256-element chunks
-// (chunk c, c + gridDim.x, ...: the grid is capped at XGMI_GRID_CAP blocks so the
-// all-reduce, which overlaps the conv backward on its own stream, keeps few waves
-// resident while it waits in its barriers).  All N loads of a chunk - two chunks at a
-// time - are in flight at once, so each phase is about one xGMI round trip per two chunks.
-__device__ __forceinline__ float rank_sum(const XgmiArgs& a, float* const* src, long k, int N) {
-  float v[XGMI_MAX_RANKS];
-#pragma unroll
-  for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld_sys(src[p] + k) : 0.f;
-  float sum = v[0];
-#pragma unroll
-  for (int p = 1; p < XGMI_MAX_RANKS; ++p)
-    if (p < N) sum += v[p];
-  return sum;
+// Data movement is in 16-byte quads (4 floats): thread t of block b handles quad
+// q = b * XGMI_THREADS + t, then q + G, q + 2G, ... (G = grid x XGMI_THREADS quads), two
+// quads at a time, with all N ranks' loads of both in flight at once - 32 B x N per lane,
+// so a small grid (XGMI_GRID_CAP blocks, leaving most CUs to the concurrent backward)
+// still keeps megabytes in flight over the 7 links.  Peer memory is read with
+// system-scope (sc0 sc1) buffer loads, stage buffers written with system-scope stores.
+// Two-shot slices are whole quads (XgmiComm rounds the slice up to a multiple of 4), so
+// every rank's slice starts on a quad; the bucket's last quad may be partial and takes
+// the per-element path.
+constexpr int SYS_CPOL = 1 | 16;  // sc0 | sc1: system scope
+typedef __attribute__((ext_vector_type(4))) int ar_i32x4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 ld4_sys(__amdgpu_buffer_rsrc_t r, long q) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(q * 16), 0, SYS_CPOL));
+}
+__device__ __forceinline__ void st4_sys(__amdgpu_buffer_rsrc_t r, long q, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ar_i32x4, v), r, (int)(q * 16), 0, SYS_CPOL);
+}
+__device__ __forceinline__ float4 add4(float4 x, float4 y) {
+  return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
 }
 
-// the reduced gradient g of flat bucket element k -> my gradient buffer (+ fused SGD)
-__device__ __forceinline__ void finish(const XgmiArgs& a, long k, float g) {
-  a.data[a.rank][a.off + k] = g;
-  if (a.sgd.update) {  // fused optimizer: same update on every rank
-    const long j = a.off + k;
-    float m = a.mbuf ? a.mbuf[j] : 0.f;
-    const float pn = sgd_one(a.params[j], g, &m, a.sgd);
-    a.params[j] = pn;
-    if (a.mbuf) a.mbuf[j] = m;
-    shadow_one(a.sh, j, pn);
+// fixed rank-order (0..N-1) sum of quad q of every rank's source
+__device__ __forceinline__ float4 rank_sum4(const __amdgpu_buffer_rsrc_t* src, long q, int N) {
+  float4 v[XGMI_MAX_RANKS];
+#pragma unroll
+  for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld4_sys(src[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 sum = v[0];
+#pragma unroll
+  for (int p = 1; p < XGMI_MAX_RANKS; ++p)
+    if (p < N) sum = add4(sum, v[p]);
+  return sum;
+}
+// the same for the elements [4q, lim) of a partial last quad (element loads)
+__device__ __forceinline__ float4 rank_sum_tail(float* const* src, long q, long lim, int N) {
+  float e[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long k = 4 * q + j;
+    float sum = 0.f;
+    if (k < lim) {
+      sum = ld_sys(src[0] + k);
+#pragma unroll
+      for (int p = 1; p < XGMI_MAX_RANKS; ++p)
+        if (p < N) sum += ld_sys(src[p] + k);
+    }
+    e[j] = sum;
   }
+  return make_float4(e[0], e[1], e[2], e[3]);
+}
+
+// the fused optimizer on flat bucket element k with reduced gradient g: same update on
+// every rank, so parameters stay bitwise identical
+__device__ __forceinline__ void sgd_elem(const XgmiArgs& a, long k, float g) {
+  const long j = a.off + k;
+  float m = a.mbuf ? a.mbuf[j] : 0.f;
+  const float pn = sgd_one(a.params[j], g, &m, a.sgd);
+  a.params[j] = pn;
+  if (a.mbuf) a.mbuf[j] = m;
+  shadow_one(a.sh, j, pn);
+}
+// quad q (elements 4q.., below lim) of the reduced bucket times scale -> my gradient
+// buffer; without SGD when `sgd` is false (the caller runs sgd4 afterwards)
+__device__ __forceinline__ float4 scale4(const XgmiArgs& a, float4 v) {
+  return make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
+}
+__device__ __forceinline__ void store4(const XgmiArgs& a, long q, float4 v, long lim) {
+  float* d = a.data[a.rank] + a.off + 4 * q;
+  if (4 * q + 3 < lim) {
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  } else {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * q + j < lim) d[j] = e[j];
+  }
+}
+__device__ __forceinline__ void sgd4(const XgmiArgs& a, long q, float4 v, long lim) {
+  const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (4 * q + j < lim) sgd_elem(a, 4 * q + j, e[j]);
+}
+__device__ __forceinline__ void finish4(const XgmiArgs& a, long q, float4 v, long lim) {
+  v = scale4(a, v);
+  store4(a, q, v, lim);
+  if (a.sgd.update) sgd4(a, q, v, lim);
 }
 
 __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
@@ -142,79 +211,129 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
   }
   __syncthreads();
   const unsigned e = s_epoch;
-  const long G = (long)gridDim.x * XGMI_THREADS;     // elements per grid stride
-  const long i0 = (long)blockIdx.x * XGMI_THREADS + threadIdx.x;
+  const long G = (long)gridDim.x * XGMI_THREADS;     // quads per grid stride
+  const long q0 = (long)blockIdx.x * XGMI_THREADS + threadIdx.x;
 
   if (a.oneshot) {
     // ---- publish my whole bucket, one barrier, sum every rank's copy in rank order
-    const long par1 = (long)(e & 1u) * a.n;
-    for (long i = i0; i < a.n; i += G) st_sys(a.stage[r] + par1 + i, a.data[r][a.off + i]);
+    const long n = a.n, nq = (n + 3) / 4, fq = n / 4;  // quads, full quads
+    const long par1 = (long)(e & 1u) * ((nq * 4 + 3) & ~3L);
+    const float* mine = a.data[r] + a.off;
+    const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par1);
+    for (long q = q0; q < nq; q += G) {
+      float4 v;
+      if (q < fq) {
+        v = make_float4(mine[4 * q], mine[4 * q + 1], mine[4 * q + 2], mine[4 * q + 3]);
+      } else {
+        float t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = 4 * q + j < n ? mine[4 * q + j] : 0.f;
+        v = make_float4(t[0], t[1], t[2], t[3]);
+      }
+      st4_sys(mystage, q, v);  // the stage holds whole quads (zero-padded tail)
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_ONESHOT);
     if (!s_fail) {
-      float* src[XGMI_MAX_RANKS];
+      __amdgpu_buffer_rsrc_t src[XGMI_MAX_RANKS];
 #pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) src[p] = p < N ? a.stage[p] + par1 : nullptr;
-      long i = i0;
-      for (; i + G < a.n; i += 2 * G) {
-        const float s0 = rank_sum(a, src, i, N), s1 = rank_sum(a, src, i + G, N);
-        finish(a, i, s0 * a.scale);
-        finish(a, i + G, s1 * a.scale);
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p) src[p] = sys_rsrc(p < N ? a.stage[p] + par1 : a.stage[r]);
+      long q = q0;
+      for (; q + G < nq; q += 2 * G) {
+        const float4 s0 = rank_sum4(src, q, N), s1 = rank_sum4(src, q + G, N);
+        finish4(a, q, s0, n);
+        finish4(a, q + G, s1, n);
       }
-      if (i < a.n) finish(a, i, rank_sum(a, src, i, N) * a.scale);
+      if (q < nq) finish4(a, q, rank_sum4(src, q, N), n);
     }
     if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
     return;
   }
-  const long slice = a.slice;  // elements per rank slice (the last rank's may be shorter)
+  const long slice = a.slice;  // elements per rank slice, a multiple of 4 (the last rank's may be shorter)
+  const long sq = slice / 4;
   const long par = (long)(e & 1u) * slice;
   if (a.publish) {
-    // the peers' block b reads element i of every slice of my bucket for exactly this
-    // block's i: make those elements system-visible (write-through) before arriving
+    // the peers' block b reads quad q of every slice of my bucket for exactly this
+    // block's q: make those elements system-visible (write-through) before arriving.
+    // Slice-relative quads, the same thread <-> quad map as RS / AG below: the AG's
+    // reduced value must land after (program order) this re-store of the local value.
     float* mine = a.data[r] + a.off;
+    const __amdgpu_buffer_rsrc_t rm = sys_rsrc(mine);
     for (int p = 0; p < N; ++p) {
       const long lim = min(slice, a.n - (long)p * slice);
-      for (long i = i0; i < lim; i += G) st_sys(mine + (long)p * slice + i, mine[(long)p * slice + i]);
+      for (long q = q0; 4 * q < lim; q += G) {
+        const long k = (long)p * slice + 4 * q;
+        if (4 * q + 3 < lim) {
+          st4_sys(rm, k / 4, make_float4(mine[k], mine[k + 1], mine[k + 2], mine[k + 3]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (4 * q + j < lim) st_sys(mine + k + j, mine[k + j]);
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_B0);  // B0
   if (!s_fail) {
-    // ---- RS: elements of my slice, fixed-order sum over ranks 0..N-1
-    float* src[XGMI_MAX_RANKS];
+    // ---- RS: quads of my slice, fixed-order sum over ranks 0..N-1
+    float* srcp[XGMI_MAX_RANKS];
+    __amdgpu_buffer_rsrc_t src[XGMI_MAX_RANKS];
 #pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p) src[p] = p < N ? a.data[p] + a.off + (long)r * slice : nullptr;
-    const long lim = min(slice, a.n - (long)r * slice);  // my slice's real length
-    long i = i0;
-    for (; i + G < lim; i += 2 * G) {
-      const float s0 = rank_sum(a, src, i, N), s1 = rank_sum(a, src, i + G, N);
-      st_sys(a.stage[r] + par + i, s0);
-      st_sys(a.stage[r] + par + i + G, s1);
+    for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
+      srcp[p] = (p < N ? a.data[p] : a.data[r]) + a.off + (long)r * slice;
+      src[p] = sys_rsrc(srcp[p]);
     }
-    if (i < lim) st_sys(a.stage[r] + par + i, rank_sum(a, src, i, N));
+    const long lim = min(slice, a.n - (long)r * slice);  // my slice's real length (may be <= 0)
+    const long fq = lim > 0 ? lim / 4 : 0, nq = lim > 0 ? (lim + 3) / 4 : 0;
+    const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par);
+    long q = q0;
+    for (; q + G < fq; q += 2 * G) {
+      const float4 s0 = rank_sum4(src, q, N), s1 = rank_sum4(src, q + G, N);
+      st4_sys(mystage, q, s0);
+      st4_sys(mystage, q + G, s1);
+    }
+    for (; q < nq; q += G) st4_sys(mystage, q, q < fq ? rank_sum4(src, q, N) : rank_sum_tail(srcp, q, lim, N));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   xgmi_barrier(a, 2u * e + 1u, &s_fail, XGMI_PHASE_B1);  // B1
   if (!s_fail) {
-    // ---- AG: element i of every rank's reduced slice into my gradient buffer
-    for (long i = i0; i < slice; i += G) {
-      float v[XGMI_MAX_RANKS];
+    // ---- AG: quad q of every rank's reduced slice into my gradient buffer
+    __amdgpu_buffer_rsrc_t st[XGMI_MAX_RANKS];
+#pragma unroll
+    for (int p = 0; p < XGMI_MAX_RANKS; ++p) st[p] = sys_rsrc((p < N ? a.stage[p] : a.stage[r]) + par);
+    for (long q = q0; q < sq; q += G) {
+      float4 v[XGMI_MAX_RANKS];
 #pragma unroll
       for (int p = 0; p < XGMI_MAX_RANKS; ++p)
-        v[p] = (p < N && (long)p * slice + i < a.n) ? ld_sys(a.stage[p] + par + i) : 0.f;
+        v[p] = (p < N && (long)p * slice + 4 * q < a.n) ? ld4_sys(st[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
-        const long k = (long)p * slice + i;
-        if (p < N && k < a.n) finish(a, k, v[p] * a.scale);
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p)
+        if (p < N && (long)p * slice + 4 * q < a.n) store4(a, (long)p * sq + q, scale4(a, v[p]), a.n);
+      if (a.sgd.update) {
+        // the optimizer per peer slice from the quads just stored (this thread's own
+        // plain stores: coherent), keeping one copy of the SGD + shadow code
+#pragma unroll 1
+        for (int p = 0; p < N; ++p) {
+          const long qq = (long)p * sq + q;
+          if (4 * qq >= a.n) break;
+          const float* d = a.data[r] + a.off + 4 * qq;
+          float t[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) t[j] = 4 * qq + j < a.n ? d[j] : 0.f;
+          sgd4(a, qq, make_float4(t[0], t[1], t[2], t[3]), a.n);
+        }
       }
     }
   }
   if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
 }
 
+long xgmi_slice(long n, int world) { return (((n + world - 1) / world) + 3) & ~3L; }
+
 int xgmi_blocks(long n, int world, bool oneshot) {
-  const long slice = oneshot ? n : (n + world - 1) / world;
-  long b = (slice + XGMI_THREADS - 1) / XGMI_THREADS;
+  const long quads = ((oneshot ? n : xgmi_slice(n, world)) + 3) / 4;
+  long b = (quads + XGMI_THREADS - 1) / XGMI_THREADS;
   if (b > XGMI_GRID_CAP) b = XGMI_GRID_CAP;
   return (int)(b < 1 ? 1 : b);
 }

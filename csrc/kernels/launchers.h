@@ -345,7 +345,7 @@ struct XgmiArgs {
   float* data[XGMI_MAX_RANKS];    // every rank's gradient buffer (peer-mapped; [rank] = own)
   float* stage[XGMI_MAX_RANKS];   // every rank's stage buffer, 2 x slice floats (one-shot: 2 x n)
   unsigned* sig[XGMI_MAX_RANKS];  // every rank's signal words (uncached)
-  long off, n, slice;             // bucket offset / length in the gradient buffer; n / world rounded up
+  long off, n, slice;             // bucket offset / length in the gradient buffer; xgmi_slice(n, world)
   int oneshot;                    // 1: publish whole bucket, one barrier, every rank sums all (small buckets)
   int publish;                    // two-shot: re-store my bucket system-scope before B0 (producers used
                                   // plain stores, e.g. autograd kernels in the module path)
@@ -362,6 +362,7 @@ struct XgmiArgs {
   ShadowSet sh;
   int* step_ctr;  // += 1 by block 0 at the end (the step's last kernel), may be null
 };
+long xgmi_slice(long n, int world);  // two-shot slice: n / world rounded up to whole quads
 int xgmi_blocks(long n, int world, bool oneshot = false);
 void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s);
 

@@ -70,7 +70,11 @@ class XgmiComm {
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
-  int add_channel(long off, long n, bool oneshot = false);
+  // grid_cap: most blocks for this channel's kernel (0: XGMI_GRID_CAP); a channel whose
+  // all-reduce overlaps compute keeps its spinning grid small
+  int add_channel(long off, long n, bool oneshot = false, int grid_cap = 0);
+  int blocks(int channel) const { return ch_.at(channel).blocks; }
+  std::string bus_id() const;  // PCI bus id of the device (ranks sharing a GPU compare these)
   bool oneshot(int channel) const { return ch_.at(channel).oneshot; }
   void set_data(float* data, long numel);
   std::string export_handles() const;

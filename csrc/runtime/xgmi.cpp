@@ -45,19 +45,21 @@ XgmiComm::~XgmiComm() {
   }
 }
 
-int XgmiComm::add_channel(long off, long n, bool oneshot) {
+int XgmiComm::add_channel(long off, long n, bool oneshot, int grid_cap) {
   if (imported_) throw std::runtime_error("xgmi: add channels before import_handles");
   Channel c;
   c.off = off;
   c.n = n;
   c.oneshot = oneshot;
-  c.slice = (n + world_ - 1) / world_;
+  c.slice = xgmi_slice(n, world_);
   c.blocks = xgmi_blocks(n, world_, oneshot);
+  if (grid_cap > 0) c.blocks = std::min(c.blocks, grid_cap);
   // and a smaller grid, so the ranks' spinning blocks leave CUs to the others' kernels
   // (the kernel is block-strided; every rank must see the same value)
   if (const char* e = std::getenv("DDP_AMD_XGMI_GRID_CAP")) c.blocks = std::max(1, std::min(c.blocks, std::atoi(e)));
   if (c.blocks > XGMI_MAX_BLOCKS) throw std::runtime_error("xgmi: bucket too large for one channel");
-  const long stage = oneshot ? n : c.slice;  // per parity
+  if (n * 4 >= (1L << 31)) throw std::runtime_error("xgmi: bucket over 2 GiB (32-bit buffer offsets)");
+  const long stage = oneshot ? (n + 3) & ~3L : c.slice;  // per parity, whole quads
   DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&c.stage_local), sizeof(float) * 2 * stage));
   DDP_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c.sig_local),
                                       sizeof(unsigned) * XGMI_SIG_WORDS, hipDeviceMallocUncached));
@@ -78,6 +80,12 @@ void XgmiComm::set_data(float* data, long numel) {
   DDP_HIP_CHECK(hipMemGetAddressRange(&base, &size, data));
   data_base_ = reinterpret_cast<char*>(base);
   data_off_ = reinterpret_cast<char*>(data) - data_base_;
+}
+
+std::string XgmiComm::bus_id() const {
+  char buf[64] = {0};
+  DDP_HIP_CHECK(hipDeviceGetPCIBusId(buf, sizeof(buf) - 1, device_));
+  return std::string(buf);
 }
 
 std::string XgmiComm::export_handles() const {

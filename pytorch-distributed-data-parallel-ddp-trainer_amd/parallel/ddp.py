@@ -106,7 +106,7 @@ class _NativeReducer:
         self.kind = "rccl"
         self.xgmi = None
         if comm == "xgmi":
-            from .xgmi import channel_plan, create_xgmi
+            from .xgmi import MODULE_GRID_CAP, channel_plan, create_xgmi
 
             from .bucket_model import XgmiCost
 
@@ -114,8 +114,9 @@ class _NativeReducer:
             # model's crossover for this world size
             lim = XgmiCost(dist.get_world_size()).oneshot_max_elems()
             oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
+            # the bucket kernels run next to the backward: small spinning grid
             self.xgmi = create_xgmi(fs.grads, ranges, dist.get_rank(), dist.get_world_size(),
-                                    oneshot=oneshot)
+                                    oneshot=oneshot, grid_cap=MODULE_GRID_CAP)
             if self.xgmi is None and not rccl:
                 raise RuntimeError("xGMI self-test failed and the gloo group has no RCCL plane")
             if self.xgmi is not None:

@@ -40,8 +40,28 @@ def _pattern(n: int, rank: int, device) -> torch.Tensor:
     return (((i * 7 + rank * 13) % 101).to(torch.float32) * 0.25 - 12.0)
 
 
+# Grid of one bucket kernel.  The kernel spins in its cross-GPU barriers with one block
+# per CU it occupies, and a spinning block pins registers a full-width compute block would
+# need: an all-reduce that overlaps the backward (the module reducer) keeps a small grid
+# (MODULE_GRID_CAP: 2 x 16 B quads x 8 ranks per lane still keep ~2 MB in flight), one
+# that runs alone (the fused engine's, after the conv backward) may take the whole chip.
+ENGINE_GRID_CAP = 256
+MODULE_GRID_CAP = 32
+# Ranks sharing one GPU (same-GPU rehearsals): every rank's spinning grid must leave room
+# for the others' compute kernels, or a rank that has not reached the all-reduce yet can
+# never get its producers onto a CU (a cross-process deadlock until the barrier timeout).
+SHARED_GPU_CUS = 64
+
+
+def grid_cap_for(requested: int, ranks_on_device: int) -> int:
+    """Blocks per bucket kernel for ``requested`` and the number of ranks on this GPU."""
+    if ranks_on_device > 1:
+        return max(4, min(requested, SHARED_GPU_CUS // ranks_on_device))
+    return requested
+
+
 def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
-                self_test: bool = True, verbose: bool = True, oneshot=()):
+                self_test: bool = True, verbose: bool = True, oneshot=(), grid_cap: int = ENGINE_GRID_CAP):
     """Build an XgmiComm over ``grads`` (flat fp32, CUDA), or return ``None`` when the direct
     path is unusable here.
 
@@ -60,8 +80,12 @@ def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
     x = None
     try:
         x = C.XgmiComm(rank, world, grads.device.index)
+        bus = x.bus_id()
+        store.set(f"{key}/bus/{rank}", bus.encode())
+        shared = sum(store.get(f"{key}/bus/{r}").decode() == bus for r in range(world))
+        cap = grid_cap_for(grid_cap, shared)
         for off, n, one in chans:
-            x.add_channel(off, n, one)
+            x.add_channel(off, n, one, cap)
         x.set_data(grads)
         store.set(f"{key}/h/{rank}", x.export_handles())
         blobs = [store.get(f"{key}/h/{r}") for r in range(world)]

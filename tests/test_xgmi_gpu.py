@@ -31,12 +31,16 @@ def _allreduce_worker(rank, world, port, q):
         _init(rank, world, port)
         from ddp_amd.parallel import create_xgmi
 
-        n_total = 501_770 + 18_816 + 64
-        buckets = [(0, 501_770), (501_770, 18_816)]
+        # odd lengths and offsets: 16-byte quads with partial tails, unaligned bases; the
+        # third bucket (10 elements at an odd offset, like fl.bias) leaves rank 1 a 2-element slice
+        n_total = 501_770 + 18_816 + 1 + 10 + 64
+        buckets = [(0, 501_770), (501_770, 18_816), (520_587, 10)]
         grads = torch.zeros(n_total, device="cuda")
-        x = create_xgmi(grads, buckets, rank, world, oneshot=(1,))  # channel 2: one-shot bucket 1
+        x = create_xgmi(grads, buckets, rank, world, oneshot=(1,))  # channel 3: one-shot bucket 1
         assert x is not None, "self-test failed"
-        assert x.channels == 3 and x.oneshot(2) and not x.oneshot(1)
+        assert x.channels == 4 and x.oneshot(3) and not x.oneshot(1)
+        # two ranks on one GPU: every spinning grid leaves room for the other's kernels
+        assert max(x.blocks(c) for c in range(4)) <= 32
         for it in range(4):
             g = torch.Generator().manual_seed(1000 * it + rank)
             mine = torch.randn(n_total, generator=g)
@@ -44,6 +48,7 @@ def _allreduce_worker(rank, world, port, q):
             torch.cuda.synchronize()
             x.all_reduce(0)
             x.all_reduce(1, scale=0.5)
+            x.all_reduce(2)
             torch.cuda.synchronize()
             assert x.error_flags() == 0
             allin = [None] * world
@@ -52,15 +57,18 @@ def _allreduce_worker(rank, world, port, q):
             for r in range(1, world):
                 want += allin[r]  # the kernel's fixed rank order, fp32
             got = grads.cpu()
-            b0, b1 = buckets
+            b0, b1 = buckets[:2]
             assert torch.equal(got[:b0[1]], want[:b0[1]]), f"bucket 0 it {it}"
             s1 = slice(b1[0], b1[0] + b1[1])
             assert torch.equal(got[s1], want[s1] * 0.5), f"bucket 1 it {it}"
-            assert torch.equal(got[b1[0] + b1[1]:], mine[b1[0] + b1[1]:]), "outside the buckets"
+            b2 = buckets[2]
+            assert torch.equal(got[b2[0]:b2[0] + b2[1]], want[b2[0]:b2[0] + b2[1]]), f"bucket 2 it {it}"
+            assert got[b1[0] + b1[1]] == mine[b1[0] + b1[1]], "gap between buckets touched"
+            assert torch.equal(got[b2[0] + b2[1]:], mine[b2[0] + b2[1]:]), "outside the buckets"
             # the one-shot channel over bucket 1: same bits as the two-shot one
             grads.copy_(mine.cuda())
             torch.cuda.synchronize()
-            x.all_reduce(2, scale=0.5)
+            x.all_reduce(3, scale=0.5)
             torch.cuda.synchronize()
             assert x.error_flags() == 0
             got1 = grads.cpu()
