@@ -14,6 +14,7 @@
 // 128-pixel column tile of which R*W are live), same epilogues: bf16 NHWC store with the
 // per-block BatchNorm sum / sum-of-squares partials, or fp32 split-K partials for
 // splitk_reduce.  K splits run over channel chunks (grid.z).
+#include "kernels/bn_tail.h"
 #include "kernels/common.h"
 #include "kernels/launchers.h"
 
@@ -30,7 +31,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
                                                                  bf16_t* __restrict__ Y,
                                                                  float* __restrict__ stats,
                                                                  float* __restrict__ part, int R,
-                                                                 int chunks_per_split) {
+                                                                 int chunks_per_split, BnFin fin) {
   constexpr int TCO = BC / 32, TPX = BP / 32;
   constexpr int HCH = (HL_MAXPX * 4 + 255) / 256;  // 16-B halo chunks per thread
   // weights of one kernel row (3 taps) per K-step: 3 MFMA K-steps between barriers
@@ -202,9 +203,11 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
     __syncthreads();
     for (int c = tid; c < BC; c += 256) {
       float* dst = stats + (long)bk.x * 2 * g.Cout;
-      dst[co0 + c] = s_st[0][0][c] + s_st[1][0][c];
-      dst[g.Cout + co0 + c] = s_st[0][1][c] + s_st[1][1][c];
+      st_wt(dst + co0 + c, s_st[0][0][c] + s_st[1][0][c]);
+      st_wt(dst + g.Cout + co0 + c, s_st[0][1][c] + s_st[1][1][c]);
     }
+    // (the halo buffers are dead too: the BatchNorm tail's LDS)
+    if (fin.tickets) bn_stats_tail(fin, stats, bk.x, bk.y, co0, BC, reinterpret_cast<float*>(&sH[0][0]));
   }
 }
 
@@ -406,13 +409,14 @@ bool conv_halo_fits(const ConvGeom& g, int bp) {
 int conv_halo_rows(const ConvGeom& g, int bp) { return bp / g.W; }
 
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
-                   bf16_t* Y, float* stats, float* part, hipStream_t s) {
+                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin) {
+  const BnFin f = (fin && stats && splits <= 1) ? *fin : BnFin{};
   const int R = conv_halo_rows(g, bp);
   const int RG = (g.H + R - 1) / R;
   const int nch = g.Cin / HL_KS;
   const int cps = (nch + splits - 1) / splits;
   const dim3 grid(g.N * RG, g.Cout / bc, splits);
-#define HLF(BC, BP, ST, PT) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps)
+#define HLF(BC, BP, ST, PT) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f)
 #define HLF_BP(BC, BP)                                  \
   if (splits > 1) HLF(BC, BP, false, true);             \
   else if (stats) HLF(BC, BP, true, false);             \

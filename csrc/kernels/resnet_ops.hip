@@ -14,6 +14,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "kernels/bn_tail.h"
 #include "kernels/common.h"
 #include "kernels/launchers.h"
 
@@ -26,29 +27,7 @@
 namespace ddp_amd {
 
 // ---------------------------------------------------------------- last-arrival reductions
-// A strip of blocks reduces into per-block partials; the block that takes the strip's
-// last ticket sums the partials in FIXED order (deterministic, no float atomics) and
-// resets the ticket for the next launch.  Cross-XCD visibility without fences: an
-// agent-scope release fence writes back the XCD's whole L2 (measured: ~30 us per
-// reduction at 400 blocks), so the partials are stored write-through (agent-scope
-// atomic stores, st_wt) and drained (vmcnt(0)) before the relaxed ticket increment,
-// and the last block reads them with agent-scope atomic loads.
-__device__ __forceinline__ float ld_agent(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool last_arrival(int* ticket, int expected, int* s_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's st_wt partials are out
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == expected - 1;
-    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_flag = last;
-  }
-  __syncthreads();
-  return *s_flag != 0;
-}
+// (ld_agent / last_arrival: kernels/bn_tail.h)
 
 // ---------------------------------------------------------------- BatchNorm
 // stats slab [rows][2][C] -> mean / invstd (+ running stats with torch's semantics:
@@ -190,7 +169,23 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 // groups (64 channels) x 32 pixel lanes over `rpb` pixels -> ws[y]; the strip's last
 // block sums ws[0..R) in fixed order into sums[2C] = [sum dy | sum dy*xhat] and the
 // affine gradients (dbeta = sum dy, dgamma = sum dy*xhat; `accum` adds to them).
-template <bool RELU>
+//
+// FUSED (one launch per BatchNorm backward): every block then waits for its strip's
+// finished sums (the last block raises the strip flag) and applies pass 2 to the same
+// pixels it reduced - they are still in L2 / MALL.  Needs the whole grid co-resident
+// (the launcher checks the occupancy); the wait is bounded (err word) and a second
+// arrival count re-arms the flag for the next launch / graph replay.
+struct BnBwdFused {
+  const float* gamma = nullptr;
+  float count = 1.f;
+  bf16_t* dx = nullptr;
+  bf16_t* dres = nullptr;
+  int* flags = nullptr;  // [strips] strip flags, then [strips] second-arrival tickets (zero)
+  int* err = nullptr;    // set to 1 when a wait times out
+};
+constexpr unsigned long long BN_WAIT_TICKS = 20000000;  // 200 ms of the 100 MHz clock
+
+template <bool RELU, bool FUSED>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
                                                             const bf16_t* __restrict__ dout2,
                                                             const bf16_t* __restrict__ out,
@@ -200,7 +195,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             float* __restrict__ ws, int* __restrict__ tickets,
                                                             float* __restrict__ sums,
                                                             float* __restrict__ dgamma,
-                                                            float* __restrict__ dbeta, int accum) {
+                                                            float* __restrict__ dbeta, int accum,
+                                                            BnBwdFused fz) {
   __shared__ float sred[32][2][64];
   __shared__ float sfin[8][128];
   __shared__ int s_last;
@@ -265,7 +261,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     for (int t = 0; t < 32; ++t) a += sred[t][which][cc];
     st_wt(ws + ((long)blockIdx.y * 2 + which) * C + cb + cc, a);
   }
-  if (!last_arrival(&tickets[blockIdx.x], R, &s_last)) return;
+  const bool last = last_arrival(&tickets[blockIdx.x], R, &s_last);
+  if (!FUSED && !last) return;
+  if (last) {
   // Fixed-order sum of the R partial rows: thread = 4 of the strip's 128 values (float4)
   // x one of 8 row phases, up to 8 rows in flight.  Plain loads are coherent here: the
   // rows were stored write-through and no block of this kernel read them before.
@@ -297,10 +295,74 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 #pragma unroll
     for (int k = 1; k < 8; ++k) tot += sfin[k][v];
     const int c = cb + cc;
-    sums[which * C + c] = tot;
+    if (FUSED) st_wt(sums + which * C + c, tot);
+    else sums[which * C + c] = tot;
     float* dst = which ? dgamma : dbeta;
     if (dst) dst[c] = accum ? dst[c] + tot : tot;
   }
+  }  // last
+  if (!FUSED) return;
+  // ---- pass 2 on this block's pixels, after the strip's sums are published
+  int* flag = fz.flags + blockIdx.x;
+  if (last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the st_wt sums are out
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (threadIdx.x < 64) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > BN_WAIT_TICKS) {
+        if (threadIdx.x == 0) __hip_atomic_store(fz.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  {
+    float k[8], sd[8], sq[8];
+    ld8f(fz.gamma + c0, k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k[j] = k[j] * is[j] / fz.count;
+      sd[j] = ld_agent(sums + c0 + j);
+      sq[j] = ld_agent(sums + C + c0 + j);
+    }
+    auto apply8 = [&](long o, bf16x8 gd, bf16x8 gx, bf16x8 go) {
+      float d[8], xv[8], ov[8], r[8];
+      unpack8_sum(gd, dout2, o, d);
+      unpack8(gx, xv);
+      if (RELU) unpack8(go, ov);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
+        const float xh = (xv[j] - mu[j]) * is[j];
+        r[j] = k[j] * (fz.count * d[j] - sd[j] - xh * sq[j]);
+      }
+      *reinterpret_cast<uint4*>(fz.dx + o) = pack8(r);
+      if (fz.dres) *reinterpret_cast<uint4*>(fz.dres + o) = pack8(d);
+    };
+    int pp = p0 + tp;
+    for (; pp + 96 < p1; pp += 128) {  // four pixels' loads in flight (one block per CU here)
+      bf16x8 d[4], xx[4], r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long o = (long)(pp + 32 * u) * C + c0;
+        d[u] = ld8(dout + o);
+        xx[u] = ld8(x + o);
+        r[u] = RELU ? ld8(out + o) : zero8();
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) apply8((long)(pp + 32 * u) * C + c0, d[u], xx[u], r[u]);
+    }
+    for (; pp < p1; pp += 32) {
+      const long o = (long)pp * C + c0;
+      apply8(o, ld8(dout + o), ld8(x + o), RELU ? ld8(out + o) : zero8());
+    }
+  }
+  // re-arm: the strip's last block through here lowers the flag
+  if (last_arrival(fz.flags + gridDim.x + blockIdx.x, R, &s_last) && threadIdx.x == 0)
+    __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Backward pass 2: dx = gamma*invstd/count * (count*dy - sum_dy - xhat*sum_dyxh); also
@@ -664,7 +726,9 @@ static unsigned grid_for(long n, int per_thread = 1) {
 
 // Ticket words for last_arrival: one zeroed pool per device, handed out round-robin
 // (every kernel resets the tickets it used, so a slot is clean when it comes round).
-static int* ticket_slots(int n) {
+int bn_tail_groups(int rows) { return (rows + BN_TAIL_GROUP - 1) / BN_TAIL_GROUP; }
+
+int* bn_ticket_slots(int n) {
   constexpr int kSlots = 1 << 16;
   static int* pool[64] = {};
   static int next[64] = {};
@@ -693,7 +757,7 @@ void bn_finalize(const float* slab, int rows, int C, float count, float eps, flo
   const int strips = (C + 63) / 64, G = bn_finalize_groups(rows);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(strips, G), dim3(256), 0, s, slab, rows, C, count, eps,
                      momentum, running_mean, running_var, save_mean, save_invstd, nbt, ws,
-                     ticket_slots(strips));
+                     bn_ticket_slots(strips));
 }
 
 void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* invstd,
@@ -725,6 +789,58 @@ int bn_bwd_rows(long P, int C, int* rpb) {
   return (int)((P + r - 1) / r);
 }
 
+// Single-launch backward (FUSED): used when enabled (bn_bwd_set_fused(1)) and the whole
+// grid fits half the device's resident capacity for the kernel (occupancy x CUs).  Off by
+// default: measured slower than the two launches at every ResNet-18 layer (B=32: 14.4 vs
+// 13.6 us at 7x7x512, 40.6 vs 30.8 us at 56x56x64 - its pass 2 runs on the reduce grid's
+// few fat blocks, profiles/r3_bn_fusion).
+static int g_bn_bwd_fused = 0;
+void bn_bwd_set_fused(int on) { g_bn_bwd_fused = on; }
+
+static int* bn_err_word() {
+  static int* w[64] = {};
+  int dev = 0;
+  RN_CHECK(hipGetDevice(&dev));
+  dev &= 63;
+  if (!w[dev]) {
+    RN_CHECK(hipMalloc(reinterpret_cast<void**>(&w[dev]), sizeof(int)));
+    RN_CHECK(hipMemset(w[dev], 0, sizeof(int)));
+    RN_CHECK(hipDeviceSynchronize());
+  }
+  return w[dev];
+}
+
+int bn_bwd_fused_error(bool reset) {
+  int* w = bn_err_word();
+  int v = 0;
+  RN_CHECK(hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost));
+  if (reset && v) RN_CHECK(hipMemset(w, 0, sizeof(int)));
+  return v;
+}
+
+template <bool RELU>
+static long bn_bwd_fused_capacity() {
+  static long cap[64] = {};
+  int dev = 0;
+  RN_CHECK(hipGetDevice(&dev));
+  dev &= 63;
+  if (!cap[dev]) {
+    int per_cu = 0, cus = 0;
+    RN_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bn_bwd_reduce_kernel<RELU, true>, 256, 0));
+    RN_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cap[dev] = (long)per_cu * cus;
+    if (cap[dev] <= 0) cap[dev] = -1;
+  }
+  return cap[dev];
+}
+
+bool bn_bwd_fused_ok(long P, int C, bool relu) {
+  if (!g_bn_bwd_fused) return false;
+  const long blocks = (long)(C / 64) * bn_bwd_rows(P, C, nullptr);
+  // half the resident capacity: other streams' kernels (bucket all-reduces) may hold CUs
+  return blocks <= (relu ? bn_bwd_fused_capacity<true>() : bn_bwd_fused_capacity<false>()) / 2;
+}
+
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,
             float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s,
@@ -732,11 +848,25 @@ void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int 
   int rpb = 0;
   const int R = bn_bwd_rows(P, C, &rpb);
   const dim3 grid(C / 64, R);
-  int* tk = ticket_slots(C / 64);
+  int* tk = bn_ticket_slots(C / 64);
+  BnBwdFused fz;
+  if (bn_bwd_fused_ok(P, C, out != nullptr)) {
+    fz.gamma = gamma;
+    fz.count = count;
+    fz.dx = dx;
+    fz.dres = dres;
+    fz.flags = bn_ticket_slots(2 * (C / 64));
+    fz.err = bn_err_word();
+    if (out)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
+    return;
+  }
   if (out)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
   const unsigned g = grid_for(P * C, 8);
   if (out)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
@@ -779,7 +909,7 @@ bool xent_wave_rows(const float* logits, int C, int B, const long long* labels, 
   dev &= 63;
   if (!wsp[dev]) RN_CHECK(hipMalloc(reinterpret_cast<void**>(&wsp[dev]), sizeof(float) * kMaxB));
   hipLaunchKernelGGL(xent_wave_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, s, logits, C, B, labels,
-                     dlogits, loss_out, wsp[dev], ticket_slots(1), gscale);
+                     dlogits, loss_out, wsp[dev], bn_ticket_slots(1), gscale);
   return true;
 }
 

@@ -29,16 +29,34 @@ by the reducing kernel when allowed (:mod:`.direct_grad`), otherwise returned.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import native
 from . import direct_grad
 
 BF16 = torch.bfloat16
+# Opt-in launch-count reductions of the BatchNorm (measured SLOWER on MI355X, so off by
+# default - profiles/r3_bn_fusion): DDP_AMD_BN_TAIL=1 finalises the statistics inside the
+# stats-producing conv launch (kernels/bn_tail.h; -20 bn_finalize launches, but every
+# producer block then pays a write-through drain + ticket round trip while holding its CU:
+# 13.7k vs 14.2k img/s); DDP_AMD_BN_BWD_FUSED=1 runs the BatchNorm backward as one launch
+# (resnet_ops.hip FUSED; pass 2 after an in-launch strip wait: 13.7k vs 14.2k img/s).
+BN_TAIL = os.environ.get("DDP_AMD_BN_TAIL", "0") == "1"
+
+
+_configured = False
 
 
 def _C():
-    return native.require()
+    global _configured
+    C = native.require()
+    if not _configured:
+        # one-launch BatchNorm backward (resnet_ops.hip FUSED): opt-in, see BN_TAIL above
+        C.bn_bwd_set_fused(1 if os.environ.get("DDP_AMD_BN_BWD_FUSED", "0") == "1" else 0)
+        _configured = True
+    return C
 
 
 def to_nhwc4(x: torch.Tensor) -> torch.Tensor:
@@ -112,16 +130,23 @@ class _ConvBNAct(torch.autograd.Function):
         _, _, splits, rows, _, _ = C.conv_gemm_plan(x, y, KH, KW, stride, pad)
         part = torch.empty(splits * P * Cout, device=x.device) if splits > 1 else None
         stats = torch.empty(rows, 2, Cout, device=x.device) if training else None
-        C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part)
         if training:
             mean = torch.empty(Cout, device=x.device)
             invstd = torch.empty(Cout, device=x.device)
-            ws = torch.empty(C.bn_finalize_groups(rows), 2, Cout, device=x.device)
-            C.bn_finalize(stats, rows, Cout, float(P), eps, momentum, running_mean, running_var,
-                          mean, invstd, nbt, ws)
+        if training and BN_TAIL:
+            # the stats-producing launch finalises the BatchNorm itself (no bn_finalize)
+            ws = torch.empty(C.bn_tail_groups(rows), 2, Cout, device=x.device)
+            C.conv_bn_fwd(x, wk, y, KH, KW, stride, pad, stats, part, ws, float(P), eps, momentum,
+                          running_mean, running_var, mean, invstd, nbt)
         else:
-            mean = running_mean.float().contiguous()
-            invstd = torch.rsqrt(running_var.float() + eps).contiguous()
+            C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part)
+            if training:
+                ws = torch.empty(C.bn_finalize_groups(rows), 2, Cout, device=x.device)
+                C.bn_finalize(stats, rows, Cout, float(P), eps, momentum, running_mean, running_var,
+                              mean, invstd, nbt, ws)
+            else:
+                mean = running_mean.float().contiguous()
+                invstd = torch.rsqrt(running_var.float() + eps).contiguous()
         out = torch.empty_like(y)
         C.bn_apply(y, mean, invstd, gamma.detach(), beta.detach(),
                    res.contiguous() if res is not None else None, bool(relu), out)
