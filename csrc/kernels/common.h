@@ -33,6 +33,14 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;  // v_dot2c_f32_bf16
 
 constexpr int WAVE = 64;
 
+// Block barrier that orders LDS only: each wave waits for its own LDS (and scalar-memory)
+// operations, then s_barrier.  HIP's __syncthreads() also drains vmcnt, i.e. waits for the
+// wave's outstanding GLOBAL loads and stores - a prefetch meant to land during the next
+// phase, or write-through stores nobody in the block reads, would be waited for.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ---- diagnostic in-kernel phase stamps (scripts/stamps.py) ---------------------------
 // Each kernel TU has its own device pointer (set by stamps_set(); null in normal runs,
 // so a stamp costs one scalar load + branch).  DDP_STAMP(kid, slot) makes lane 0 of the

@@ -285,7 +285,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
           wv[pt][t][o] = *reinterpret_cast<const uint2*>(
               wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
   }
-  __syncthreads();
+  // LDS-only barrier: the fc weight prefetch stays in flight through the MFMA loop
+  // (__syncthreads drained it here: ~2 us per block, stamps s5 -> s2)
+  lds_barrier();
   DDP_STAMP(STAMP_K_CONV_FWD, 2);
   if (A1X && !F32 && c1.a1_out) {
     // the block's own a1 rows (LDS rows W+1 .. W+CH) -> a1_out, 16 bytes per thread-step
@@ -392,7 +394,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   }
   DDP_STAMP(STAMP_K_CONV_FWD, 6);
   if (NOF > 0) {
-    __syncthreads();
+    lds_barrier();  // (the a2 write-through stores need not land before the tile sums)
     // per (image slot, class): fixed-order sum over the block's tiles of that image and
     // the 4 channel groups.  Slot 0 = the image of the block's first pixel, slot 1 = the
     // next one (a block of 64*PXT <= HW pixels spans at most two images).
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     DDP_STAMP(STAMP_K_FWD_DZ, 3);
     // dZ2 = relu2'(a2) * sum_o dL[o] W[o][p][c], in fc_bwd's order (o = 0..9, fma from 0)
 #pragma unroll
@@ -660,7 +662,7 @@ __device__ __forceinline__ void dgrad_body(
       }
     }
   }
-  __syncthreads();
+  lds_barrier();  // (the mask prefetch above stays in flight through the MFMA loop)
   DDP_STAMP(STAMP_K_DGRAD, 1);
 
   f32x4 acc[PXT][2];
