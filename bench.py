@@ -157,6 +157,9 @@ def main():
                     help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch on "
                          "persistent blocks after every conv block (1) or right after the dgrad blocks (2), "
                          "or as its own kernel between forward and conv backward (0)")
+    ap.add_argument("--fuse_reduce", type=int, default=None, choices=[0, 1, 2],
+                    help="slab reduction in the conv backward: 2 = reducer budget the whole resident "
+                         "capacity when single-process (default), 1 = half, 0 = separate kernel")
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")
@@ -272,7 +275,8 @@ def main():
                            bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
                            bucket_plan=args.bucket_plan)
         eo.comm = args.comm
-        for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role"):
+        for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role",
+                  "fuse_reduce"):
             if getattr(args, f) is not None and not (dtype == "fp32" and f in ("fuse_level", "store_a1")):
                 setattr(eo, f, getattr(args, f))
         if dtype == "fp32":

@@ -878,7 +878,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_opt = cfgd.contains("fuse_opt") ? (int)cfgd["fuse_opt"].cast<bool>() : 1;
              c.store_a1 = cfgd.contains("store_a1") ? cfgd["store_a1"].cast<int>() : 0;
              c.f32 = cfgd.contains("f32") ? (int)cfgd["f32"].cast<bool>() : 0;
-             c.fuse_reduce = cfgd.contains("fuse_reduce") ? (int)cfgd["fuse_reduce"].cast<bool>() : 1;
+             c.fuse_reduce = cfgd.contains("fuse_reduce") ? cfgd["fuse_reduce"].cast<int>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
              TORCH_CHECK(c.l3_fc_role >= 0 && c.l3_fc_role <= 2, "engine: l3_fc_role must be 0, 1 or 2");

@@ -1483,15 +1483,20 @@ size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es) {
 // reducers starved the rest of that grid.)  Returns the number of reducers (all the wgrad
 // blocks), 0 when they do not fit (fewer reducers, two passes each, measured slower than
 // the separate grad_reduce kernel: fp32 364k vs 383k img/s) or the capacity is unknown.
+// exclusive (single process, no bucket all-reduce kernel on another stream): the budget is
+// the whole resident capacity - all reducers can then be resident at once, and every other
+// block of the grid runs to completion without waiting, so the argument above holds with
+// nothing else on the GPU.  This lets the exact-fp32 step (one block per CU, 224 wgrad
+// blocks at batch 32) fuse its reduction.
 template <typename K>
-static int fused_reducers(K kernel, size_t lds, int nblocks) {
+static int fused_reducers(K kernel, size_t lds, int nblocks, bool exclusive) {
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), 256, lds) != hipSuccess)
     return 0;
-  const int half = occ * cus / 2;
-  return nblocks <= half ? nblocks : 0;
+  const int budget = exclusive ? occ * cus : occ * cus / 2;
+  return nblocks <= budget ? nblocks : 0;
 }
 
 template <typename T>
@@ -1536,7 +1541,7 @@ template <typename T>
 static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
                        int Cin, int Cout, int pxt, int R, const C1Src& c1, const T* Xact,
                        bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err,
-                       int csplit, const BwdFc* fc) {
+                       int csplit, const BwdFc* fc, bool exclusive) {
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   // the channel split is the bf16 SimpleCNN variant (wgrad_body); otherwise one block per row
   const int cs = (csplit == 2 && g && sizeof(T) == 2) ? 2 : 1;
@@ -1581,7 +1586,7 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     // Residency of the exact instantiation that will run.
     const BwdKFn<T> kf = pick_bwd<T>(pxt, da, wa, g, true, cs, fc != nullptr);
     lds_optin(kf, lds);
-    const int nr = (g && red_done) ? fused_reducers(kf, lds, nrows) : 0;
+    const int nr = (g && red_done) ? fused_reducers(kf, lds, nrows, exclusive) : 0;
     if (nr <= 0) fused = nullptr;  // the caller reduces with grad_reduce
     else red.first_reducer = nd + nw - nr;
   }
@@ -1603,16 +1608,16 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
-                 int wgrad_split, const BwdFc* fc) {
+                 int wgrad_split, const BwdFc* fc, bool exclusive) {
   return bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                     fused_reduce, red_done, red_err, wgrad_split, fc);
+                     fused_reduce, red_done, red_err, wgrad_split, fc, exclusive);
 }
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
-                 int wgrad_split) {
+                 int wgrad_split, bool exclusive) {
   return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                    fused_reduce, red_done, red_err, wgrad_split, nullptr);
+                    fused_reduce, red_done, red_err, wgrad_split, nullptr, exclusive);
 }
 
 int fc_conv_bwd_fc_blocks(long K) { return (int)((K + 64 * FCC_CPL - 1) / (64 * FCC_CPL)); }

@@ -71,7 +71,8 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // blocks reduce the slabs after an in-launch arrival count, red_done: 8 counters 32 ints
 // apart, zeroed beforehand - by the step's forward, C1Src::zero_i32); red_err[0] = 2 if
 // that wait timed out.  SimpleCNN geometry only, and only while the wgrad blocks fit in
-// half the launch's resident capacity; returns whether the reduction was fused (false:
+// half the launch's resident capacity (the whole capacity when `exclusive`: nothing else
+// runs on the GPU meanwhile); returns whether the reduction was fused (false:
 // the caller runs grad_reduce).  wgrad_split == 2 (bf16, SimpleCNN geometry): two wgrad
 // blocks per slab row, one per half of the input channels (bit-identical slabs).
 struct SlabSet;
@@ -82,12 +83,13 @@ constexpr int SYNC_RED_INTS = 256;  // ints of the 8 arrival counters (32 apart)
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
-                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr);
+                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr,
+                 bool exclusive = false);
 bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split);
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
-                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1);
+                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, bool exclusive = false);
 size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false, int es = 2);

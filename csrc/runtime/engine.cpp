@@ -349,7 +349,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                           cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
                           fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
-                          fc_role ? &fcr : nullptr);
+                          fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
   } else {
     conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
                   b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
@@ -488,7 +488,8 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   ss.sys_store = use_x ? 1 : 0;
   const bool reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2,
                                    cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr),
-                                   false, cs_, fred ? &ss : nullptr, b_.sync_flags, b_.sync_err);
+                                   false, cs_, fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, 1,
+                                   !dist && cfg_.fuse_reduce == 2);
   if (!reduced) grad_reduce(ss, cs_);
   last_fused_reduce_ = reduced;
   if (fopt) return;

@@ -231,7 +231,10 @@ struct EngineConfig {
   //    activations), the reference's precision; needs fuse_level 1 and store_a1 0
   int f32 = 0;
   // 1: the conv backward launch also reduces the split-K slabs + fused SGD (no separate
-  //    grad_reduce kernel; level >= 1, needs sync_flags); 0: grad_reduce kernel
+  //    grad_reduce kernel; level >= 1, needs sync_flags) while its reducers fit half the
+  //    launch's resident capacity; 2: the whole capacity when the step has no bucket
+  //    all-reduce on another stream (single process: the exact-fp32 step fuses too);
+  //    0: grad_reduce kernel
   int fuse_reduce = 1;
   // 2: the fused conv backward's wgrad role runs two blocks per slab row, one per half of
   //    conv2's input channels (bf16; bit-identical slabs); 1: one block per row

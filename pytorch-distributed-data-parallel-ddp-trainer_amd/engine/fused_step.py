@@ -75,7 +75,10 @@ class EngineOptions:
     fuse_opt: bool = True
     # level >= 1: the conv backward launch also reduces the split-K weight-gradient slabs
     # (+ fused SGD) after an in-launch arrival count - no separate grad_reduce kernel
-    fuse_reduce: bool = True
+    # 2: slab reduction inside the conv backward, reducer budget = the launch's whole
+    # resident capacity when nothing else runs (single process), else half; 1: half
+    # always; 0: the separate grad_reduce kernel
+    fuse_reduce: int = 2
     # level 1: 0 = the conv backward recomputes conv1 from the compact uint8 batch;
     # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
     # wgrad role reads a1 tiles too.  None = 1 for bf16 (with the wgrad role split over
@@ -250,13 +253,13 @@ class FusedSimpleCNNEngine:
             return 1
         return lvl
 
-    def _fuse_reduce_ok(self, world_size: int) -> bool:
+    def _fuse_reduce_ok(self, world_size: int) -> int:
         """The fused reduction's waiting blocks are sized against ONE launch's share of the
         GPU; ranks that share a device (same-GPU rehearsals: more ranks than devices) each
         hold waiting blocks at once, so they keep the separate grad_reduce kernel."""
         if not self.opts.fuse_reduce:
-            return False
-        return world_size <= 1 or torch.cuda.device_count() >= world_size
+            return 0
+        return int(self.opts.fuse_reduce) if (world_size <= 1 or torch.cuda.device_count() >= world_size) else 0
 
     def sync_from_torch(self):
         """Order the engine stream after work queued on torch's current stream."""

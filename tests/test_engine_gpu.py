@@ -160,7 +160,7 @@ def test_fused_reduce_bitwise_equals_grad_reduce(dtype, B, opt):
     kw = dict(B=B, use_graph=True, momentum=0.9, weight_decay=1e-4, fuse_level=1, fuse_opt=opt,
               store_a1=0, dtype=dtype)
     m1, o1, _, e1, _, _ = _setup(fuse_reduce=False, **kw)
-    m2, o2, _, e2, _, _ = _setup(fuse_reduce=True, **kw)
+    m2, o2, _, e2, _, _ = _setup(fuse_reduce=2, **kw)
     e1.run_steps(11)
     e2.run_steps(11)
     e1.synchronize(); e2.synchronize()
@@ -172,11 +172,10 @@ def test_fused_reduce_bitwise_equals_grad_reduce(dtype, B, opt):
     assert torch.equal(e1.t["step_ctr"], e2.t["step_ctr"])
     assert e2.eng.sync_error == 0
     assert not e1.eng.last_fused_reduce
-    # the wgrad blocks (the reducers) fuse while they fit half the resident capacity: bf16
-    # (2 blocks per CU) up to B = 64 (256 slab rows); fp32 (1 block per CU, 4-row chunks:
-    # 224 slab rows at B = 32) keeps the separate kernel - bitwise either way
-    if dtype == "bf16":
-        assert e2.eng.last_fused_reduce
+    # the wgrad blocks (the reducers) fuse while they fit the resident capacity (single
+    # process: all of it): bf16 (2 blocks per CU) and fp32 (1 block per CU, 4-row chunks:
+    # 224 slab rows at B = 32) - bitwise equal to the separate kernel either way
+    assert e2.eng.last_fused_reduce
     print(f"fused reduce {dtype} B={B}: {e2.eng.last_fused_reduce}")
 
 
