@@ -158,8 +158,8 @@ def main():
                          "persistent blocks after every conv block (1) or right after the dgrad blocks (2), "
                          "or as its own kernel between forward and conv backward (0)")
     ap.add_argument("--fuse_reduce", type=int, default=None, choices=[0, 1, 2],
-                    help="slab reduction in the conv backward: 2 = reducer budget the whole resident "
-                         "capacity when single-process (default), 1 = half, 0 = separate kernel")
+                    help="slab reduction in the conv backward: 1 = reducers within half the resident "
+                         "capacity (default), 2 = the whole capacity when single-process, 0 = separate kernel")
     ap.add_argument("--pxt_fwd", type=int, default=None, help="conv fwd pixel tiles per wave (1|2)")
     ap.add_argument("--pxt_dgrad", type=int, default=None, help="conv dgrad pixel tiles per wave (1|2)")
     ap.add_argument("--wgrad_rows", type=int, default=None, help="conv wgrad image rows per block")

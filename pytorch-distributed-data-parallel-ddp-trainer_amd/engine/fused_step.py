@@ -75,10 +75,12 @@ class EngineOptions:
     fuse_opt: bool = True
     # level >= 1: the conv backward launch also reduces the split-K weight-gradient slabs
     # (+ fused SGD) after an in-launch arrival count - no separate grad_reduce kernel
-    # 2: slab reduction inside the conv backward, reducer budget = the launch's whole
-    # resident capacity when nothing else runs (single process), else half; 1: half
-    # always; 0: the separate grad_reduce kernel
-    fuse_reduce: int = 2
+    # 1: slab reduction inside the conv backward while its reducers fit half the launch's
+    # resident capacity; 2: the whole capacity when nothing else runs (single process) -
+    # lets the exact-fp32 step fuse, measured slower there (385-386k vs 389-391k img/s,
+    # profiles/r3_fp32: its 224 waiting reducers hold the CUs the one-block-per-CU dgrad /
+    # wgrad roles need); 0: the separate grad_reduce kernel
+    fuse_reduce: int = 1
     # level 1: 0 = the conv backward recomputes conv1 from the compact uint8 batch;
     # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
     # wgrad role reads a1 tiles too.  None = 1 for bf16 (with the wgrad role split over
