@@ -157,6 +157,8 @@ def main():
                     help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch on "
                          "persistent blocks after every conv block (1) or right after the dgrad blocks (2), "
                          "or as its own kernel between forward and conv backward (0)")
+    ap.add_argument("--sync_spin", type=int, default=0, choices=[0, 1],
+                    help="1: hipDeviceScheduleSpin (synchronize polls instead of sleeping)")
     ap.add_argument("--fuse_reduce", type=int, default=None, choices=[0, 1, 2],
                     help="slab reduction in the conv backward: 1 = reducers within half the resident "
                          "capacity (default), 2 = the whole capacity when single-process, 0 = separate kernel")
@@ -229,6 +231,11 @@ def main():
     lrank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "gloo":  # rehearsal: several ranks may share the visible GPUs
         lrank %= max(1, torch.cuda.device_count())
+    if args.sync_spin:  # before torch creates the device context
+        rc = native.require().hip_set_device_flags(lrank, 1)  # hipDeviceScheduleSpin
+        if rc != 0:
+            print(f"[bench] hipSetDeviceFlags(spin) returned {rc}; keeping the default wait policy",
+                  file=sys.stderr)
     torch.cuda.set_device(lrank)
     dev = torch.device("cuda", lrank)
     comm = None

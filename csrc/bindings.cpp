@@ -760,6 +760,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("mean"),
         py::arg("invstd"), py::arg("nbt"));
   m.def("bn_tail_groups", &bn_tail_groups);
+  // host-side wait policy of the device (before torch creates its context): 1 =
+  // hipDeviceScheduleSpin - synchronize() polls the completion signal instead of sleeping
+  m.def("hip_set_device_flags", [](int dev, unsigned flags) {
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipSetDeviceFlags(flags);
+    return (int)e;
+  });
   m.def("bn_apply", &op_bn_apply);
   m.def("bn_finalize_groups", &bn_finalize_groups);
   m.def("bn_bwd_rows", [](long P, int C) { return bn_bwd_rows(P, C, nullptr); });
