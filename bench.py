@@ -157,6 +157,8 @@ def main():
                     help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch on "
                          "persistent blocks after every conv block (1) or right after the dgrad blocks (2), "
                          "or as its own kernel between forward and conv backward (0)")
+    ap.add_argument("--graph_head", type=int, default=None,
+                    help="timed steps launched eagerly before the graph replays (default 0)")
     ap.add_argument("--sync_spin", type=int, default=0, choices=[0, 1],
                     help="1: hipDeviceScheduleSpin (synchronize polls instead of sleeping)")
     ap.add_argument("--fuse_reduce", type=int, default=None, choices=[0, 1, 2],
@@ -277,7 +279,12 @@ def main():
                 dist.broadcast(t, src=0)
                 fs.params.data.copy_(t)
         opt = FusedSGD(model, lr=args.lr)
-        k = args.graph_steps or graph_chunk(args.steps)
+        # --graph_head: the first steps launch eagerly while the host submits the graph
+        # (measured neutral on the driver-shaped run: profiles/r3_spin/README.md)
+        head = args.graph_head or 0
+        head = 0 if args.no_graph else min(head, args.steps)
+        k = args.graph_steps or graph_chunk(max(1, args.steps - head))
+        args.graph_head_used = head
         eo = EngineOptions(graph_steps=k, use_graph=not args.no_graph, dtype=dtype,
                            bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
                            bucket_plan=args.bucket_plan)
@@ -298,7 +305,7 @@ def main():
         eng.synchronize()
         barrier()
         t0 = time.perf_counter()
-        eng.run_steps(args.steps)
+        eng.run_steps(args.steps, head=head)
         barrier()  # torch.cuda.synchronize() waits for the engine's streams too
         dt = time.perf_counter() - t0
         eng.synchronize()  # (idle by now) raises if an in-launch / cross-GPU wait timed out
@@ -355,7 +362,7 @@ def main():
                        "global_batch": ws * args.batch_size, "per_rank_batch": args.batch_size,
                        "seq_len": None, "image": "1x28x28", "parallelism": f"dp{ws}",
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
-                       "graph_steps": k, "fuse_level": eo.fuse_level, "level3": level3,
+                       "graph_steps": k, "graph_head": getattr(args, "graph_head_used", 0), "fuse_level": eo.fuse_level, "level3": level3,
                        "kernels_per_step": kps,
                        "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
                                   "wgrad_rows": eng.wgrad_rows, "store_a1": eng.store_a1,
