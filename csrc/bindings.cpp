@@ -493,7 +493,7 @@ void op_bn_apply(const Tensor& x, const Tensor& mean, const Tensor& invstd, cons
 void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, const Tensor& mean,
                const Tensor& invstd, const Tensor& gamma, double count, Tensor& ws, Tensor& sums,
                std::optional<Tensor> dgamma, std::optional<Tensor> dbeta, bool accum, Tensor& dx,
-               std::optional<Tensor> dres, std::optional<Tensor> dout2) {
+               std::optional<Tensor> dres, std::optional<Tensor> dout2, std::optional<Tensor> mask_beta) {
   check(dout, "dout", at::kBFloat16); check(x, "x", at::kBFloat16); check(dx, "dx", at::kBFloat16);
   check(sums, "sums", at::kFloat); check(ws, "ws", at::kFloat);
   const int C = x.size(-1);
@@ -511,9 +511,16 @@ void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, c
   bf16_t* dr = nullptr;
   if (dres) { check(*dres, "dres", at::kBFloat16); TORCH_CHECK(dres->sizes() == x.sizes(), "dres"); dr = bf(*dres); }
   if (dout2) TORCH_CHECK(dout2->sizes() == x.sizes(), "dout2 shape");
+  const float* mb = nullptr;
+  if (mask_beta) {
+    TORCH_CHECK(!out, "bn_bwd: give the saved output OR mask_beta (recomputed ReLU mask), not both");
+    check(*mask_beta, "mask_beta", at::kFloat);
+    TORCH_CHECK(mask_beta->numel() == C, "mask_beta size");
+    mb = mask_beta->data_ptr<float>();
+  }
   bn_bwd(cbf(dout), obf(out, "out"), cbf(x), P, C, mean.data_ptr<float>(), invstd.data_ptr<float>(),
          gamma.data_ptr<float>(), (float)count, ws.data_ptr<float>(), sums.data_ptr<float>(), dg, db,
-         accum, bf(dx), dr, cur_stream(), obf(dout2, "dout2"));
+         accum, bf(dx), dr, cur_stream(), obf(dout2, "dout2"), mb);
   kcheck();
 }
 
@@ -773,7 +780,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &op_bn_bwd, py::arg("dout"), py::arg("out"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("count"), py::arg("ws"), py::arg("sums"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dx"), py::arg("dres"),
-        py::arg("dout2") = py::none());
+        py::arg("dout2") = py::none(), py::arg("mask_beta") = py::none());
   m.def("bn_bwd_set_px_per_block", &bn_bwd_set_px_per_block);
   m.def("bn_bwd_set_fused", &bn_bwd_set_fused);
   m.def("bn_bwd_fused_ok", &bn_bwd_fused_ok);

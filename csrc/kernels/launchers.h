@@ -182,7 +182,10 @@ int bn_bwd_rows(long P, int C, int* rpb);  // ws of bn_bwd: [rows][2][C]
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,
             float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s,
-            const bf16_t* dout2 = nullptr);
+            const bf16_t* dout2 = nullptr, const float* mask_beta = nullptr);
+// out == nullptr && mask_beta != nullptr: the ReLU mask is recomputed from x (the BN input)
+// as bf16(x * invstd * gamma + (beta - mean * invstd * gamma)) > 0 - bitwise the sign of
+// the output bn_apply stored (no residual add); saves reading the output tensor
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
                  unsigned char* amax, hipStream_t s);
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,

@@ -31,9 +31,39 @@ namespace ddp_amd {
 
 // ---------------------------------------------------------------- BatchNorm
 // stats slab [rows][2][C] -> mean / invstd (+ running stats with torch's semantics:
-// momentum, unbiased running variance; + num_batches_tracked).  grid (ceil(C/64), G):
-// block (strip, y) sums rows y, y+G, ... of its 64 channels (4 row groups, fixed
-// combine order) into ws[y]; the last block of the strip sums ws[0..G) and finalises.
+// momentum, unbiased running variance; + num_batches_tracked).  Latency-bound (a few KB
+// per layer), so the kernel is built around memory round trips: grid (ceil(C/64), G),
+// block (strip, y) owns rows [y*RPB, (y+1)*RPB) (RPB = 64 up to 4096 rows); its 4 row
+// phases x 64 channels issue ALL their loads (16 rows each) before summing in row order,
+// phases combined in order -> ws[y].  G == 1 finalises straight away (no ticket, one
+// round trip); otherwise the strip's last block (ticket) sums ws[0..G) the same way
+// (G <= 64: one batch) and finalises.
+constexpr int BNF_RPB = 64;
+constexpr int BNF_MAXG = 64;
+
+// rows [r0, r1) (<= 64 of them) of a [rows][2][C] slab, channel c: phase grp sums rows
+// r0 + grp, r0 + grp + 4, ... (all 16 loads in flight), in order
+template <bool AGENT>
+__device__ __forceinline__ void bnf_rows(const float* slab, long C2, int C, int c, int r0, int r1, int grp,
+                                         float& s, float& q) {
+  s = q = 0.f;
+  for (int rb = r0; rb < r1; rb += 64) {  // one batch unless a block owns > 64 rows
+    float a[16], b[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = rb + grp + 4 * u;
+      const bool ok = r < r1;
+      const float* p = slab + (long)(ok ? r : r0) * C2 + c;
+      a[u] = ok ? (AGENT ? ld_agent(p) : *p) : 0.f;
+      b[u] = ok ? (AGENT ? ld_agent(p + C) : p[C]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (rb + grp + 4 * u < r1) { s += a[u]; q += b[u]; }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ slab, int rows,
                                                           int C, float count, float eps, float momentum,
                                                           float* __restrict__ running_mean,
@@ -41,7 +71,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ save_mean,
                                                           float* __restrict__ save_invstd,
                                                           long long* __restrict__ nbt,
-                                                          float* __restrict__ ws, int* __restrict__ tickets) {
+                                                          float* __restrict__ ws, int* __restrict__ tickets,
+                                                          int rpb) {
   __shared__ float ps[4][64], pq[4][64];
   __shared__ int s_last;
   const int l = threadIdx.x & 63, grp = threadIdx.x >> 6;
@@ -49,41 +80,23 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   const int G = gridDim.y, y = blockIdx.y;
   const long C2 = 2L * C;
   float s = 0.f, q = 0.f;
-  if (c < C) {
-    int r = y + G * grp;
-    for (; r + 12 * G < rows; r += 16 * G) {  // 4 rows in flight
-      float a[4], b[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[u] = slab[(long)(r + 4 * u * G) * C2 + c];
-        b[u] = slab[(long)(r + 4 * u * G) * C2 + C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { s += a[u]; q += b[u]; }
-    }
-    for (; r < rows; r += 4 * G) {
-      s += slab[(long)r * C2 + c];
-      q += slab[(long)r * C2 + C + c];
-    }
-  }
+  if (c < C) bnf_rows<false>(slab, C2, C, c, y * rpb, min(rows, (y + 1) * rpb), grp, s, q);
   ps[grp][l] = s;
   pq[grp][l] = q;
   __syncthreads();
-  if (grp == 0 && c < C) {
-    st_wt(ws + (long)y * C2 + c, ((ps[0][l] + ps[1][l]) + ps[2][l]) + ps[3][l]);
-    st_wt(ws + (long)y * C2 + C + c, ((pq[0][l] + pq[1][l]) + pq[2][l]) + pq[3][l]);
-  }
-  if (!last_arrival(&tickets[blockIdx.x], G, &s_last)) return;
-  s = q = 0.f;
-  if (c < C)
-    for (int yy = grp; yy < G; yy += 4) {
-      s += ld_agent(ws + (long)yy * C2 + c);
-      q += ld_agent(ws + (long)yy * C2 + C + c);
+  if (G > 1) {
+    if (grp == 0 && c < C) {
+      st_wt(ws + (long)y * C2 + c, ((ps[0][l] + ps[1][l]) + ps[2][l]) + ps[3][l]);
+      st_wt(ws + (long)y * C2 + C + c, ((pq[0][l] + pq[1][l]) + pq[2][l]) + pq[3][l]);
     }
-  __syncthreads();
-  ps[grp][l] = s;
-  pq[grp][l] = q;
-  __syncthreads();
+    if (!last_arrival(&tickets[blockIdx.x], G, &s_last)) return;
+    s = q = 0.f;
+    if (c < C) bnf_rows<true>(ws, C2, C, c, 0, G, grp, s, q);
+    __syncthreads();
+    ps[grp][l] = s;
+    pq[grp][l] = q;
+    __syncthreads();
+  }
   if (grp == 0 && c < C) {
     const float S = ((ps[0][l] + ps[1][l]) + ps[2][l]) + ps[3][l];
     const float Q = ((pq[0][l] + pq[1][l]) + pq[2][l]) + pq[3][l];
@@ -121,9 +134,46 @@ __device__ __forceinline__ void unpack8_sum(bf16x8 a, const bf16_t* b2, long off
     for (int j = 0; j < 8; ++j) o[j] = bf16_round(o[j] + t[j]);
   }
 }
+// ReLU mask source of the BatchNorm backward: MSK 0 none, 1 the saved output (out > 0),
+// 2 recomputed from the BN input y: bf16(y * sc + sh) > 0 - bitwise the stored output's
+// sign (same affine, same rounding), for BatchNorms without a residual add; saves the
+// read of the output tensor in both backward passes.
+template <int MSK>
+__device__ __forceinline__ void bn_mask8(bf16x8 go, const float* xv, const float* msc, const float* msh,
+                                         float* d) {
+  if constexpr (MSK == 1) {
+    float ov[8];
+    unpack8(go, ov);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(ov[j] > 0.f)) d[j] = 0.f;
+  } else if constexpr (MSK == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(bf16_round(fmaf(xv[j], msc[j], msh[j])) > 0.f)) d[j] = 0.f;
+  }
+}
+
 __device__ __forceinline__ uint4 pack8(const float* v) {
   const uint2 lo = pack4(v[0], v[1], v[2], v[3]), hi = pack4(v[4], v[5], v[6], v[7]);
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// The BatchNorm affine of 8 channels: sc = invstd * gamma, sh = beta - mean * sc (explicit
+// fma) - ONE definition, so the backward's recomputed ReLU mask (MSK 2 below) sees exactly
+// the values bn_apply stored.
+__device__ __forceinline__ void bn_affine8(const float* invstd, const float* gamma, const float* mean,
+                                           const float* beta, int c0, float* sc, float* sh) {
+  float g[8], mu[8], be[8];
+  ld8f(invstd + c0, sc);
+  ld8f(gamma + c0, g);
+  ld8f(mean + c0, mu);
+  ld8f(beta + c0, be);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] *= g[j];
+    sh[j] = fmaf(-mu[j], sc[j], be[j]);
+  }
 }
 
 // y = act(x * sc + sh [+ res]), sc = invstd * gamma, sh = beta - mean * sc; 8 channels per
@@ -140,16 +190,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   const int c0 = (int)(t0 % (C / 8)) * 8;
-  float sc[8], sh[8], mu[8], be[8];
-  ld8f(invstd + c0, sc);
-  ld8f(gamma + c0, sh);
-  ld8f(mean + c0, mu);
-  ld8f(beta + c0, be);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] *= sh[j];
-    sh[j] = be[j] - mu[j] * sc[j];
-  }
+  float sc[8], sh[8];
+  bn_affine8(invstd, gamma, mean, beta, c0, sc, sh);
   for (long i = t0; i < n8; i += stride) {
     float v[8], r[8];
     unpack8(ld8(x + i * 8), v);
@@ -185,7 +227,7 @@ struct BnBwdFused {
 };
 constexpr unsigned long long BN_WAIT_TICKS = 20000000;  // 200 ms of the 100 MHz clock
 
-template <bool RELU, bool FUSED>
+template <int MSK, bool FUSED>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
                                                             const bf16_t* __restrict__ dout2,
                                                             const bf16_t* __restrict__ out,
@@ -196,7 +238,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             float* __restrict__ sums,
                                                             float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta, int accum,
-                                                            BnBwdFused fz) {
+                                                            BnBwdFused fz, const float* __restrict__ mgamma,
+                                                            const float* __restrict__ mbeta) {
   __shared__ float sred[32][2][64];
   __shared__ float sfin[8][128];
   __shared__ int s_last;
@@ -206,17 +249,18 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   float mu[8], is[8], s[8], q[8];
   ld8f(mean + c0, mu);
   ld8f(invstd + c0, is);
+  float msc[8], msh[8];  // MSK 2: the forward's affine (bn_affine8)
+  if constexpr (MSK == 2) bn_affine8(invstd, mgamma, mean, mbeta, c0, msc, msh);
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
   const int p0 = blockIdx.y * rpb, p1 = min(P, p0 + rpb);
   auto acc8 = [&](bf16x8 gd, long off, bf16x8 gx, bf16x8 go) {
-    float d[8], xv[8], ov[8];
+    float d[8], xv[8];
     unpack8_sum(gd, dout2, off, d);
     unpack8(gx, xv);
-    if (RELU) unpack8(go, ov);
+    bn_mask8<MSK>(go, xv, msc, msh, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
       s[j] += d[j];
       q[j] = fmaf(d[j], (xv[j] - mu[j]) * is[j], q[j]);
     }
@@ -232,7 +276,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
       const long o = (long)(p + 32 * u) * C + c0;
       d[u] = ld8(dout + o);
       xx[u] = ld8(x + o);
-      r[u] = RELU ? ld8(out + o) : zero8();
+      r[u] = MSK == 1 ? ld8(out + o) : zero8();
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc8(d[u], (long)(p + 32 * u) * C + c0, xx[u], r[u]);
@@ -240,13 +284,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   for (; p + 32 < p1; p += 64) {  // two pixels' loads in flight
     const long o0 = (long)p * C + c0, o1 = o0 + 32L * C;
     const bf16x8 d0 = ld8(dout + o0), x0 = ld8(x + o0), d1 = ld8(dout + o1), x1 = ld8(x + o1);
-    const bf16x8 r0 = RELU ? ld8(out + o0) : zero8(), r1 = RELU ? ld8(out + o1) : zero8();
+    const bf16x8 r0 = MSK == 1 ? ld8(out + o0) : zero8(), r1 = MSK == 1 ? ld8(out + o1) : zero8();
     acc8(d0, o0, x0, r0);
     acc8(d1, o1, x1, r1);
   }
   for (; p < p1; p += 32) {
     const long o0 = (long)p * C + c0;
-    acc8(ld8(dout + o0), o0, ld8(x + o0), RELU ? ld8(out + o0) : zero8());
+    acc8(ld8(dout + o0), o0, ld8(x + o0), MSK == 1 ? ld8(out + o0) : zero8());
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -329,13 +373,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
       sq[j] = ld_agent(sums + C + c0 + j);
     }
     auto apply8 = [&](long o, bf16x8 gd, bf16x8 gx, bf16x8 go) {
-      float d[8], xv[8], ov[8], r[8];
+      float d[8], xv[8], r[8];
       unpack8_sum(gd, dout2, o, d);
       unpack8(gx, xv);
-      if (RELU) unpack8(go, ov);
+      bn_mask8<MSK>(go, xv, msc, msh, d);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
         const float xh = (xv[j] - mu[j]) * is[j];
         r[j] = k[j] * (fz.count * d[j] - sd[j] - xh * sq[j]);
       }
@@ -350,14 +393,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
         const long o = (long)(pp + 32 * u) * C + c0;
         d[u] = ld8(dout + o);
         xx[u] = ld8(x + o);
-        r[u] = RELU ? ld8(out + o) : zero8();
+        r[u] = MSK == 1 ? ld8(out + o) : zero8();
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) apply8((long)(pp + 32 * u) * C + c0, d[u], xx[u], r[u]);
     }
     for (; pp < p1; pp += 32) {
       const long o = (long)pp * C + c0;
-      apply8(o, ld8(dout + o), ld8(x + o), RELU ? ld8(out + o) : zero8());
+      apply8(o, ld8(dout + o), ld8(x + o), MSK == 1 ? ld8(out + o) : zero8());
     }
   }
   // re-arm: the strip's last block through here lowers the flag
@@ -368,7 +411,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 // Backward pass 2: dx = gamma*invstd/count * (count*dy - sum_dy - xhat*sum_dyxh); also
 // writes the residual-branch gradient (= dy masked) when dres != null.  Same
 // fixed-channel-group grid stride as bn_apply.
-template <bool RELU>
+template <int MSK>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ dout2,
                                                            const bf16_t* __restrict__ out,
@@ -378,7 +421,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ sums,
                                                            float count, bf16_t* __restrict__ dx,
-                                                           bf16_t* __restrict__ dres) {
+                                                           bf16_t* __restrict__ dres,
+                                                           const float* __restrict__ mbeta) {
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long stride = (long)gridDim.x * blockDim.x;
   const int c0 = (int)(t0 % (C / 8)) * 8;
@@ -388,16 +432,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
   ld8f(gamma + c0, k);
   ld8f(sums + c0, sd);
   ld8f(sums + C + c0, sq);
+  float msc[8], msh[8];
+  if constexpr (MSK == 2) bn_affine8(invstd, gamma, mean, mbeta, c0, msc, msh);
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = k[j] * is[j] / count;
   for (long i = t0; i < n8; i += stride) {
-    float d[8], xv[8], ov[8], o[8];
+    float d[8], xv[8], o[8];
     unpack8_sum(ld8(dout + i * 8), dout2, i * 8, d);
     unpack8(ld8(x + i * 8), xv);
-    if (RELU) unpack8(ld8(out + i * 8), ov);
+    bn_mask8<MSK>(MSK == 1 ? ld8(out + i * 8) : zero8(), xv, msc, msh, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (RELU && !(ov[j] > 0.f)) d[j] = 0.f;
       const float xh = (xv[j] - mu[j]) * is[j];
       o[j] = k[j] * (count * d[j] - sd[j] - xh * sq[j]);
     }
@@ -746,18 +791,21 @@ int* bn_ticket_slots(int n) {
   return p;
 }
 
-int bn_finalize_groups(int rows) {
-  const int g = rows / 32;
-  return g < 1 ? 1 : (g > 64 ? 64 : g);
+// blocks per strip: one per BNF_RPB rows (more only past BNF_MAXG * BNF_RPB rows)
+static int bnf_rpb(int rows) {
+  int r = BNF_RPB;
+  while ((rows + r - 1) / r > BNF_MAXG) r *= 2;
+  return r;
 }
+int bn_finalize_groups(int rows) { return (rows + bnf_rpb(rows) - 1) / bnf_rpb(rows); }
 
 void bn_finalize(const float* slab, int rows, int C, float count, float eps, float momentum,
                  float* running_mean, float* running_var, float* save_mean, float* save_invstd,
                  long long* nbt, float* ws, hipStream_t s) {
-  const int strips = (C + 63) / 64, G = bn_finalize_groups(rows);
+  const int strips = (C + 63) / 64, G = bn_finalize_groups(rows), rpb = bnf_rpb(rows);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(strips, G), dim3(256), 0, s, slab, rows, C, count, eps,
                      momentum, running_mean, running_var, save_mean, save_invstd, nbt, ws,
-                     bn_ticket_slots(strips));
+                     G > 1 ? bn_ticket_slots(strips) : nullptr, rpb);
 }
 
 void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* invstd,
@@ -818,7 +866,7 @@ int bn_bwd_fused_error(bool reset) {
   return v;
 }
 
-template <bool RELU>
+template <int MSK>
 static long bn_bwd_fused_capacity() {
   static long cap[64] = {};
   int dev = 0;
@@ -826,7 +874,7 @@ static long bn_bwd_fused_capacity() {
   dev &= 63;
   if (!cap[dev]) {
     int per_cu = 0, cus = 0;
-    RN_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bn_bwd_reduce_kernel<RELU, true>, 256, 0));
+    RN_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bn_bwd_reduce_kernel<MSK, true>, 256, 0));
     RN_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     cap[dev] = (long)per_cu * cus;
     if (cap[dev] <= 0) cap[dev] = -1;
@@ -834,44 +882,45 @@ static long bn_bwd_fused_capacity() {
   return cap[dev];
 }
 
+static long bn_bwd_capacity(int msk) {
+  return msk == 1 ? bn_bwd_fused_capacity<1>() : msk == 2 ? bn_bwd_fused_capacity<2>() : bn_bwd_fused_capacity<0>();
+}
+
 bool bn_bwd_fused_ok(long P, int C, bool relu) {
   if (!g_bn_bwd_fused) return false;
   const long blocks = (long)(C / 64) * bn_bwd_rows(P, C, nullptr);
   // half the resident capacity: other streams' kernels (bucket all-reduces) may hold CUs
-  return blocks <= (relu ? bn_bwd_fused_capacity<true>() : bn_bwd_fused_capacity<false>()) / 2;
+  return blocks <= bn_bwd_capacity(relu ? 1 : 0) / 2;
 }
 
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,
             float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s,
-            const bf16_t* dout2) {
+            const bf16_t* dout2, const float* mask_beta) {
   int rpb = 0;
   const int R = bn_bwd_rows(P, C, &rpb);
   const dim3 grid(C / 64, R);
   int* tk = bn_ticket_slots(C / 64);
+  // ReLU mask: the saved output, or (no output given, mask_beta given) recomputed from x
+  const int msk = out ? 1 : (mask_beta ? 2 : 0);
   BnBwdFused fz;
-  if (bn_bwd_fused_ok(P, C, out != nullptr)) {
+#define BNR(M, F) hipLaunchKernelGGL((bn_bwd_reduce_kernel<M, F>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz, gamma, mask_beta)
+  if (g_bn_bwd_fused && (long)(C / 64) * R <= bn_bwd_capacity(msk) / 2) {
     fz.gamma = gamma;
     fz.count = count;
     fz.dx = dx;
     fz.dres = dres;
     fz.flags = bn_ticket_slots(2 * (C / 64));
     fz.err = bn_err_word();
-    if (out)
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
-    else
-      hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, true>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
+    if (msk == 1) BNR(1, true); else if (msk == 2) BNR(2, true); else BNR(0, true);
     return;
   }
-  if (out)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz);
+  if (msk == 1) BNR(1, false); else if (msk == 2) BNR(2, false); else BNR(0, false);
+#undef BNR
   const unsigned g = grid_for(P * C, 8);
-  if (out)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres);
+#define BNA(M) hipLaunchKernelGGL(bn_bwd_apply_kernel<M>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres, mask_beta)
+  if (msk == 1) BNA(1); else if (msk == 2) BNA(2); else BNA(0);
+#undef BNA
 }
 
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,

@@ -44,6 +44,9 @@ BF16 = torch.bfloat16
 # 13.7k vs 14.2k img/s); DDP_AMD_BN_BWD_FUSED=1 runs the BatchNorm backward as one launch
 # (resnet_ops.hip FUSED; pass 2 after an in-launch strip wait: 13.7k vs 14.2k img/s).
 BN_TAIL = os.environ.get("DDP_AMD_BN_TAIL", "0") == "1"
+# BatchNorm backward of a ReLU without a residual add: the mask recomputed from the BN input
+# (no read of the saved output in either pass); DDP_AMD_BN_MASK_FROM_Y=0 reads the output
+MASK_FROM_Y = os.environ.get("DDP_AMD_BN_MASK_FROM_Y", "1") != "0"
 
 
 _configured = False
@@ -150,7 +153,10 @@ class _ConvBNAct(torch.autograd.Function):
         out = torch.empty_like(y)
         C.bn_apply(y, mean, invstd, gamma.detach(), beta.detach(),
                    res.contiguous() if res is not None else None, bool(relu), out)
-        ctx.save_for_backward(x, wb, y, out, mean, invstd)
+        # the backward's ReLU mask: without a residual add it is recomputed from y (bitwise
+        # the sign of `out`, resnet_ops.hip bn_mask8), so `out` is kept only for a join
+        keep_out = bool(relu) and (res is not None or not MASK_FROM_Y)
+        ctx.save_for_backward(x, wb, y, out if keep_out else None, mean, invstd)
         ctx.params = (w, gamma, beta)
         ctx.cfg = (stride, pad, bool(relu), res is not None, stem, P)
         # stash: this Function is the residual branch of a block; its gradient w.r.t. the
@@ -178,8 +184,9 @@ class _ConvBNAct(torch.autograd.Function):
         sums = torch.empty(2 * Cout, device=dev)
         dy = torch.empty_like(y)
         dres = torch.empty_like(y) if has_res else None
+        mask_beta = beta.detach() if (relu and out is None) else None
         C.bn_bwd(dout, out if relu else None, y, mean, invstd, gamma.detach(), float(P), ws, sums,
-                 dgamma, dbeta, direct_bn, dy, dres, _take_stash(ctx))
+                 dgamma, dbeta, direct_bn, dy, dres, _take_stash(ctx), mask_beta)
         # data gradient (the stem's input is the image: none)
         dx = None
         if ctx.needs_input_grad[0] and not stem:

@@ -352,6 +352,48 @@ def test_bn_bwd_single_launch_bitwise(C, N, H, Cc, relu, two):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("N,H,Cc", [(32, 56, 64), (8, 14, 256), (4, 7, 512), (2, 5, 64)])
+@pytest.mark.parametrize("fused", [0, 1])
+def test_bn_bwd_mask_from_input_bitwise(C, N, H, Cc, fused):
+    """BatchNorm + ReLU backward with the mask recomputed from the BN input (mask_beta:
+    bf16(y * sc + sh) > 0 through bn_apply's own affine) == the backward that reads the
+    output bn_apply stored: dx, sums, dgamma / dbeta bit for bit - including values that
+    land exactly on / next to zero (a channel with beta = 0 and y == mean)."""
+    P = N * H * H
+    y = rnd(N, H, H, Cc, seed=41)
+    y[..., 0] = 0  # channel 0: y == mean == 0 and beta 0 -> bn output exactly 0
+    dout = rnd(N, H, H, Cc, seed=42)
+    mean = torch.randn(Cc, device=dev) * 0.1
+    mean[0] = 0
+    invstd = torch.rand(Cc, device=dev) + 0.5
+    gamma = torch.rand(Cc, device=dev) + 0.5
+    beta = torch.randn(Cc, device=dev) * 0.3
+    beta[0] = 0
+    out = torch.empty_like(y)
+    C.bn_apply(y, mean, invstd, gamma, beta, None, True, out)
+    assert (out[..., 0] == 0).all() and (out > 0).any() and (out == 0).any()
+    res = []
+    C.bn_bwd_set_fused(fused)
+    try:
+        for mode in ("out", "y"):
+            ws = torch.empty(C.bn_bwd_rows(P, Cc), 2, Cc, device=dev)
+            sums = torch.empty(2 * Cc, device=dev)
+            dg, db = torch.zeros(Cc, device=dev), torch.zeros(Cc, device=dev)
+            dx = torch.empty_like(y)
+            if mode == "out":
+                C.bn_bwd(dout, out, y, mean, invstd, gamma, float(P), ws, sums, dg, db, False, dx, None)
+            else:
+                C.bn_bwd(dout, None, y, mean, invstd, gamma, float(P), ws, sums, dg, db, False, dx, None,
+                         None, beta)
+            torch.cuda.synchronize()
+            res.append((dx, sums, dg, db))
+    finally:
+        C.bn_bwd_set_fused(0)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert C.bn_bwd_fused_error(True) == 0
+
+
 @pytest.mark.parametrize("H,W", [(56, 56), (8, 11)])
 def test_maxpool_bwd_quad_shapes(C, H, W):
     """maxpool backward (one thread per 2x2 input quad) on even and odd / non-square inputs."""
