@@ -936,6 +936,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                b.a2_f32 = need("a2", at::kFloat, B * HW * c.C2).data_ptr<float>();
                b.dz2_f32 = need("dz2", at::kFloat, B * HW * c.C2).data_ptr<float>();
                b.w2t_f32 = need("w2t_f32", at::kFloat, 9L * c.C1 * c.C2).data_ptr<float>();
+               b.wfc_frag32 = need("wfc_frag32", at::kFloat, (long)c.NO * HW * c.C2).data_ptr<float>();
              } else {
                b.w2_bf16 = bf(need("w2_bf16", at::kBFloat16, 9L * c.C1 * c.C2));
                b.w2t_bf16 = bf(need("w2t_bf16", at::kBFloat16, 9L * c.C1 * c.C2));

@@ -54,6 +54,8 @@ __device__ __forceinline__ void shadow_one(const ShadowSet& sh, long j, float v)
       sh.r[r].dst[k] = b;
     } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
       sh.r[r].dst[fcfrag_index((int)k, sh.r[r].a, sh.r[r].b)] = b;
+    } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
+      sh.r[r].dst32[fcfrag_index((int)k, sh.r[r].a, sh.r[r].b)] = v;
     } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {  // [..][3] -> [..][4], 4th stays zero
       sh.r[r].dst[(k / 3) * 4 + k % 3] = b;
     } else if (sh.r[r].kind == SHADOW_F32_TAPT) {  // exact fp32 [tap][ci][co] copy

@@ -272,7 +272,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     rowc[pt] = lp + W + 1;  // sX row of the pixel itself
   }
   // fc weight prefetch (lands while the MFMAs run; issued before the staging it delayed
-  // it - in-order vmcnt - by more than it saved); fp32 reads its native-layout weight in
+  // it - in-order vmcnt - by more than it saved); fp32 reads its FCFRAG-order fp32 weight in
   // the epilogue instead (160 more VGPRs would not fit next to the fp32 fragments)
   uint2 wv[NOF > 0 && !F32 ? PXT : 1][4][NOF > 0 && !F32 ? NOF : 1];
   if (NOF > 0 && !F32) {
@@ -366,8 +366,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 #pragma unroll
         for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
           float s = fcs[o];
-          if constexpr (F32) {  // native [o][hw][c] fp32 weight: 4 consecutive channels
-            const float4 w4 = *reinterpret_cast<const float4*>(wfc + ((long)o * HW + rem[pt]) * Cout + co);
+          if constexpr (F32) {  // fp32 FCFRAG weight: 4 consecutive channels, 1 KB per wave load
+            const float4 w4 = *reinterpret_cast<const float4*>(
+                wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
             s = fmaf(q[0], w4.x, s); s = fmaf(q[1], w4.y, s);
             s = fmaf(q[2], w4.z, s); s = fmaf(q[3], w4.w, s);
           } else {

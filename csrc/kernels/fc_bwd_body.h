@@ -403,6 +403,7 @@ __device__ __forceinline__ void fc_bwd_body(const float* __restrict__ dL, const 
         const bf16_t pb = f2bf(pn);
         if (ex.sh_plain) st_wt(ex.sh_plain + idx, pb);
         if (ex.sh_frag) st_wt(ex.sh_frag + fcfrag_index((int)idx, ex.frag_HW, ex.frag_C), pb);
+        if (ex.sh_frag32) st_wt(ex.sh_frag32 + fcfrag_index((int)idx, ex.frag_HW, ex.frag_C), pn);
       }
     }
   }

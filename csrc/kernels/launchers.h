@@ -52,7 +52,7 @@ bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt);
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const bf16_t* wfc, float* fc_part, int NO,
                  int pxt, hipStream_t s, const C1Src* c1 = nullptr, const FwdDz* dz = nullptr);
-// fp32: wfc (fused fc epilogue) is the fc weight in its native [NO][H*W][C] layout
+// fp32: wfc (fused fc epilogue) is the fc weight in the FCFRAG order, fp32 (SHADOW_F32_FCFRAG)
 void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
                  int pxt, hipStream_t s, const C1Src* c1 = nullptr);
@@ -232,6 +232,7 @@ struct FcBwdExtras {
   float* m_w = nullptr;       // momentum buffer [NO][K] (momentum != 0)
   bf16_t* sh_plain = nullptr;  // bf16 shadow [NO][K]
   bf16_t* sh_frag = nullptr;   // FCFRAG shadow (conv3x3_fwd epilogue order)
+  float* sh_frag32 = nullptr;  // fp32 FCFRAG copy (the exact-fp32 forward's fc operand)
   int frag_HW = 0, frag_C = 0;
   int sys_store = 0;  // dW / dbias with system-scope stores (read by peers over xGMI)
   // Last-block epilogue (fuse level 3: this kernel runs BESIDE the conv backward, so nothing
@@ -307,8 +308,11 @@ void xent_rows(const float* part, int HW, int CH, const float* bias, int NO, int
 // fused-SGD all-gather (shadow_one).
 // SHADOW_F32_TAPT: the exact-fp32 engine's [tap][ci][co] copy of the conv2 weight (the
 // data-gradient operand), a transposed fp32 copy - not a reduced-precision shadow; dst32.
+// SHADOW_F32_FCFRAG: the exact-fp32 engine's fc weight in the FCFRAG order (fp32, dst32):
+// the forward's fused fc epilogue then loads 1 KB contiguous per wave-instruction instead
+// of 16 strided 64-byte runs.
 enum { SHADOW_BF16 = 1, SHADOW_BF16_TAPT = 2, SHADOW_BF16_FCFRAG = 3, SHADOW_BF16_PAD4 = 4,
-       SHADOW_F32_TAPT = 5 };
+       SHADOW_F32_TAPT = 5, SHADOW_F32_FCFRAG = 6 };
 constexpr int MAX_SHADOWS = 4;
 struct ShadowRegion {
   long off, n;

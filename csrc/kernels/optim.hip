@@ -51,6 +51,9 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
             // C % 4 == 0: the quad is 4 consecutive channels of one (o, hw) -> 8 contiguous bytes
             *reinterpret_cast<uint2*>(sh.r[r].dst + fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)) =
                 pack4(e[0], e[1], e[2], e[3]);
+          } else if (sh.r[r].kind == SHADOW_F32_FCFRAG && whole) {
+            *reinterpret_cast<float4*>(sh.r[r].dst32 + fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)) =
+                make_float4(e[0], e[1], e[2], e[3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -60,6 +63,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
                 sh.r[r].dst[jj] = f2bf(e[u]);
               } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
                 sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(e[u]);
+              } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
+                sh.r[r].dst32[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = e[u];
               } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
                 sh.r[r].dst[(jj / 3) * 4 + jj % 3] = f2bf(e[u]);
               } else if (sh.r[r].kind == SHADOW_F32_TAPT) {
@@ -95,6 +100,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
         sh.r[r].dst[j] = f2bf(v);
       } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
         sh.r[r].dst[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = f2bf(v);
+      } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
+        sh.r[r].dst32[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = v;
       } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
         sh.r[r].dst[(j / 3) * 4 + j % 3] = f2bf(v);
       } else if (sh.r[r].kind == SHADOW_F32_TAPT) {

@@ -49,8 +49,8 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   if (cfg_.NO != 10) throw std::runtime_error("engine: the fused fc epilogue is built for 10 classes");
   if (cfg_.f32 && (cfg_.fuse_level < 1 || cfg_.store_a1 != 0))
     throw std::runtime_error("engine: fp32 mode needs fuse_level >= 1 (runs the level-1 chain) and store_a1 0");
-  if (cfg_.f32 && !(b_.a2_f32 && b_.dz2_f32 && b_.w2t_f32))
-    throw std::runtime_error("engine: fp32 mode needs the a2 / dz2 / w2t fp32 buffers");
+  if (cfg_.f32 && !(b_.a2_f32 && b_.dz2_f32 && b_.w2t_f32 && b_.wfc_frag32))
+    throw std::runtime_error("engine: fp32 mode needs the a2 / dz2 / w2t / wfc_frag32 fp32 buffers");
   // bucket plan: in-range, ordered, non-overlapping; stage by the first conv gradient
   const long conv0 = std::min(std::min(b_.off_w2, b_.off_b2), std::min(b_.off_w1, b_.off_b1));
   const long fc_hi = std::max(b_.off_wfc + (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, b_.off_bfc + cfg_.NO);
@@ -130,7 +130,9 @@ void SimpleCNNEngine::refresh_shadows() {
   const long n_w2 = (long)cfg_.C2 * 9 * cfg_.C1;
   if (cfg_.f32) {
     sh.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, cfg_.C2, 9, cfg_.C1, b_.w2t_f32};
-    sh.count = 1;
+    sh.r[1] = ShadowRegion{b_.off_wfc, (long)cfg_.NO * cfg_.H * cfg_.W * cfg_.C2, nullptr, SHADOW_F32_FCFRAG,
+                           cfg_.H * cfg_.W, cfg_.C2, 0, b_.wfc_frag32};
+    sh.count = 2;
     sgd_step(b_.params, b_.grads, nullptr, b_.n_params, a, sh, nullptr, cs_);
     DDP_HIP_CHECK(hipGetLastError());
     return;
@@ -433,7 +435,7 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
 
   // ---- forward: conv1 (recomputed) + conv2 + bias + ReLU -> a2, fused fc partial logits
   conv3x3_fwd(static_cast<const float*>(nullptr), P + b_.off_w2, P + b_.off_b2, b_.a2_f32, B, H, W, C1, C2,
-              true, P + b_.off_wfc, b_.fc_part, NO, cfg_.pxt_fwd, cs_, &c1);
+              true, b_.wfc_frag32, b_.fc_part, NO, cfg_.pxt_fwd, cs_, &c1);
   // ---- loss + fc backward (bucket 0)
   FcBwdExtras ex;
   ex.dbias = G + b_.off_bfc;
@@ -452,12 +454,16 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     ex.sgd = sa;
     ex.p_w = P + b_.off_wfc;
     ex.m_w = M ? M + b_.off_wfc : nullptr;
+    ex.sh_frag32 = b_.wfc_frag32;  // the forward's fc operand
+    ex.frag_HW = HW;
+    ex.frag_C = C2;
   }
   fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
          (long)HW * C2, NO, /*mask=*/true, cs_, ex);
   ShadowSet sh1{};
   sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
-  sh1.count = 1;
+  sh1.r[1] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, nullptr, SHADOW_F32_FCFRAG, HW, C2, 0, b_.wfc_frag32};
+  sh1.count = 2;
   if (dist) launch_buckets(0, use_x, sa, M, sh1);
   // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
   SlabSet ss{};

@@ -170,6 +170,7 @@ struct EngineBuffers {
   // exact-fp32 engine (EngineConfig::f32): fp32 activations and the conv2 weight's
   // [tap][ci][co] fp32 copy (the data-gradient operand); the bf16 buffers are unused
   float *a2_f32 = nullptr, *dz2_f32 = nullptr, *w2t_f32 = nullptr;
+  float* wfc_frag32 = nullptr;  // the fc weight in FCFRAG order, fp32 (the forward's fc operand)
   // activations / scratch (sized for max batch)
   bf16_t *a1, *a2, *dz2, *dz1;
   float *fc_part, *dlogits, *loss_rows, *loss_hist, *w2slab, *w1slab;

@@ -152,7 +152,8 @@ class FusedSimpleCNNEngine:
         e = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
         self.steps_per_epoch = math.ceil(n_rank / B)
         if f32:  # fp32 activations + the conv2 weight's fp32 [tap][ci][co] copy; no bf16 buffers
-            act = dict(a2=e(B * HW * 64), dz2=e(B * HW * 64), w2t_f32=e(64 * 9 * 32))
+            act = dict(a2=e(B * HW * 64), dz2=e(B * HW * 64), w2t_f32=e(64 * 9 * 32),
+                       wfc_frag32=e(10 * HW * 64))
         else:
             act = dict(w2_bf16=e(64 * 9 * 32, dt=BF16), w2t_bf16=e(64 * 9 * 32, dt=BF16),
                        wfc_bf16=e(10 * HW * 64, dt=BF16), wfc_frag=e(10 * HW * 64, dt=BF16),

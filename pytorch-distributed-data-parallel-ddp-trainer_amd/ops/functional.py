@@ -178,13 +178,13 @@ def cross_entropy(logits, labels):
     return _CrossEntropy.apply(logits, labels)
 
 
-def fc_weight_frag(w: torch.Tensor, hw: int, c: int) -> torch.Tensor:
+def fc_weight_frag(w: torch.Tensor, hw: int, c: int, dtype=torch.bfloat16) -> torch.Tensor:
     """fc weight [out][H*W][C] (NHWC order) -> the MFMA-fragment order read by the fused
-    FC epilogue of conv3x3_fwd (csrc SHADOW_BF16_FCFRAG):
-    [out][hw/16][c/16][(c/4)%4][hw%16][c%4], bf16."""
+    FC epilogue of conv3x3_fwd (csrc SHADOW_BF16_FCFRAG / SHADOW_F32_FCFRAG):
+    [out][hw/16][c/16][(c/4)%4][hw%16][c%4], bf16 (fp32 for the exact-fp32 forward)."""
     no = w.numel() // (hw * c)
     v = w.reshape(no, hw // 16, 16, c // 16, 4, 4)
-    return v.permute(0, 1, 3, 4, 2, 5).contiguous().to(torch.bfloat16)
+    return v.permute(0, 1, 3, 4, 2, 5).contiguous().to(dtype)
 
 
 def fold_block_partials(part: torch.Tensor, B: int, HW: int, CH: int) -> torch.Tensor:

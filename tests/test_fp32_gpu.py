@@ -59,8 +59,8 @@ def test_conv3x3_fwd_fp32(C, B, pxt):
 
 @pytest.mark.parametrize("B", [1, 16, 32])
 def test_conv3x3_fwd_fused_fc_fp32(C, B):
-    """fp32 fused fc epilogue reads the fc weight in its native [o][hw][c] layout."""
-    from ddp_amd.ops.functional import fold_block_partials
+    """fp32 fused fc epilogue reads the fc weight in the fp32 FCFRAG order (coalesced)."""
+    from ddp_amd.ops.functional import fc_weight_frag, fold_block_partials
 
     H = W = 28
     x = rnd(B, H, W, 32, relu=True, seed=5)
@@ -71,7 +71,7 @@ def test_conv3x3_fwd_fused_fc_fp32(C, B):
     y = torch.empty(B, H, W, 64, device=dev)
     nblk = C.conv3x3_dgrad_blocks(B, H, W, 2)
     part = torch.full((nblk, 2, 10), float("nan"), device=dev)
-    C.conv3x3_fwd(x, w, b, y, True, wfc, part, 10, 2)
+    C.conv3x3_fwd(x, w, b, y, True, fc_weight_frag(wfc, H * W, 64, torch.float32), part, 10, 2)
     logits = fold_block_partials(part, B, H * W, 128) + bfc
     ref = R.fc_nhwc(R.conv3x3(d(x), d(w), d(b)), d(wfc), d(bfc))
     assert relerr(logits, ref) < 1e-5
