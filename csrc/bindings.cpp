@@ -524,13 +524,28 @@ void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, c
   kcheck();
 }
 
-void op_maxpool_fwd(const Tensor& x, Tensor& y, Tensor& amax) {
+// bn (optional): (mean, invstd, gamma, beta) - x is the raw stem conv output and the window
+// reads its BatchNorm + ReLU (no bn_apply pass)
+static BnAffine bn_affine_of(const std::optional<std::vector<Tensor>>& bn, long C) {
+  BnAffine a;
+  if (!bn) return a;
+  TORCH_CHECK(bn->size() == 4, "bn affine: (mean, invstd, gamma, beta)");
+  for (const Tensor& t : *bn) { check(t, "bn affine", at::kFloat); TORCH_CHECK(t.numel() == C, "bn affine size"); }
+  a.mean = (*bn)[0].data_ptr<float>();
+  a.invstd = (*bn)[1].data_ptr<float>();
+  a.gamma = (*bn)[2].data_ptr<float>();
+  a.beta = (*bn)[3].data_ptr<float>();
+  return a;
+}
+
+void op_maxpool_fwd(const Tensor& x, Tensor& y, Tensor& amax, std::optional<std::vector<Tensor>> bn) {
   check(x, "x", at::kBFloat16); check(y, "y", at::kBFloat16); check(amax, "amax", at::kByte);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), OH = y.size(1), OW = y.size(2);
   TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 && y.size(3) == C, "maxpool 3x3/s2/p1 shape");
   TORCH_CHECK(amax.numel() == y.numel(), "amax size");
   TORCH_CHECK(C % 8 == 0 && x.numel() / 8 < (1L << 31), "maxpool: C % 8 (8 channels per thread)");
-  maxpool_fwd(cbf(x), N, H, W, C, OH, OW, bf(y), amax.data_ptr<unsigned char>(), cur_stream());
+  const BnAffine aff = bn_affine_of(bn, C);
+  maxpool_fwd(cbf(x), N, H, W, C, OH, OW, bf(y), amax.data_ptr<unsigned char>(), cur_stream(), &aff);
   kcheck();
 }
 
@@ -785,7 +800,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_set_fused", &bn_bwd_set_fused);
   m.def("bn_bwd_fused_ok", &bn_bwd_fused_ok);
   m.def("bn_bwd_fused_error", &bn_bwd_fused_error, py::arg("reset") = true);
-  m.def("maxpool_fwd", &op_maxpool_fwd);
+  m.def("maxpool_fwd", &op_maxpool_fwd, py::arg("x"), py::arg("y"), py::arg("amax"), py::arg("bn") = py::none());
   m.def("maxpool_bwd", &op_maxpool_bwd, py::arg("dy"), py::arg("amax"), py::arg("dx"),
         py::arg("dy2") = py::none());
   m.def("avgpool_fwd", &op_avgpool_fwd);

@@ -186,8 +186,17 @@ void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int 
 // out == nullptr && mask_beta != nullptr: the ReLU mask is recomputed from x (the BN input)
 // as bf16(x * invstd * gamma + (beta - mean * invstd * gamma)) > 0 - bitwise the sign of
 // the output bn_apply stored (no residual add); saves reading the output tensor
+// A BatchNorm (+ ReLU) applied by the CONSUMER of a conv output while it loads it:
+// value = bf16(relu(x * invstd * gamma + (beta - mean * invstd * gamma))), bitwise what
+// bn_apply would have stored (resnet_ops.hip bn_affine8).  mean == nullptr: none.
+struct BnAffine {
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+};
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
-                 unsigned char* amax, hipStream_t s);
+                 unsigned char* amax, hipStream_t s, const BnAffine* bn = nullptr);
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,
                  int OW, bf16_t* dx, hipStream_t s, const bf16_t* dy2 = nullptr);
 void image_gather_nhwc4(const unsigned char* imgs, const long long* idx, int B, int HW, long N,

@@ -454,15 +454,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
 // ---------------------------------------------------------------- pooling
 // 3x3 / stride 2 / pad 1 max pool, 8 channels per thread (16-B loads); argmax (window
 // index 0..8, first max in row-major window order = torch's tie rule) saved as uint8.
+// AFF: x is the stem conv's raw output and the window reads the BatchNorm + ReLU of it
+// (bn_apply's exact value, bn_affine8): the stem's bn_apply pass (51 MB read + write at
+// batch 32) disappears; the BN backward recomputes its mask from x (MSK 2).
+template <bool AFF>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, int N, int H,
                                                           int W, int C, int OH, int OW,
                                                           bf16_t* __restrict__ y,
-                                                          unsigned char* __restrict__ amax) {
+                                                          unsigned char* __restrict__ amax, BnAffine bn) {
   const int cg = C / 8;
   const int total = N * OH * OW * cg;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int g8 = (i % cg) * 8;
+  float sc[8], sh[8];
+  if constexpr (AFF) bn_affine8(bn.invstd, bn.gamma, bn.mean, bn.beta, g8, sc, sh);
   const int p = i / cg;
   const int n = p / (OH * OW);
   const int r = p - n * OH * OW;
@@ -477,6 +483,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
     if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
       float v[8];
       unpack8(ld8(x + (((long)n * H + ih) * W + iw) * C + g8), v);
+      if constexpr (AFF) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf16_round(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f));
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) { best[j] = v[j]; bi[j] = k; }
@@ -924,10 +934,13 @@ void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int 
 }
 
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
-                 unsigned char* amax, hipStream_t s) {
+                 unsigned char* amax, hipStream_t s, const BnAffine* bn) {
   const long total = (long)N * OH * OW * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, N,
-                     H, W, C, OH, OW, y, amax);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (bn && bn->mean)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<true>, grid, dim3(256), 0, s, x, N, H, W, C, OH, OW, y, amax, *bn);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<false>, grid, dim3(256), 0, s, x, N, H, W, C, OH, OW, y, amax, BnAffine{});
 }
 
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,

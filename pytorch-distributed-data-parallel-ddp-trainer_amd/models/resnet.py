@@ -117,7 +117,7 @@ class ResNet(nn.Module):
 
         if x.dim() == 4 and x.shape[1] == 3:
             x = R.to_nhwc4(x)
-        h = R.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        h = R.conv_bn_act(x, self.conv1, self.bn1, relu=True, defer=True)  # BN + ReLU in the maxpool
         h = R.maxpool3x3s2(h)
         for b in self.blocks():
             h = b.forward_hip(h)

@@ -47,6 +47,9 @@ BN_TAIL = os.environ.get("DDP_AMD_BN_TAIL", "0") == "1"
 # BatchNorm backward of a ReLU without a residual add: the mask recomputed from the BN input
 # (no read of the saved output in either pass); DDP_AMD_BN_MASK_FROM_Y=0 reads the output
 MASK_FROM_Y = os.environ.get("DDP_AMD_BN_MASK_FROM_Y", "1") != "0"
+# the stem's BatchNorm + ReLU applied by the maxpool's loads (no bn_apply pass);
+# DDP_AMD_DEFER_BN=0 materialises it.  Needs MASK_FROM_Y (the output is never stored).
+DEFER_BN = os.environ.get("DDP_AMD_DEFER_BN", "1") != "0" and MASK_FROM_Y
 
 
 _configured = False
@@ -115,7 +118,7 @@ def _weight_bf16(w: torch.Tensor) -> torch.Tensor:
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, running_mean, running_var, nbt, res, stride, pad, relu,
-                training, momentum, eps, stash=None):
+                training, momentum, eps, stash=None, defer=False):
         N, H, W_, Cin = x.shape
         Cout, KH, KW, wcin = w.shape
         stem = Cin == 4 and wcin == 3
@@ -150,9 +153,17 @@ class _ConvBNAct(torch.autograd.Function):
             else:
                 mean = running_mean.float().contiguous()
                 invstd = torch.rsqrt(running_var.float() + eps).contiguous()
-        out = torch.empty_like(y)
-        C.bn_apply(y, mean, invstd, gamma.detach(), beta.detach(),
-                   res.contiguous() if res is not None else None, bool(relu), out)
+        if defer:
+            # the consumer applies BN + ReLU while loading (BnAffine); the returned tensor
+            # holds the RAW conv output, tagged with the affine, and stands for relu(bn(y))
+            # in autograd (its gradient is d loss / d relu(bn(y)), as without deferral)
+            assert relu and res is None, "deferred BatchNorm: ReLU, no residual add"
+            out = y
+            out._ddp_amd_bn = [mean, invstd, gamma.detach(), beta.detach()]
+        else:
+            out = torch.empty_like(y)
+            C.bn_apply(y, mean, invstd, gamma.detach(), beta.detach(),
+                       res.contiguous() if res is not None else None, bool(relu), out)
         # the backward's ReLU mask: without a residual add it is recomputed from y (bitwise
         # the sign of `out`, resnet_ops.hip bn_mask8), so `out` is kept only for a join
         keep_out = bool(relu) and (res is not None or not MASK_FROM_Y)
@@ -215,7 +226,7 @@ class _ConvBNAct(torch.autograd.Function):
             else:
                 ctx.stash.put(dx)
                 dx = None
-        return dx, rw, rg, rb, None, None, None, dres, None, None, None, None, None, None, None
+        return dx, rw, rg, rb, None, None, None, dres, None, None, None, None, None, None, None, None
 
 
 class _MaxPool(torch.autograd.Function):
@@ -225,7 +236,8 @@ class _MaxPool(torch.autograd.Function):
         OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         y = torch.empty(N, OH, OW, Cc, dtype=BF16, device=x.device)
         am = torch.empty(N, OH, OW, Cc, dtype=torch.uint8, device=x.device)
-        _C().maxpool_fwd(x.contiguous(), y, am)
+        # a deferred BatchNorm + ReLU of the producer (conv_bn_act(defer=True)) is applied here
+        _C().maxpool_fwd(x.contiguous(), y, am, getattr(x, "_ddp_amd_bn", None))
         ctx.save_for_backward(am)
         ctx.shape = x.shape
         return y
@@ -301,12 +313,16 @@ class _LinearHead(torch.autograd.Function):
         return dx, rw, rb
 
 
-def conv_bn_act(x, conv, bn, res=None, relu=True, stash=None):
+def conv_bn_act(x, conv, bn, res=None, relu=True, stash=None, defer=False):
+    """conv -> BatchNorm -> (+ res) -> (ReLU).  defer=True (ReLU, no residual): the BN + ReLU
+    is left to the consumer's loads (maxpool3x3s2 reads the tag); the result must only be
+    passed to such a consumer."""
     training = bn.training
     nbt = bn.num_batches_tracked if (training and bn.track_running_stats) else None
     momentum = bn.momentum if bn.momentum is not None else 0.1
     return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                            nbt, res, conv.stride, conv.padding, relu, training, momentum, bn.eps, stash)
+                            nbt, res, conv.stride, conv.padding, relu, training, momentum, bn.eps, stash,
+                            bool(defer) and DEFER_BN)
 
 
 def maxpool3x3s2(x):

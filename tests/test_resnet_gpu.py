@@ -543,6 +543,57 @@ def test_resnet18_direct_grads_and_bf16_weight_copy():
                        F.pad(b.conv1.weight.detach().to(torch.bfloat16), (0, 1)))
 
 
+@pytest.mark.parametrize("H", [112, 9])
+def test_maxpool_reads_deferred_batchnorm_bitwise(C, H):
+    """maxpool_fwd with the producer's BatchNorm + ReLU applied on load (BnAffine) ==
+    bn_apply then maxpool: outputs and argmax bit for bit (ties and exact zeros included:
+    channel 0 is all-zero after the ReLU)."""
+    N, Cc = 2, 64
+    yraw = rnd(N, H, H, Cc, seed=51)
+    mean = torch.randn(Cc, device=dev) * 0.1
+    invstd = torch.rand(Cc, device=dev) + 0.5
+    gamma = torch.rand(Cc, device=dev) + 0.5
+    beta = torch.randn(Cc, device=dev) * 0.3
+    beta[0] = -100.0
+    out = torch.empty_like(yraw)
+    C.bn_apply(yraw, mean, invstd, gamma, beta, None, True, out)
+    OH = (H - 1) // 2 + 1
+    y0, y1 = (torch.empty(N, OH, OH, Cc, dtype=BF, device=dev) for _ in range(2))
+    a0, a1 = (torch.empty(N, OH, OH, Cc, dtype=torch.uint8, device=dev) for _ in range(2))
+    C.maxpool_fwd(out, y0, a0)
+    C.maxpool_fwd(yraw, y1, a1, [mean, invstd, gamma, beta])
+    assert torch.equal(y0, y1) and torch.equal(a0, a1)
+    assert (y1[..., 0] == 0).all()
+
+
+def test_resnet18_deferred_stem_bn_bitwise(monkeypatch):
+    """The stem's BatchNorm + ReLU deferred into the maxpool's loads (no bn_apply pass, the
+    BN backward's mask recomputed from the conv output) trains bit-identically to the
+    materialised chain: loss, every gradient and the BN running statistics."""
+    from ddp_amd.models import resnet18
+    from ddp_amd.ops import CrossEntropyLoss, resnet_fn
+
+    torch.manual_seed(0)
+    base = resnet18(num_classes=10).to(dev)
+    x = torch.randn(4, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (4,), device=dev)
+    res = []
+    for defer in (False, True):
+        monkeypatch.setattr(resnet_fn, "DEFER_BN", defer)
+        m = resnet18(num_classes=10).to(dev)
+        m.load_state_dict(base.state_dict())
+        loss = CrossEntropyLoss()(m(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                    {n: b.clone() for n, b in m.named_buffers()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n
+    for n in res[0][2]:
+        assert torch.equal(res[0][2][n], res[1][2][n]), n
+
+
 def test_graphed_step_equals_eager():
     """GraphedStep (whole training step in one hipGraph: forward, backward with direct
     gradients, FusedSGD with the bf16 weight copy, BN running stats) replays exactly the
