@@ -336,6 +336,20 @@ ConvPlan plan_of(const ConvGeom& g, bool dgrad, int bp, int bc, int splits, int 
   return conv_gemm_plan(g, dgrad, bp, bc, splits, parity, halo);
 }
 
+// bn (optional): (mean, invstd, gamma, beta) - x is the raw stem conv output and the window
+// reads its BatchNorm + ReLU (no bn_apply pass)
+static BnAffine bn_affine_of(const std::optional<std::vector<Tensor>>& bn, long C) {
+  BnAffine a;
+  if (!bn) return a;
+  TORCH_CHECK(bn->size() == 4, "bn affine: (mean, invstd, gamma, beta)");
+  for (const Tensor& t : *bn) { check(t, "bn affine", at::kFloat); TORCH_CHECK(t.numel() == C, "bn affine size"); }
+  a.mean = (*bn)[0].data_ptr<float>();
+  a.invstd = (*bn)[1].data_ptr<float>();
+  a.gamma = (*bn)[2].data_ptr<float>();
+  a.beta = (*bn)[3].data_ptr<float>();
+  return a;
+}
+
 // (bp, bc, splits, stat_rows) of the plan; for dgrad X = dX-shaped layer input, Y = dY
 py::tuple op_conv_gemm_plan(const Tensor& X, const Tensor& Y, int KH, int KW, int stride, int pad,
                             bool dgrad, int bp, int bc, int splits, int parity, int halo) {
@@ -346,7 +360,8 @@ py::tuple op_conv_gemm_plan(const Tensor& X, const Tensor& Y, int KH, int KW, in
 
 void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> bias, Tensor& Y,
                       int KH, int KW, int stride, int pad, bool relu, std::optional<Tensor> stats,
-                      std::optional<Tensor> part, int bp, int bc, int splits, int halo) {
+                      std::optional<Tensor> part, int bp, int bc, int splits, int halo,
+                      std::optional<std::vector<Tensor>> bn) {
   check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(Y, "Y", at::kBFloat16);
   const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
   TORCH_CHECK(g.Cin % 32 == 0 || (g.Cin == 4 && g.Cout % 64 == 0), "conv_gemm: Cin % 32 (or stem Cin=4)");
@@ -368,7 +383,9 @@ void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> b
     TORCH_CHECK(part->numel() >= (long)pl.splits * g.N * g.OH * g.OW * g.Cout, "part workspace too small");
     pt = part->data_ptr<float>();
   }
-  conv_gemm_fwd(g, pl, cbf(X), cbf(Wt), bp_, bf(Y), relu, st, pt, cur_stream());
+  const BnAffine aff = bn_affine_of(bn, g.Cin);
+  TORCH_CHECK(!aff.mean || (pl.halo && g.Cin <= 512), "conv_gemm_fwd: an input BatchNorm affine needs the halo plan");
+  conv_gemm_fwd(g, pl, cbf(X), cbf(Wt), bp_, bf(Y), relu, st, pt, cur_stream(), nullptr, &aff);
   kcheck();
 }
 
@@ -398,7 +415,7 @@ int op_conv_gemm_wgrad_chunks(const Tensor& X, const Tensor& dY, int KH, int KW,
 }
 
 void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& out, int KH, int KW, int stride,
-                        int pad, int ppc, bool accum, int ks) {
+                        int pad, int ppc, bool accum, int ks, std::optional<std::vector<Tensor>> bn) {
   check(dY, "dY", at::kBFloat16); check(X, "X", at::kBFloat16); check(out, "out", at::kFloat);
   const ConvGeom g = geom_of(X, dY, KH, KW, stride, pad);
   TORCH_CHECK((g.Cin % 64 == 0 || g.Cin == 4) && g.Cout % 64 == 0, "conv_gemm_wgrad: Cin % 64 (or 4), Cout % 64");
@@ -407,7 +424,10 @@ void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& out, int KH, 
   const long row = (long)g.Cout * KH * KW * (g.Cin == 4 ? 3 : g.Cin);
   TORCH_CHECK(out.numel() >= (long)conv_gemm_wgrad_chunks(g, ppc) * row, "wgrad output too small");
   TORCH_CHECK(ks == 0 || ks == 32 || ks == 64, "conv_gemm_wgrad: ks 0 (auto), 32 or 64");
-  conv_gemm_wgrad(g, cbf(dY), cbf(X), out.data_ptr<float>(), ppc, accum, cur_stream(), ks);
+  const BnAffine aff = bn_affine_of(bn, g.Cin);
+  TORCH_CHECK(!aff.mean || conv_gemm_wgrad_uses_halo(g, ppc),
+              "conv_gemm_wgrad: an input BatchNorm affine needs the halo weight gradient");
+  conv_gemm_wgrad(g, cbf(dY), cbf(X), out.data_ptr<float>(), ppc, accum, cur_stream(), ks, &aff);
   kcheck();
 }
 
@@ -522,20 +542,6 @@ void op_bn_bwd(const Tensor& dout, std::optional<Tensor> out, const Tensor& x, c
          gamma.data_ptr<float>(), (float)count, ws.data_ptr<float>(), sums.data_ptr<float>(), dg, db,
          accum, bf(dx), dr, cur_stream(), obf(dout2, "dout2"), mb);
   kcheck();
-}
-
-// bn (optional): (mean, invstd, gamma, beta) - x is the raw stem conv output and the window
-// reads its BatchNorm + ReLU (no bn_apply pass)
-static BnAffine bn_affine_of(const std::optional<std::vector<Tensor>>& bn, long C) {
-  BnAffine a;
-  if (!bn) return a;
-  TORCH_CHECK(bn->size() == 4, "bn affine: (mean, invstd, gamma, beta)");
-  for (const Tensor& t : *bn) { check(t, "bn affine", at::kFloat); TORCH_CHECK(t.numel() == C, "bn affine size"); }
-  a.mean = (*bn)[0].data_ptr<float>();
-  a.invstd = (*bn)[1].data_ptr<float>();
-  a.gamma = (*bn)[2].data_ptr<float>();
-  a.beta = (*bn)[3].data_ptr<float>();
-  return a;
 }
 
 void op_maxpool_fwd(const Tensor& x, Tensor& y, Tensor& amax, std::optional<std::vector<Tensor>> bn) {
@@ -752,7 +758,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_gemm_fwd", &op_conv_gemm_fwd, py::arg("X"), py::arg("W"), py::arg("bias"), py::arg("Y"),
         py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("relu") = false,
         py::arg("stats") = py::none(), py::arg("part") = py::none(), py::arg("bp") = 0, py::arg("bc") = 0,
-        py::arg("splits") = 0, py::arg("halo") = -1);
+        py::arg("splits") = 0, py::arg("halo") = -1, py::arg("bn") = py::none());
   m.def("conv_gemm_dgrad", &op_conv_gemm_dgrad, py::arg("dY"), py::arg("W"), py::arg("Xact"), py::arg("dX"),
         py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("part") = py::none(),
         py::arg("bp") = 0, py::arg("bc") = 0, py::arg("splits") = 0, py::arg("parity") = -1,
@@ -772,7 +778,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("conv_gemm_wgrad", &op_conv_gemm_wgrad, py::arg("dY"), py::arg("X"), py::arg("out"), py::arg("KH"),
         py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("ppc"), py::arg("accum") = false,
-        py::arg("ks") = 0);
+        py::arg("ks") = 0, py::arg("bn") = py::none());
+  m.def("conv_gemm_wgrad_uses_halo", [](const Tensor& X, const Tensor& dY, int KH, int KW, int stride, int pad,
+                                        int ppc) { return conv_gemm_wgrad_uses_halo(geom_of(X, dY, KH, KW, stride, pad), ppc); });
   m.def("conv_gemm_plan", &op_conv_gemm_plan, py::arg("X"), py::arg("Y"), py::arg("KH"), py::arg("KW"),
         py::arg("stride"), py::arg("pad"), py::arg("dgrad") = false, py::arg("bp") = 0, py::arg("bc") = 0,
         py::arg("splits") = 0, py::arg("parity") = -1, py::arg("halo") = -1);

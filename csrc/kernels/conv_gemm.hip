@@ -793,11 +793,13 @@ int conv_gemm_stat_colblocks(const ConvGeom& g, const ConvPlan& pl) {
 
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,
                    const float* bias, bf16_t* Y, bool relu, float* stats, float* part, hipStream_t s,
-                   const BnFin* fin) {
+                   const BnFin* fin, const BnAffine* aff) {
   if (fin && (!stats || fin->rows != conv_gemm_stat_rows(g, pl) || fin->C != g.Cout))
     throw std::runtime_error("conv_gemm_fwd: BatchNorm tail needs the stats slab of this plan");
+  if (aff && aff->mean && !pl.halo)
+    throw std::runtime_error("conv_gemm_fwd: an input BatchNorm affine needs the halo plan");
   if (pl.halo) {  // no bias / ReLU epilogue on this path (the host plans it off then)
-    conv_halo_fwd(g, pl.bp, pl.bc, pl.splits, X, Wt, Y, stats, part, s, pl.splits > 1 ? nullptr : fin);
+    conv_halo_fwd(g, pl.bp, pl.bc, pl.splits, X, Wt, Y, stats, part, s, pl.splits > 1 ? nullptr : fin, aff);
     if (pl.splits > 1) splitk_reduce(part, pl.splits, (long)g.N * g.OH * g.OW, g.Cout, nullptr, Y, stats, s, fin);
     return;
   }
@@ -944,14 +946,20 @@ int conv_gemm_wgrad_ppc(const ConvGeom& g) {
 // barriers per MFMA but measured neutral on every ResNet-18 layer (conv_sweep.jsonl,
 // "auto/ks32" vs "auto/ks64"): the 64 x 64 tiles are bound by L2 traffic - dY and the
 // gathered X are re-read once per tap block - not by the barrier.
+bool conv_gemm_wgrad_uses_halo(const ConvGeom& g, int px_per_chunk) {
+  return wgrad_use_halo(g) && px_per_chunk % (g.W * conv_halo_wgrad_row_quantum(g)) == 0;  // whole rows
+}
+
 void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out,
-                     int px_per_chunk, bool accum, hipStream_t s, int ks) {
+                     int px_per_chunk, bool accum, hipStream_t s, int ks, const BnAffine* aff) {
   const int ch = conv_gemm_wgrad_chunks(g, px_per_chunk);
   const int acc = (accum && ch == 1) ? 1 : 0;
-  if (wgrad_use_halo(g) && px_per_chunk % (g.W * conv_halo_wgrad_row_quantum(g)) == 0) {  // whole rows
-    conv_halo_wgrad(g, dY, X, out, px_per_chunk / g.W, acc != 0, s, wgrad_halo_cit(g));
+  if (conv_gemm_wgrad_uses_halo(g, px_per_chunk)) {
+    conv_halo_wgrad(g, dY, X, out, px_per_chunk / g.W, acc != 0, s, wgrad_halo_cit(g), aff);
     return;
   }
+  if (aff && aff->mean)
+    throw std::runtime_error("conv_gemm_wgrad: an input BatchNorm affine needs the halo weight gradient");
   int bm, bn;
   wgrad_tile(g, &bm, &bn);
   if (ks != 32 && ks != 64) ks = 32;

@@ -14,6 +14,9 @@
 // 128-pixel column tile of which R*W are live), same epilogues: bf16 NHWC store with the
 // per-block BatchNorm sum / sum-of-squares partials, or fp32 split-K partials for
 // splitk_reduce.  K splits run over channel chunks (grid.z).
+#include <stdexcept>
+
+#include "kernels/bn_affine.h"
 #include "kernels/bn_tail.h"
 #include "kernels/common.h"
 #include "kernels/launchers.h"
@@ -25,13 +28,16 @@ constexpr int HL_RS = 48;   // LDS row stride (elements) per pixel / weight row:
 constexpr int HL_BP = 128;  // pixel columns of the MFMA tile
 constexpr int HL_MAXPX = 232;     // largest halo: (R+2) x (W+2) = 4 x 58 at W = 56 (R = 2)
 
-template <int BC, int BP, bool STATS, bool PART>
+// AFF: X is the producer conv's RAW output; the halo staging applies its BatchNorm + ReLU
+// (BnAffine, bitwise bn_apply's value; the zero padding stays zero) - the producer's
+// bn_apply pass disappears.  The per-channel sc / sh table sits in LDS (4 KB).
+template <int BC, int BP, bool STATS, bool PART, bool AFF = false>
 __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ Wt,
                                                                  bf16_t* __restrict__ Y,
                                                                  float* __restrict__ stats,
                                                                  float* __restrict__ part, int R,
-                                                                 int chunks_per_split, BnFin fin) {
+                                                                 int chunks_per_split, BnFin fin, BnAffine bn) {
   constexpr int TCO = BC / 32, TPX = BP / 32;
   constexpr int HCH = (HL_MAXPX * 4 + 255) / 256;  // 16-B halo chunks per thread
   // weights of one kernel row (3 taps) per K-step: 3 MFMA K-steps between barriers
@@ -53,7 +59,12 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
   const int KWC = 9 * Cin;
 
   // halo chunk h of this thread: pixel hp = (tid + 256u) / 4, quarter (8 channels) = & 3
+  // AFF: the loaded chunks that lie inside the image (hin) and the raw BatchNorm parameters
+  // of this thread's 8 channels of the chunk travel with the halo registers
+  unsigned hin = 0;
+  BnRaw8 braw;
   auto load_halo = [&](int ch, bf16x8* rh) {
+    if constexpr (AFF) hin = 0;
 #pragma unroll
     for (int u = 0; u < HCH; ++u) {
       const int e = tid + 256 * u;
@@ -62,17 +73,29 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
       if (hp < HPX) {
         const int hr = hp / HW2, hc = hp - hr * HW2;
         const int ih = oh0 - 1 + hr, iw = hc - 1;
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
           rh[u] = ld8(X + (((long)n_ * H + ih) * W + iw) * Cin + ch * HL_KS + qq * 8);
+          if constexpr (AFF) hin |= 1u << u;
+        }
       }
     }
+    if constexpr (AFF) braw = bn_raw8(bn.invstd, bn.gamma, bn.mean, bn.beta, ch * HL_KS + (tid & 3) * 8);
   };
-  auto store_halo = [&](int buf, const bf16x8* rh) {
+  auto store_halo = [&](int buf, const bf16x8* rh, int ch) {
+    (void)ch;
+    float sc[8], sh[8];
+    if constexpr (AFF) bn_affine8_of(braw, sc, sh);  // this thread's 8 channels (qq = tid & 3)
 #pragma unroll
     for (int u = 0; u < HCH; ++u) {
       const int e = tid + 256 * u;
       const int hp = e >> 2, qq = e & 3;
-      if (hp < HPX) *reinterpret_cast<bf16x8*>(&sH[buf][hp * HL_RS + qq * 8]) = rh[u];
+      if (hp < HPX) {
+        bf16x8 v = rh[u];
+        if constexpr (AFF) {
+          if ((hin >> u) & 1u) v = bn_relu8(v, sc, sh);
+        }
+        *reinterpret_cast<bf16x8*>(&sH[buf][hp * HL_RS + qq * 8]) = v;
+      }
     }
   };
   // weight rows of kernel row kh: sA row = t * BC + co (t = kw), 32 channels each
@@ -113,7 +136,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
   if (c_beg < c_end) {
     load_halo(c_beg, rh);
     load_w(c_beg, 0, ra);
-    store_halo(0, rh);
+    store_halo(0, rh, c_beg);
     store_w(0, ra);
   }
   __syncthreads();
@@ -142,7 +165,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
 #pragma unroll
           for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
       }
-      if (last && next_chunk) store_halo(hb ^ 1, rh);  // buffer hb^1 was last read a chunk ago
+      if (last && next_chunk) store_halo(hb ^ 1, rh, ch + 1);  // buffer hb^1 was last read a chunk ago
       if (more) store_w(cur ^ 1, ra);
       __syncthreads();
     }
@@ -409,14 +432,21 @@ bool conv_halo_fits(const ConvGeom& g, int bp) {
 int conv_halo_rows(const ConvGeom& g, int bp) { return bp / g.W; }
 
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
-                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin) {
+                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin, const BnAffine* aff) {
   const BnFin f = (fin && stats && splits <= 1) ? *fin : BnFin{};
+  const bool af = aff && aff->mean;
+  if (af && g.Cin > 512) throw std::runtime_error("conv_halo_fwd: input BatchNorm affine needs Cin <= 512");
+  const BnAffine a = af ? *aff : BnAffine{};
   const int R = conv_halo_rows(g, bp);
   const int RG = (g.H + R - 1) / R;
   const int nch = g.Cin / HL_KS;
   const int cps = (nch + splits - 1) / splits;
   const dim3 grid(g.N * RG, g.Cout / bc, splits);
-#define HLF(BC, BP, ST, PT) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f)
+#define HLF(BC, BP, ST, PT)                                                                                     \
+  do {                                                                                                          \
+    if (af) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, true>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
+    else hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, false>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
+  } while (0)
 #define HLF_BP(BC, BP)                                  \
   if (splits > 1) HLF(BC, BP, false, true);             \
   else if (stats) HLF(BC, BP, true, false);             \
@@ -461,11 +491,14 @@ size_t conv_halo_wgrad_lds() {
 // CIT: input channels per block (32: 4 waves = 2 co pairs x 2 ci halves; 16: 4 waves x one
 // 16-wide co tile - twice the blocks per chunk, so half the chunks and slab bytes for the
 // same launch size, at twice the dY re-reads)
-template <int CIT>
+// AFF: X is the producer conv's RAW output; the staging applies its BatchNorm + ReLU
+// (BnAffine) to the in-image halo positions - each thread's 8 input channels are fixed
+// (chunk c % (CIT / 8) == tid % (CIT / 8)), so its sc / sh are computed once.
+template <int CIT, bool AFF = false>
 __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                                       const bf16_t* __restrict__ X,
                                                                       float* __restrict__ out, int rows_per_chunk,
-                                                                      int accum) {
+                                                                      int accum, BnAffine bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = g.H, W = g.W, Cin = g.Cin, Cout = g.Cout;
   const int Wp = hwg_wp(W), R = HWG_SLOTS / Wp, XW = Wp + 2;
@@ -503,10 +536,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
     const int k = hr / (Hs + 2), loc = hr - k * (Hs + 2);
     xgeo[u] = c < nxc ? ((unsigned)k | (unsigned)loc << 8 | (unsigned)cc << 16 | (unsigned)chk << 24) : 0xffu;
   }
+  float asc[8], ash[8];
+  unsigned xin = 0;  // AFF: bit u = X chunk u of the loaded group lies inside an image
   auto load = [&](int r, int cnt) {
     // group start: image n0, row h0 (stacked groups start on an image: h0 = 0, segment k
     // is image n0 + k; a single-image group has k = 0 only)
     const int n0 = r / H, h0 = r - n0 * H;
+    if constexpr (AFF) xin = 0;
 #pragma unroll
     for (int u = 0; u < HWG_DYC; ++u) {
       const int rr = dgeo[u] & 0xff, col = dgeo[u] >> 8, ch = ((tid + 256 * u) & 7) * 8;
@@ -519,8 +555,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
       const int n = n0 + k, hh = h0 - 1 + loc, ww = cc - 1;
       // segments past the group's rows (a partial stacked group at the end of a chunk:
       // their images may not exist) stay zero, like the halo outside the image
-      vx[u] = (k != 0xff && k * Hs < cnt && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W)
-                  ? ld8(X + ((long)(n * H + hh) * W + ww) * Cin + ci0 + ch) : zero8();
+      const bool in = k != 0xff && k * Hs < cnt && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+      vx[u] = in ? ld8(X + ((long)(n * H + hh) * W + ww) * Cin + ci0 + ch) : zero8();
+      if constexpr (AFF) xin |= (in ? 1u : 0u) << u;
     }
   };
   auto store = [&]() {
@@ -532,7 +569,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
 #pragma unroll
     for (int u = 0; u < HWG_XC; ++u) {
       const int c = tid + 256 * u;
-      if (c < nxc) *reinterpret_cast<bf16x8*>(sX + (c / XCP) * HWG_XS + (c % XCP) * 8) = vx[u];
+      bf16x8 v = vx[u];
+      if constexpr (AFF) {
+        if ((xin >> u) & 1u) v = bn_relu8(v, asc, ash);
+      }
+      if (c < nxc) *reinterpret_cast<bf16x8*>(sX + (c / XCP) * HWG_XS + (c % XCP) * 8) = v;
     }
   };
   // wave tile: co pair (wave >> 1: 2 x 16 co) x ci half (wave & 1: 16 ci), all 9 taps
@@ -548,6 +589,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
   const int ldsX = HWG_SLOTS * HWG_DS;  // element offset of sX
   int r0 = rbeg, cnt = r0 < rend ? group_rows(r0) : 0;
   if (cnt > 0) load(r0, cnt);
+  // (after the first group's loads are in flight: the parameters land behind them)
+  if constexpr (AFF) bn_affine8(bn.invstd, bn.gamma, bn.mean, bn.beta, ci0 + (tid % XCP) * 8, asc, ash);
   while (cnt > 0) {
     store();
     __syncthreads();
@@ -616,22 +659,28 @@ int conv_halo_wgrad_row_quantum(const ConvGeom& g) {
 }
 
 void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out, int rows_per_chunk,
-                     bool accum, hipStream_t s, int cit) {
+                     bool accum, hipStream_t s, int cit, const BnAffine* aff) {
+  const bool af = aff && aff->mean;
+  const BnAffine a = af ? *aff : BnAffine{};
   const int chunks = (g.N * g.H + rows_per_chunk - 1) / rows_per_chunk;
   const dim3 grid(g.Cout / 64, g.Cin / cit, chunks);
   const size_t lds = conv_halo_wgrad_lds();
   static bool opted = false;
   if (!opted) {
-    for (const void* k : {reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<32>),
-                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<16>)})
+    for (const void* k : {reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<32, false>),
+                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<16, false>),
+                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<32, true>),
+                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<16, true>)})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     opted = true;
   }
   const int acc = accum && chunks == 1 ? 1 : 0;
   if (cit == 16)
-    hipLaunchKernelGGL(conv3x3s1_halo_wgrad_kernel<16>, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc);
+    { if (af) hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<16, true>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a);
+      else hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<16, false>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a); }
   else
-    hipLaunchKernelGGL(conv3x3s1_halo_wgrad_kernel<32>, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc);
+    { if (af) hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<32, true>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a);
+      else hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<32, false>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a); }
 }
 
 }  // namespace ddp_amd

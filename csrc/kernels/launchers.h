@@ -104,6 +104,15 @@ void conv3x3_wgrad(const float* dY, const float* Yact, const float* X, float* sl
 struct ConvGeom {
   int N, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad;
 };
+// A BatchNorm (+ ReLU) applied by the CONSUMER of a conv output while it loads it:
+// value = bf16(relu(x * invstd * gamma + (beta - mean * invstd * gamma))), bitwise what
+// bn_apply would have stored (resnet_ops.hip bn_affine8).  mean == nullptr: none.
+struct BnAffine {
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+};
 // BatchNorm finalisation folded into the stats-producing launch (kernels/bn_tail.h):
 // tickets == nullptr means "stats only" (a separate bn_finalize follows)
 struct BnFin {
@@ -134,7 +143,8 @@ int conv_halo_rows(const ConvGeom& g, int bp);
 bool conv_halo_wgrad_ok(const ConvGeom& g);
 int conv_halo_wgrad_row_quantum(const ConvGeom& g);  // rows per chunk must be a multiple
 void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out, int rows_per_chunk,
-                     bool accum, hipStream_t s, int cit = 32);  // cit: input channels per block (16 | 32)
+                     bool accum, hipStream_t s, int cit = 32,  // cit: input channels per block (16 | 32)
+                     const BnAffine* aff = nullptr);           // aff: X is raw, BN + ReLU applied on load
 // wgrad plan overrides for sweeps / A-B: halo 0 = never, 1 / 2 = every eligible stride-1
 // 3x3 layer (default 1); target = blocks per launch
 void conv_gemm_wgrad_set_halo(int halo, int target, int cit = 0);  // cit 0 = auto, 16, 32
@@ -142,14 +152,15 @@ void conv_gemm_wgrad_set_halo(int halo, int target, int cit = 0);  // cit 0 = au
 // whole-row chunks for the halo kernel
 bool conv_gemm_wgrad_ppc_ok(const ConvGeom& g, int ppc);
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
-                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin = nullptr);
+                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin = nullptr,
+                   const BnAffine* aff = nullptr);
 void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* dY, const bf16_t* Wt,
                      const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s);
 int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl);  // BN stats slab rows (fwd)
 // splits > 1: `part` = fp32 workspace [splits][P][C]; no bias / ReLU on the split path
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,
                    const float* bias, bf16_t* Y, bool relu, float* stats, float* part, hipStream_t s,
-                   const BnFin* fin = nullptr);
+                   const BnFin* fin = nullptr, const BnAffine* aff = nullptr);  // aff: halo plans only
 // column blocks of the stats producer (its ticket strips) for a BnFin of this plan
 int conv_gemm_stat_colblocks(const ConvGeom& g, const ConvPlan& pl);
 // W: the OHWI forward weight itself (read transposed through LDS)
@@ -162,7 +173,10 @@ int conv_gemm_wgrad_ppc(const ConvGeom& g);    // tuned pixels per chunk
 // one chunk: out = the gradient ([Cout][T][Cin], stem: [Cout][T][3]), `accum` adds to it;
 // several: out = slab [chunks][...] for grad_reduce
 void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float* out,
-                     int px_per_chunk, bool accum, hipStream_t s, int ks = 0);
+                     int px_per_chunk, bool accum, hipStream_t s, int ks = 0,
+                     const BnAffine* aff = nullptr);  // aff: only where the halo kernel runs
+// whether conv_gemm_wgrad runs the halo kernel for this layer at this chunking
+bool conv_gemm_wgrad_uses_halo(const ConvGeom& g, int px_per_chunk);
 
 // ---- ResNet ops (resnet_ops.hip) -----------------------------------------------------
 int bn_finalize_groups(int rows);  // ws of bn_finalize: [groups][2][C]
@@ -186,15 +200,6 @@ void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int 
 // out == nullptr && mask_beta != nullptr: the ReLU mask is recomputed from x (the BN input)
 // as bf16(x * invstd * gamma + (beta - mean * invstd * gamma)) > 0 - bitwise the sign of
 // the output bn_apply stored (no residual add); saves reading the output tensor
-// A BatchNorm (+ ReLU) applied by the CONSUMER of a conv output while it loads it:
-// value = bf16(relu(x * invstd * gamma + (beta - mean * invstd * gamma))), bitwise what
-// bn_apply would have stored (resnet_ops.hip bn_affine8).  mean == nullptr: none.
-struct BnAffine {
-  const float* mean = nullptr;
-  const float* invstd = nullptr;
-  const float* gamma = nullptr;
-  const float* beta = nullptr;
-};
 void maxpool_fwd(const bf16_t* x, int N, int H, int W, int C, int OH, int OW, bf16_t* y,
                  unsigned char* amax, hipStream_t s, const BnAffine* bn = nullptr);
 void maxpool_bwd(const bf16_t* dy, const unsigned char* amax, int N, int H, int W, int C, int OH,

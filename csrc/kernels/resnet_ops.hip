@@ -14,6 +14,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "kernels/bn_affine.h"
 #include "kernels/bn_tail.h"
 #include "kernels/common.h"
 #include "kernels/launchers.h"
@@ -159,22 +160,7 @@ __device__ __forceinline__ uint4 pack8(const float* v) {
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
-// The BatchNorm affine of 8 channels: sc = invstd * gamma, sh = beta - mean * sc (explicit
-// fma) - ONE definition, so the backward's recomputed ReLU mask (MSK 2 below) sees exactly
-// the values bn_apply stored.
-__device__ __forceinline__ void bn_affine8(const float* invstd, const float* gamma, const float* mean,
-                                           const float* beta, int c0, float* sc, float* sh) {
-  float g[8], mu[8], be[8];
-  ld8f(invstd + c0, sc);
-  ld8f(gamma + c0, g);
-  ld8f(mean + c0, mu);
-  ld8f(beta + c0, be);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] *= g[j];
-    sh[j] = fmaf(-mu[j], sc[j], be[j]);
-  }
-}
+// (bn_affine8: kernels/bn_affine.h - shared with the consumer-side applications)
 
 // y = act(x * sc + sh [+ res]), sc = invstd * gamma, sh = beta - mean * sc; 8 channels per
 // thread.  The grid stride is a multiple of C/8 (which divides 256), so a thread's

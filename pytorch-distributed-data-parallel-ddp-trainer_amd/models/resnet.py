@@ -69,7 +69,7 @@ class BasicBlock(nn.Module):
         # x feeds two branches: the residual one hands its gradient to x's producer, which
         # adds it inside its own backward (no separate gradient-add kernel)
         stash = attach_stash(x) if torch.is_grad_enabled() and x.requires_grad else None
-        out = conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        out = conv_bn_act(x, self.conv1, self.bn1, relu=True, defer=True)  # BN + ReLU in conv2's loads
         if self.downsample is not None:
             idt = conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False, stash=stash)
             return conv_bn_act(out, self.conv2, self.bn2, res=idt, relu=True)

@@ -47,8 +47,10 @@ BN_TAIL = os.environ.get("DDP_AMD_BN_TAIL", "0") == "1"
 # BatchNorm backward of a ReLU without a residual add: the mask recomputed from the BN input
 # (no read of the saved output in either pass); DDP_AMD_BN_MASK_FROM_Y=0 reads the output
 MASK_FROM_Y = os.environ.get("DDP_AMD_BN_MASK_FROM_Y", "1") != "0"
-# the stem's BatchNorm + ReLU applied by the maxpool's loads (no bn_apply pass);
-# DDP_AMD_DEFER_BN=0 materialises it.  Needs MASK_FROM_Y (the output is never stored).
+# BatchNorm + ReLU without a residual add applied by the consumer's loads (no bn_apply
+# pass): the stem's by the maxpool, each block's bn1 by conv2's halo forward and halo
+# weight gradient; DDP_AMD_DEFER_BN=0 materialises them.  Needs MASK_FROM_Y (the output is
+# never stored).
 DEFER_BN = os.environ.get("DDP_AMD_DEFER_BN", "1") != "0" and MASK_FROM_Y
 
 
@@ -133,7 +135,18 @@ class _ConvBNAct(torch.autograd.Function):
         y = torch.empty(N, OH, OW, Cout, dtype=BF16, device=x.device)
         C = _C()
         P = N * OH * OW
-        _, _, splits, rows, _, _ = C.conv_gemm_plan(x, y, KH, KW, stride, pad)
+        _, _, splits, rows, _, halo = C.conv_gemm_plan(x, y, KH, KW, stride, pad)
+        # x may be the producer's deferred BatchNorm + ReLU (raw conv output + affine): the
+        # halo forward and the halo weight gradient apply it while staging; any other plan
+        # gets the activation materialised here
+        xbn = getattr(x, "_ddp_amd_bn", None)
+        if xbn is not None:
+            ppc = C.conv_gemm_wgrad_ppc(x, y, KH, KW, stride, pad)
+            if not (halo == 1 and not (training and BN_TAIL)
+                    and C.conv_gemm_wgrad_uses_halo(x, y, KH, KW, stride, pad, ppc)):
+                xm = torch.empty_like(x)
+                C.bn_apply(x, xbn[0], xbn[1], xbn[2], xbn[3], None, True, xm)
+                x, xbn = xm, None
         part = torch.empty(splits * P * Cout, device=x.device) if splits > 1 else None
         stats = torch.empty(rows, 2, Cout, device=x.device) if training else None
         if training:
@@ -145,7 +158,7 @@ class _ConvBNAct(torch.autograd.Function):
             C.conv_bn_fwd(x, wk, y, KH, KW, stride, pad, stats, part, ws, float(P), eps, momentum,
                           running_mean, running_var, mean, invstd, nbt)
         else:
-            C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part)
+            C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part, bn=xbn)
             if training:
                 ws = torch.empty(C.bn_finalize_groups(rows), 2, Cout, device=x.device)
                 C.bn_finalize(stats, rows, Cout, float(P), eps, momentum, running_mean, running_var,
@@ -169,6 +182,7 @@ class _ConvBNAct(torch.autograd.Function):
         keep_out = bool(relu) and (res is not None or not MASK_FROM_Y)
         ctx.save_for_backward(x, wb, y, out if keep_out else None, mean, invstd)
         ctx.params = (w, gamma, beta)
+        ctx.xbn = xbn
         ctx.cfg = (stride, pad, bool(relu), res is not None, stem, P)
         # stash: this Function is the residual branch of a block; its gradient w.r.t. the
         # block input (res's for a join, x's for a downsample conv) goes to the stash
@@ -212,10 +226,10 @@ class _ConvBNAct(torch.autograd.Function):
         row = w.numel()
         dw = gw if gw is not None else torch.empty(w.shape, device=dev)
         if chunks == 1:
-            C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, gw is not None)
+            C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, gw is not None, bn=ctx.xbn)
         else:
             slab = torch.empty(chunks, row, device=dev)
-            C.conv_gemm_wgrad(dy, x, slab, KH, KW, stride, pad, ppc, False)
+            C.conv_gemm_wgrad(dy, x, slab, KH, KW, stride, pad, ppc, False, bn=ctx.xbn)
             C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, gw is not None)])
         rw = None if gw is not None else dw
         rg, rb = (None, None) if direct_bn else (dgamma, dbeta)
@@ -315,8 +329,8 @@ class _LinearHead(torch.autograd.Function):
 
 def conv_bn_act(x, conv, bn, res=None, relu=True, stash=None, defer=False):
     """conv -> BatchNorm -> (+ res) -> (ReLU).  defer=True (ReLU, no residual): the BN + ReLU
-    is left to the consumer's loads (maxpool3x3s2 reads the tag); the result must only be
-    passed to such a consumer."""
+    is left to the consumer's loads (maxpool3x3s2, or conv_bn_act: halo plans apply it while
+    staging, others materialise it); the result must only be passed to such a consumer."""
     training = bn.training
     nbt = bn.num_batches_tracked if (training and bn.track_running_stats) else None
     momentum = bn.momentum if bn.momentum is not None else 0.1

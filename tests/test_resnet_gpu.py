@@ -566,10 +566,49 @@ def test_maxpool_reads_deferred_batchnorm_bitwise(C, H):
     assert (y1[..., 0] == 0).all()
 
 
+@pytest.mark.parametrize("N,H,Cin,Cout", [(4, 56, 64, 64), (4, 28, 128, 128), (8, 14, 256, 256), (8, 7, 512, 512)])
+def test_halo_conv_reads_deferred_batchnorm_bitwise(C, N, H, Cin, Cout):
+    """conv2 of a BasicBlock staging its input as the producer's BatchNorm + ReLU (BnAffine
+    in the halo forward and the halo weight gradient) == bn_apply first: the forward output,
+    its BatchNorm statistics and the weight gradient bit for bit; the zero padding stays 0."""
+    xraw = rnd(N, H, H, Cin, seed=61)
+    w = rnd(Cout, 3, 3, Cin, scale=0.05, seed=62)
+    dy = rnd(N, H, H, Cout, scale=0.5, seed=63)
+    mean = torch.randn(Cin, device=dev) * 0.1
+    invstd = torch.rand(Cin, device=dev) + 0.5
+    gamma = torch.rand(Cin, device=dev) + 0.5
+    beta = torch.randn(Cin, device=dev) * 0.3
+    bn = [mean, invstd, gamma, beta]
+    xact = torch.empty_like(xraw)
+    C.bn_apply(xraw, mean, invstd, gamma, beta, None, True, xact)
+    outs = []
+    for x, b in ((xact, None), (xraw, bn)):
+        y = torch.empty(N, H, H, Cout, dtype=BF, device=dev)
+        _, _, sp, rows, _, halo = C.conv_gemm_plan(x, y, 3, 3, 1, 1, False, 0, 0, 0, -1, 1)  # halo forced
+        assert halo == 1
+        stats = torch.empty(rows, 2, Cout, device=dev)
+        part = torch.empty(sp * y.numel(), device=dev) if sp > 1 else None
+        C.conv_gemm_fwd(x, w, None, y, 3, 3, 1, 1, False, stats, part, 0, 0, 0, 1, bn=b)
+        ppc = C.conv_gemm_wgrad_ppc(x, dy, 3, 3, 1, 1)
+        assert C.conv_gemm_wgrad_uses_halo(x, dy, 3, 3, 1, 1, ppc)
+        ch = C.conv_gemm_wgrad_chunks(x, dy, 3, 3, 1, 1, ppc)
+        row = Cout * 9 * Cin
+        slab = torch.empty(ch, row, device=dev)
+        C.conv_gemm_wgrad(dy, x, slab, 3, 3, 1, 1, ppc, False, bn=b)
+        dw = torch.zeros(row, device=dev)
+        C.grad_reduce([(slab, row, 0, row, ch, dw, 1.0, False)])
+        torch.cuda.synchronize()
+        outs.append((y, stats, dw))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_resnet18_deferred_stem_bn_bitwise(monkeypatch):
-    """The stem's BatchNorm + ReLU deferred into the maxpool's loads (no bn_apply pass, the
-    BN backward's mask recomputed from the conv output) trains bit-identically to the
-    materialised chain: loss, every gradient and the BN running statistics."""
+    """Every BatchNorm + ReLU without a residual add deferred into its consumer's loads (the
+    stem's into the maxpool, each block's bn1 into conv2's halo forward / weight gradient; no
+    bn_apply pass, the BN backward's mask recomputed from the conv output) trains
+    bit-identically to the materialised chain: loss, every gradient and the BN running
+    statistics."""
     from ddp_amd.models import resnet18
     from ddp_amd.ops import CrossEntropyLoss, resnet_fn
 
