@@ -1146,7 +1146,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       // every row offset / guard of the unrolled body out of it: 300 spilled registers)
       const int nch = (int)((fcr.K + 127) / 128);
       const int q = f * 4 + (threadIdx.x >> 6);
-      if (q < nch) fc_dw_wave_chunk<BFC_MAXB>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, (long)q * 128);
+      // (B <= 32, the reference batch: 32 row loads per lane instead of 48 clamped ones)
+      if (q < nch) {
+        if (B <= 32) fc_dw_wave_chunk<32>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, (long)q * 128);
+        else fc_dw_wave_chunk<BFC_MAXB>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, (long)q * 128);
+      }
       DDP_STAMP(STAMP_K_FC_BWD, 4);
       return;
     }
