@@ -290,14 +290,21 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   lds_barrier();
   DDP_STAMP(STAMP_K_CONV_FWD, 2);
   if (A1X && !F32 && c1.a1_out) {
-    // the block's own a1 rows (LDS rows W+1 .. W+CH) -> a1_out, 16 bytes per thread-step
+    // the block's own a1 rows (LDS rows W+1 .. W+CH) -> a1_out, 16 bytes per thread-step,
+    // write-through (sc1): no dirty L2 lines for the kernel-end release to write back
     const int xc8 = Cin / 8;
+    typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+    const long a1_bytes = Ptot * Cin * (long)sizeof(T);
+    const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(
+        c1.a1_out, (short)0, (int)(a1_bytes < 0x7fffffffL ? a1_bytes : 0x7fffffffL), 0x00020000);
     for (int i = threadIdx.x; i < CH * xc8; i += NT) {
       const int lp = i / xc8, c = (i - lp * xc8) * 8;
       const long P = P0 + lp;
       if (P < Ptot)
-        *reinterpret_cast<bf16x8*>(c1.a1_out + P * Cin + c) =
-            *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(sX) + (lp + W + 1) * XS + c);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(i32x4_t, *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(sX) +
+                                                                        (lp + W + 1) * XS + c)),
+            ra1, (int)((P * Cin + c) * (long)sizeof(T)), 0, 16 /* sc1: write-through */);
     }
   }
 
