@@ -918,7 +918,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? cfgd["fuse_reduce"].cast<int>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
-             TORCH_CHECK(c.l3_fc_role >= 0 && c.l3_fc_role <= 2, "engine: l3_fc_role must be 0, 1 or 2");
+             TORCH_CHECK(c.l3_fc_role >= 0 && c.l3_fc_role <= 3, "engine: l3_fc_role must be 0..3");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;
              TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");

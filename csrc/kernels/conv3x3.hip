@@ -1123,6 +1123,27 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // fc bias, the loss and the step counter (launchers.h BwdFc).
 constexpr int BFC_MAXB = 48;  // batch capacity of the fc role (level 3 needs B <= 41 anyway)
 
+// dL of the batch into LDS ([B][FCDW_LD] padded rows); the fc role's block 0 (first0) also
+// finishes the fc bias, the loss and the step counter (nothing else in the launch reads them)
+__device__ __forceinline__ float* fc_role_prologue(const BwdFc& fcr, int B, char* smem, bool first0) {
+  float* s_dl = reinterpret_cast<float*>(smem);  // [B][FCDW_LD] (padded rows)
+  for (int i = threadIdx.x; i < B * 10; i += 256) s_dl[(i / 10) * FCDW_LD + i % 10] = fcr.dl[i];
+  __syncthreads();
+  if (first0 && threadIdx.x < 64) {  // fc_bwd_bias_loss reads dense [B][10] rows
+    float* s_dd = s_dl + B * FCDW_LD;
+    for (int i = threadIdx.x; i < B * 10; i += 64) s_dd[i] = s_dl[(i / 10) * FCDW_LD + i % 10];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (same wave: the copy is in LDS)
+    fc_bwd_bias_loss<false>(fcr.ex, s_dd, nullptr, B, 10, true);
+  }
+  return s_dl;
+}
+// one 128-column chunk of the fc weight gradient + SGD on this wave
+__device__ __forceinline__ void fc_role_chunk(const BwdFc& fcr, const float* s_dl, int B, long q) {
+  // (B <= 32, the reference batch: 32 row loads per lane instead of 48 clamped ones)
+  if (B <= 32) fc_dw_wave_chunk<32>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
+  else fc_dw_wave_chunk<BFC_MAXB>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
+}
+
 template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
           bool FCR = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kernel(
@@ -1139,29 +1160,21 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       // the loss and the step counter (nothing else in this launch reads them), then every
       // wave takes 128-column chunks f * 4 + wave, + 4 * nfc, ... (fc_dw_wave_chunk)
       DDP_STAMP(STAMP_K_FC_BWD, 0);
-      float* s_dl = reinterpret_cast<float*>(smem);  // [B][FCDW_LD] (padded rows)
-      for (int i = threadIdx.x; i < B * 10; i += 256) s_dl[(i / 10) * FCDW_LD + i % 10] = fcr.dl[i];
-      __syncthreads();
-      if (f == 0 && threadIdx.x < 64) {  // fc_bwd_bias_loss reads dense [B][10] rows
-        float* s_dd = s_dl + B * FCDW_LD;
-        for (int i = threadIdx.x; i < B * 10; i += 64) s_dd[i] = s_dl[(i / 10) * FCDW_LD + i % 10];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (same wave: the copy is in LDS)
-        fc_bwd_bias_loss<false>(fcr.ex, s_dd, nullptr, B, 10, true);
-      }
+      if (fcr.prio) __builtin_amdgcn_s_setprio(2);
+      const float* s_dl = fc_role_prologue(fcr, B, smem, f == 0);
       DDP_STAMP(STAMP_K_FC_BWD, 1);
       // one 128-column chunk per wave, straight-line (a chunk loop let the compiler hoist
       // every row offset / guard of the unrolled body out of it: 300 spilled registers)
       const int nch = (int)((fcr.K + 127) / 128);
       const int q = f * 4 + (threadIdx.x >> 6);
-      // (B <= 32, the reference batch: 32 row loads per lane instead of 48 clamped ones)
-      if (q < nch) {
-        if (B <= 32) fc_dw_wave_chunk<32>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, (long)q * 128);
-        else fc_dw_wave_chunk<BFC_MAXB>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, (long)q * 128);
-      }
+      if (q < nch) fc_role_chunk(fcr, s_dl, B, q);
       DDP_STAMP(STAMP_K_FC_BWD, 4);
       return;
     }
     if (f >= 0) cb -= fcr.nfc;
+  }
+  if constexpr (FCR) {
+    if (fcr.prio >= 2 && cb >= nd) __builtin_amdgcn_s_setprio(1);  // wgrad role: between fc and dgrad
   }
   if (cb < nd)
     dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
@@ -1169,12 +1182,32 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
   else
     wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, false, true, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
                                                                   W, Cin, Cout, R, c1, smem, cb - nd, 0);
+  // fc_pos 2: each dgrad block runs fc chunks 2 * cb + wave (waves 0, 1) after its own
+  // work (and its arrival: the reducers never wait for the fc work)
+  auto dgrad_fc = [&]() {
+    if constexpr (FCR) {
+      if (fcr.fc_pos == 2 && cb < nd) {
+        __syncthreads();  // every wave is done with the dgrad LDS
+        const float* s_dl = fc_role_prologue(fcr, B, smem, cb == 0);
+        DDP_STAMP(STAMP_K_FC_BWD, 1);
+        const int wv = threadIdx.x >> 6;
+        const long nch = (fcr.K + 127) / 128;
+        if (wv < 2)
+          for (long q = 2L * cb + wv; q < nch; q += 2L * nd) fc_role_chunk(fcr, s_dl, B, q);
+        DDP_STAMP(STAMP_K_FC_BWD, 4);
+      }
+    }
+  };
+  if constexpr (!FRED) dgrad_fc();
   if constexpr (FRED) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
     __syncthreads();
     if (threadIdx.x == 0)
       __hip_atomic_fetch_add(red.done + 32 * (blockIdx.x & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cb < red.first_reducer) return;
+    if (cb < red.first_reducer) {
+      dgrad_fc();
+      return;
+    }
     // reducer w of nr: the LAST nr conv blocks of the grid (dispatched after every block they
     // wait for; the host keeps nr within a quarter of the resident capacity)
     const int nblk = red.nconv > 0 ? red.nconv : (int)gridDim.x;
@@ -1574,11 +1607,11 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     fcr.nconv = nd + nw;
     // one 128-column chunk per wave (4 per block): the first blocks take the resident slots
     // the conv blocks leave free, the rest those the dgrad blocks free first
-    nfc = (int)((fc->K + 127) / 128 + 3) / 4;
+    nfc = fc->fc_pos == 2 ? 0 : (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
     // fc blocks after every conv block (fc_pos 0: dispatched into the slots the conv blocks
-    // leave free) or right after the dgrad role (fc_pos 1)
-    fcr.fc0 = fc->fc_pos == 1 ? nd : nd + nw;
+    // leave free) or right after the dgrad role (fc_pos 1); fc_pos 2: the dgrad blocks
+    fcr.fc0 = fc->fc_pos == 1 ? nd : nd + nw;  // (the reducers are wgrad blocks: never a dgrad one)
     if ((size_t)B * (FCDW_LD + 10) * sizeof(float) > lds)
       throw std::runtime_error("conv3x3_bwd: LDS too small for the fc role");
   }

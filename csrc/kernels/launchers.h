@@ -276,8 +276,12 @@ struct BwdFc {
   float* dW = nullptr;         // null: fused optimizer only
   float scale = 1.f;
   long K = 0;
-  int fc_pos = 0;              // 0: fc blocks after every conv block, 1: right after the dgrad blocks
+  int fc_pos = 0;              // 0: fc blocks after every conv block, 1: right after the dgrad blocks,
+                               // 2: no fc blocks - each dgrad block runs 2 chunks (waves 0, 1) after
+                               //    its arrival (the fc work leaves the launch's first-wave slots)
   int nconv = 0, fc0 = 0, nfc = 0;  // (set by the launcher: nfc = one 128-column chunk per wave)
+  int prio = 0;                // 1: the fc-role waves raise their issue priority (s_setprio 2);
+                               // 2: and the wgrad role's to 1
   FcBwdExtras ex{};
 };
 size_t fc_bwd_lds(int B, int NO, bool xent, long npart = 0);  // npart: see linear.hip

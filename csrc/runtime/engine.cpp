@@ -281,7 +281,12 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       ex.sh_plain = nullptr;  // level 3 never reads the plain bf16 fc shadow (stale until refreshed)
       fcr.a2 = b_.a2;
       fcr.dl = b_.dlogits;
-      fcr.fc_pos = cfg_.l3_fc_role == 2 ? 1 : 0;
+      fcr.fc_pos = cfg_.l3_fc_role == 3 ? 2 : (cfg_.l3_fc_role == 2 ? 1 : 0);
+      {  // wave issue priority of the roles: fc role 2 (default: +0.9 %, profiles/r3_cnn/prio),
+         // DDP_AMD_FC_PRIO=0 none, =2 also the wgrad role at 1
+        const char* e = std::getenv("DDP_AMD_FC_PRIO");
+        fcr.prio = e && e[0] ? (e[0] - '0') : 1;
+      }
       fcr.dW = fopt ? nullptr : G + b_.off_wfc;
       fcr.scale = inv_ws;
       fcr.K = (long)HW * C2;

@@ -217,7 +217,8 @@ struct EngineConfig {
   //    all-reduce overlaps the conv backward).  bf16, where every forward block fits on the
   //    GPU at once (conv3x3_fwd_dz_fits); otherwise the level-1 chain
   int fuse_level = 0;
-  // level 3, single process: 1 = fc role after every conv block (on the resident slots they
+  // level 3, single process: 3 = the dgrad blocks run the fc chunks after their own work,
+  // 1 = fc role after every conv block (on the resident slots they
   // leave free), 2 = right after the dgrad blocks, 0 = the fc weight gradient as its own
   // kernel (what world size > 1 runs)
   int l3_fc_role = 1;

@@ -95,7 +95,8 @@ def test_fuse_level2_bitwise_equals_level1(B):
 
 @pytest.mark.parametrize("B,opt,momentum,role", [(32, True, 0.9, 1), (32, False, 0.9, 1), (20, True, 0.0, 1),
                                                   (1, True, 0.9, 1), (40, True, 0.9, 1), (32, True, 0.9, 2),
-                                                  (32, True, 0.9, 0), (20, False, 0.9, 0)])
+                                                  (32, True, 0.9, 0), (20, False, 0.9, 0),
+                                                  (32, True, 0.9, 3), (20, True, 0.0, 3), (40, True, 0.9, 3)])
 def test_fuse_level3_bitwise_equals_level1(B, opt, momentum, role):
     """Level 3: the forward computes dZ2 itself (per-image in-launch wait, then dL and
     dZ2 from its fc weight fragments) and the fc weight gradient + SGD runs as a third role
