@@ -31,6 +31,8 @@
 //           reduction in grad_reduce (bitwise reproducible, no float atomics).
 #include <stdexcept>
 
+#include <cstdlib>
+
 #include "kernels/common.h"
 #include "kernels/fc_bwd_body.h"
 #include "kernels/launchers.h"
@@ -96,6 +98,7 @@ struct BwdReduce {
   int nconv = 0;          // conv-role blocks (the arrivals the reducers wait for); fc-role blocks follow
   int* done = nullptr;  // 8 arrival counters, 32 ints apart (zeroed by the step's forward)
   int* err = nullptr;   // set to 2 when the wait times out
+  int prio = 0;         // issue priority of the reducer waves once the wait is over (0, 2, 3)
 };
 
 // Block-wide wait until every fc-role block whose columns cover the flattened pixels
@@ -1160,7 +1163,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       // the loss and the step counter (nothing else in this launch reads them), then every
       // wave takes 128-column chunks f * 4 + wave, + 4 * nfc, ... (fc_dw_wave_chunk)
       DDP_STAMP(STAMP_K_FC_BWD, 0);
-      if (fcr.prio) __builtin_amdgcn_s_setprio(2);
+      if (fcr.prio == 3) __builtin_amdgcn_s_setprio(3);
+      else if (fcr.prio) __builtin_amdgcn_s_setprio(2);
       const float* s_dl = fc_role_prologue(fcr, B, smem, f == 0);
       DDP_STAMP(STAMP_K_FC_BWD, 1);
       // one 128-column chunk per wave, straight-line (a chunk loop let the compiler hoist
@@ -1174,7 +1178,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
     if (f >= 0) cb -= fcr.nfc;
   }
   if constexpr (FCR) {
-    if (fcr.prio >= 2 && cb >= nd) __builtin_amdgcn_s_setprio(1);  // wgrad role: between fc and dgrad
+    if (fcr.prio == 2 && cb >= nd) __builtin_amdgcn_s_setprio(1);  // wgrad role: between fc and dgrad
   }
   if (cb < nd)
     dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
@@ -1234,6 +1238,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       }
     }
     __syncthreads();
+    if (red.prio == 3) __builtin_amdgcn_s_setprio(3);
+    else if (red.prio == 2) __builtin_amdgcn_s_setprio(2);
     DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
     float* part = reinterpret_cast<float*>(smem);
     slab_fused_run<J>(red.ss, pl, part);
@@ -1640,6 +1646,10 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     red.nchunks = slab_chunks(*fused);
     red.done = red_done;
     red.err = red_err;
+    {  // (A/B knob) DDP_AMD_RED_PRIO=2|3: reducer waves at raised issue priority
+      const char* e = std::getenv("DDP_AMD_RED_PRIO");
+      red.prio = e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 0;
+    }
     if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");
   }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32

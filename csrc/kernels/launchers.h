@@ -281,7 +281,7 @@ struct BwdFc {
                                //    its arrival (the fc work leaves the launch's first-wave slots)
   int nconv = 0, fc0 = 0, nfc = 0;  // (set by the launcher: nfc = one 128-column chunk per wave)
   int prio = 0;                // 1: the fc-role waves raise their issue priority (s_setprio 2);
-                               // 2: and the wgrad role's to 1
+                               // 2: and the wgrad role's to 1; 3: fc role at s_setprio 3
   FcBwdExtras ex{};
 };
 size_t fc_bwd_lds(int B, int NO, bool xent, long npart = 0);  // npart: see linear.hip
