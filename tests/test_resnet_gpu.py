@@ -314,6 +314,36 @@ def test_conv_bn_fwd_tail_matches_finalize(C, N, H, Cin, Cout, K, s, p):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("rows,Cc", [(10, 64), (64, 128), (100, 512), (3136, 64), (5000, 64)])
+def test_bn_finalize_row_counts(C, rows, Cc):
+    """bn_finalize over 1 block per strip (<= 64 rows: no ticket), two levels (the ResNet-18
+    stem's 3136 rows: 49 blocks) and more than 64 x 64 rows (128 rows per block, two load
+    batches): mean / invstd / running stats against an fp64 reference, num_batches_tracked
+    once, and bitwise reproducible."""
+    g = torch.Generator().manual_seed(71)
+    slab = (torch.randn(rows, 2, Cc, generator=g) * torch.tensor([1.0, 0.0])[None, :, None]).to(dev)
+    slab[:, 1] = (torch.rand(rows, Cc, generator=g) * 4 + 1).to(dev)  # positive sums of squares
+    count = float(rows * 64)
+    res = []
+    for _ in range(2):
+        rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+        nbt = torch.zeros((), dtype=torch.long, device=dev)
+        mean, invstd = torch.empty(Cc, device=dev), torch.empty(Cc, device=dev)
+        ws = torch.full((C.bn_finalize_groups(rows), 2, Cc), float("nan"), device=dev)
+        C.bn_finalize(slab, rows, Cc, count, 1e-5, 0.1, rm, rv, mean, invstd, nbt, ws)
+        torch.cuda.synchronize()
+        assert nbt.item() == 1
+        res.append((mean, invstd, rm, rv))
+    sd = slab.double().sum(0).cpu()
+    m_ref = sd[0] / count
+    v_ref = (sd[1] / count - m_ref * m_ref).clamp_min(0)
+    assert relerr(res[0][0], m_ref) < 1e-5
+    assert relerr(res[0][1], torch.rsqrt(v_ref + 1e-5)) < 1e-5
+    assert relerr(res[0][3], 0.9 + 0.1 * v_ref * count / (count - 1)) < 1e-5
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("N,H,Cc,relu,two", [(32, 112, 64, 1, 0), (32, 56, 64, 1, 1), (32, 28, 128, 0, 0),
                                             (32, 14, 256, 1, 1), (32, 7, 512, 1, 0), (2, 5, 64, 1, 0)])
 def test_bn_bwd_single_launch_bitwise(C, N, H, Cc, relu, two):
