@@ -1196,8 +1196,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
         DDP_STAMP(STAMP_K_FC_BWD, 1);
         const int wv = threadIdx.x >> 6;
         const long nch = (fcr.K + 127) / 128;
-        if (wv < 2)
-          for (long q = 2L * cb + wv; q < nch; q += 2L * nd) fc_role_chunk(fcr, s_dl, B, q);
+        // one chunk per wave, straight-line (a chunk loop makes the compiler hoist the
+        // unrolled body's row offsets: the whole kernel then spills); the host checks
+        // nch <= 2 * nd
+        const long q = 2L * cb + wv;
+        if (wv < 2 && q < nch) fc_role_chunk(fcr, s_dl, B, q);
         DDP_STAMP(STAMP_K_FC_BWD, 4);
       }
     }
@@ -1613,11 +1616,15 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     fcr.nconv = nd + nw;
     // one 128-column chunk per wave (4 per block): the first blocks take the resident slots
     // the conv blocks leave free, the rest those the dgrad blocks free first
-    nfc = fc->fc_pos == 2 ? 0 : (int)((fc->K + 127) / 128 + 3) / 4;
+    // fc_pos 2 runs one chunk per dgrad-block wave 0 / 1: with fewer than nch / 2 dgrad
+    // blocks (small batches) the fc role keeps its own blocks (fc_pos 0)
+    const int fpos = (fc->fc_pos == 2 && (fc->K + 127) / 128 > 2L * nd) ? 0 : fc->fc_pos;
+    fcr.fc_pos = fpos;
+    nfc = fpos == 2 ? 0 : (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
     // fc blocks after every conv block (fc_pos 0: dispatched into the slots the conv blocks
     // leave free) or right after the dgrad role (fc_pos 1); fc_pos 2: the dgrad blocks
-    fcr.fc0 = fc->fc_pos == 1 ? nd : nd + nw;  // (the reducers are wgrad blocks: never a dgrad one)
+    fcr.fc0 = fpos == 1 ? nd : nd + nw;  // (the reducers are wgrad blocks: never a dgrad one)
     if ((size_t)B * (FCDW_LD + 10) * sizeof(float) > lds)
       throw std::runtime_error("conv3x3_bwd: LDS too small for the fc role");
   }
