@@ -71,14 +71,47 @@ def _free_port() -> int:
 
 
 def _child_json(cmd, env, timeout):
-    """Run one launcher child; return its last JSON stdout line (stderr passes through)."""
-    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True,
-                       timeout=timeout)
+    """Run one launcher child; return (its last JSON stdout line or None, reason)."""
+    try:
+        p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True,
+                           timeout=timeout)
+    except subprocess.TimeoutExpired as e:
+        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
+        sys.stdout.write(out)
+        return None, f"timed out after {timeout:.0f} s"
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     if p.returncode != 0 or not lines:
         sys.stdout.write(p.stdout)
-        raise SystemExit(f"[bench] launcher child failed (rc={p.returncode}): {' '.join(cmd)}")
-    return json.loads(lines[-1])
+        return None, f"rc={p.returncode}"
+    return json.loads(lines[-1]), None
+
+
+# What the parent retries with when an N-rank child fails or times out (VERDICT r3 #3b):
+# the production chain first, then the conservative kernel chain (level 1, separate slab
+# reduction), then the same over RCCL instead of the direct xGMI kernels.  Each attempt is
+# a fresh child (fresh processes, fresh GPU contexts); the parent never touches the GPU.
+FALLBACKS = (
+    ("production", ()),
+    ("conservative chain", ("--fuse_level", "1", "--fuse_reduce", "0")),
+    ("conservative chain over RCCL", ("--fuse_level", "1", "--fuse_reduce", "0", "--comm", "rccl")),
+)
+
+
+def run_with_fallback(launch, timeout):
+    """``launch(extra_args, timeout)`` -> (record | None, reason) for each FALLBACKS entry in
+    turn until one succeeds; the record carries ``config.fallback`` (None when the first
+    attempt succeeded) and ``config.failed_attempts``."""
+    failed = []
+    for name, extra in FALLBACKS:
+        rec, why = launch(extra, timeout)
+        if rec is not None:
+            cfg = rec.setdefault("config", {})
+            cfg["fallback"] = None if not failed else name
+            cfg["failed_attempts"] = failed
+            return rec
+        print(f"[bench] {name} attempt failed ({why}); retrying in a fresh child", file=sys.stderr, flush=True)
+        failed.append({"attempt": name, "reason": why})
+    raise SystemExit(f"[bench] every attempt failed: {failed}")
 
 
 def self_launch(args, argv):
@@ -89,12 +122,14 @@ def self_launch(args, argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / xGMI peer mappings)
 
-    def run(nproc, extra=()):
-        port = _free_port()
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-               f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={port}",
-               here, *_with_gpus(argv, nproc), *extra]
-        return _child_json(cmd, env, args.launch_timeout)
+    def run(nproc):
+        def launch(extra, timeout):
+            port = _free_port()
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={port}",
+                   here, *_with_gpus(argv, nproc), *extra]
+            return _child_json(cmd, env, timeout)
+        return run_with_fallback(launch, args.launch_timeout)
 
     if args.dry_launch:
         rec = run(n)
@@ -131,13 +166,17 @@ def dry_worker(args):
     """--dry_launch inside a worker: report what the launcher gave this rank, gathered on
     rank 0 over a gloo group (no GPU)."""
     rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    # test hook of the parent's fallback: fail unless this child runs fallback #dry_fail
+    level = 2 if args.comm == "rccl" else (1 if args.fuse_level == 1 else 0)
+    if level < args.dry_fail:
+        raise SystemExit(3)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     mine = {k: os.environ.get(k) for k in LAUNCH_ENV}
     allenv = [None] * ws
     dist.all_gather_object(allenv, mine)
     if rank == 0:
         print(json.dumps({"dry_launch": True, "n_gpus": args.gpus, "ranks_seen": dist.get_world_size(),
-                          "children": allenv}), flush=True)
+                          "children": allenv, "fuse_level": args.fuse_level, "comm": args.comm}), flush=True)
     dist.destroy_process_group()
 
 
@@ -200,8 +239,13 @@ def main():
                     help="resnet18: input channels per halo wgrad block (0 = planner default)")
     ap.add_argument("--no_fp32", action="store_true",
                     help="skip the exact-fp32 (reference precision) run after the bf16 headline")
+    ap.add_argument("--no_chain_check", action="store_true",
+                    help="N>1: skip the start-up check that the production kernel chain gives the "
+                         "conservative chain's bits across the ranks")
     ap.add_argument("--dry_launch", action="store_true",
                     help="self-launch test hook: workers report their launcher env and exit (no GPU)")
+    ap.add_argument("--dry_fail", type=int, default=0,
+                    help="test hook (--dry_launch): workers exit 3 unless launched as fallback >= this")
     ap.add_argument("--no_scaling_ref", action="store_true",
                     help="self-launch: skip the 1-rank reference run (scaling_efficiency null)")
     ap.add_argument("--launch_timeout", type=float, default=900.0, help="self-launch: per-child seconds")
@@ -298,6 +342,8 @@ def main():
             eo.fuse_level, eo.store_a1 = 1, 0  # the exact-fp32 chain (engine.cpp launch_step_f32)
         eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
         eng.refresh()
+        if ws > 1 and not args.no_chain_check:
+            eng.verify_chain()  # untimed: production vs conservative chain, bitwise, all ranks
         if not args.no_graph:
             eng.run_steps(0)           # uploads epoch 0's indices
             eng._ensure_graph()        # capture outside the timed region
@@ -377,6 +423,7 @@ def main():
                        "bucket_plan": {"rule": args.bucket_plan, "buckets": plan,
                                        "pred_last_allreduce_done_us": (round(eng.pred_comm_us, 2)
                                                                        if ws > 1 and eng.pred_comm_us else None)},
+                       "chain_check": eng.chain_check, "downgrades": getattr(eng, "downgrades", []),
                        "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
                        "fp32_ms_per_step": fp32["ms_per_step"] if fp32 else None},
         }), flush=True)

@@ -819,6 +819,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("alpha"), py::arg("accum") = false);
   m.def("transpose_w", &op_transpose_w);
   m.def("rccl_version", []() { int v = 0; ncclGetVersion(&v); return v; });
+  // PCI bus id of a device: ranks compare these through the store to detect a shared GPU
+  // (device counts cannot: HIP_VISIBLE_DEVICES-isolated ranks each see one device)
+  m.def("pci_bus_id", [](int dev) {
+    char buf[64] = {0};
+    if (hipDeviceGetPCIBusId(buf, sizeof(buf) - 1, dev) != hipSuccess)
+      throw std::runtime_error("hipDeviceGetPCIBusId failed");
+    return std::string(buf);
+  });
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
       .def_static("new_unique_id", []() { return py::bytes(Comm::new_unique_id()); })
@@ -866,9 +874,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         for (const auto& b : all) v.emplace_back(b);
         x.import_handles(v);
       })
-      .def("all_reduce", [](XgmiComm& x, int ch, double scale, bool publish) {
-        x.all_reduce(ch, cur_stream(), (float)scale, publish);
-      }, py::arg("channel"), py::arg("scale") = 1.0, py::arg("publish") = false)
+      .def("all_reduce", [](XgmiComm& x, int ch, double scale, bool publish, double prescale) {
+        x.all_reduce(ch, cur_stream(), (float)scale, publish, (float)prescale);
+      }, py::arg("channel"), py::arg("scale") = 1.0, py::arg("publish") = false, py::arg("prescale") = 1.0)
       .def("error_flags", &XgmiComm::error_flags)
       .def("set_timeout", &XgmiComm::set_timeout)
       .def_property_readonly("rank", &XgmiComm::rank)
@@ -980,8 +988,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.xb = need("xb", at::kByte, B * HW).data_ptr<unsigned char>();
              b.yb = need("yb", at::kInt, B).data_ptr<int>();
              if (t.contains("sync_flags")) {  // in-launch hand-offs (fused reduction, level 2)
-               const long nfl = SYNC_RED_INTS + fc_conv_bwd_fc_blocks(HW * c.C2) +
-                                conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_fwd);
+               long nfl = SYNC_RED_INTS + fc_conv_bwd_fc_blocks(HW * c.C2) +
+                          conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_fwd);
+               // level 3: the forward's per-image arrival counters, FWD_DZ_CNT_STRIDE ints apart
+               if (c.fuse_level >= 3) nfl = std::max(nfl, (long)L3_IMG_OFF + (long)FWD_DZ_CNT_STRIDE * B);
                b.sync_flags = need("sync_flags", at::kInt, nfl).data_ptr<int>();
                b.sync_err = need("sync_err", at::kInt, 1).data_ptr<int>();
              }

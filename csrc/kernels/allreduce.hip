@@ -224,12 +224,13 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
     const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par1);
     for (long q = q0; q < nq; q += G) {
       float4 v;
+      const float ps = a.prescale;
       if (q < fq) {
-        v = make_float4(mine[4 * q], mine[4 * q + 1], mine[4 * q + 2], mine[4 * q + 3]);
+        v = make_float4(mine[4 * q] * ps, mine[4 * q + 1] * ps, mine[4 * q + 2] * ps, mine[4 * q + 3] * ps);
       } else {
         float t[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = 4 * q + j < n ? mine[4 * q + j] : 0.f;
+        for (int j = 0; j < 4; ++j) t[j] = 4 * q + j < n ? mine[4 * q + j] * ps : 0.f;
         v = make_float4(t[0], t[1], t[2], t[3]);
       }
       st4_sys(mystage, q, v);  // the stage holds whole quads (zero-padded tail)
@@ -261,16 +262,17 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
     // reduced value must land after (program order) this re-store of the local value.
     float* mine = a.data[r] + a.off;
     const __amdgpu_buffer_rsrc_t rm = sys_rsrc(mine);
+    const float ps = a.prescale;  // (x * 1.f == x: the plain re-store when not prescaling)
     for (int p = 0; p < N; ++p) {
       const long lim = min(slice, a.n - (long)p * slice);
       for (long q = q0; 4 * q < lim; q += G) {
         const long k = (long)p * slice + 4 * q;
         if (4 * q + 3 < lim) {
-          st4_sys(rm, k / 4, make_float4(mine[k], mine[k + 1], mine[k + 2], mine[k + 3]));
+          st4_sys(rm, k / 4, make_float4(mine[k] * ps, mine[k + 1] * ps, mine[k + 2] * ps, mine[k + 3] * ps));
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (4 * q + j < lim) st_sys(mine + k + j, mine[k + j]);
+            if (4 * q + j < lim) st_sys(mine + k + j, mine[k + j] * ps);
         }
       }
     }

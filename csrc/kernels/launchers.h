@@ -398,6 +398,8 @@ struct XgmiArgs {
   int publish;                    // two-shot: re-store my bucket system-scope before B0 (producers used
                                   // plain stores, e.g. autograd kernels in the module path)
   float scale;                    // applied to the result (1: producers prescaled by 1/world)
+  float prescale;                 // publish pass / one-shot publish: my values times this before the
+                                  // rank-order sum (DDP's prescale-by-1/world, then SUM; 1 otherwise)
   int rank, world;
   unsigned long long timeout_ticks;  // per barrier spin, 100 MHz ticks
   // Optional optimizer fused into the all-gather (sgd.update != 0): every rank applies

@@ -55,29 +55,34 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
             *reinterpret_cast<float4*>(sh.r[r].dst32 + fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)) =
                 make_float4(e[0], e[1], e[2], e[3]);
           } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const long jj = j + u;
-              if (jj < 0 || jj >= sh.r[r].n) continue;
+            // element by element (a unit-stride quad straddling the region, or a transposed
+            // layout); four explicit calls, not a loop over e[u]: the dynamic index put the
+            // quad in scratch (68 bytes per lane, utils/kernel_resources.py)
+            auto put = [&](long jj, float ev) {
+              if (jj < 0 || jj >= sh.r[r].n) return;
               if (sh.r[r].kind == SHADOW_BF16) {
-                sh.r[r].dst[jj] = f2bf(e[u]);
+                sh.r[r].dst[jj] = f2bf(ev);
               } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
-                sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(e[u]);
+                sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(ev);
               } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
-                sh.r[r].dst32[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = e[u];
+                sh.r[r].dst32[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = ev;
               } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
-                sh.r[r].dst[(jj / 3) * 4 + jj % 3] = f2bf(e[u]);
+                sh.r[r].dst[(jj / 3) * 4 + jj % 3] = f2bf(ev);
               } else if (sh.r[r].kind == SHADOW_F32_TAPT) {
                 const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
                 const long co = jj / ((long)T * Ci);
-                sh.r[r].dst32[(jj - co * T * Ci) * Co + co] = e[u];
+                sh.r[r].dst32[(jj - co * T * Ci) * Co + co] = ev;
               } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
                 const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
                 const long co = jj / ((long)T * Ci);
                 const long rr = jj - co * T * Ci;
-                sh.r[r].dst[rr * Co + co] = f2bf(e[u]);
+                sh.r[r].dst[rr * Co + co] = f2bf(ev);
               }
-            }
+            };
+            put(j, v.x);
+            put(j + 1, v.y);
+            put(j + 2, v.z);
+            put(j + 3, v.w);
           }
         }
       }
@@ -93,7 +98,9 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
       p[i] = v;
       if (a.momentum != 0.f) mbuf[i] = m;
     }
-    for (int r = 0; r < sh.count; ++r) {
+#pragma unroll
+    for (int r = 0; r < MAX_SHADOWS; ++r) {  // (constant trip count: a loop to sh.count indexed the
+      if (r >= sh.count) break;              //  by-value ShadowSet dynamically -> scratch)
       const long j = i - sh.r[r].off;
       if (j < 0 || j >= sh.r[r].n) continue;
       if (sh.r[r].kind == SHADOW_BF16) {

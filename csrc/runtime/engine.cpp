@@ -551,6 +551,14 @@ void SimpleCNNEngine::capture(int nsteps) {
   }
   DDP_HIP_CHECK(hipStreamEndCapture(cs_, &graph_));
   DDP_HIP_CHECK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+  // upload the exec's kernel-argument / node state now, on the engine stream, so its
+  // first hipGraphLaunch (often inside a timed bracket) does not pay for it
+  // (DDP_AMD_GRAPH_UPLOAD=0 skips it: A/B knob)
+  const char* up = std::getenv("DDP_AMD_GRAPH_UPLOAD");
+  if (!(up && up[0] == '0')) {
+    DDP_HIP_CHECK(hipGraphUpload(graph_exec_, cs_));
+    DDP_HIP_CHECK(hipStreamSynchronize(cs_));
+  }
   graph_steps_ = nsteps;
 }
 

@@ -3,7 +3,8 @@
 // loss.backward() at train_ddp.py:199).
 //
 // Semantics kept from the reference DDP: gradients are averaged as
-// sum_r(g_r * 1/ws) (prescale, then SUM), buckets are launched as soon as their
+// sum_r(g_r * 1/ws) (prescale, then SUM - per bucket at launch, or per parameter in
+// mark_ready when constructed with prescale), buckets are launched as soon as their
 // last gradient is ready (overlapping backward), and the optimizer only runs
 // after every bucket finished.  What differs: buckets are views of one flat fp32
 // gradient buffer owned by the model, the all-reduce runs on a dedicated HIP
@@ -66,14 +67,16 @@ int Reducer::world() const {
 void Reducer::launch_bucket(int b, hipStream_t compute) {
   DDP_HIP_CHECK(hipEventRecord(ready_[b], compute));
   DDP_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready_[b], 0));
+  const float inv = 1.f / (float)world();
   if (xgmi_ && xgmi_->world() > 1) {
-    // fixed rank-order sum, then the mean (unless the gradients were prescaled)
-    xgmi_->all_reduce(xch_[b], comm_stream_, prescale_ ? 1.f : 1.f / (float)xgmi_->world(), true);
+    // torch DDP's averaging: every rank's gradient times 1/world (inside the kernel's publish
+    // pass, no extra launch), then the fixed rank-order SUM
+    xgmi_->all_reduce(xch_[b], comm_stream_, 1.f, true, prescale_ ? 1.f : inv);
     ++calls_;
   } else if (comm_ && comm_->world() > 1) {
-    // prescaled gradients -> SUM == mean; otherwise let RCCL average
-    comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, prescale_ ? 0 : 1,
-                      comm_stream_);
+    // prescale by 1/world on the comm stream (one pass over the bucket), then SUM
+    if (!prescale_) scale_copy(flat_ + bucket_off_[b], flat_ + bucket_off_[b], bucket_num_[b], inv, comm_stream_);
+    comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
     ++calls_;
   }
   DDP_HIP_CHECK(hipEventRecord(done_[b], comm_stream_));

@@ -82,10 +82,12 @@ class XgmiComm {
   // publish: the bucket's producers used plain stores (module path): each block re-stores
   // its part system-scope before the entry barrier (no effect on one-shot channels, which
   // always copy the bucket to their stage buffer that way)
-  void all_reduce(int channel, hipStream_t s, float scale = 1.f, bool publish = false);
+  // prescale (publish / one-shot only): my values times prescale before the rank-order sum
+  void all_reduce(int channel, hipStream_t s, float scale = 1.f, bool publish = false, float prescale = 1.f);
   // the same, with SGD fused into the all-gather (see XgmiArgs)
   void all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
-                      const ShadowSet& sh, int* step_ctr, float scale = 1.f, bool publish = false);
+                      const ShadowSet& sh, int* step_ctr, float scale = 1.f, bool publish = false,
+                      float prescale = 1.f);
   // != 0: a barrier timed out (result invalid) - the first failed channel's error word
   // (xgmi_error_code: block, peer, barrier)
   unsigned error_flags() const;

@@ -140,15 +140,18 @@ void XgmiComm::import_handles(const std::vector<std::string>& all) {
   imported_ = true;
 }
 
-void XgmiComm::all_reduce(int channel, hipStream_t s, float scale, bool publish) {
-  all_reduce_sgd(channel, s, SgdArgs{}, nullptr, nullptr, ShadowSet{}, nullptr, scale, publish);
+void XgmiComm::all_reduce(int channel, hipStream_t s, float scale, bool publish, float prescale) {
+  all_reduce_sgd(channel, s, SgdArgs{}, nullptr, nullptr, ShadowSet{}, nullptr, scale, publish, prescale);
 }
 
 void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params,
-                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale, bool publish) {
+                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale, bool publish,
+                              float prescale) {
   if (!imported_) throw std::runtime_error("xgmi: import_handles first");
   if (channel < 0 || channel >= (int)ch_.size()) throw std::runtime_error("xgmi: bad channel");
   const Channel& c = ch_[channel];
+  if (prescale != 1.f && !publish && !c.oneshot)
+    throw std::runtime_error("xgmi: prescale needs the publish pass (or a one-shot channel)");
   XgmiArgs a{};
   for (int r = 0; r < world_; ++r) {
     a.data[r] = data_peer_[r];
@@ -161,6 +164,7 @@ void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, fl
   a.oneshot = c.oneshot ? 1 : 0;
   a.publish = publish ? 1 : 0;
   a.scale = scale;
+  a.prescale = prescale;
   a.rank = rank_;
   a.world = world_;
   a.timeout_ticks = (unsigned long long)(timeout_s_ * 1e8);

@@ -33,8 +33,10 @@ from ..parallel.ddp import bucket_plan, bucket_ranges
 
 # buckets up to this many fp32 elements may get a one-shot xGMI channel: the bucket must
 # fit one kernel grid (1024 x 256); below it the cost model's crossover decides
-# (parallel/bucket_model.py: SimpleCNN's 75 KB conv bucket is one-shot at every N, the
-# 2 MB fc bucket one-shot at N = 2 and two-shot at N >= 4)
+# (parallel/bucket_model.py: SimpleCNN's 75 KB conv bucket is one-shot at every N; the
+# 2 MB fc bucket (501,770 elements) is above this cap, so it is always two-shot - the
+# cost model's N = 2 one-shot crossover for it is not applied).  The module path (ddp.py)
+# uses the same cap.
 ONESHOT_MAX_ELEMS = 1024 * 256
 
 BF16 = torch.bfloat16
@@ -106,6 +108,14 @@ class EngineOptions:
     # bit-identical slabs - measured 801k -> 811k img/s at B = 32, 1.04M -> 1.06M at B = 64,
     # profiles/r2_split); 1 = one block per row.  fp32 always runs 1.
     wgrad_split: int = 2
+
+
+def agree(store, key: str, rank: int, world: int, ok: bool) -> bool:
+    """True when every rank reported ``ok`` under ``key`` (a c10d store; None = one rank)."""
+    if store is None or world <= 1:
+        return bool(ok)
+    store.set(f"{key}/{rank}", b"1" if ok else b"0")
+    return all(store.get(f"{key}/{r}") == b"1" for r in range(world))
 
 
 class FusedSimpleCNNEngine:
@@ -233,6 +243,8 @@ class FusedSimpleCNNEngine:
             raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
         self.comm_kind = (self.xgmi_plan or "xgmi") if self.xgmi is not None else ("rccl" if use_comm else "none")
         self.ranges, self.xch, self.comm = ranges, xch, (comm if use_comm else None)
+        self.cfg, self.offs = cfg, offs
+        self.chain_check = None  # verify_chain's outcome (dict), when it ran
         self.eng = self.C.SimpleCNNEngine(cfg, self.t, offs, comm if use_comm else None)
         if self.xgmi is not None:
             self.eng.set_xgmi(self.xgmi, xch)
@@ -246,23 +258,161 @@ class FusedSimpleCNNEngine:
         self.steps_done = 0
         self._need_barrier = world_size > 1
 
+    # ------------------------------------------------------------------ start-up chain check
+    def conservative_cfg(self) -> dict | None:
+        """The conservative chain's config (level 1, separate grad_reduce kernel, same data
+        plane), or None when the production chain already is that."""
+        ref = dict(self.cfg, fuse_level=min(int(self.cfg["fuse_level"]), 1), fuse_reduce=0)
+        return None if ref == self.cfg else ref
+
+    def verify_chain(self, nsteps: int = 2, store=None, _corrupt_rank: int | None = None) -> bool:
+        """VERDICT r3 #3a: before training commits to the production chain (level 3 + the
+        fused slab reduction + the chosen data plane), run ``nsteps`` eager steps on it, then
+        the same steps from the same snapshot on the conservative chain (level 1, separate
+        grad_reduce, same plane), and compare parameters, momentum and losses bitwise.
+        Every rank publishes its verdict through the store (:func:`agree`); if any rank saw
+        a mismatch or an in-launch / cross-GPU wait timeout, EVERY rank switches to the
+        conservative chain (and, after an xGMI timeout, to RCCL), deterministically, and logs
+        it.  The snapshot (parameters, momentum, step counter, loss history, momentum state)
+        is restored afterwards, so training starts exactly where it would have.  Collective
+        at world size > 1.  Returns True when the production chain was kept."""
+        ref_cfg = self.conservative_cfg()
+        if ref_cfg is None:
+            self.chain_check = {"ran": False, "reason": "production chain is the conservative one"}
+            return True
+        import torch.distributed as dist
+
+        if store is None and dist.is_initialized() and self.world_size > 1:
+            store = dist.distributed_c10d._get_default_store()
+        t = self.t
+        keys = ("params", "momentum", "step_ctr", "loss_hist")
+        self.synchronize()
+        torch.cuda.synchronize()
+        snap = {k: t[k].clone() for k in keys}
+        started = self.opt.momentum_buffer is not None and self.opt.steps > 0
+        B = self.B
+
+        def restore(e):
+            with torch.cuda.stream(self.stream):
+                for k in keys:
+                    t[k].copy_(snap[k])
+            e.set_momentum_started(started)
+            e.refresh_shadows()
+
+        def run(e):
+            """nsteps on engine e from the snapshot -> (params, momentum, losses) or an error."""
+            self.start_epoch(0)
+            restore(e)
+            try:
+                for _ in range(nsteps):
+                    e.step(B, B)
+                e.synchronize()
+            except RuntimeError as ex:  # an in-launch wait timed out
+                return None, f"in-launch wait: {ex}"
+            if self.xgmi is not None and self.xgmi.error_flags():
+                from ..parallel.xgmi import describe_xgmi_error
+
+                return None, "xgmi: " + describe_xgmi_error(self.xgmi.error_flags())
+            torch.cuda.synchronize()
+            return [t[k].clone() for k in ("params", "momentum")] + [t["loss_hist"][:nsteps].clone()], None
+
+        ref = self.C.SimpleCNNEngine(ref_cfg, t, self.offs, self.comm)
+        if self.xgmi is not None:
+            ref.set_xgmi(self.xgmi, self.xch)
+        got, err_p = run(self.eng)
+        if got is not None and _corrupt_rank == self.rank:  # test hook: a one-ulp disagreement
+            got[0][0] = torch.nextafter(got[0][0], torch.tensor(float("inf"), device=got[0].device))
+        want, err_r = run(ref)
+        same = got is not None and want is not None and all(torch.equal(a, b) for a, b in zip(got, want))
+        xgmi_bad = (err_p or "").startswith("xgmi") or (err_r or "").startswith("xgmi")
+        key = f"ddp_amd/chain/{FusedSimpleCNNEngine._chain_gen}"
+        FusedSimpleCNNEngine._chain_gen += 1
+        ok_all = agree(store, key + "/same", self.rank, self.world_size, same)
+        x_ok_all = agree(store, key + "/xgmi", self.rank, self.world_size, not xgmi_bad)
+        chosen = self.eng
+        if not x_ok_all:
+            if self.comm is None:
+                raise RuntimeError("start-up chain check: the xGMI data plane timed out and there is no RCCL plane")
+            self.xgmi, self.xgmi_plan, self.comm_kind = None, "rccl", "rccl"
+            chosen = self.C.SimpleCNNEngine(ref_cfg, t, self.offs, self.comm)
+            self._log_downgrade("start-up chain check: xGMI wait timed out -> conservative chain over RCCL")
+        elif not ok_all:
+            chosen = ref
+            self._log_downgrade("start-up chain check: production chain differs from the conservative one "
+                                f"(here: {'same' if same else err_p or err_r or 'bits differ'}) -> conservative chain")
+        if chosen is not self.eng:
+            self.eng = chosen
+            self.cfg = ref_cfg
+            self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.fs.params.device)
+            self.level2 = bool(self.eng.level2_active)
+            self.level3 = bool(self.eng.level3_active(B))
+            self._captured = 0
+        self.start_epoch(0)
+        restore(self.eng)
+        torch.cuda.synchronize()
+        self.chain_check = {"ran": True, "steps": nsteps, "identical_here": same, "identical_all": ok_all,
+                            "xgmi_ok_all": x_ok_all, "kept_production": chosen is not ref and x_ok_all,
+                            "error": err_p or err_r}
+        return self.chain_check["kept_production"]
+
+    _chain_gen = 0
+
     # ------------------------------------------------------------------ helpers
+    def _device_shared(self, world_size: int) -> bool:
+        """Whether any GPU of the job runs more than one rank (same-GPU rehearsals).
+
+        Decided from every rank's PCI bus id through the c10d store, so it is right when
+        each rank sees only its own device (HIP_VISIBLE_DEVICES isolation) and across nodes
+        (ADVICE r3); without a process group, by the visible device count.  Cached."""
+        if getattr(self, "_shared", None) is not None:
+            return self._shared
+        shared = False
+        if world_size > 1:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                from ..parallel.xgmi import max_sharing
+
+                store = dist.distributed_c10d._get_default_store()
+                key = f"ddp_amd/engine_bus/{FusedSimpleCNNEngine._bus_gen}"
+                FusedSimpleCNNEngine._bus_gen += 1
+                dev = self.fs.params.device.index
+                store.set(f"{key}/{self.rank}", self.C.pci_bus_id(dev).encode())
+                shared = max_sharing(store.get(f"{key}/{r}").decode() for r in range(world_size)) > 1
+            else:
+                shared = torch.cuda.device_count() < world_size
+        self._shared = shared
+        return shared
+
+    _bus_gen = 0
+
     def _fuse_level_ok(self, world_size: int) -> int:
         """Level 3's forward spins on the other blocks of its images, which must all be
         resident: ranks that share a device (same-GPU rehearsals) would split the GPU
-        between two such forwards, so they run the level-1 chain instead."""
+        between two such forwards, so they run the level-1 chain instead (logged)."""
         lvl = int(self.opts.fuse_level)
-        if lvl >= 3 and world_size > 1 and torch.cuda.device_count() < world_size:
+        if lvl >= 3 and self._device_shared(world_size):
+            self._log_downgrade("fuse level 3 -> 1 (a GPU is shared by several ranks)")
             return 1
         return lvl
 
     def _fuse_reduce_ok(self, world_size: int) -> int:
         """The fused reduction's waiting blocks are sized against ONE launch's share of the
-        GPU; ranks that share a device (same-GPU rehearsals: more ranks than devices) each
-        hold waiting blocks at once, so they keep the separate grad_reduce kernel."""
+        GPU; ranks that share a device (same-GPU rehearsals) each hold waiting blocks at
+        once, so they keep the separate grad_reduce kernel (logged)."""
         if not self.opts.fuse_reduce:
             return 0
-        return int(self.opts.fuse_reduce) if (world_size <= 1 or torch.cuda.device_count() >= world_size) else 0
+        if self._device_shared(world_size):
+            self._log_downgrade("fused slab reduction off (a GPU is shared by several ranks)")
+            return 0
+        return int(self.opts.fuse_reduce)
+
+    def _log_downgrade(self, what: str):
+        self.downgrades = getattr(self, "downgrades", []) + [what]
+        if self.rank == 0:
+            import sys
+
+            print(f"[ddp_amd] engine: {what}", file=sys.stderr)
 
     def sync_from_torch(self):
         """Order the engine stream after work queued on torch's current stream."""

@@ -54,10 +54,32 @@ SHARED_GPU_CUS = 64
 
 
 def grid_cap_for(requested: int, ranks_on_device: int) -> int:
-    """Blocks per bucket kernel for ``requested`` and the number of ranks on this GPU."""
+    """Blocks per bucket kernel for ``requested`` and the number of ranks on the most
+    shared GPU of the job (every rank must pass the same value: see :func:`max_sharing`)."""
     if ranks_on_device > 1:
         return max(4, min(requested, SHARED_GPU_CUS // ranks_on_device))
     return requested
+
+
+def max_sharing(bus_ids) -> int:
+    """Ranks on the most shared device, from every rank's PCI bus id.
+
+    The bucket kernel's barriers pair block b of one rank with block b of each peer, and
+    its publish / reduce passes assume one thread-to-quad map on every rank, so every rank
+    must size its grid from the SAME number - the job-wide maximum, not its own device's
+    count (3 ranks on 2 GPUs: ranks 0 and 2 share one, rank 1 is alone; all three use 2)."""
+    counts: dict = {}
+    for b in bus_ids:
+        counts[b] = counts.get(b, 0) + 1
+    return max(counts.values()) if counts else 1
+
+
+def check_blocks_agree(blocks_per_rank) -> None:
+    """Raise unless every rank built every channel with the same grid (list per rank)."""
+    first = list(blocks_per_rank[0])
+    for r, b in enumerate(blocks_per_rank):
+        if list(b) != first:
+            raise RuntimeError(f"xGMI channel grids differ across ranks (rank 0 {first}, rank {r} {list(b)})")
 
 
 def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
@@ -82,10 +104,13 @@ def create_xgmi(grads: torch.Tensor, buckets, rank: int, world: int, store=None,
         x = C.XgmiComm(rank, world, grads.device.index)
         bus = x.bus_id()
         store.set(f"{key}/bus/{rank}", bus.encode())
-        shared = sum(store.get(f"{key}/bus/{r}").decode() == bus for r in range(world))
-        cap = grid_cap_for(grid_cap, shared)
+        cap = grid_cap_for(grid_cap, max_sharing(store.get(f"{key}/bus/{r}").decode() for r in range(world)))
         for off, n, one in chans:
             x.add_channel(off, n, one, cap)
+        mine = [x.blocks(ch) for ch in range(len(chans))]
+        store.set(f"{key}/blk/{rank}", ",".join(map(str, mine)).encode())
+        check_blocks_agree([[int(v) for v in store.get(f"{key}/blk/{r}").decode().split(",") if v]
+                            for r in range(world)])
         x.set_data(grads)
         store.set(f"{key}/h/{rank}", x.export_handles())
         blobs = [store.get(f"{key}/h/{r}") for r in range(world)]

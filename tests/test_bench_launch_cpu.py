@@ -47,3 +47,38 @@ def test_with_gpus_rewrites_argv():
     assert bench._with_gpus(["--gpus", "8", "--steps", "5"], 1) == ["--gpus", "1", "--steps", "5"]
     assert bench._with_gpus(["--gpus=4", "--warmup", "2"], 4) == ["--gpus", "4", "--warmup", "2"]
     assert bench._with_gpus(["--steps", "5"], 2) == ["--gpus", "2", "--steps", "5"]
+
+
+def test_fallback_order_unit():
+    """VERDICT r3 #3b: a failing N-rank child is retried in a fresh child with the
+    conservative chain, then over RCCL; the record says which attempt produced it."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    seen = []
+
+    def launch(extra, timeout):
+        seen.append(tuple(extra))
+        if "--comm" not in extra:
+            return None, "rc=1"
+        return {"value": 1.0, "config": {}}, None
+
+    rec = bench.run_with_fallback(launch, 5.0)
+    assert [("production"), ("conservative chain")] == [a["attempt"] for a in rec["config"]["failed_attempts"]]
+    assert rec["config"]["fallback"] == "conservative chain over RCCL"
+    assert seen[0] == () and seen[1] == ("--fuse_level", "1", "--fuse_reduce", "0")
+    ok = bench.run_with_fallback(lambda e, t: ({"value": 2.0}, None), 5.0)
+    assert ok["config"]["fallback"] is None and ok["config"]["failed_attempts"] == []
+    with pytest.raises(SystemExit):
+        bench.run_with_fallback(lambda e, t: (None, "timed out"), 5.0)
+
+
+@pytest.mark.slow
+def test_self_launch_falls_back_on_failing_child():
+    """The real launcher path: the workers exit non-zero until the parent retries with the
+    conservative chain (``--dry_fail 1``)."""
+    rec = _run(["--gpus", "2", "--backend", "gloo", "--comm", "xgmi", "--dry_launch", "--dry_fail", "1"])
+    assert rec["ranks_seen"] == 2
+    assert rec["config"]["fallback"] == "conservative chain", rec
+    assert rec["fuse_level"] == 1 and rec["comm"] == "xgmi"
+    assert rec["config"]["failed_attempts"][0]["attempt"] == "production"

@@ -420,3 +420,45 @@ def test_engine_xgmi_world1_beside_fused_reduce(fuse_level, use_graph):
         assert torch.equal(out[0], out[1])
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_verify_chain_world1_forced(corrupt):
+    """VERDICT r3 #3a on one GPU: the start-up chain check (production = level 3 + fused
+    slab reduction + the xGMI kernels forced at world size 1; conservative = level 1 +
+    grad_reduce over the same plane) passes bitwise and restores its snapshot exactly (the
+    following training equals a run without the check); with a forced one-ulp disagreement
+    the engine downgrades to the conservative chain and trains to the same bits."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import free_port
+
+    dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}")
+    try:
+        imgs, labels = synthetic_mnist(2048)
+        data = DeviceMNIST(imgs, labels, dev)
+        out = []
+        for check in (False, True):
+            torch.manual_seed(0)
+            m = SimpleCNN().to(dev)
+            e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, None,
+                                     EngineOptions(graph_steps=5, force_allreduce=True, comm="xgmi"))
+            assert e.level3 and e.comm_kind.startswith("xgmi")
+            e.refresh()
+            if check:
+                kept = e.verify_chain(_corrupt_rank=0 if corrupt else None)
+                assert e.chain_check["ran"]
+                assert kept == (not corrupt), e.chain_check
+                assert e.chain_check["identical_here"] == (not corrupt)
+                assert e.level3 == (not corrupt) and (e.cfg["fuse_level"] == (3 if not corrupt else 1))
+            e.run_steps(12)
+            e.synchronize()
+            assert e.eng.sync_error == 0
+            out.append((e.fs.params.clone(), e.opt.momentum_buffer.clone()))
+        assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    finally:
+        dist.destroy_process_group()

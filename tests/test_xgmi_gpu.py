@@ -74,6 +74,19 @@ def _allreduce_worker(rank, world, port, q):
             got1 = grads.cpu()
             assert torch.equal(got1[s1], want[s1] * 0.5), f"one-shot bucket 1 it {it}"
             assert torch.equal(got1[:b0[1]], mine[:b0[1]]), "one-shot touched bucket 0"
+            # DDP's averaging: every rank's values times 1/3 BEFORE the
+            # rank-order sum (publish pass of the two-shot kernel / the one-shot publish)
+            s3 = torch.tensor(1.0 / 3.0, dtype=torch.float32)
+            want3 = allin[0] * s3
+            for r in range(1, world):
+                want3 = want3 + allin[r] * s3
+            for ch, sl in ((0, slice(0, b0[1])), (3, s1)):
+                grads.copy_(mine.cuda())
+                torch.cuda.synchronize()
+                x.all_reduce(ch, publish=True, prescale=1.0 / 3.0)
+                torch.cuda.synchronize()
+                assert x.error_flags() == 0
+                assert torch.equal(grads.cpu()[sl], want3[sl]), f"prescaled channel {ch} it {it}"
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok"))
@@ -136,6 +149,49 @@ def _engine_worker(rank, world, port, q, comm="xgmi2"):
         q.put((rank, repr(e), None))
 
 
+def _module_grad_worker(rank, world, port, q):
+    """Module-path DDP (native reducer, xGMI data plane): the all-reduced gradient is
+    bitwise the rank-order sum of every rank's local gradient times 1/world."""
+    try:
+        _init(rank, world, port)
+        from ddp_amd.models import SimpleCNN
+        from ddp_amd.models.layers import flat_space
+        from ddp_amd.ops import CrossEntropyLoss
+        from ddp_amd.parallel import DistributedDataParallel
+
+        dev = torch.device("cuda", 0)
+        lossf = CrossEntropyLoss()
+        g = torch.Generator().manual_seed(100 + rank)
+        x = torch.randn(8, 1, 28, 28, generator=g).to(dev)
+        y = torch.randint(0, 10, (8,), generator=g).to(dev)
+        torch.manual_seed(0)
+        twin = SimpleCNN(compute_dtype=torch.float32).to(dev)  # no DDP: the local gradient
+        lossf(twin(x), y).backward()
+        local = flat_space(twin).grads.detach().cpu().clone()
+        torch.manual_seed(0)
+        model = SimpleCNN(compute_dtype=torch.float32).to(dev)
+        ddp = DistributedDataParallel(model, comm="xgmi", bucket_cap_mb=0.05, first_bucket_mb=0.05)
+        assert ddp.comm_kind == "xgmi", ddp.comm_kind
+        lossf(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        got = flat_space(model).grads.detach().cpu()
+        alll = [None] * world
+        dist.all_gather_object(alll, local)
+        s = torch.tensor(1.0 / world, dtype=torch.float32)
+        want = alll[0] * s
+        for r in range(1, world):
+            want = want + alll[r] * s
+        ok = torch.equal(got, want) and ddp._native.xgmi.error_flags() == 0
+        msg = "ok" if ok else f"mismatch: max |diff| {(got - want).abs().max().item():.3e}, nb {len(ddp.buckets)}"
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, msg))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-600:]))
+
+
 def _run(worker, world, port, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -164,6 +220,17 @@ def test_engine_two_ranks_xgmi_identical_params(comm):
 
     res = _run(_engine_worker, 2, free_port(), comm)
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_module_ddp_prescale_sum_bitwise(world):
+    """module-path DDP averages like torch DDP - prescale by 1/world, then a
+    SUM in fixed rank order - bitwise against a CPU oracle, at world 2 and at 3 (where
+    sum-then-scale differs in the last bit)."""
+    from ddp_amd.parallel import free_port
+
+    res = _run(_module_grad_worker, world, free_port())
+    assert all(r[1] == "ok" for r in res), res
 
 
 def _plan_worker(rank, world, port, q, cap_mb, first_mb, dtype):
