@@ -189,14 +189,13 @@ def main():
     ap.add_argument("--graph_steps", type=int, default=None)
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--fuse_level", type=int, default=None,
-                    help="engine fusion level (0: 8 kernels/step, 1: 3 kernels/step, 2: fc + conv backward "
-                         "in one launch, 3: dZ2 in the forward, fc weight gradient inside the conv "
-                         "backward - 2 kernels/step); default = engine default (3)")
-    ap.add_argument("--l3_fc_role", type=int, default=None, choices=[0, 1, 2, 3],
+                    choices=[0, 1, 3],
+                    help="engine fusion level (0: 8 kernels/step, 1: 3 kernels/step, 3: dZ2 in the forward, "
+                         "fc weight gradient inside the conv backward - 2 kernels/step); default = engine default (3)")
+    ap.add_argument("--l3_fc_role", type=int, default=None, choices=[0, 1],
                     help="fuse level 3, one GPU: fc weight gradient inside the conv backward launch on "
-                         "persistent blocks after every conv block (1) or right after the dgrad blocks (2), "
-                         "on the dgrad blocks after their own work (3), or as its own kernel between "
-                         "forward and conv backward (0)")
+                         "blocks after every conv block (1) or as its own kernel between forward and conv "
+                         "backward (0)")
     ap.add_argument("--graph_head", type=int, default=None,
                     help="timed steps launched eagerly before the graph replays (default 0)")
     ap.add_argument("--sync_spin", type=int, default=0, choices=[0, 1],

@@ -741,7 +741,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_dgrad", &op_conv3x3_dgrad);
   m.def("conv3x3_dgrad_fused_w1", &op_conv3x3_dgrad_fused_w1);
   m.def("conv3x3_dgrad_blocks", &conv3x3_dgrad_blocks);
-  m.def("fc_conv_bwd_fc_blocks", &fc_conv_bwd_fc_blocks);
   m.def("conv3x3_wgrad", &op_conv3x3_wgrad);
   m.def("conv3x3_wgrad_blocks", &conv3x3_wgrad_blocks);
   m.def("fc_partial", &op_fc_partial);
@@ -926,11 +925,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? cfgd["fuse_reduce"].cast<int>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
-             TORCH_CHECK(c.l3_fc_role >= 0 && c.l3_fc_role <= 3, "engine: l3_fc_role must be 0..3");
+             TORCH_CHECK(c.l3_fc_role == 0 || c.l3_fc_role == 1, "engine: l3_fc_role must be 0 or 1");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;
              TORCH_CHECK(c.store_a1 >= 0 && c.store_a1 <= 2, "engine: store_a1 must be 0, 1 or 2");
-             TORCH_CHECK(c.fuse_level >= 0 && c.fuse_level <= 3, "engine: fuse_level must be 0, 1, 2 or 3");
+             TORCH_CHECK(c.fuse_level == 0 || c.fuse_level == 1 || c.fuse_level == 3,
+                         "engine: fuse_level must be 0, 1 or 3 (level 2 was removed in round 4)");
              TORCH_CHECK(conv3x3_fwd_lds(c.W, c.C1, c.pxt_fwd, c.fuse_level > 0, es) <= 160 * 1024 &&
                              conv3x3_wgrad_lds(c.W, c.C1, c.C2, c.wgrad_rows, c.fuse_level > 0, es) <= 160 * 1024 &&
                              conv3x3_dgrad_lds(c.W, c.C2, c.pxt_dgrad, true, es) <= 160 * 1024,
@@ -988,14 +988,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              b.xb = need("xb", at::kByte, B * HW).data_ptr<unsigned char>();
              b.yb = need("yb", at::kInt, B).data_ptr<int>();
              if (t.contains("sync_flags")) {  // in-launch hand-offs (fused reduction, level 2)
-               long nfl = SYNC_RED_INTS + fc_conv_bwd_fc_blocks(HW * c.C2) +
-                          conv3x3_dgrad_blocks(B, c.H, c.W, c.pxt_fwd);
+               long nfl = SYNC_RED_INTS;
                // level 3: the forward's per-image arrival counters, FWD_DZ_CNT_STRIDE ints apart
                if (c.fuse_level >= 3) nfl = std::max(nfl, (long)L3_IMG_OFF + (long)FWD_DZ_CNT_STRIDE * B);
                b.sync_flags = need("sync_flags", at::kInt, nfl).data_ptr<int>();
                b.sync_err = need("sync_err", at::kInt, 1).data_ptr<int>();
              }
-             TORCH_CHECK(c.fuse_level < 2 || c.f32 || b.sync_flags, "engine: fuse_level 2 needs sync_flags");
              Tensor images = need("images", at::kByte, HW);
              b.images = images.data_ptr<unsigned char>();
              Tensor labels = need("labels", at::kInt, 1);
@@ -1017,7 +1015,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("replay", &SimpleCNNEngine::replay)
       .def("destroy_graph", &SimpleCNNEngine::destroy_graph)
       .def("synchronize", &SimpleCNNEngine::synchronize, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("level2_active", &SimpleCNNEngine::level2_active)
       .def_property_readonly("last_fused_reduce", &SimpleCNNEngine::last_fused_reduce)
       .def_property_readonly("last_level3", &SimpleCNNEngine::last_level3)
       .def_property_readonly("last_fc_role", &SimpleCNNEngine::last_fc_role)

@@ -68,27 +68,7 @@ __device__ __forceinline__ void stage16(int n, SrcFn src, DstFn dst) {
   stage2<8>(n, src, dst, 0, src, dst);
 }
 
-// ---- in-launch dZ2 hand-off (fuse level 2: the fc role of the same launch produces dZ2)
-// fc-role block f publishes ready[f] = 1 once its COLS columns of dZ2 (all images) are
-// stored write-through and drained (fc_bwd_body.h); a conv-role block waits for the fc
-// blocks covering its staged pixel range, then reads dZ2 with sc1 loads (L1 bypass)
-// through a buffer resource - the MI355X_MICROARCH.md hand-off table's first row.
-struct DzWait {
-  const int* ready = nullptr;
-  int cols = 0;        // dZ2 columns (hw * C elements) per fc-role block
-  int* err = nullptr;  // set to 1 when a wait times out (the step's results are invalid)
-};
-constexpr unsigned long long DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 MHz clock
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t dz_rsrc(const void* base, long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                           (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000);
-}
-__device__ __forceinline__ bf16x8 ld16_sc1(__amdgpu_buffer_rsrc_t r, long byte_off) {
-  typedef __attribute__((ext_vector_type(4))) int i32x4_t;
-  const i32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16 /* sc1 */);
-  return __builtin_bit_cast(bf16x8, v);
-}
+constexpr unsigned long long DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 MHz clock (in-launch waits)
 
 // Fused slab reduction of the conv backward (conv3x3_bwd_kernel<..., FRED>)
 struct BwdReduce {
@@ -98,37 +78,7 @@ struct BwdReduce {
   int nconv = 0;          // conv-role blocks (the arrivals the reducers wait for); fc-role blocks follow
   int* done = nullptr;  // 8 arrival counters, 32 ints apart (zeroed by the step's forward)
   int* err = nullptr;   // set to 2 when the wait times out
-  int prio = 0;         // issue priority of the reducer waves once the wait is over (0, 2, 3)
 };
-
-// Block-wide wait until every fc-role block whose columns cover the flattened pixels
-// [p0, p1) (at most two images' hw ranges, p1 - p0 <= HW) has published.  Wave 0 polls
-// with sc1 loads (one flag per lane), sleeping between polls; then a block barrier.
-__device__ __noinline__ void wait_dz2(DzWait dw, long p0, long p1, int HW, int C) {
-  if ((threadIdx.x >> 6) == 0 && p0 < p1) {
-    const int lane = threadIdx.x & 63;
-    const long n0 = p0 / HW;
-    const long e0 = p1 < (n0 + 1) * HW ? p1 : (n0 + 1) * HW;
-    const int a0 = (int)(p0 - n0 * HW), a1 = (int)(e0 - n0 * HW);  // hw [a0, a1)
-    const int b1 = (int)(p1 - e0);                                  // next image: hw [0, b1)
-    const int fa0 = (int)((long)a0 * C / dw.cols), fa1 = (int)(((long)a1 * C - 1) / dw.cols);
-    const int fb1 = b1 > 0 ? (int)(((long)b1 * C - 1) / dw.cols) : -1;
-    int* rd = const_cast<int*>(dw.ready);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (true) {
-      int ok = 1;
-      for (int f = fa0 + lane; f <= fa1; f += 64) ok &= __hip_atomic_load(rd + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-      for (int f = lane; f <= fb1; f += 64) ok &= __hip_atomic_load(rd + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-      if (__all(ok)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > DZ_WAIT_TICKS) {
-        if (lane == 0 && dw.err) __hip_atomic_store(dw.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-}
 
 // Geometry specialisation: kernels take <GH, GW, GCI, GCO>; non-zero values replace
 // the runtime H, W, Cin, Cout so all index arithmetic (divisions by W, H*W, channel
@@ -530,16 +480,12 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 // ---------------------------------------------------------------- data gradient
 // A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
 // being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
-// WAITDZ (fuse level 2): dY (= dZ2) is produced by the fc role of the same launch; the
-// block stages everything that does not depend on it first (weights, x0, the ReLU1 mask),
-// then waits for its pixel range (wait_dz2) and stages dY with sc1 loads.
 template <typename T, int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI,
-          int GCO, bool WAITDZ = false>
+          int GCO>
 __device__ __forceinline__ void dgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ WT,
     const T* __restrict__ Xact, T* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
-    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by,
-    const DzWait& dzw = DzWait()) {
+    const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int CE = P::CE;
@@ -583,7 +529,7 @@ __device__ __forceinline__ void dgrad_body(
             return ld16(WT + ((long)tap * Cin + ci_blk + r) * Cout + co);
           },
           [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * CE; st16(sWT + r * WS + c, v); },
-          WAITDZ ? 0 : XR * cpc,
+          XR * cpc,
           [&](int i) {
             const int r = i / cpc, c = (i - r * cpc) * CE;
             const long Pq = Pbase + r;
@@ -629,20 +575,6 @@ __device__ __forceinline__ void dgrad_body(
     }
     DDP_STAMP(STAMP_K_CONV1, 2);  // mask computed
   }
-  if constexpr (WAITDZ) {
-    static_assert(!F32 && !MASK_DY, "the in-launch dZ2 hand-off is bf16, unmasked");
-    wait_dz2(dzw, Pbase > 0 ? Pbase : 0, Pbase + XR < Ptot ? Pbase + XR : Ptot, HW, Cout);
-    const __amdgpu_buffer_rsrc_t rs = dz_rsrc(dY, Ptot * Cout * (long)sizeof(T));
-    stage2<16>(XR * cpc,
-               [&](int i) {
-                 const int r = i / cpc, c = (i - r * cpc) * CE;
-                 const long Pq = Pbase + r;
-                 return (Pq >= 0 && Pq < Ptot) ? ld16_sc1(rs, (Pq * Cout + c) * (long)sizeof(T)) : zero8();
-               },
-               [&](int i, bf16x8 v) { const int r = i / cpc, c = (i - r * cpc) * CE; st16(sDY + r * DS + c, v); },
-               0, [&](int) { return zero8(); }, [&](int, bf16x8) {});
-  }
-
   const int kofs = P::kofs(lane);
   const int col = lane & 15;
   int h[PXT], w[PXT], rowc[PXT];
@@ -809,8 +741,6 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // so each lane reads single floats - MFMA j takes slot s0 + 4j + (lane >> 4) - with row
 // strides of 16 mod 32 dwords (Cout + 16, Cin + 16), conflict-free for ds_read_b32's two
 // 32-lane groups (lanes l and l + 16 read adjacent slots).
-// WAITDZ (fuse level 2): X staging / the conv1 recompute first, then wait_dz2 for the
-// block's rows and the dY staging with sc1 loads (see dgrad_body).
 // STAGE: the slab row goes through LDS (needs slab-row bytes of LDS, see conv3x3_bwd_lds)
 // and leaves as 16-byte write-through stores - from the MFMA layout each lane holds one
 // float per 64-byte run of the row, and 4-byte write-through stores took ~2.4 us per block.
@@ -822,15 +752,13 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // half 0 writes the ci < 16 columns and the bias, half 1 the rest.  The two halves of a
 // row chunk are 8 blocks apart (same XCD: blocks go round-robin over the 8 XCDs), so the
 // second one's dY tile reads hit the same L2.
-template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO, bool WAITDZ = false,
-          bool STAGE = false, int CS = 1>
+template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO, bool STAGE = false, int CS = 1>
 __device__ __forceinline__ void wgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ X,
-    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by,
-    const DzWait& dzw = DzWait()) {
+    float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int CE = Prec<T>::CE;
-  static_assert(CS == 1 || (CS == 2 && STAGE && !F32 && !WAITDZ && GCI == 32 && GCO == 64),
+  static_assert(CS == 1 || (CS == 2 && STAGE && !F32 && GCI == 32 && GCO == 64),
                 "the channel-split wgrad role is the bf16 staged-slab SimpleCNN variant");
   DDP_STAMP(STAMP_K_WGRAD, 0);
   DDP_GEOM_OVERRIDE();
@@ -901,7 +829,7 @@ __device__ __forceinline__ void wgrad_body(
         },
         [&](int pos, int g) { return sX + (long)pos * XS + 8 * g; });
   };
-  const int ndy = WAITDZ ? 0 : nslot * cpy_dy;
+  const int ndy = nslot * cpy_dy;
   stage2<F32 ? 32 : 16>(ndy, dy_src, dy_dst,
           A1X ? 0 : (R + 2) * XW * cpy_x,
           [&](int i) {
@@ -923,26 +851,6 @@ __device__ __forceinline__ void wgrad_body(
     __syncthreads();
     DDP_STAMP(STAMP_K_WGRAD, 1);
     recompute();
-  }
-  if constexpr (WAITDZ) {
-    static_assert(!F32 && !MASK_DY, "the in-launch dZ2 hand-off is bf16, unmasked");
-    const long pimg = (long)n * H * W;
-    wait_dz2(dzw, pimg + (long)r0 * W, pimg + (long)(r0 + R < H ? r0 + R : H) * W, H * W, Cout);
-    const __amdgpu_buffer_rsrc_t rs = dz_rsrc(dY, (long)B * H * W * Cout * (long)sizeof(T));
-    stage2<16>(nslot * cpy_dy,
-               [&](int i) {
-                 const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
-                 const int r = slot / Wp, c = slot - (slot / Wp) * Wp;
-                 const int hh = r0 + r;
-                 return (r < R && hh < H && c < W)
-                            ? ld16_sc1(rs, ((((long)n * H + hh) * W + c) * Cout + ch) * (long)sizeof(T))
-                            : zero8();
-               },
-               [&](int i, bf16x8 v) {
-                 const int slot = i / cpy_dy, ch = (i - slot * cpy_dy) * CE;
-                 st16(sdY + (long)slot * DS + ch, v);
-               },
-               0, [&](int) { return zero8(); }, [&](int, bf16x8) {});
   }
   __syncthreads();
   DDP_STAMP(STAMP_K_WGRAD, 2);
@@ -1163,8 +1071,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       // the loss and the step counter (nothing else in this launch reads them), then every
       // wave takes 128-column chunks f * 4 + wave, + 4 * nfc, ... (fc_dw_wave_chunk)
       DDP_STAMP(STAMP_K_FC_BWD, 0);
-      if (fcr.prio == 3) __builtin_amdgcn_s_setprio(3);
-      else if (fcr.prio) __builtin_amdgcn_s_setprio(2);
+      // raised issue priority: the fc role's late-dispatched blocks are one of the launch's
+      // two tails (+0.9 %, profiles/r3_cnn/prio)
+      __builtin_amdgcn_s_setprio(2);
       const float* s_dl = fc_role_prologue(fcr, B, smem, f == 0);
       DDP_STAMP(STAMP_K_FC_BWD, 1);
       // one 128-column chunk per wave, straight-line (a chunk loop let the compiler hoist
@@ -1177,44 +1086,18 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
     }
     if (f >= 0) cb -= fcr.nfc;
   }
-  if constexpr (FCR) {
-    if (fcr.prio == 2 && cb >= nd) __builtin_amdgcn_s_setprio(1);  // wgrad role: between fc and dgrad
-  }
   if (cb < nd)
     dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
         dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, cb, 0);
   else
-    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, false, true, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
+    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, true, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
                                                                   W, Cin, Cout, R, c1, smem, cb - nd, 0);
-  // fc_pos 2: each dgrad block runs fc chunks 2 * cb + wave (waves 0, 1) after its own
-  // work (and its arrival: the reducers never wait for the fc work)
-  auto dgrad_fc = [&]() {
-    if constexpr (FCR) {
-      if (fcr.fc_pos == 2 && cb < nd) {
-        __syncthreads();  // every wave is done with the dgrad LDS
-        const float* s_dl = fc_role_prologue(fcr, B, smem, cb == 0);
-        DDP_STAMP(STAMP_K_FC_BWD, 1);
-        const int wv = threadIdx.x >> 6;
-        const long nch = (fcr.K + 127) / 128;
-        // one chunk per wave, straight-line (a chunk loop makes the compiler hoist the
-        // unrolled body's row offsets: the whole kernel then spills); the host checks
-        // nch <= 2 * nd
-        const long q = 2L * cb + wv;
-        if (wv < 2 && q < nch) fc_role_chunk(fcr, s_dl, B, q);
-        DDP_STAMP(STAMP_K_FC_BWD, 4);
-      }
-    }
-  };
-  if constexpr (!FRED) dgrad_fc();
   if constexpr (FRED) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
     __syncthreads();
     if (threadIdx.x == 0)
       __hip_atomic_fetch_add(red.done + 32 * (blockIdx.x & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cb < red.first_reducer) {
-      dgrad_fc();
-      return;
-    }
+    if (cb < red.first_reducer) return;
     // reducer w of nr: the LAST nr conv blocks of the grid (dispatched after every block they
     // wait for; the host keeps nr within a quarter of the resident capacity)
     const int nblk = red.nconv > 0 ? red.nconv : (int)gridDim.x;
@@ -1241,8 +1124,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       }
     }
     __syncthreads();
-    if (red.prio == 3) __builtin_amdgcn_s_setprio(3);
-    else if (red.prio == 2) __builtin_amdgcn_s_setprio(2);
     DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
     float* part = reinterpret_cast<float*>(smem);
     slab_fused_run<J>(red.ss, pl, part);
@@ -1252,56 +1133,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
     }
     if (w == 0 && threadIdx.x == 0 && red.ss.step_ctr) red.ss.step_ctr[0] += 1;
     DDP_STAMP(STAMP_K_GRAD_REDUCE, 2);
-  }
-}
-
-// ---------------------------------------------------------------- fused fc + conv backward
-// Fuse level 2 (bf16, single process): the fc backward and the whole conv backward in ONE
-// launch.  Blocks [0, nfc) are the fc role (fc_bwd_body.h: cross-entropy prologue, dZ2,
-// fc weight gradient + fused SGD; 4 waves x 2 virtual waves, bit-identical to the 8-wave
-// fc_bwd kernel) and publish their dZ2 columns; blocks [nfc, nfc + nd) the data gradient,
-// the rest the weight gradient.  The conv roles stage what does not depend on dZ2
-// (weights, uint8 images, the conv1 recompute / ReLU1 mask) while the fc role runs, then
-// wait for the fc blocks of their own pixel range (no kernel boundary between them).
-// Deadlock-free by dispatch order: the fc blocks have the lowest indices and never wait,
-// so every fc block is dispatched before any conv block can occupy a slot it needs.
-struct FcConvBwdArgs {
-  // fc role
-  const bf16_t* a2 = nullptr;
-  const bf16_t* wfc = nullptr;  // bf16 [NO][HW*C] shadow
-  bf16_t* dz2 = nullptr;
-  float* dW = nullptr;
-  float scale = 1.f;
-  long K = 0;
-  FcBwdExtras ex{};
-  int nfc = 0;
-  // conv roles
-  const bf16_t* w2t = nullptr;
-  float* w1slab = nullptr;
-  float* w2slab = nullptr;
-  int B = 0, H = 0, W = 0, Cin = 0, Cout = 0, R = 0, nd = 0;
-  C1Src c1{};
-  const bf16_t* Xact = nullptr;
-  DzWait dzw{};
-};
-constexpr int FCC_WPB = 4, FCC_VW = 8, FCC_CPL = 2;
-
-template <int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO>
-__global__ __launch_bounds__(256, 2) void fc_conv_bwd_kernel(FcConvBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bx = blockIdx.x;
-  if (bx < a.nfc) {
-    fc_bwd_body<bf16_t, true, true, 10, FCC_WPB, FCC_VW, FCC_CPL>(
-        nullptr, a.a2, a.wfc, a.dz2, a.dW, a.scale, a.B, a.K, 10, a.ex, reinterpret_cast<float*>(smem), bx,
-        const_cast<int*>(a.dzw.ready));
-  } else if (bx < a.nfc + a.nd) {
-    dgrad_body<bf16_t, PXT, false, true, true, DA1X, GH, GW, GCI, GCO, true>(
-        a.dz2, nullptr, a.w2t, DA1X ? nullptr : a.Xact, nullptr, a.B, a.H, a.W, a.Cin, a.Cout, a.c1.x, 1, a.c1.bi,
-        a.w1slab, a.c1, smem, bx - a.nfc, 0, a.dzw);
-  } else {
-    wgrad_body<bf16_t, false, WA1X, GH, GW, GCI, GCO, true>(a.dz2, nullptr, WA1X ? nullptr : a.Xact, a.w2slab, a.B,
-                                                          a.H, a.W, a.Cin, a.Cout, a.R, a.c1, smem,
-                                                          bx - a.nfc - a.nd, 0, a.dzw);
   }
 }
 
@@ -1614,17 +1445,12 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
                                "given, B <= 48, no last-block count)");
     fcr = *fc;
     fcr.nconv = nd + nw;
-    // one 128-column chunk per wave (4 per block): the first blocks take the resident slots
-    // the conv blocks leave free, the rest those the dgrad blocks free first
-    // fc_pos 2 runs one chunk per dgrad-block wave 0 / 1: with fewer than nch / 2 dgrad
-    // blocks (small batches) the fc role keeps its own blocks (fc_pos 0)
-    const int fpos = (fc->fc_pos == 2 && (fc->K + 127) / 128 > 2L * nd) ? 0 : fc->fc_pos;
-    fcr.fc_pos = fpos;
-    nfc = fpos == 2 ? 0 : (int)((fc->K + 127) / 128 + 3) / 4;
+    // one 128-column chunk per wave (4 per block), blocks after every conv block: the first
+    // take the resident slots the conv blocks leave free, the rest those the dgrad blocks
+    // free first
+    nfc = (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
-    // fc blocks after every conv block (fc_pos 0: dispatched into the slots the conv blocks
-    // leave free) or right after the dgrad role (fc_pos 1); fc_pos 2: the dgrad blocks
-    fcr.fc0 = fpos == 1 ? nd : nd + nw;  // (the reducers are wgrad blocks: never a dgrad one)
+    fcr.fc0 = nd + nw;
     if ((size_t)B * (FCDW_LD + 10) * sizeof(float) > lds)
       throw std::runtime_error("conv3x3_bwd: LDS too small for the fc role");
   }
@@ -1653,10 +1479,6 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     red.nchunks = slab_chunks(*fused);
     red.done = red_done;
     red.err = red_err;
-    {  // (A/B knob) DDP_AMD_RED_PRIO=2|3: reducer waves at raised issue priority
-      const char* e = std::getenv("DDP_AMD_RED_PRIO");
-      red.prio = e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 0;
-    }
     if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");
   }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
@@ -1680,46 +1502,6 @@ bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, flo
                  int wgrad_split, bool exclusive) {
   return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
                     fused_reduce, red_done, red_err, wgrad_split, nullptr, exclusive);
-}
-
-int fc_conv_bwd_fc_blocks(long K) { return (int)((K + 64 * FCC_CPL - 1) / (64 * FCC_CPL)); }
-int fc_conv_bwd_cols() { return 64 * FCC_CPL; }
-
-void fc_conv_bwd(const bf16_t* a2, const bf16_t* wfc, bf16_t* dz2, float* dW, float scale, long K,
-                 const FcBwdExtras& ex, const bf16_t* w2t, float* w1slab, float* w2slab, int B, int H, int W,
-                 int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact, bool wgrad_load_a1,
-                 const int* ready, int* err, hipStream_t s) {
-  if (!ex.part || K != (long)H * W * Cout || (long)K % (64 * FCC_CPL) != 0)
-    throw std::runtime_error("fc_conv_bwd: needs the cross-entropy prologue and K = H*W*C, a multiple of the fc columns");
-  if (64L * pxt + 2 * W + 2 > (long)H * W || (long)(R < H ? R : H) * W > (long)H * W)
-    throw std::runtime_error("fc_conv_bwd: a conv block's pixel range must fit one image");
-  FcConvBwdArgs a;
-  a.a2 = a2; a.wfc = wfc; a.dz2 = dz2; a.dW = dW; a.scale = scale; a.K = K; a.ex = ex;
-  a.nfc = fc_conv_bwd_fc_blocks(K);
-  a.w2t = w2t; a.w1slab = w1slab; a.w2slab = w2slab;
-  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.R = R;
-  a.nd = conv3x3_dgrad_blocks(B, H, W, pxt);
-  a.c1 = c1; a.Xact = Xact;
-  a.dzw.ready = ready; a.dzw.cols = 64 * FCC_CPL; a.dzw.err = err;
-  const int nw = conv3x3_wgrad_blocks(B, H, R);
-  const long npart = ((long)B * ex.HW + ex.CH - 1) / ex.CH * 2 * 10;
-  const size_t fc_lds = sizeof(float) * (size_t)fcb_lds_floats(B, 10, true, npart, fcb_red_floats<FCC_WPB, 10, FCC_CPL>());
-  const size_t cv_lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, 2);
-  const size_t lds = fc_lds > cv_lds ? fc_lds : cv_lds;
-  if (lds > 160 * 1024) throw std::runtime_error("fc_conv_bwd: LDS over 160 KiB");
-  if (!(H == 28 && W == 28 && Cin == 32 && Cout == 64))
-    throw std::runtime_error("fc_conv_bwd: built for SimpleCNN's conv2 (28x28, 32 -> 64)");
-  const dim3 grid((unsigned)(a.nfc + a.nd + nw));
-#define LFC(PX, DA, WA)                                                                               \
-  do {                                                                                                \
-    auto k = fc_conv_bwd_kernel<PX, DA, WA, 28, 28, 32, 64>;                                          \
-    lds_optin(k, lds);                                                                                \
-    hipLaunchKernelGGL(k, grid, dim3(256), lds, s, a);                                                \
-  } while (0)
-  if (!Xact) { if (pxt == 2) LFC(2, true, true); else LFC(1, true, true); }
-  else if (wgrad_load_a1) { if (pxt == 2) LFC(2, false, false); else LFC(1, false, false); }
-  else { if (pxt == 2) LFC(2, false, true); else LFC(1, false, true); }
-#undef LFC
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv3x3)

@@ -276,12 +276,7 @@ struct BwdFc {
   float* dW = nullptr;         // null: fused optimizer only
   float scale = 1.f;
   long K = 0;
-  int fc_pos = 0;              // 0: fc blocks after every conv block, 1: right after the dgrad blocks,
-                               // 2: no fc blocks - each dgrad block runs 2 chunks (waves 0, 1) after
-                               //    its arrival (the fc work leaves the launch's first-wave slots)
   int nconv = 0, fc0 = 0, nfc = 0;  // (set by the launcher: nfc = one 128-column chunk per wave)
-  int prio = 0;                // 1: the fc-role waves raise their issue priority (s_setprio 2);
-                               // 2: and the wgrad role's to 1; 3: fc role at s_setprio 3
   FcBwdExtras ex{};
 };
 size_t fc_bwd_lds(int B, int NO, bool xent, long npart = 0);  // npart: see linear.hip
@@ -292,17 +287,6 @@ void fc_bwd(const float* dL, const bf16_t* X, const bf16_t* Wf, bf16_t* dX, floa
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
 void fc_bwd(const float* dL, const float* X, const float* Wf, float* dX, float* dW, float scale,
             int B, long K, int NO, bool mask, hipStream_t s, const FcBwdExtras& ex = FcBwdExtras());
-
-// Fuse level 2 (bf16, single process): fc backward (cross-entropy prologue, dZ2, dW /
-// fused SGD, as fc_bwd with ex.part set) and the conv backward (as conv3x3_bwd) in ONE
-// launch, with an in-launch dZ2 hand-off through ready[fc_conv_bwd_fc_blocks(K)] flags
-// (zeroed by the step's conv3x3_fwd, C1Src::zero_i32); err[0] = 1 if a wait timed out.
-int fc_conv_bwd_fc_blocks(long K);
-int fc_conv_bwd_cols();
-void fc_conv_bwd(const bf16_t* a2, const bf16_t* wfc, bf16_t* dz2, float* dW, float scale, long K,
-                 const FcBwdExtras& ex, const bf16_t* w2t, float* w1slab, float* w2slab, int B, int H, int W,
-                 int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact, bool wgrad_load_a1,
-                 const int* ready, int* err, hipStream_t s);
 
 // ---- cross-entropy --------------------------------------------------------------------
 void xent(const float* part, int G, const float* bias, int C, int B, const long long* labels64,

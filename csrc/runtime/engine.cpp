@@ -26,8 +26,6 @@
 //   level 1: conv1 recomputed inside conv2 fwd / dgrad / wgrad, cross-entropy in the
 //            fc_bwd prologue, optimizer in the epilogues, the slab reduction inside the
 //            conv backward: 3 kernels (forward -> fc_bwd -> conv backward);
-//   level 2: level 1 with fc_bwd and the conv backward in one launch (dZ2 handed off
-//            inside it; slower - its blocks are not co-resident);
 //   f32 = 1 (--dtype fp32): the level-1 chain with exact fp32 operands (launch_step_f32).
 //
 // Buckets follow the reference DDP's rebuilt layout by default:
@@ -105,19 +103,13 @@ void SimpleCNNEngine::synchronize() {
   DDP_HIP_CHECK(hipStreamSynchronize(cs_));
   if (const int e = sync_error()) {
     throw std::runtime_error(std::string("engine: an in-launch hand-off wait timed out (") +
-                             (e == 1 ? "level-2 dZ2" : e == 2 ? "fused slab reduction" : "level-3 forward dZ2") +
+                             (e == 2 ? "fused slab reduction" : "level-3 forward dZ2") +
                              "); results invalid");
   }
 }
 
-bool SimpleCNNEngine::level2_active() const {
-  const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
-  const bool dist = use_x || (comm_ && (comm_->world() > 1 || cfg_.force_allreduce));
-  return cfg_.fuse_level == 2 && !cfg_.f32 && !dist && cfg_.fuse_opt && b_.sync_flags && b_.sync_err;
-}
-
 bool SimpleCNNEngine::level3_active(int batch) {
-  if (cfg_.fuse_level < 3 || cfg_.f32 || !b_.sync_flags || !b_.sync_err || level2_active()) return false;
+  if (cfg_.fuse_level < 3 || cfg_.f32 || !b_.sync_flags || !b_.sync_err) return false;
   if (batch <= 0 || batch > cfg_.max_batch) return false;
   signed char& f = l3_fits_[batch];
   if (f < 0) f = conv3x3_fwd_dz_fits(batch, cfg_.H, cfg_.W, cfg_.pxt_fwd) && cfg_.C1 == 32 && cfg_.C2 == 64 ? 1 : 0;
@@ -177,19 +169,18 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   c1.yb_out = b_.yb;
   c1.labels = b_.labels;
   if (cfg_.store_a1) c1.a1_out = b_.a1;
-  const bool l2 = level2_active();
   const bool l3 = level3_active(B);
-  const bool fred = f1 && !l2 && cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
+  const bool fred = f1 && cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
   const long n_fc = (long)NO * HW * C2;
-  if (l2 || fred || l3) {  // the forward resets the step's hand-off counters / flags
+  if (fred || l3) {  // the forward resets the step's hand-off counters
     const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
-    const int nsync = SYNC_RED_INTS + (l2 ? fc_conv_bwd_fc_blocks((long)HW * C2) : 0) + (l3 ? L3_FC_INTS : 0);
+    const int nsync = SYNC_RED_INTS + (l3 ? L3_FC_INTS : 0);
     c1.zero_i32 = b_.sync_flags;
     c1.zero_per_block = (nsync + nfwd - 1) / nfwd;
     c1.zero_total = nsync;  // level 3: the per-image counters follow (L3_IMG_OFF)
   }
   if (!l3 && plain_stale_) {
-    // the plain bf16 fc shadow (read by the level-1/2 fc backward) was not refreshed by the
+    // the plain bf16 fc shadow (read by the level-1 fc backward) was not refreshed by the
     // level-3 steps before this one: re-derive every shadow from the fp32 master first
     refresh_shadows();
     plain_stale_ = false;
@@ -281,12 +272,6 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       ex.sh_plain = nullptr;  // level 3 never reads the plain bf16 fc shadow (stale until refreshed)
       fcr.a2 = b_.a2;
       fcr.dl = b_.dlogits;
-      fcr.fc_pos = cfg_.l3_fc_role == 3 ? 2 : (cfg_.l3_fc_role == 2 ? 1 : 0);
-      {  // wave issue priority of the roles: fc role 2 (default: +0.9 %, profiles/r3_cnn/prio),
-         // DDP_AMD_FC_PRIO=0 none, =2 also the wgrad role at 1
-        const char* e = std::getenv("DDP_AMD_FC_PRIO");
-        fcr.prio = e && e[0] ? (e[0] - '0') : 1;
-      }
       fcr.dW = fopt ? nullptr : G + b_.off_wfc;
       fcr.scale = inv_ws;
       fcr.K = (long)HW * C2;
@@ -297,11 +282,6 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
              /*mask=*/true, cs_, ex);
     }
     plain_stale_ = true;
-  } else if (l2) {
-    // level 2: fc backward + conv backward in one launch (dZ2 handed off inside it)
-    fc_conv_bwd(b_.a2, b_.wfc_bf16, b_.dz2, nullptr, inv_ws, (long)HW * C2, ex, b_.w2t_bf16, b_.w1slab,
-                b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b,
-                cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, b_.sync_flags + SYNC_RED_INTS, b_.sync_err, cs_);
   } else {
     fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
            (long)HW * C2, NO, /*mask=*/true, cs_, ex);
@@ -349,9 +329,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   }
   ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
   bool reduced = false;  // the conv backward launch also did grad_reduce's work
-  if (l2) {
-    // (inside fc_conv_bwd)
-  } else if (f1) {
+  if (f1) {
     // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
     reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                           cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,

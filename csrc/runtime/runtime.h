@@ -208,9 +208,8 @@ struct EngineConfig {
   // 1: 6 kernels - conv1 recomputed inside conv2 fwd/dgrad/wgrad from the uint8
   //    images (a1 never touches HBM) and cross-entropy folded into fc_bwd
   //    (4 per step with the fused optimizer: conv fwd, fc_bwd, conv bwd, grad_reduce)
-  // 2: level 1 with fc_bwd and the conv backward in ONE launch (in-launch dZ2 hand-off,
-  //    fc_conv_bwd) where it applies - bf16, single process, fused optimizer: 3 kernels
-  //    per step; otherwise (world > 1, fp32, fuse_opt 0) the level-1 chain
+  // (2: a level-1 variant with fc_bwd and the conv backward in one launch - measured
+  //    slower than level 1 and removed in round 4)
   // 3: the fc backward leaves the critical path - the conv forward computes dZ2 itself
   //    (FwdDz: per-image in-launch wait, then dL and dZ2 from the fc weight fragments it
   //    holds) and the fc weight gradient + fused SGD (fc_bwd without dX, dL given) runs as
@@ -219,10 +218,10 @@ struct EngineConfig {
   //    all-reduce overlaps the conv backward).  bf16, where every forward block fits on the
   //    GPU at once (conv3x3_fwd_dz_fits); otherwise the level-1 chain
   int fuse_level = 0;
-  // level 3, single process: 3 = the dgrad blocks run the fc chunks after their own work,
-  // 1 = fc role after every conv block (on the resident slots they
-  // leave free), 2 = right after the dgrad blocks, 0 = the fc weight gradient as its own
-  // kernel (what world size > 1 runs)
+  // level 3, single process: 1 = the fc weight gradient as a role of the conv backward
+  // launch, on blocks after every conv block (the resident slots they leave free); 0 = as
+  // its own kernel (what world size > 1 runs).  (Placements 2 / 3 - right after the dgrad
+  // blocks, on the dgrad blocks - measured slower and were removed in round 4.)
   int l3_fc_role = 1;
   // 1: single-process steps apply SGD in the epilogues of fc_bwd / grad_reduce (no
   //    separate optimizer kernel); 0: always the flat SGD kernel (equivalence tests)
@@ -273,7 +272,6 @@ class SimpleCNNEngine {
   // in-launch wait-timeout word (0 = ok, 1 = level-2 dZ2 wait, 2 = fused reduction,
   // 3 = level-3 forward's per-image wait); sticky
   int sync_error() const { return err_host_ ? __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) : 0; }
-  bool level2_active() const;
   // whether a step of `batch` images runs the level-3 chain (fuse_level 3 and it applies)
   bool level3_active(int batch);
   // whether the last launched step reduced its weight-gradient slabs inside the conv

@@ -59,8 +59,7 @@ class EngineOptions:
     # 0: 8 kernels/step (a1 stored, separate xent); 1: 6 kernels/step (conv1 recomputed
     # inside conv2 fwd/dgrad/wgrad from the uint8 images, xent folded into fc_bwd; 3 with
     # the fused optimizer and the fused slab reduction: forward -> fc_bwd -> conv backward);
-    # 2: level 1 with fc_bwd and the conv backward in ONE launch (in-launch dZ2 hand-off)
-    # where it applies - bf16, world size 1, fused optimizer (slower: kept for reference);
+    # (2 - fc_bwd and the conv backward in one launch - measured slower, removed in round 4);
     # 3: the fc backward off the critical path - the forward computes dZ2 itself (per-image
     # in-launch wait for the logits) and the fc weight gradient + SGD runs on a side stream
     # beside the conv backward (critical path: forward -> conv backward).  bf16 where every
@@ -69,9 +68,9 @@ class EngineOptions:
     fuse_level: int = 3
     # level 3, single process: the fc weight gradient as a third role of the conv backward
     # launch (2 kernels per step) - 1: its blocks (one 128-column chunk per wave) after every
-    # conv block, on the resident slots the conv blocks leave free; 2: the same blocks right
-    # after the dgrad blocks; 0: its own light kernel between forward and conv backward (what
-    # world size > 1 always runs, so the fc bucket's all-reduce overlaps the conv backward)
+    # conv block, on the resident slots the conv blocks leave free; 0: its own light kernel
+    # between forward and conv backward (what world size > 1 always runs, so the fc bucket's
+    # all-reduce overlaps the conv backward)
     l3_fc_role: int = 1
     # single-process steps: SGD in the epilogues of fc_bwd / grad_reduce (no optimizer kernel)
     fuse_opt: bool = True
@@ -187,12 +186,11 @@ class FusedSimpleCNNEngine:
                     else data.labels_i32),
             idx=torch.zeros(n_rank, dtype=torch.int32, device=dev),
         )
-        # in-launch hand-offs (fused slab reduction, level-2 dZ2 flags), zeroed by each
+        # in-launch hand-offs (fused slab reduction, level-3 arrival counters), zeroed by each
         # step's forward, and their wait-timeout word
         # (level 3: [256] the fc side kernel's last-block counter, [288, 288 + B) the
         # forward's per-image arrival counters - engine.cpp L3_IMG_OFF)
-        nfl = 256 + self.C.fc_conv_bwd_fc_blocks(HW * 64) + self.C.conv3x3_dgrad_blocks(B, 28, 28, self.opts.pxt_fwd)
-        nfl = max(nfl, 256 + 32 + 64 * B)  # (counters 64 ints apart: FWD_DZ_CNT_STRIDE)
+        nfl = 256 + 32 + 64 * B  # (counters 64 ints apart: FWD_DZ_CNT_STRIDE)
         self.t["sync_flags"] = torch.zeros(nfl, dtype=torch.int32, device=dev)
         # (the engine replaces it by a coherent host word: eng.sync_error)
         self.t["sync_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -252,7 +250,6 @@ class FusedSimpleCNNEngine:
             self.eng.set_momentum_started(True)
         self.stream = torch.cuda.ExternalStream(self.eng.stream, device=dev)
         # kernels per step of the chain that actually runs (engine.cpp / EngineConfig)
-        self.level2 = bool(self.eng.level2_active)
         self.level3 = bool(self.eng.level3_active(B))
         self._captured = 0
         self.steps_done = 0
@@ -344,7 +341,6 @@ class FusedSimpleCNNEngine:
             self.eng = chosen
             self.cfg = ref_cfg
             self.stream = torch.cuda.ExternalStream(self.eng.stream, device=self.fs.params.device)
-            self.level2 = bool(self.eng.level2_active)
             self.level3 = bool(self.eng.level3_active(B))
             self._captured = 0
         self.start_epoch(0)

@@ -73,30 +73,9 @@ def test_fuse_level1_bitwise_equals_level0(B):
     assert torch.equal(e0.t["loss_hist"][:7], e1.t["loss_hist"][:7])
 
 
-@pytest.mark.parametrize("B", [32, 20, 64])
-def test_fuse_level2_bitwise_equals_level1(B):
-    """Level 2 runs fc_bwd and the conv backward as ONE launch with an in-launch dZ2
-    hand-off (fc role: 4 waves x 2 virtual waves); params, momentum and losses must equal
-    the level-1 chain bit for bit, graph-captured, and no hand-off wait may time out."""
-    m1, o1, _, e1, _, _ = _setup(B=B, use_graph=True, momentum=0.9, fuse_level=1)
-    m2, o2, _, e2, _, _ = _setup(B=B, use_graph=True, momentum=0.9, fuse_level=2)
-    assert not e1.level2 and e2.level2
-    e1.run_steps(12)
-    e2.run_steps(12)
-    e1.synchronize(); e2.synchronize()
-    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
-        assert torch.equal(a, b), n
-    assert torch.equal(o1.momentum_buffer, o2.momentum_buffer)
-    assert torch.equal(e1.t["loss_hist"][:12], e2.t["loss_hist"][:12])
-    for k in ("w2_bf16", "w2t_bf16", "wfc_bf16", "wfc_frag"):
-        assert torch.equal(e1.t[k], e2.t[k]), k
-    assert e2.eng.sync_error == 0
-
-
 @pytest.mark.parametrize("B,opt,momentum,role", [(32, True, 0.9, 1), (32, False, 0.9, 1), (20, True, 0.0, 1),
-                                                  (1, True, 0.9, 1), (40, True, 0.9, 1), (32, True, 0.9, 2),
-                                                  (32, True, 0.9, 0), (20, False, 0.9, 0),
-                                                  (32, True, 0.9, 3), (20, True, 0.0, 3), (40, True, 0.9, 3)])
+                                                  (1, True, 0.9, 1), (40, True, 0.9, 1),
+                                                  (32, True, 0.9, 0), (20, False, 0.9, 0)])
 def test_fuse_level3_bitwise_equals_level1(B, opt, momentum, role):
     """Level 3: the forward computes dZ2 itself (per-image in-launch wait, then dL and
     dZ2 from its fc weight fragments) and the fc weight gradient + SGD runs as a third role
@@ -204,19 +183,6 @@ def test_wgrad_channel_split_bitwise(B, fred, store_a1):
     assert e1.eng.last_fused_reduce == e2.eng.last_fused_reduce
 
 
-def test_fuse_level2_ragged_epoch_matches_level1():
-    """A whole epoch with a ragged last batch (eager steps at B < max_batch re-zero fewer
-    flags per forward block) - still bit-identical to level 1."""
-    m1, _, _, e1, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=1)
-    m2, _, _, e2, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=2)
-    for e in (e1, e2):
-        e.run_epoch(0)
-        e.run_epoch(1)
-        e.synchronize()
-    for (n, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
-        assert torch.equal(a, b), n
-
-
 @pytest.mark.parametrize("momentum,wd", [(0.0, 0.0), (0.9, 1e-4)])
 def test_fused_optimizer_bitwise_equals_sgd_kernel(momentum, wd):
     """Single-process steps apply SGD in the fc_bwd / grad_reduce epilogues; the result
@@ -265,7 +231,7 @@ def test_fuse_level1_one_step_matches_bf16_reference():
     assert abs(eng.t["loss_hist"][0].item() - loss.item()) < 1e-4
 
 
-@pytest.mark.parametrize("fuse_level", [0, 1, 2, 3])
+@pytest.mark.parametrize("fuse_level", [0, 1, 3])
 @pytest.mark.parametrize("B", [1, 12, 16, 24, 48, 64])
 def test_engine_batch_sweep_nan_poisoned(B, fuse_level):
     """SURVEY §4.1 batch sizes; every intermediate buffer starts as NaN so a kernel that
