@@ -238,6 +238,8 @@ def main():
                     help="resnet18: input channels per halo wgrad block (0 = planner default)")
     ap.add_argument("--no_fp32", action="store_true",
                     help="skip the exact-fp32 (reference precision) run after the bf16 headline")
+    ap.add_argument("--no_comm_calibration", action="store_true",
+                    help="N>1: skip the post-run sweep that refits the xGMI all-reduce cost model")
     ap.add_argument("--no_chain_check", action="store_true",
                     help="N>1: skip the start-up check that the production kernel chain gives the "
                          "conservative chain's bits across the ranks")
@@ -335,10 +337,10 @@ def main():
         eo.comm = args.comm
         for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role",
                   "fuse_reduce"):
-            if getattr(args, f) is not None and not (dtype == "fp32" and f in ("fuse_level", "store_a1")):
+            if getattr(args, f) is not None and not (dtype == "fp32" and f == "store_a1"):
                 setattr(eo, f, getattr(args, f))
         if dtype == "fp32":
-            eo.fuse_level, eo.store_a1 = 1, 0  # the exact-fp32 chain (engine.cpp launch_step_f32)
+            eo.store_a1 = 0  # the exact-fp32 chains recompute conv1 (engine.cpp launch_step_f32)
         eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
         eng.refresh()
         if ws > 1 and not args.no_chain_check:
@@ -365,6 +367,14 @@ def main():
     ms = dt * 1000.0 / args.steps
     img_s = ws * args.batch_size * args.steps / dt
     bucket_us = eng.measure_bucket_allreduce() if ws > 1 else None  # after the timed region
+    # refit the xGMI cost model on this node's real kernels: a few ms, untimed
+    calib = None
+    if ws > 1 and eng.comm_kind.startswith("xgmi") and not args.no_comm_calibration:
+        from ddp_amd.parallel.comm_calibration import calibrate, topology
+
+        calib = calibrate(rank, ws, dev)
+        if calib is not None:
+            calib["topology"] = topology(ws, rank=rank)
     from ddp_amd.parallel.bucket_model import describe
 
     plan = describe(eng.buckets, fs, eng.cost) if ws > 1 else None
@@ -387,7 +397,8 @@ def main():
         dt32, eng32, _, _, _, _ = timed_run("fp32")
         fp32 = {"images_per_sec": round(ws * args.batch_size * args.steps / dt32, 1),
                 "ms_per_step": round(dt32 * 1000.0 / args.steps, 5),
-                "kernels": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32), level-1 chain"}
+                "level3": bool(eng32.eng.last_level3),
+                "kernels_per_step": (2 if eng32.eng.last_fc_role else 3) if eng32.eng.last_level3 else None}
         del eng32
     if rank == 0:
         base = BASELINE_IMG_S.get(ws)
@@ -423,7 +434,10 @@ def main():
                                        "pred_last_allreduce_done_us": (round(eng.pred_comm_us, 2)
                                                                        if ws > 1 and eng.pred_comm_us else None)},
                        "chain_check": eng.chain_check, "downgrades": getattr(eng, "downgrades", []),
+                       "comm_calibration": calib,
                        "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
+                       "fp32_level3": fp32["level3"] if fp32 else None,
+                       "fp32_kernels_per_step": fp32["kernels_per_step"] if fp32 else None,
                        "fp32_ms_per_step": fp32["ms_per_step"] if fp32 else None},
         }), flush=True)
     if ws > 1:

@@ -963,7 +963,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              TORCH_CHECK(fc_bwd_lds(c.max_batch, c.NO, true, ((long)c.max_batch * HW + 64L * c.pxt_fwd - 1) / (64L * c.pxt_fwd) * 2 * c.NO) <= 160 * 1024,
                          "engine: batch too large for fc_bwd LDS");
              if (c.f32) {  // exact fp32: fp32 activations + the conv2 weight's fp32 [tap][ci][co] copy
-               TORCH_CHECK(c.fuse_level >= 1 && c.store_a1 == 0, "engine: fp32 needs fuse_level >= 1 (runs level 1), store_a1 0");
+               TORCH_CHECK(c.fuse_level >= 1 && c.store_a1 == 0, "engine: fp32 needs fuse_level 1 or 3 and store_a1 0");
                b.a2_f32 = need("a2", at::kFloat, B * HW * c.C2).data_ptr<float>();
                b.dz2_f32 = need("dz2", at::kFloat, B * HW * c.C2).data_ptr<float>();
                b.w2t_f32 = need("w2t_f32", at::kFloat, 9L * c.C1 * c.C2).data_ptr<float>();

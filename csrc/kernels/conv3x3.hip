@@ -130,7 +130,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1, FwdDz dzo) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
-  static_assert(!DZ || (!F32 && NOF == 10 && A1X), "level-3 dZ2 needs the bf16 fc epilogue and the conv1 recompute");
+  static_assert(!DZ || (NOF == 10 && A1X), "level-3 dZ2 needs the fc epilogue and the conv1 recompute");
   constexpr int CE = P::CE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DDP_STAMP(STAMP_K_CONV_FWD, 0);
@@ -300,7 +300,10 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
   float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X, (int)sizeof(T)));
-  uint2 a2pk[DZ ? PXT : 1][4];  // DZ: the stored bf16 a2 quads (dZ2's ReLU mask)
+  uint2 a2pk[DZ && !F32 ? PXT : 1][4];  // DZ: the stored bf16 a2 quads (dZ2's ReLU mask)
+  // DZ, exact fp32: the stored a2 quads and the fc weight quads of the epilogue, kept for dZ2
+  float4 a2q[DZ && F32 ? PXT : 1][4];
+  float4 wq[DZ && F32 ? PXT : 1][DZ && F32 ? 4 : 1][DZ && F32 ? NOF : 1];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -316,6 +319,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       float q[4] = {v0, v1, v2, v3};  // the values actually stored (what backward re-reads)
       if constexpr (F32) {
         if (valid[pt]) st_wt(reinterpret_cast<float4*>(Y + Pp[pt] * Cout + co), make_float4(v0, v1, v2, v3));
+        if constexpr (DZ) a2q[pt][t] = make_float4(v0, v1, v2, v3);
       } else {
         const uint2 pk = pack4(v0, v1, v2, v3);
         if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
@@ -329,6 +333,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
           if constexpr (F32) {  // fp32 FCFRAG weight: 4 consecutive channels, 1 KB per wave load
             const float4 w4 = *reinterpret_cast<const float4*>(
                 wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
+            if constexpr (DZ) wq[pt][t][o] = w4;
             s = fmaf(q[0], w4.x, s); s = fmaf(q[1], w4.y, s);
             s = fmaf(q[2], w4.z, s); s = fmaf(q[3], w4.w, s);
           } else {
@@ -460,16 +465,29 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 #pragma unroll
         for (int o = 0; o < NOF; ++o) {
           float w4[4];
-          unpack4(wv[pt][t][o], w4);
+          if constexpr (F32) {
+            const float4 wf = wq[pt][t][o];
+            w4[0] = wf.x; w4[1] = wf.y; w4[2] = wf.z; w4[3] = wf.w;
+          } else {
+            unpack4(wv[pt][t][o], w4);
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) dz[j] = fmaf(d[o], w4[j], dz[j]);
         }
         float q[4];
-        unpack4(a2pk[pt][t], q);
+        if constexpr (F32) {
+          q[0] = a2q[pt][t].x; q[1] = a2q[pt][t].y; q[2] = a2q[pt][t].z; q[3] = a2q[pt][t].w;
+        } else {
+          unpack4(a2pk[pt][t], q);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) dz[j] = q[j] > 0.f ? dz[j] : 0.f;
         const int co = co0 + 16 * t + 4 * (lane >> 4);
-        if (valid[pt]) st_wt(reinterpret_cast<uint2*>(dzo.dz2 + Pp[pt] * Cout + co), pack4(dz[0], dz[1], dz[2], dz[3]));
+        if constexpr (F32) {
+          if (valid[pt]) st_wt(reinterpret_cast<float4*>(dzo.dz2_f32 + Pp[pt] * Cout + co), make_float4(dz[0], dz[1], dz[2], dz[3]));
+        } else {
+          if (valid[pt]) st_wt(reinterpret_cast<uint2*>(dzo.dz2 + Pp[pt] * Cout + co), pack4(dz[0], dz[1], dz[2], dz[3]));
+        }
       }
     }
     DDP_STAMP(STAMP_K_CONV_FWD, 7);
@@ -480,31 +498,46 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 // ---------------------------------------------------------------- data gradient
 // A1X (with FUSE_W1, uint8 x0): the ReLU-input mask is recomputed from conv1 instead of
 // being read from a stored a1 tensor (mask = bf16(relu(conv1(x))) > 0, bit-exact).
+// WG (exact fp32, SimpleCNN geometry): the block computes ONE 16-channel half `by` of the
+// input channels (two blocks per pixel chunk) and reads its weight fragments straight from
+// the [tap][ci][co] fp32 copy in global memory (16-byte loads, one tap ahead of the MFMAs,
+// L1/L2-resident: 73 KB) instead of staging 73 KB of fp32 weights in LDS - the block then
+// needs ~60 KB of LDS, so two fit a CU (the fp32 conv backward ran at one block per CU,
+// its dgrad and wgrad blocks serialised by residency: profiles/r3_fp32).  Each output's
+// MFMA chain (tap-major, 32-wide K steps over the output channels) is unchanged, and the
+// conv1 weight-gradient partials of a channel are summed over the same pixels in the same
+// order, so dZ1 and the w1 slab row are bit-identical to the one-block-per-chunk kernel
+// (each half writes its own 16 channels of the row).
 template <typename T, int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI,
-          int GCO>
+          int GCO, bool WG = false>
 __device__ __forceinline__ void dgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ WT,
     const T* __restrict__ Xact, T* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
+  static_assert(!WG || (F32 && GCI == 32 && GCO == 64 && FUSE_W1), "weights-from-global dgrad: fp32 SimpleCNN conv2");
   constexpr int CE = P::CE;
+  constexpr int NCT = WG ? 1 : 2;  // 16-wide input-channel tiles per wave
   DDP_STAMP(STAMP_K_DGRAD, 0);
   DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
-  const int ci_blk = by * 32;
+  const int ci_blk = WG ? by * 16 : by * 32;
   const int KW = 9 * Cout, WS = KW + P::PAD, DS = Cout + P::PAD;  // row strides = 8 mod 16 dwords (conflict-free)
   const int XR = CH + 2 * W + 2;
-  T* sWT = reinterpret_cast<T*>(smem);                   // [32 ci][9*Cout]
-  T* sDY = sWT + 32 * WS;                                // [XR][Cout]
+  T* sWT = reinterpret_cast<T*>(smem);                   // [32 ci][9*Cout] (not WG)
+  T* sDY = sWT + (WG ? 0 : 32 * WS);                     // [XR][Cout]
   float* sx0 = reinterpret_cast<float*>(sDY + XR * DS);  // [XR] conv1 input (FUSE_W1)
   float* s_w1 = sx0 + XR;                                // [4][320] (FUSE_W1)
   unsigned char* s_m1 = reinterpret_cast<unsigned char*>(s_w1 + 4 * 320);  // [CH][4] a1>0 bits (A1X)
   const long P0 = (long)bx * CH;
   const long Pbase = P0 - W - 1;
+  // conv1 channel group of this wave's mask work: WG - the half's two groups, waves
+  // (w, w + 2) splitting the pixels; otherwise group = wave
+  const int mg = WG ? 2 * by + (wave & 1) : wave;
 
   // conv1 input values for the fused w1 gradient: loads issued before the staging
   // round so the dependent index -> image chain overlaps it
@@ -520,9 +553,9 @@ __device__ __forceinline__ void dgrad_body(
   };
   const float x0_pre = (FUSE_W1 && (int)threadIdx.x < XR) ? x0_at(threadIdx.x) : 0.f;
   Conv1Group cg;
-  if (A1X) cg = conv1_group_load(c1.w, c1.b, wave);  // lands during the staging round
+  if (A1X) cg = conv1_group_load(c1.w, c1.b, mg);  // lands during the staging round
   const int wc = KW / CE, cpc = Cout / CE;
-  stage2<F32 ? 32 : 16>(32 * wc,
+  stage2<F32 ? 32 : 16>(WG ? 0 : 32 * wc,
           [&](int i) {
             const int r = i / wc, rest = (i - r * wc) * CE;  // rest = tap*Cout + co
             const int tap = rest / Cout, co = rest - tap * Cout;
@@ -551,8 +584,8 @@ __device__ __forceinline__ void dgrad_body(
     // ReLU-input mask of the block's own pixels: bit j of s_m1[lp*4 + g] = (a1[lp][8g+j] > 0),
     // a1 recomputed from conv1 exactly as stored (bf16-rounded), channel group wave-uniform
     __syncthreads();
-    const int g = wave;
-    for (int lp = lane; lp < CH; lp += 64) {
+    const int g = mg;
+    for (int lp = lane + (WG ? 64 * (wave >> 1) : 0); lp < CH; lp += WG ? 128 : 64) {
       const long P = P0 + lp;
       unsigned m = 0;
       if (P < Ptot) {
@@ -594,7 +627,7 @@ __device__ __forceinline__ void dgrad_body(
     rowc[pt] = lp + W + 1;
     if (MASK_X && !A1X) {  // prefetch the ReLU-input mask (lands during the MFMAs)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < NCT; ++t) {
         const T* xp = Xact + Pc * Cin + ci_blk + 16 * t + 4 * (lane >> 4);
         if constexpr (F32) {
           const float4 x4 = *reinterpret_cast<const float4*>(xp);
@@ -608,37 +641,60 @@ __device__ __forceinline__ void dgrad_body(
   lds_barrier();  // (the mask prefetch above stays in flight through the MFMA loop)
   DDP_STAMP(STAMP_K_DGRAD, 1);
 
-  f32x4 acc[PXT][2];
+  f32x4 acc[PXT][NCT];
 #pragma unroll
-  for (int pt = 0; pt < PXT; ++pt) acc[pt][0] = acc[pt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const T* wrow = sWT + col * WS + kofs;
+  for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
+    for (int t = 0; t < NCT; ++t) acc[pt][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // one 32-wide K step (output channels co0 .. co0 + 31) of tap `tap` against A fragments a[]
+  auto kstep = [&](int tap, int co0, const typename P::Frag* a) {
     const int dh = 1 - tap / 3, dw = 1 - tap % 3;  // dY pixel = (h + 1 - kh, w + 1 - kw)
-    for (int co0 = 0; co0 < Cout; co0 += 32) {
-      const typename P::Frag a0 = P::frag(wrow + tap * Cout + co0);
-      const typename P::Frag a1 = P::frag(wrow + 16 * WS + tap * Cout + co0);
-      typename P::Frag b[PXT];
+    typename P::Frag b[PXT];
 #pragma unroll
-      for (int pt = 0; pt < PXT; ++pt) {
-        const int hh = h[pt] + dh, ww = w[pt] + dw;
-        const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
-        const typename P::Frag v = P::frag(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs);
-        b[pt] = fsel(ok, v, P::zero());  // unconditional read + select (see the forward)
+    for (int pt = 0; pt < PXT; ++pt) {
+      const int hh = h[pt] + dh, ww = w[pt] + dw;
+      const bool ok = valid[pt] && (unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W;
+      const typename P::Frag v = P::frag(sDY + (rowc[pt] + dh * W + dw) * DS + co0 + kofs);
+      b[pt] = fsel(ok, v, P::zero());  // unconditional read + select (see the forward)
+    }
+#pragma unroll
+    for (int pt = 0; pt < PXT; ++pt)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) acc[pt][t] = P::mma(a[t], b[pt], acc[pt][t]);
+  };
+  if constexpr (WG) {
+    // A fragments from the global [tap][ci][co] copy: lane (row ci_blk + col, K offset kofs)
+    // reads 2 x 16 bytes per 32-wide K step; the next tap's are requested before this one's
+    // MFMAs (Cout == 64: two K steps per tap)
+    const T* wg = WT + (long)(ci_blk + col) * Cout + kofs;
+    const long tstr = (long)Cin * Cout;
+    typename P::Frag an[2] = {P::frag(wg), P::frag(wg + 32)};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const typename P::Frag a0 = an[0], a1 = an[1];
+      if (tap + 1 < 9) {
+        an[0] = P::frag(wg + (tap + 1) * tstr);
+        an[1] = P::frag(wg + (tap + 1) * tstr + 32);
       }
+      kstep(tap, 0, &a0);
+      kstep(tap, 32, &a1);
+    }
+  } else {
+    const T* wrow = sWT + col * WS + kofs;
 #pragma unroll
-      for (int pt = 0; pt < PXT; ++pt) {
-        acc[pt][0] = P::mma(a0, b[pt], acc[pt][0]);
-        acc[pt][1] = P::mma(a1, b[pt], acc[pt][1]);
+    for (int tap = 0; tap < 9; ++tap) {
+      for (int co0 = 0; co0 < Cout; co0 += 32) {
+        const typename P::Frag a[2] = {P::frag(wrow + tap * Cout + co0), P::frag(wrow + 16 * WS + tap * Cout + co0)};
+        kstep(tap, co0, a);
       }
     }
   }
 
   DDP_STAMP(STAMP_K_DGRAD, 2);
-  float w1a[FUSE_W1 ? 2 : 1][4][10];
+  float w1a[FUSE_W1 ? NCT : 1][4][10];
   if (FUSE_W1) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NCT; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -657,7 +713,7 @@ __device__ __forceinline__ void dgrad_body(
       }
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < NCT; ++t) {
       const int ci = ci_blk + 16 * t + 4 * (lane >> 4);
       float v[4] = {acc[pt][t][0], acc[pt][t][1], acc[pt][t][2], acc[pt][t][3]};
       if (MASK_X && A1X) {
@@ -692,25 +748,28 @@ __device__ __forceinline__ void dgrad_body(
   if (FUSE_W1) {
     // reduce over the 16 pixel lanes that share a channel group, then over waves (fixed order)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NCT; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int k = 0; k < 10; ++k) w1a[t][j][k] = sum16(w1a[t][j][k]);
     if (col == 0) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NCT; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int ci = 16 * t + 4 * (lane >> 4) + j;  // conv1 output channel (Cin == 32)
+          const int ci = ci_blk + 16 * t + 4 * (lane >> 4) + j;  // conv1 output channel (Cin == 32)
 #pragma unroll
           for (int k = 0; k < 9; ++k) s_w1[wave * 320 + ci * 9 + k] = w1a[t][j][k];
           s_w1[wave * 320 + 288 + ci] = w1a[t][j][9];
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 320; i += 256)
+    for (int i = threadIdx.x; i < 320; i += 256) {
+      // WG: only this half's 16 channels (the other half-block writes the rest of the row)
+      if (WG && ((i < 288 ? i / 9 : i - 288) >> 4) != by) continue;
       st_wt(w1slab + (long)bx * 320 + i, ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i]);
+    }
   }
   DDP_STAMP(STAMP_K_DGRAD, 4);
 }
@@ -752,14 +811,19 @@ __global__ __launch_bounds__(256) void conv3x3_dgrad_kernel(
 // half 0 writes the ci < 16 columns and the bias, half 1 the rest.  The two halves of a
 // row chunk are 8 blocks apart (same XCD: blocks go round-robin over the 8 XCDs), so the
 // second one's dY tile reads hit the same L2.
+// CS == 2 also for exact fp32 (slab rows stored directly): the half's 16 X channels are
+// staged compactly (row stride 16 floats - the lanes of a ds_read_b32 then read 64
+// consecutive dwords), so the block needs ~56 KB of LDS instead of ~82 KB and two blocks
+// fit a CU next to the dgrad role (dgrad_body WG).
 template <typename T, bool MASK_DY, bool A1X, int GH, int GW, int GCI, int GCO, bool STAGE = false, int CS = 1>
 __device__ __forceinline__ void wgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ X,
     float* __restrict__ slab, int B, int H, int W, int Cin, int Cout, int R, C1Src c1, char* smem, int bx, int by) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int CE = Prec<T>::CE;
-  static_assert(CS == 1 || (CS == 2 && STAGE && !F32 && GCI == 32 && GCO == 64),
-                "the channel-split wgrad role is the bf16 staged-slab SimpleCNN variant");
+  static_assert(CS == 1 || (CS == 2 && (STAGE || F32) && !(STAGE && F32) && GCI == 32 && GCO == 64),
+                "the channel-split wgrad role: bf16 with a staged slab row, or fp32 with direct stores");
+  constexpr bool XC = F32 && CS == 2;  // compact X tile: only the half's 16 channels
   DDP_STAMP(STAMP_K_WGRAD, 0);
   DDP_GEOM_OVERRIDE();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -777,7 +841,7 @@ __device__ __forceinline__ void wgrad_body(
   const int n = rb / nRC;
   const int r0 = (rb - n * nRC) * R;
   const int Wp = (W + 7) & ~7;
-  const int DS = Cout + 16, XS = Cin + 16;  // LDS row strides (elements)
+  const int DS = Cout + 16, XS = XC ? 16 : Cin + 16;  // LDS row strides (elements)
   const int nslot = ((R * Wp + 31) / 32) * 32;
   T* sdY = reinterpret_cast<T*>(smem);
   T* sX = sdY + (long)nslot * DS;
@@ -827,7 +891,7 @@ __device__ __forceinline__ void wgrad_body(
           const int rr = pos / XW, cc = pos - (pos / XW) * XW;
           return sxx[(rr + k / 3) * XW2 + cc + k % 3];
         },
-        [&](int pos, int g) { return sX + (long)pos * XS + 8 * g; });
+        [&](int pos, int g) { return sX + (long)pos * XS + 8 * (XC ? g - 2 * half : g); });
   };
   const int ndy = nslot * cpy_dy;
   stage2<F32 ? 32 : 16>(ndy, dy_src, dy_dst,
@@ -841,7 +905,7 @@ __device__ __forceinline__ void wgrad_body(
           },
           [&](int i, bf16x8 v) {
             const int pos = i / cpy_x, ch = cx0 + (i - pos * cpy_x) * CE;
-            st16(sX + (long)pos * XS + ch, v);
+            st16(sX + (long)pos * XS + (XC ? ch - cx0 : ch), v);
           });
   if (A1X) {
     for (int i = threadIdx.x; i < NXX; i += 256) {
@@ -872,24 +936,29 @@ __device__ __forceinline__ void wgrad_body(
     for (int k = 0; k < 9; ++k) acc[c][k] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   if constexpr (F32) {
+    const int ciL = XC ? 0 : ciT;  // the tile's column in the staged X rows
+    const bool bias = CS == 1 || ciT == 0;  // CS == 2: only half 0 computes the bias (block-uniform)
 #pragma unroll 1
     for (int s0 = 0; s0 < nslot; s0 += 32) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int sl = s0 + 4 * j + g;  // this lane's K slot of MFMA j
-        const float a0 = sdY[(long)sl * DS + coT + i16];
-        const float a1 = sdY[(long)sl * DS + coT + 16 + i16];
+        float a[NCT];
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) a[c] = sdY[(long)sl * DS + coT + 16 * c + i16];
         // padding slots (r >= R) carry dY == 0; clamp their row into initialised LDS
         const int rs0 = sl / Wp, cs = sl - rs0 * Wp, rs = min(rs0, R - 1);
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const int kh = tap / 3, kw = tap % 3;
-          const float bx_ = sX[(long)((rs + kh) * XW + cs + kw) * XS + ciT + i16];
-          acc[0][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bx_, acc[0][tap], 0, 0, 0);
-          acc[1][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bx_, acc[1][tap], 0, 0, 0);
+          const float bx_ = sX[(long)((rs + kh) * XW + cs + kw) * XS + ciL + i16];
+#pragma unroll
+          for (int c = 0; c < NCT; ++c) acc[c][tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], bx_, acc[c][tap], 0, 0, 0);
         }
-        accb[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, 1.f, accb[0], 0, 0, 0);
-        accb[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, 1.f, accb[1], 0, 0, 0);
+        if (bias) {
+#pragma unroll
+          for (int c = 0; c < NCT; ++c) accb[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], 1.f, accb[c], 0, 0, 0);
+        }
       }
     }
   } else {
@@ -1032,7 +1101,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(
 // dispatch-order argument above is unchanged (every block a reducer waits for has a lower
 // index than the reducer); the fc role's own last block (FcBwdExtras::last_ctr) finishes the
 // fc bias, the loss and the step counter (launchers.h BwdFc).
-constexpr int BFC_MAXB = 48;  // batch capacity of the fc role (level 3 needs B <= 41 anyway)
+constexpr int BFC_MAXB = 64;  // batch capacity of the fc role (the README's B = 64 example runs level 3)
 
 // dL of the batch into LDS ([B][FCDW_LD] padded rows); the fc role's block 0 (first0) also
 // finishes the fc bias, the loss and the step counter (nothing else in the launch reads them)
@@ -1049,15 +1118,17 @@ __device__ __forceinline__ float* fc_role_prologue(const BwdFc& fcr, int B, char
   return s_dl;
 }
 // one 128-column chunk of the fc weight gradient + SGD on this wave
+template <typename T>
 __device__ __forceinline__ void fc_role_chunk(const BwdFc& fcr, const float* s_dl, int B, long q) {
+  const T* a2 = static_cast<const T*>(fcr.a2);
   // (B <= 32, the reference batch: 32 row loads per lane instead of 48 clamped ones)
-  if (B <= 32) fc_dw_wave_chunk<32>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
-  else fc_dw_wave_chunk<BFC_MAXB>(s_dl, fcr.a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
+  if (B <= 32) fc_dw_wave_chunk<32>(s_dl, a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
+  else fc_dw_wave_chunk<BFC_MAXB>(s_dl, a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
 }
 
 template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
           bool FCR = false>
-__global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kernel(
+__global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv3x3_bwd_kernel(
     const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
     int R, int nd, C1Src c1, const T* __restrict__ Xact, BwdReduce red, BwdFc fcr) {
@@ -1080,18 +1151,33 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 2 : 1) void conv3x3_bwd_kerne
       // every row offset / guard of the unrolled body out of it: 300 spilled registers)
       const int nch = (int)((fcr.K + 127) / 128);
       const int q = f * 4 + (threadIdx.x >> 6);
-      if (q < nch) fc_role_chunk(fcr, s_dl, B, q);
+      if (q < nch) fc_role_chunk<T>(fcr, s_dl, B, q);
       DDP_STAMP(STAMP_K_FC_BWD, 4);
       return;
     }
     if (f >= 0) cb -= fcr.nfc;
   }
-  if (cb < nd)
-    dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO>(
-        dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, cb, 0);
-  else
-    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, true, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
-                                                                  W, Cin, Cout, R, c1, smem, cb - nd, 0);
+  // exact fp32 with the channel split: the dgrad role is split over input-channel halves too
+  // (weights from global: dgrad_body WG), two blocks per pixel chunk, paired 8 apart (same
+  // XCD, as the wgrad halves) - nd counts both halves
+  constexpr bool WG = sizeof(T) == 4 && CS == 2;
+  if (cb < nd) {
+    int px = cb, hf = 0;
+    if constexpr (WG) {
+      if (((nd >> 1) & 7) == 0) {
+        hf = (cb >> 3) & 1;
+        px = ((cb >> 4) << 3) | (cb & 7);
+      } else {
+        hf = cb & 1;
+        px = cb >> 1;
+      }
+    }
+    dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO, WG>(
+        dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, px, hf);
+  } else {
+    wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, !WG, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
+                                                         W, Cin, Cout, R, c1, smem, cb - nd, 0);
+  }
   if constexpr (FRED) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
     __syncthreads();
@@ -1161,28 +1247,41 @@ static void lds_optin(K kernel, size_t bytes) {
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-// the level-3 forward of SimpleCNN's conv2 (bf16, fc epilogue, conv1 recompute, pxt 1 / 2)
-template <int PX>
+// the level-3 forward of SimpleCNN's conv2 (fc epilogue, conv1 recompute, pxt 1 / 2)
+template <typename T, int PX>
 static auto fwd_dz_kernel() {
-  return conv3x3_fwd_kernel<bf16_t, 1, 4 * PX, true, 10, true, 28, 28, 32, 64, true>;
+  return conv3x3_fwd_kernel<T, 1, 4 * PX, true, 10, true, 28, 28, 32, 64, true>;
 }
 
-bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt) {
+template <typename T>
+static bool fwd_dz_fits(int B, int H, int W, int pxt) {
   if (H != 28 || W != 28 || (pxt != 1 && pxt != 2) || B <= 0) return false;
   const long P = (long)B * H * W;
   const int per_blk = 64 * pxt;
   if (per_blk > H * W || P >= (1L << 31)) return false;
   const long grid = (P + per_blk - 1) / per_blk;
-  const size_t lds = conv3x3_fwd_lds(W, 32, pxt, true, 2);
-  const void* k = pxt == 2 ? reinterpret_cast<const void*>(fwd_dz_kernel<2>())
-                           : reinterpret_cast<const void*>(fwd_dz_kernel<1>());
-  lds_optin(pxt == 2 ? fwd_dz_kernel<2>() : fwd_dz_kernel<1>(), lds);
+  const size_t lds = conv3x3_fwd_lds(W, 32, pxt, true, (int)sizeof(T));
+  const void* k = pxt == 2 ? reinterpret_cast<const void*>(fwd_dz_kernel<T, 2>())
+                           : reinterpret_cast<const void*>(fwd_dz_kernel<T, 1>());
+  lds_optin(pxt == 2 ? fwd_dz_kernel<T, 2>() : fwd_dz_kernel<T, 1>(), lds);
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256 * pxt, lds) != hipSuccess) return false;
-  // every block of the grid spins on its image's other blocks: all of them must be resident
-  return grid <= (long)occ * cus;
+  // Every block spins on the other blocks of its image (a window of <= 8 consecutive block
+  // indices: a block covers 64 * pxt <= H*W pixels).  The grid need NOT be resident at once
+  // (B = 64: 392 blocks on 256 slots): workgroups are dispatched in index order round-robin
+  // over the XCDs, so on the XCD with the lowest dispatch frontier F the oldest resident block
+  // b satisfies b + 8 < F whenever that XCD holds >= 3 resident blocks (they sit 8 indices
+  // apart) - every block of b's image is dispatched (lower frontiers nowhere), b's image
+  // completes and frees a slot; an XCD with a free slot dispatches its next block.  So the
+  // forward cannot deadlock while every XCD holds >= 3 of these blocks; 8 per XCD is asked
+  // (the launch runs alone on its stream - a step's kernels are stream-ordered).
+  (void)grid;
+  return (long)occ * cus >= 64;
+}
+bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt, int es) {
+  return es == 4 ? fwd_dz_fits<float>(B, H, W, pxt) : fwd_dz_fits<bf16_t>(B, H, W, pxt);
 }
 
 template <typename T>
@@ -1199,15 +1298,13 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   const FwdDz dzo = dz ? *dz : FwdDz();
   if (dz) {
-    if (sizeof(T) != 2 || !g || !fc || !a1x || !(pxt == 1 || pxt == 2) || !dz->dz2 || !dz->img_cnt || !dz->fc_bias)
-      throw std::runtime_error("conv3x3_fwd: the level-3 dZ2 epilogue is the bf16 SimpleCNN forward with the fc "
+    if (!g || !fc || !a1x || !(pxt == 1 || pxt == 2) || !(sizeof(T) == 2 ? (void*)dz->dz2 : (void*)dz->dz2_f32) ||
+        !dz->img_cnt || !dz->fc_bias)
+      throw std::runtime_error("conv3x3_fwd: the level-3 dZ2 epilogue is the SimpleCNN forward with the fc "
                                "epilogue and the conv1 recompute");
-    if constexpr (sizeof(T) == 2) {
-      auto k = pxt == 2 ? fwd_dz_kernel<2>() : fwd_dz_kernel<1>();
-      lds_optin(k, lds);
-      hipLaunchKernelGGL(k, grid, dim3(256 * pxt), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs,
-                         dzo);
-    }
+    auto k = pxt == 2 ? fwd_dz_kernel<T, 2>() : fwd_dz_kernel<T, 1>();
+    lds_optin(k, lds);
+    hipLaunchKernelGGL(k, grid, dim3(256 * pxt), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo);
     return;
   }
   // one 16-pixel tile per wave: pxt 2 -> 8 waves (2 per SIMD), pxt 1 -> 4 waves
@@ -1243,9 +1340,9 @@ void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y
 }
 void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s, const C1Src* c1) {
-  (void)NO;
-  fwd_launch<float>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1, nullptr);
+                 int pxt, hipStream_t s, const C1Src* c1, const FwdDz* dz) {
+  if (dz && NO != 10) throw std::runtime_error("conv3x3_fwd: the level-3 dZ2 epilogue is built for 10 classes");
+  fwd_launch<float>(X, Wt, bias, Y, B, H, W, Cin, Cout, relu, wfc, fc_part, pxt, s, c1, dz);
 }
 
 template <typename T>
@@ -1350,7 +1447,21 @@ void conv3x3_wgrad(const float* dY, const float* Yact, const float* X, float* sl
   wgrad_launch<float>(dY, Yact, X, slab, B, H, W, Cin, Cout, R, s, c1);
 }
 
-size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es) {
+size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es, int cs) {
+  if (es == 4 && cs == 2) {
+    // exact fp32, both roles channel-split: dgrad (weights from global) = the dY tile + the
+    // conv1 weight-gradient scratch; wgrad = dY slots + the half's compact X tile (+ the
+    // conv1 recompute input); slab rows stored directly (no staging)
+    const size_t XR = 64 * pxt + 2 * W + 2;
+    const size_t a = 4 * (XR * (Cout + 8)) + sizeof(float) * (XR + 4 * 320) + 4 * 64 * pxt;
+    const int Wp = (W + 7) & ~7;
+    const size_t nslot = ((R * Wp + 31) / 32) * 32;
+    const size_t b = 4 * (nslot * (Cout + 16) + (size_t)(R + 2) * (Wp + 2) * 16) +
+                     sizeof(float) * ((size_t)(R + 4) * (Wp + 4) + Cin * 10);
+    const size_t red = sizeof(float) * 3 * 16 * 64;  // the fused reducer's partials
+    const size_t m = a > b ? a : b;
+    return ((m > red ? m : red) + 15) & ~(size_t)15;
+  }
   const size_t a = conv3x3_dgrad_lds(W, Cout, pxt, true, es), b = conv3x3_wgrad_lds(W, Cin, Cout, R, true, es);
   // the wgrad role's staged slab row (+ its bank skew, 4 floats per output channel)
   const size_t row = sizeof(float) * ((size_t)Cout * 9 * Cin + Cout + 4 * (size_t)Cout);
@@ -1404,6 +1515,17 @@ static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr) {
       return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2>
                   : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2>;
     }
+  } else {
+    // exact fp32, two blocks per CU (both roles channel-split): pxt 2, conv1 recomputed
+    if constexpr (PX == 2 && DA && WA) {
+      if (cs == 2) {
+        if (fcr)
+          return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true>
+                      : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, true>;
+        return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2>
+                    : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2>;
+      }
+    }
   }
   return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true>
               : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false>;
@@ -1428,21 +1550,25 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
                        bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err,
                        int csplit, const BwdFc* fc, bool exclusive) {
   const bool g = simplecnn_geom(H, W, Cin, Cout);
-  // the channel split is the bf16 SimpleCNN variant (wgrad_body); otherwise one block per row
-  const int cs = (csplit == 2 && g && sizeof(T) == 2) ? 2 : 1;
+  // the channel split (SimpleCNN geometry): bf16 - two wgrad blocks per slab row; exact fp32
+  // (pxt 2, conv1 recomputed) - two wgrad blocks per row AND two dgrad blocks per pixel
+  // chunk, at two blocks per CU; otherwise one block each
+  constexpr bool F32 = sizeof(T) == 4;
+  const int cs = (csplit == 2 && g && (!F32 || (pxt == 2 && !Xact))) ? 2 : 1;
+  const int dcs = F32 && cs == 2 ? 2 : 1;
   const int nrows = conv3x3_wgrad_blocks(B, H, R);
-  const int nd = conv3x3_dgrad_blocks(B, H, W, pxt), nw = nrows * cs;
-  size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T));
+  const int nd = conv3x3_dgrad_blocks(B, H, W, pxt) * dcs, nw = nrows * cs;
+  size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T), cs);
   if (((long)Cout * 9 * Cin + Cout) % 4 != 0 || (reinterpret_cast<uintptr_t>(slab) & 15) != 0)
     throw std::runtime_error("conv3x3_bwd: slab rows must be 16-byte multiples on a 16-byte aligned buffer");
   BwdFc fcr;
   int nfc = 0;
   const bool da = !Xact, wa = !Xact || !wgrad_load_a1;
   if (fc) {
-    if (sizeof(T) != 2 || !conv3x3_bwd_fc_role_ok(H, W, Cin, Cout, pxt, cs) || !fc->dl || !fc->a2 ||
-        fc->K % 2 != 0 || B > BFC_MAXB || fc->ex.last_ctr)
-      throw std::runtime_error("conv3x3_bwd: the fc role is the bf16 SimpleCNN variant (pxt 2, channel split, dL "
-                               "given, B <= 48, no last-block count)");
+    if (!conv3x3_bwd_fc_role_ok(H, W, Cin, Cout, pxt, cs) || !fc->dl || !fc->a2 || fc->K % 2 != 0 || B > BFC_MAXB ||
+        fc->ex.last_ctr)
+      throw std::runtime_error("conv3x3_bwd: the fc role is the SimpleCNN variant (pxt 2, channel split, dL "
+                               "given, B <= 64, no last-block count)");
     fcr = *fc;
     fcr.nconv = nd + nw;
     // one 128-column chunk per wave (4 per block), blocks after every conv block: the first
@@ -1499,9 +1625,9 @@ bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, 
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
-                 int wgrad_split, bool exclusive) {
+                 int wgrad_split, const BwdFc* fc, bool exclusive) {
   return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                    fused_reduce, red_done, red_err, wgrad_split, nullptr, exclusive);
+                    fused_reduce, red_done, red_err, wgrad_split, fc, exclusive);
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv3x3)

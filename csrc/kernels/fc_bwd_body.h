@@ -133,11 +133,15 @@ __device__ __forceinline__ void fc_bwd_bias_loss(const FcBwdExtras& ex, const fl
 // then all B rows) is issued up front; a scheduling barrier per virtual wave keeps only
 // that wave's dL values live.  The level-3 conv backward's fc role runs it on the launch's
 // otherwise idle resident slots (conv3x3.hip FCR).
+// X is the bf16 activation (4-byte loads: the lane's column pair) or, for the exact-fp32
+// step, the fp32 one (8-byte loads); the fp32 step's fc operand copy is the fp32 FCFRAG
+// shadow (ex.sh_frag32).
 constexpr int FCDW_LD = 12;
-template <int MAXB>
-__device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const bf16_t* __restrict__ X,
+template <int MAXB, typename T>
+__device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const T* __restrict__ X,
                                                  float* __restrict__ dW, float scale, int B, long K,
                                                  const FcBwdExtras& ex, long col0) {
+  constexpr bool F32 = sizeof(T) == 4;
   constexpr int NO = 10, VW = 8, RPV = (MAXB + VW - 1) / VW;
   const int lane = threadIdx.x & 63;
   const long col = col0 + 2 * lane;
@@ -160,12 +164,17 @@ __device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const bf16_t
                      : make_float2(0.f, 0.f);
     }
   }
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X), (short)0, 0x7fffffff,
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(X), (short)0, 0x7fffffff,
                                                                       0x00020000);
-  unsigned xw[MAXB];
+  unsigned xw[F32 ? 1 : MAXB];
+  float2 xf[F32 ? MAXB : 1];
 #pragma unroll
-  for (int b = 0; b < MAXB; ++b)
-    xw[b] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rx, vo2, (int)((long)min(b, B - 1) * K * 2), 0);
+  for (int b = 0; b < MAXB; ++b) {
+    if constexpr (F32)
+      xf[b] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, vo4, (int)((long)min(b, B - 1) * K * 4), 0));
+    else
+      xw[b] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rx, vo2, (int)((long)min(b, B - 1) * K * 2), 0);
+  }
   float acc[NO][2];
 #pragma unroll
   for (int v = 0; v < VW; ++v) {
@@ -177,8 +186,8 @@ __device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const bf16_t
     for (int u = 0; u < RPV; ++u) {
       const int b = v + VW * u;
       if (b < MAXB && b < B) {  // wave-uniform
-        const float x0 = __builtin_bit_cast(float, xw[b] << 16);
-        const float x1 = __builtin_bit_cast(float, xw[b] & 0xffff0000u);
+        const float x0 = F32 ? xf[F32 ? b : 0].x : __builtin_bit_cast(float, xw[F32 ? 0 : b] << 16);
+        const float x1 = F32 ? xf[F32 ? b : 0].y : __builtin_bit_cast(float, xw[F32 ? 0 : b] & 0xffff0000u);
         const float4 d0 = *reinterpret_cast<const float4*>(s_dl + b * FCDW_LD);
         const float4 d1 = *reinterpret_cast<const float4*>(s_dl + b * FCDW_LD + 4);
         const float2 d2 = *reinterpret_cast<const float2*>(s_dl + b * FCDW_LD + 8);
@@ -198,7 +207,7 @@ __device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const bf16_t
   }
   __builtin_amdgcn_sched_barrier(0);
   if (!active) return;
-  const long frag0 = ex.sh_frag ? fcfrag_index((int)col, ex.frag_HW, ex.frag_C) : 0;
+  const long frag0 = (ex.sh_frag || ex.sh_frag32) ? fcfrag_index((int)col, ex.frag_HW, ex.frag_C) : 0;
 #pragma unroll
   for (int o = 0; o < NO; ++o) {
     const float g0 = acc[o][0] * scale, g1 = acc[o][1] * scale;
@@ -221,6 +230,7 @@ __device__ __forceinline__ void fc_dw_wave_chunk(const float* s_dl, const bf16_t
       // FCFRAG keeps channel pairs (c, c + 1), c even, adjacent: one 4-byte store; the class
       // is its outermost dimension, so class o's index is class 0's + o * K
       if (ex.sh_frag) st_wt(reinterpret_cast<unsigned*>(ex.sh_frag + frag0 + (long)o * K), pb);
+      if (ex.sh_frag32) st_wt(reinterpret_cast<float2*>(ex.sh_frag32 + frag0 + (long)o * K), make_float2(p0, p1));
     }
   }
 }

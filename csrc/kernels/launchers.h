@@ -34,6 +34,7 @@ void conv1_wgrad(const void* x, bool x_is_u8, BatchIdx bi, const float* dy, cons
 constexpr int FWD_DZ_CNT_STRIDE = 64;  // ints between two images' counters (256 B: no shared line)
 struct FwdDz {
   bf16_t* dz2 = nullptr;          // [B*H*W][Cout] out (write-through)
+  float* dz2_f32 = nullptr;       // the same, exact-fp32 step
   int* img_cnt = nullptr;         // [B][FWD_DZ_CNT_STRIDE] arrival counters (first int of each
                                   // row), zero on entry (re-zeroed by the step's fc backward:
                                   // FcBwdExtras::zero_i32)
@@ -46,7 +47,7 @@ struct FwdDz {
   float* loss_rows = nullptr;
 };
 // whether a level-3 forward of this shape keeps every block resident at once
-bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt);
+bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt, int es = 2);
 // bf16 operands (v_mfma_f32_16x16x32_bf16) or exact fp32 operands (v_mfma_f32_16x16x4_f32,
 // the float overloads); `es` = element size of the LDS-size helpers (2 or 4).
 void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y, int B, int H,
@@ -55,7 +56,7 @@ void conv3x3_fwd(const bf16_t* X, const bf16_t* Wt, const float* bias, bf16_t* Y
 // fp32: wfc (fused fc epilogue) is the fc weight in the FCFRAG order, fp32 (SHADOW_F32_FCFRAG)
 void conv3x3_fwd(const float* X, const float* Wt, const float* bias, float* Y, int B, int H,
                  int W, int Cin, int Cout, bool relu, const float* wfc, float* fc_part, int NO,
-                 int pxt, hipStream_t s, const C1Src* c1 = nullptr);
+                 int pxt, hipStream_t s, const C1Src* c1 = nullptr, const FwdDz* dz = nullptr);
 void conv3x3_dgrad(const bf16_t* dY, const bf16_t* Yact, const bf16_t* WT, const bf16_t* Xact,
                    bf16_t* dX, int B, int H, int W, int Cin, int Cout, const void* x0, bool x0_u8,
                    BatchIdx bi, float* w1slab, int pxt, hipStream_t s, const C1Src* c1 = nullptr);
@@ -86,11 +87,14 @@ bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, 
                  int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr,
                  bool exclusive = false);
 bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split);
+// exact fp32: wgrad_split 2 (pxt 2, conv1 recomputed) splits both roles over input-channel
+// halves at two blocks per CU (dgrad weights read from global); bit-identical to split 1
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
-                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, bool exclusive = false);
-size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2);
+                 int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr,
+                 bool exclusive = false);
+size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2, int cs = 1);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false, int es = 2);
 size_t conv3x3_fwd_lds(int W, int Cin, int pxt, bool a1x = false, int es = 2);
@@ -271,7 +275,7 @@ struct FcBwdExtras {
 // Block 0 of the role finishes the fc bias (gradient + SGD), the loss and the step counter -
 // nothing else in the launch reads them (ex.last_ctr must be null).
 struct BwdFc {
-  const bf16_t* a2 = nullptr;  // ReLU2 output [B][K]
+  const void* a2 = nullptr;    // ReLU2 output [B][K] (bf16, or fp32 for the exact-fp32 step)
   const float* dl = nullptr;   // dL [B][10]
   float* dW = nullptr;         // null: fused optimizer only
   float scale = 1.f;

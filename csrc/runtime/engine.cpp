@@ -26,7 +26,8 @@
 //   level 1: conv1 recomputed inside conv2 fwd / dgrad / wgrad, cross-entropy in the
 //            fc_bwd prologue, optimizer in the epilogues, the slab reduction inside the
 //            conv backward: 3 kernels (forward -> fc_bwd -> conv backward);
-//   f32 = 1 (--dtype fp32): the level-1 chain with exact fp32 operands (launch_step_f32).
+//   f32 = 1 (--dtype fp32): the same chains with exact fp32 operands (launch_step_f32): level 3
+//            with both conv backward roles channel-split at two blocks per CU, or level 1.
 //
 // Buckets follow the reference DDP's rebuilt layout by default:
 // bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB); any
@@ -46,7 +47,7 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   if ((cfg_.H * cfg_.W) % 16 != 0) throw std::runtime_error("engine: H*W must be a multiple of 16");
   if (cfg_.NO != 10) throw std::runtime_error("engine: the fused fc epilogue is built for 10 classes");
   if (cfg_.f32 && (cfg_.fuse_level < 1 || cfg_.store_a1 != 0))
-    throw std::runtime_error("engine: fp32 mode needs fuse_level >= 1 (runs the level-1 chain) and store_a1 0");
+    throw std::runtime_error("engine: fp32 mode needs fuse_level >= 1 (level 1 or 3) and store_a1 0");
   if (cfg_.f32 && !(b_.a2_f32 && b_.dz2_f32 && b_.w2t_f32 && b_.wfc_frag32))
     throw std::runtime_error("engine: fp32 mode needs the a2 / dz2 / w2t / wfc_frag32 fp32 buffers");
   // bucket plan: in-range, ordered, non-overlapping; stage by the first conv gradient
@@ -109,10 +110,12 @@ void SimpleCNNEngine::synchronize() {
 }
 
 bool SimpleCNNEngine::level3_active(int batch) {
-  if (cfg_.fuse_level < 3 || cfg_.f32 || !b_.sync_flags || !b_.sync_err) return false;
+  if (cfg_.fuse_level < 3 || !b_.sync_flags || !b_.sync_err) return false;
   if (batch <= 0 || batch > cfg_.max_batch) return false;
   signed char& f = l3_fits_[batch];
-  if (f < 0) f = conv3x3_fwd_dz_fits(batch, cfg_.H, cfg_.W, cfg_.pxt_fwd) && cfg_.C1 == 32 && cfg_.C2 == 64 ? 1 : 0;
+  if (f < 0)
+    f = conv3x3_fwd_dz_fits(batch, cfg_.H, cfg_.W, cfg_.pxt_fwd, cfg_.f32 ? 4 : 2) && cfg_.C1 == 32 && cfg_.C2 == 64
+            ? 1 : 0;
   return f == 1;
 }
 
@@ -375,9 +378,12 @@ void SimpleCNNEngine::join_buckets() {
   DDP_HIP_CHECK(hipStreamWaitEvent(cs_, stage_used_[1] ? e_d1_ : e_d0_, 0));
 }
 
-// The exact-fp32 step: same kernel chain as level 1 (conv2 fwd + fused fc partials with
-// conv1 recomputed from the uint8 batch; fc backward with the cross-entropy prologue;
-// one fused conv backward; slab reduction) on fp32 operands.
+// The exact-fp32 step: the bf16 chains on fp32 operands.  Level 3 (default): the forward
+// also computes dL and dZ2 (per-image in-launch wait), and one conv backward launch runs the
+// dgrad and wgrad roles (both split over input-channel halves at two blocks per CU:
+// wgrad_split 2), the fc weight gradient + SGD as a third role (single process) and the
+// fused slab reduction + SGD.  Level 1: forward -> fc backward (cross-entropy prologue) ->
+// conv backward (+ the slab reduction).  Both chains give the same bits.
 void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_step) {
   const int H = cfg_.H, W = cfg_.W, HW = H * W, C1 = cfg_.C1, C2 = cfg_.C2, NO = cfg_.NO;
   if (B <= 0 || B > cfg_.max_batch) throw std::runtime_error("engine: bad batch size");
@@ -405,35 +411,58 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   c1b.bi = bid;
   c1b.w = c1.w;
   c1b.b = c1.b;
+  const bool l3 = level3_active(B);
   const bool fred = cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
-  if (fred) {
+  if (fred || l3) {  // the forward resets the step's hand-off counters
     const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
+    const int nsync = SYNC_RED_INTS + (l3 ? L3_FC_INTS : 0);
     c1.zero_i32 = b_.sync_flags;
-    c1.zero_per_block = (SYNC_RED_INTS + nfwd - 1) / nfwd;
+    c1.zero_per_block = (nsync + nfwd - 1) / nfwd;
+    c1.zero_total = nsync;
   }
-  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
+  const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2, n_fc = (long)NO * HW * C2;
   const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
                    cfg_.maximize, first_momentum_step ? 1 : 0, 1};
   const bool fopt = !dist && cfg_.fuse_opt;
+  FwdDz dzo;
+  if (l3) {
+    dzo.dz2_f32 = b_.dz2_f32;
+    dzo.img_cnt = b_.sync_flags + L3_IMG_OFF;
+    dzo.fc_bias = P + b_.off_bfc;
+    dzo.gscale = 1.f / (float)B;
+    dzo.err = b_.sync_err;
+    dzo.dl_out = b_.dlogits;
+    dzo.loss_rows = b_.loss_rows;
+  }
+  const bool fc_role = l3 && !dist && cfg_.l3_fc_role &&
+                       conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
 
   // ---- forward: conv1 (recomputed) + conv2 + bias + ReLU -> a2, fused fc partial logits
+  //      (level 3: then dL and dZ2 after the per-image wait)
   conv3x3_fwd(static_cast<const float*>(nullptr), P + b_.off_w2, P + b_.off_b2, b_.a2_f32, B, H, W, C1, C2,
-              true, b_.wfc_frag32, b_.fc_part, NO, cfg_.pxt_fwd, cs_, &c1);
+              true, b_.wfc_frag32, b_.fc_part, NO, cfg_.pxt_fwd, cs_, &c1, l3 ? &dzo : nullptr);
   // ---- loss + fc backward (bucket 0)
   FcBwdExtras ex;
   ex.dbias = G + b_.off_bfc;
   ex.dbias_scale = inv_ws;
   ex.loss_out = b_.loss_hist;
   ex.step_ctr = b_.step_ctr;
-  ex.part = b_.fc_part;
-  ex.HW = HW;
-  ex.CH = 64 * cfg_.pxt_fwd;
-  ex.fc_bias = P + b_.off_bfc;
-  ex.labels32 = b_.yb;
-  ex.bi = bid;
-  ex.gscale = 1.f / (float)B;
   ex.sys_store = use_x ? 1 : 0;
-  if (fopt) {  // each block updates only the fc columns it alone reads: race free in place
+  if (l3) {
+    ex.loss_rows = b_.loss_rows;  // dL and the row losses come from the forward
+    ex.zero_i32 = dzo.img_cnt;    // re-arm the forward's per-image counters
+    ex.n_zero = B;
+    ex.zero_stride = FWD_DZ_CNT_STRIDE;
+  } else {
+    ex.part = b_.fc_part;
+    ex.HW = HW;
+    ex.CH = 64 * cfg_.pxt_fwd;
+    ex.fc_bias = P + b_.off_bfc;
+    ex.labels32 = b_.yb;
+    ex.bi = bid;
+    ex.gscale = 1.f / (float)B;
+  }
+  if (fopt) {  // each block / wave updates only the fc columns it alone reads: race free in place
     ex.sgd = sa;
     ex.p_w = P + b_.off_wfc;
     ex.m_w = M ? M + b_.off_wfc : nullptr;
@@ -441,11 +470,31 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     ex.frag_HW = HW;
     ex.frag_C = C2;
   }
-  fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
-         (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+  BwdFc fcr;
+  if (fc_role) {
+    // inside the conv backward launch: block 0 of the fc role owns the fc bias, the loss and
+    // the step counter (nothing else in the launch reads them)
+    if (fopt) {
+      ex.p_b = P + b_.off_bfc;
+      ex.m_b = M ? M + b_.off_bfc : nullptr;
+      ex.step_inc = b_.step_ctr;
+    }
+    fcr.a2 = b_.a2_f32;
+    fcr.dl = b_.dlogits;
+    fcr.dW = fopt ? nullptr : G + b_.off_wfc;
+    fcr.scale = inv_ws;
+    fcr.K = (long)HW * C2;
+    fcr.ex = ex;
+  } else if (l3) {
+    fc_bwd(b_.dlogits, b_.a2_f32, nullptr, nullptr, fopt ? nullptr : G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
+           /*mask=*/true, cs_, ex);
+  } else {
+    fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
+           (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+  }
   ShadowSet sh1{};
   sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
-  sh1.r[1] = ShadowRegion{b_.off_wfc, (long)NO * HW * C2, nullptr, SHADOW_F32_FCFRAG, HW, C2, 0, b_.wfc_frag32};
+  sh1.r[1] = ShadowRegion{b_.off_wfc, n_fc, nullptr, SHADOW_F32_FCFRAG, HW, C2, 0, b_.wfc_frag32};
   sh1.count = 2;
   if (dist) launch_buckets(0, use_x, sa, M, sh1);
   // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
@@ -468,19 +517,24 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     opt(ss.s[1], b_.off_b2);
     opt(ss.s[2], b_.off_w1);
     opt(ss.s[3], b_.off_b1);
-    ss.s[4] = SlabSeg{G + b_.off_bfc, (long)NO, 0, (long)NO, 1, G + b_.off_bfc, 1.f};
-    opt(ss.s[4], b_.off_bfc);
-    ss.count = 5;
+    if (!fc_role) {
+      // fc bias: its gradient (fc_bwd block 0) is already final; a 1-row "slab" in place
+      ss.s[4] = SlabSeg{G + b_.off_bfc, (long)NO, 0, (long)NO, 1, G + b_.off_bfc, 1.f};
+      opt(ss.s[4], b_.off_bfc);
+      ss.count = 5;
+      ss.step_ctr = b_.step_ctr;
+    }
     ss.sgd = sa;
-    ss.step_ctr = b_.step_ctr;
   }
   ss.sys_store = use_x ? 1 : 0;
   const bool reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2,
                                    cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr),
-                                   false, cs_, fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, 1,
-                                   !dist && cfg_.fuse_reduce == 2);
+                                   false, cs_, fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
+                                   fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
   if (!reduced) grad_reduce(ss, cs_);
   last_fused_reduce_ = reduced;
+  last_level3_ = l3;
+  last_fc_role_ = fc_role;
   if (fopt) return;
   if (dist) {
     launch_buckets(1, use_x, sa, M, sh1);

@@ -61,10 +61,12 @@ class EngineOptions:
     # the fused optimizer and the fused slab reduction: forward -> fc_bwd -> conv backward);
     # (2 - fc_bwd and the conv backward in one launch - measured slower, removed in round 4);
     # 3: the fc backward off the critical path - the forward computes dZ2 itself (per-image
-    # in-launch wait for the logits) and the fc weight gradient + SGD runs on a side stream
-    # beside the conv backward (critical path: forward -> conv backward).  bf16 where every
-    # forward block is resident at once (B <= 40 on MI355X) and the GPU is not shared by
-    # several ranks; elsewhere the level-1 chain runs.  Bit-identical to level 1.
+    # in-launch wait for the logits) and the fc weight gradient + SGD runs as a role of the
+    # conv backward launch (critical path: forward -> conv backward).  bf16 and fp32, any
+    # batch up to 64 (in-order dispatch: a forward block only waits for its own image's
+    # blocks, so the grid need not be resident at once - conv3x3_fwd_dz_fits) where the GPU
+    # is not shared by several ranks; elsewhere the level-1 chain runs.  Bit-identical to
+    # level 1.
     fuse_level: int = 3
     # level 3, single process: the fc weight gradient as a third role of the conv backward
     # launch (2 kernels per step) - 1: its blocks (one 128-column chunk per wave) after every
@@ -100,12 +102,13 @@ class EngineOptions:
     epoch_order: bool = True
     # compute precision: "bf16" (bf16 MFMA operands, fp32 master weights / gradients /
     # optimizer) or "fp32" (exact fp32 operands on v_mfma_f32_16x16x4_f32 - the
-    # reference's precision; always the level-1 kernel chain)
+    # reference's precision; the same level-3 / level-1 chains)
     dtype: str = "bf16"
-    # fused conv backward (bf16): 2 = two wgrad blocks per slab row, one per half of conv2's
-    # input channels (half the conv1 recompute and MFMAs on the role's critical path;
-    # bit-identical slabs - measured 801k -> 811k img/s at B = 32, 1.04M -> 1.06M at B = 64,
-    # profiles/r2_split); 1 = one block per row.  fp32 always runs 1.
+    # fused conv backward: 2 = two wgrad blocks per slab row, one per half of conv2's input
+    # channels (half the conv1 recompute and MFMAs on the role's critical path; bit-identical
+    # slabs - bf16: 801k -> 811k img/s at B = 32, 1.04M -> 1.06M at B = 64, profiles/r2_split);
+    # for fp32 the dgrad role is split the same way (weights read from global) so both roles
+    # run at two blocks per CU; 1 = one block per row (fp32: the round-3 kernels, 1 block/CU)
     wgrad_split: int = 2
 
 
@@ -135,7 +138,7 @@ class FusedSimpleCNNEngine:
         # final (fc-only buckets right after fc_bwd, overlapping the conv backward)
         from ..parallel.bucket_model import XgmiCost, engine_plan
 
-        self.cost = XgmiCost(world_size)
+        self.cost = XgmiCost.calibrated(world_size)
         if self.opts.bucket_plan == "model":
             self.buckets, self.pred_comm_us = engine_plan(fs, world_size, self.cost)
         elif self.opts.bucket_plan == "torch":
@@ -153,7 +156,7 @@ class FusedSimpleCNNEngine:
         f32 = self.opts.dtype == "fp32"
         self.store_a1 = self.opts.store_a1 if self.opts.store_a1 is not None else (0 if f32 else 1)
         if f32 and (self.opts.fuse_level < 1 or self.store_a1 != 0):
-            raise ValueError("the fp32 engine runs the level-1 chain (fuse_level >= 1, store_a1 0)")
+            raise ValueError("the fp32 engine runs the level-1 or level-3 chain (fuse_level >= 1, store_a1 0)")
         R = self.wgrad_rows = self.opts.wgrad_rows or wgrad_rows(28, B, torch.float32 if f32 else BF16)
         g = self.opt.param_groups[0]
         if g["momentum"] != 0 and self.opt.momentum_buffer is None:
@@ -228,18 +231,25 @@ class FusedSimpleCNNEngine:
             elif self.xgmi is not None:
                 # "tune": measure one step's bucket all-reduces under each plan on this node
                 # and keep the fastest (rank 0 decides for everyone); RCCL competes
-                plan, self.allreduce_us = pick_data_plane(
-                    self.xgmi, comm, fs.grads, ranges, rank, oneshot=oneshot)
+                from ..parallel.xgmi import rccl_candidate_comms
+
+                variants = rccl_candidate_comms(rank, world_size) if comm is not None else {}
+                plan, self.allreduce_us, chosen = pick_data_plane(
+                    self.xgmi, comm, fs.grads, ranges, rank, oneshot=oneshot, rccl_variants=variants)
+                if plan.startswith("rccl"):
+                    comm = chosen  # the tuned communicator (algorithm / protocol) becomes the plane
             if self.xgmi is not None:
                 self.xgmi_plan = plan
-                if plan == "rccl":
+                if plan.startswith("rccl"):
                     self.xgmi = None
                 else:
                     cp = channel_plan(len(ranges), oneshot)
                     xch = [cp[(b, plan == "xgmi1" and b in oneshot)] for b in range(len(ranges))]
         if use_comm and self.xgmi is None and comm is None:
             raise RuntimeError("world size > 1 needs an RCCL communicator or the xGMI path")
-        self.comm_kind = (self.xgmi_plan or "xgmi") if self.xgmi is not None else ("rccl" if use_comm else "none")
+        self.comm_kind = ((self.xgmi_plan or "xgmi") if self.xgmi is not None
+                          else ((self.xgmi_plan if (self.xgmi_plan or "").startswith("rccl") else "rccl")
+                                if use_comm else "none"))
         self.ranges, self.xch, self.comm = ranges, xch, (comm if use_comm else None)
         self.cfg, self.offs = cfg, offs
         self.chain_check = None  # verify_chain's outcome (dict), when it ran

@@ -19,10 +19,13 @@ the LAST all-reduce - the only comm time left on the critical path - by dynamic
 programming; ties go to fewer buckets.  Each bucket also gets its kernel (one-shot below
 the crossover size, :meth:`XgmiCost.oneshot_max_elems`).
 
-The fixed terms are defaults until measured on an 8-GPU node (``--comm tune`` times the
-real kernels there): ``barrier_us`` is a cross-GPU flag round trip (a system-scope store
-seen by a peer's poll over xGMI, ~1.5 us each way), ``launch_us`` the graph-node/event
-hop of one more bucket kernel on the comm stream.
+The fixed terms are defaults until measured: ``barrier_us`` is a cross-GPU flag round trip
+(a system-scope store seen by a peer's poll over xGMI, ~1.5 us each way), ``launch_us`` the
+graph-node/event hop of one more bucket kernel on the comm stream, ``link_eff`` the share
+of a link's 153 GB/s the pulls reach.  ``parallel/comm_calibration.py`` fits all three to
+timed sweeps of the real kernels; :meth:`XgmiCost.calibrated` uses a stored fit measured on
+real peers at the same world size (``xgmi_calibration.json``, with provenance), and
+``bench.py`` refits on every N > 1 run (``config.comm_calibration``).
 """
 from __future__ import annotations
 
@@ -39,6 +42,18 @@ class XgmiCost:
     link_eff: float = 0.7     # achievable share with system-scope 4-byte pulls
     barrier_us: float = 3.0   # one cross-GPU barrier
     launch_us: float = 1.5    # one more bucket kernel on the comm stream (graph node + event)
+
+    @classmethod
+    def calibrated(cls, world: int, path: str | None = None) -> "XgmiCost":
+        """The model with the constants of a stored fit for this world size measured on real
+        xGMI peers (comm_calibration.json key "xgmi/<world>"), else the defaults."""
+        from .comm_calibration import CAL_PATH, load
+
+        rec = load(path or CAL_PATH).get(f"xgmi/{world}")
+        if not rec:
+            return cls(world)
+        return cls(world, link_gbps=rec.get("link_gbps", 153.0), link_eff=rec["link_eff"],
+                   barrier_us=rec["barrier_us"], launch_us=rec["launch_us"])
 
     def _link_us(self, nbytes: float) -> float:
         return nbytes / (self.link_gbps * self.link_eff * 1e3)  # bytes / (GB/s) -> us

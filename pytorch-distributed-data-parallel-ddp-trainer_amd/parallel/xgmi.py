@@ -178,19 +178,62 @@ def _self_test(x, grads, chans, rank, world) -> bool:
         torch.cuda.current_stream().synchronize()
 
 
+# RCCL algorithm / protocol candidates of ``--comm tune``: RCCL reads
+# NCCL_ALGO / NCCL_PROTO when it tunes a NEW communicator, so each candidate is a fresh
+# communicator created with them set.
+RCCL_CANDIDATES = (("Ring", "Simple"), ("Ring", "LL"), ("Ring", "LL128"), ("Tree", "Simple"), ("Tree", "LL"))
+
+
+def rccl_candidate_comms(rank: int, world: int, store=None, candidates=RCCL_CANDIDATES) -> dict:
+    """{"rccl:<algo>/<proto>": communicator} for every candidate whose communicator
+    initialised on EVERY rank (collective; a candidate that failed anywhere is left out)."""
+    import os
+
+    from ..engine.fused_step import agree
+
+    C = native.require()
+    store = store or dist.distributed_c10d._get_default_store()
+    gen = next(_gen)
+    out = {}
+    for i, (algo, proto) in enumerate(candidates):
+        key = f"ddp_amd/rccl_cand/{gen}/{i}"
+        saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO")}
+        os.environ["NCCL_ALGO"], os.environ["NCCL_PROTO"] = algo, proto
+        comm = None
+        try:
+            if rank == 0:
+                store.set(key, C.Comm.new_unique_id())
+            comm = C.Comm(store.get(key), rank, world, torch.cuda.current_device())
+        except Exception as e:  # noqa: BLE001 - an unsupported combination on this node
+            print(f"[ddp_amd] rank {rank}: RCCL {algo}/{proto} communicator failed ({e})", file=sys.stderr)
+            comm = None
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        if agree(store, key + "/ok", rank, world, comm is not None):
+            out[f"rccl:{algo}/{proto}"] = comm
+    return out
+
+
 def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int = 30, store=None,
-                    oneshot=()):
+                    oneshot=(), rccl_variants: dict | None = None):
     """Time the engine's bucket all-reduces under every available plan on this node.
 
     Candidates:
 
     * ``"xgmi"``: two-shot kernels for every bucket;
     * ``"xgmi1"``: the same, except the one-shot kernel for the buckets in ``oneshot``;
-    * ``"rccl"``: RCCL.
+    * ``"rccl"``: RCCL (the default communicator);
+    * ``"rccl:<algo>/<proto>"``: one per communicator in ``rccl_variants``
+      (:func:`rccl_candidate_comms`) - timed only because it initialised everywhere.
 
     Each candidate runs ``iters`` back-to-back rounds after a warm-up.  Returns
-    ``(plan, {plan: us})``. ``plan`` is the fastest candidate by rank 0's measurement,
-    broadcast through the store so that every rank picks the same one.
+    ``(plan, {plan: us}, comm)``: ``plan`` is the fastest candidate by rank 0's measurement,
+    broadcast through the store so that every rank picks the same one; ``comm`` the RCCL
+    communicator to use when the plan is an RCCL one.
 
     The gradient buffer's contents are clobbered; the engine rewrites every bucket each
     step."""
@@ -209,9 +252,11 @@ def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int
                 x.all_reduce(ch)
         return f
 
-    def t_rccl():
-        for v in views:
-            comm.all_reduce(v)
+    def run_rccl(c):
+        def f():
+            for v in views:
+                c.all_reduce(v)
+        return f
 
     def timed(fn):
         for _ in range(3):
@@ -226,15 +271,19 @@ def pick_data_plane(x, comm, grads: torch.Tensor, buckets, rank: int, iters: int
         return e0.elapsed_time(e1) * 1000.0 / iters
 
     times = {name: timed(run_x(chs)) for name, chs in plans.items()}
+    comms = {}
     if comm is not None:
-        times["rccl"] = timed(t_rccl)
+        comms["rccl"] = comm
+    comms.update(rccl_variants or {})
+    for name, c in comms.items():
+        times[name] = timed(run_rccl(c))
     ok = x.error_flags() == 0
     key = f"ddp_amd/xgmi/pick/{gen}"
     if rank == 0:
-        cand = {k: v for k, v in times.items() if ok or k == "rccl"}
+        cand = {k: v for k, v in times.items() if ok or k.startswith("rccl")}
         best = min(cand, key=cand.get)
         store.set(key, (best + " " + " ".join(f"{k}={v:.2f}" for k, v in times.items())).encode())
     parts = store.get(key).decode().split()
     best = parts[0]
     measured = {k: float(v) for k, v in (p.split("=") for p in parts[1:])}
-    return best, measured
+    return best, measured, comms.get(best)

@@ -33,11 +33,14 @@ def main(d, n=20, marker="conv3x3_fwd"):
         raise SystemExit(f"only {len(starts)} {marker} launches in {d}")
     first = starts[-n:]
     out = []
+    # the last step: as many kernels as the other steps have (what follows belongs to the
+    # run's tail - isolated all-reduce timings, synchronisation)
+    kps = statistics.median(first[j + 1] - first[j] for j in range(n - 1)) if n > 1 else len(rows) - first[0]
     for j, i0 in enumerate(first):
-        i1 = first[j + 1] if j + 1 < n else len(rows)
+        i1 = first[j + 1] if j + 1 < n else min(len(rows), i0 + int(kps))
         seg = rows[i0:i1]
         t0 = seg[0][0]
-        t1 = rows[i1][0] if i1 < len(rows) else max(r[1] for r in seg)
+        t1 = rows[i1][0] if (i1 < len(rows) and j + 1 < n) else max(r[1] for r in seg)
         busy = sum(r[1] - r[0] for r in seg)
         out.append(((t1 - t0) / 1000.0, busy / 1000.0, len(seg), [(r[1] - r[0]) / 1000.0 for r in seg]))
     gap = (rows[first[0]][0] - rows[first[0] - 1][1]) / 1000.0 if first[0] > 0 else float("nan")

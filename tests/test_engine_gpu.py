@@ -108,26 +108,25 @@ def test_fuse_level3_bitwise_equals_level1(B, opt, momentum, role):
     assert e3.eng.sync_error == 0
 
 
-def test_fuse_level3_ragged_epoch_and_fallback():
-    """A whole epoch with a ragged last batch (eager level-3 step at B = 8, counters of
-    fewer images), bit-identical to level 1; at B = 64 the forward grid (392 blocks) does
-    not fit the GPU at once, so level 3 falls back to the level-1 chain."""
-    m1, _, _, e1, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=1, momentum=0.9)
-    m3, _, _, e3, _, _ = _setup(n=1000, B=32, graph_steps=10, fuse_level=3, momentum=0.9)
+@pytest.mark.parametrize("B,n", [(32, 1000), (64, 2000)])
+def test_fuse_level3_ragged_epoch(B, n):
+    """A whole epoch with a ragged last batch (eager level-3 step at B = 8 / 16, counters of
+    fewer images), bit-identical to level 1 - also at the README's B = 64,
+    whose 392 forward blocks exceed the resident capacity: a block waits only for its own
+    image's blocks, which in-order dispatch always provides (conv3x3_fwd_dz_fits), and the
+    fc role holds 64 rows - 2 kernels per step."""
+    m1, _, _, e1, _, _ = _setup(n=n, B=B, graph_steps=10, fuse_level=1, momentum=0.9)
+    m3, _, _, e3, _, _ = _setup(n=n, B=B, graph_steps=10, fuse_level=3, momentum=0.9)
     losses = ([], [])
     for e, ls in ((e1, losses[0]), (e3, losses[1])):  # one engine at a time (see above)
         e.run_epoch(0, on_loss=lambda b, l, ls=ls: ls.append(l), log_every=5)
         e.run_epoch(1)
         e.synchronize()
-    assert e3.eng.level3_active(8) and e3.eng.last_level3
-    for (n, a), (_, b) in zip(m1.named_parameters(), m3.named_parameters()):
-        assert torch.equal(a, b), n
+    assert e3.level3 and e3.eng.level3_active(n % B) and e3.eng.last_level3 and e3.eng.last_fc_role
+    for (k, a), (_, b) in zip(m1.named_parameters(), m3.named_parameters()):
+        assert torch.equal(a, b), k
     assert losses[0] == losses[1]
-    _, _, _, e64, _, _ = _setup(B=64, fuse_level=3)
-    assert not e64.level3  # capacity check: 392 blocks > resident capacity
-    e64.run_steps(2)
-    e64.synchronize()
-    assert not e64.eng.last_level3 and e64.eng.sync_error == 0
+    assert e3.eng.sync_error == 0
 
 
 @pytest.mark.parametrize("dtype,B,opt", [("bf16", 32, True), ("bf16", 20, True), ("bf16", 64, False),
@@ -426,5 +425,49 @@ def test_verify_chain_world1_forced(corrupt):
             assert e.eng.sync_error == 0
             out.append((e.fs.params.clone(), e.opt.momentum_buffer.clone()))
         assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_tune_rccl_candidates_world1():
+    """``--comm tune`` also times RCCL algorithm / protocol variants - one
+    fresh communicator per (NCCL_ALGO, NCCL_PROTO) candidate, timed only if it initialised -
+    and the engine trains on whichever plane won (bitwise the comm-free run at world 1)."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import free_port, native_comm
+    from ddp_amd.parallel.xgmi import rccl_candidate_comms
+
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}",
+                            device_id=torch.device("cuda", 0))
+    try:
+        variants = rccl_candidate_comms(0, 1)
+        assert len(variants) >= 1, variants
+        t = torch.ones(1000, device=dev)
+        for name, c in variants.items():
+            assert name.startswith("rccl:")
+            c.all_reduce(t)
+        torch.cuda.synchronize()
+        assert torch.equal(t, torch.ones(1000, device=dev))
+        imgs, labels = synthetic_mnist(2048)
+        data = DeviceMNIST(imgs, labels, dev)
+        out = []
+        for force in (False, True):
+            torch.manual_seed(0)
+            m = SimpleCNN().to(dev)
+            e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01), data, 32, 1, 0, native_comm(),
+                                     EngineOptions(graph_steps=5, force_allreduce=force, comm="tune"))
+            if force:
+                assert e.allreduce_us and any(k.startswith("rccl:") for k in e.allreduce_us), e.allreduce_us
+                assert e.comm_kind in ("xgmi", "xgmi1") or e.comm_kind.startswith("rccl"), e.comm_kind
+            e.refresh()
+            e.run_steps(10)
+            e.synchronize()
+            out.append(e.fs.params.clone())
+        assert torch.equal(out[0], out[1])
     finally:
         dist.destroy_process_group()

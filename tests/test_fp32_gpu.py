@@ -174,7 +174,8 @@ def test_simple_cnn_fp32_module_path_matches_stock_fp32_model():
         assert e < 1e-4, f"{n}: rel err {e:.2e}"
 
 
-def _engine(B=32, momentum=0.0, fuse_opt=True, use_graph=False, graph_steps=5, dtype="fp32", seed=0):
+def _engine(B=32, momentum=0.0, fuse_opt=True, use_graph=False, graph_steps=5, dtype="fp32", seed=0,
+            fuse_level=1, wgrad_split=1, weight_decay=0.0, l3_fc_role=1):
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
     from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
     from ddp_amd.models import SimpleCNN
@@ -182,12 +183,13 @@ def _engine(B=32, momentum=0.0, fuse_opt=True, use_graph=False, graph_steps=5, d
 
     torch.manual_seed(seed)
     model = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
-    opt = FusedSGD(model, lr=0.01, momentum=momentum)
+    opt = FusedSGD(model, lr=0.01, momentum=momentum, weight_decay=weight_decay)
     imgs, labels = synthetic_mnist(2048)
     data = DeviceMNIST(imgs, labels, dev)
     eng = FusedSimpleCNNEngine(model, opt, data, B, 1, 0,
                                opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph,
-                                                  fuse_level=1, fuse_opt=fuse_opt, dtype=dtype))
+                                                  fuse_level=fuse_level, fuse_opt=fuse_opt, dtype=dtype,
+                                                  wgrad_split=wgrad_split, l3_fc_role=l3_fc_role))
     eng.refresh()
     return model, opt, eng, imgs, labels
 
@@ -198,10 +200,15 @@ def _native(model):
 
 
 @pytest.mark.parametrize("B", [32, 12])
-def test_fp32_engine_step_matches_float64_oracle(B):
+@pytest.mark.parametrize("chain", ["level1", "level3"])
+def test_fp32_engine_step_matches_float64_oracle(B, chain):
     """One fp32 engine step (separate SGD kernel so the gradient buffer holds the averaged
-    gradients): every gradient within 1e-5 of the float64 oracle, loss too."""
-    model, opt, eng, imgs, labels = _engine(B=B, fuse_opt=False)
+    gradients): every gradient within 1e-5 of the float64 oracle, loss too - for the
+    round-3 level-1 chain and the level-3 chain (dZ2 in the forward, channel-split conv
+    backward at two blocks per CU)."""
+    kw = dict(fuse_level=1, wgrad_split=1) if chain == "level1" else dict(fuse_level=3, wgrad_split=2)
+    model, opt, eng, imgs, labels = _engine(B=B, fuse_opt=False, **kw)
+    assert eng.level3 == (chain == "level3")
     assert eng.dtype == "fp32"
     before = {k: v.detach().cpu().clone() for k, v in _native(model).items()}
     eng.fs.grads.fill_(float("nan"))
@@ -250,3 +257,60 @@ def test_fp32_engine_batch_sweep_nan_poisoned():
             delta = (before[k].double() - after[k].double()) / 0.01
             assert torch.isfinite(delta).all(), (B, k)
             assert relerr(delta, g[k]) < 1e-3, (B, k)  # lr-division of an fp32 update: ~1e-4 noise
+
+
+@pytest.mark.parametrize("B,momentum,role,fuse_opt", [(32, 0.9, 1, True), (32, 0.0, 1, True), (20, 0.9, 1, True),
+                                                      (1, 0.9, 1, True), (40, 0.9, 1, True), (32, 0.9, 0, True),
+                                                      (32, 0.9, 1, False)])
+def test_fp32_level3_bitwise_equals_round3_level1(B, momentum, role, fuse_opt):
+    """the exact-fp32 step on the level-3 structure - dL and dZ2 in the
+    forward, the fc weight gradient + SGD as a role of the conv backward launch (role 1) or
+    its own kernel (role 0), both conv backward roles split over input-channel halves at two
+    blocks per CU, the fused slab reduction - gives parameters, momentum, losses, the fp32
+    weight copies and the step counter bit-identical to round 3's fp32 level-1 chain (one
+    conv backward block per row / chunk) after 12 graph-captured steps."""
+    kw = dict(B=B, momentum=momentum, weight_decay=1e-4, use_graph=True, graph_steps=4, fuse_opt=fuse_opt)
+    m1, o1, e1, _, _ = _engine(fuse_level=1, wgrad_split=1, **kw)
+    m3, o3, e3, _, _ = _engine(fuse_level=3, wgrad_split=2, l3_fc_role=role, **kw)
+    assert e3.level3 and not e1.level3
+    e1.run_steps(12)
+    e1.synchronize()
+    e3.run_steps(12)
+    e3.synchronize()
+    assert e3.eng.last_level3 and e3.eng.last_fc_role == (role == 1)
+    if B == 32:
+        assert e3.eng.last_fused_reduce  # two blocks per CU: the 224 wgrad rows fit the reducer budget
+    for (n, a), (_, b) in zip(m1.named_parameters(), m3.named_parameters()):
+        assert torch.equal(a, b), n
+    if momentum:
+        assert torch.equal(o1.momentum_buffer, o3.momentum_buffer)
+    assert torch.equal(e1.t["loss_hist"][:12], e3.t["loss_hist"][:12])
+    assert torch.equal(e1.t["step_ctr"], e3.t["step_ctr"])
+    assert torch.equal(e1.t["dz2"], e3.t["dz2"])
+    for k in ("w2t_f32", "wfc_frag32"):
+        assert torch.equal(e1.t[k], e3.t[k]), k
+    if not fuse_opt:
+        assert torch.equal(e1.fs.grads, e3.fs.grads)
+    assert e3.eng.sync_error == 0
+
+
+def test_fp32_level3_ragged_epoch_bitwise():
+    """A whole epoch with a ragged last batch (eager level-3 steps at B < max_batch) on the
+    fp32 level-3 chain == the round-3 fp32 level-1 chain, bit for bit."""
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+
+    imgs, labels = synthetic_mnist(1000)
+    out = []
+    for lvl, split in ((1, 1), (3, 2)):
+        torch.manual_seed(0)
+        m = SimpleCNN(compute_dtype=torch.float32).to(dev)
+        e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), DeviceMNIST(imgs, labels, dev), 32, 1, 0,
+                                 opts=EngineOptions(graph_steps=10, fuse_level=lvl, wgrad_split=split, dtype="fp32"))
+        e.refresh()
+        e.run_epoch(0)
+        e.synchronize()
+        out.append(e.fs.params.clone())
+    assert torch.equal(out[0], out[1])

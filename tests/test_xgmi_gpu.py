@@ -222,6 +222,44 @@ def test_engine_two_ranks_xgmi_identical_params(comm):
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
 
 
+def _calib_worker(rank, world, port, q, out):
+    try:
+        _init(rank, world, port)
+        from ddp_amd.parallel import comm_calibration as cc
+
+        fit = cc.calibrate(rank, world, torch.device("cuda", 0))
+        topo = cc.topology(world, rank=rank)
+        if rank == 0:
+            cc.save(fit, world, topo, path=out)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok", fit, topo))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, None))
+
+
+def test_comm_calibration_same_gpu(tmp_path):
+    """the cost-model fit from timed sweeps of both bucket kernels (2 ranks on
+    one GPU): every rank gets rank 0's constants, the fit is finite and explains the
+    timings, and it is stored as a same-GPU record (not used for real xGMI plans)."""
+    from ddp_amd.parallel import free_port
+    from ddp_amd.parallel import comm_calibration as cc
+    from ddp_amd.parallel.bucket_model import XgmiCost
+
+    out = str(tmp_path / "cal.json")
+    res = _run(_calib_worker, 2, free_port(), out)
+    assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
+    fits = [r[2] for r in res]
+    assert fits[0] == fits[1] and fits[0] is not None
+    f = fits[0]
+    assert f["n"] == 2 * len(cc.SWEEP_ELEMS) and all(v >= 0 for v in (f["launch_us"], f["barrier_us"]))
+    assert f["rms_us"] < 0.25 * max(t for _, _, t in f["samples"])
+    assert res[0][3] == "same-gpu"
+    assert cc.load(out)["same-gpu/2"]["world"] == 2
+    assert XgmiCost.calibrated(2, path=out) == XgmiCost(2)
+    print("same-GPU fit:", {k: v for k, v in f.items() if k != "samples"})
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_module_ddp_prescale_sum_bitwise(world):
     """module-path DDP averages like torch DDP - prescale by 1/world, then a
