@@ -78,6 +78,11 @@ struct BwdReduce {
   int nconv = 0;          // conv-role blocks (the arrivals the reducers wait for); fc-role blocks follow
   int* done = nullptr;  // 8 arrival counters, 32 ints apart (zeroed by the step's forward)
   int* err = nullptr;   // set to 2 when the wait times out
+  // role order of the conv blocks: 0 = all dgrad blocks, then all wgrad blocks; 1 =
+  // interleaved (d, w, d, w, ..., then the longer role's rest) so every CU holds a mix
+  // of both roles instead of a dgrad phase followed by a wgrad phase (the reducers are the
+  // last nr blocks whatever their role).  Set by the launcher (also without FRED).
+  int interleave = 0;
 };
 
 // Geometry specialisation: kernels take <GH, GW, GCI, GCO>; non-zero values replace
@@ -121,6 +126,10 @@ __host__ __device__ inline size_t fc_epi_lds(int pxt, int nof) { return sizeof(f
 // DZ (fuse level 3, launchers.h FwdDz): after the fc partials, wait for every block of the
 // block's image(s), evaluate dL and write dZ2 for the block's own pixels (see FwdDz).
 constexpr unsigned long long FWD_DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 MHz clock
+#ifndef DDP_AMD_F32_FC_PREFETCH
+#define DDP_AMD_F32_FC_PREFETCH 1
+#endif
+constexpr bool F32_FC_PREFETCH = DDP_AMD_F32_FC_PREFETCH;  // see conv3x3_fwd_kernel (DZ, fp32)
 
 template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
           bool DZ = false>
@@ -238,6 +247,21 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
           wv[pt][t][o] = *reinterpret_cast<const uint2*>(
               wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
   }
+  // DZ, exact fp32: the fc weight quads are needed twice (fc partials, then dZ2) and held in
+  // registers anyway - request them here too, so they land during the MFMA loop (the fp32
+  // MFMA loop reads only LDS: no vmcnt wait inside it); F32_FC_PREFETCH = 0 loads them in
+  // the epilogue instead
+  float4 wq[DZ && F32 ? PXT : 1][DZ && F32 ? 4 : 1][DZ && F32 ? NOF : 1];
+  if constexpr (DZ && F32 && F32_FC_PREFETCH) {
+#pragma unroll
+    for (int pt = 0; pt < PXT; ++pt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int o = 0; o < NOF; ++o)
+          wq[pt][t][o] = *reinterpret_cast<const float4*>(
+              wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
+  }
   // LDS-only barrier: the fc weight prefetch stays in flight through the MFMA loop
   // (__syncthreads drained it here: ~2 us per block, stamps s5 -> s2)
   lds_barrier();
@@ -301,9 +325,8 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
   float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X, (int)sizeof(T)));
   uint2 a2pk[DZ && !F32 ? PXT : 1][4];  // DZ: the stored bf16 a2 quads (dZ2's ReLU mask)
-  // DZ, exact fp32: the stored a2 quads and the fc weight quads of the epilogue, kept for dZ2
+  // DZ, exact fp32: the stored a2 quads (and wq, the fc weight quads), kept for dZ2
   float4 a2q[DZ && F32 ? PXT : 1][4];
-  float4 wq[DZ && F32 ? PXT : 1][DZ && F32 ? 4 : 1][DZ && F32 ? NOF : 1];
 #pragma unroll
   for (int pt = 0; pt < PXT; ++pt) {
     float fcs[NOF > 0 ? NOF : 1];
@@ -331,9 +354,14 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
         for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) {
           float s = fcs[o];
           if constexpr (F32) {  // fp32 FCFRAG weight: 4 consecutive channels, 1 KB per wave load
-            const float4 w4 = *reinterpret_cast<const float4*>(
-                wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
-            if constexpr (DZ) wq[pt][t][o] = w4;
+            float4 w4;
+            if constexpr (DZ && F32_FC_PREFETCH) {
+              w4 = wq[pt][t][o];
+            } else {
+              w4 = *reinterpret_cast<const float4*>(
+                  wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
+              if constexpr (DZ) wq[pt][t][o] = w4;
+            }
             s = fmaf(q[0], w4.x, s); s = fmaf(q[1], w4.y, s);
             s = fmaf(q[2], w4.z, s); s = fmaf(q[3], w4.w, s);
           } else {
@@ -509,23 +537,26 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
 // order, so dZ1 and the w1 slab row are bit-identical to the one-block-per-chunk kernel
 // (each half writes its own 16 channels of the row).
 template <typename T, int PXT, bool MASK_DY, bool MASK_X, bool FUSE_W1, bool A1X, int GH, int GW, int GCI,
-          int GCO, bool WG = false>
+          int GCO, int WGS = 0>
 __device__ __forceinline__ void dgrad_body(
     const T* __restrict__ dY, const T* __restrict__ Yact, const T* __restrict__ WT,
     const T* __restrict__ Xact, T* __restrict__ dX, int B, int H, int W, int Cin, int Cout,
     const void* __restrict__ x0, int x0_u8, BatchIdx bi, float* __restrict__ w1slab, C1Src c1, char* smem, int bx, int by) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
+  // WGS: 0 = weights staged in LDS; 1 = from global, one 16-channel half `by` per block;
+  // 2 = from global, both halves (all 32 input channels) per block
+  constexpr bool WG = WGS > 0, HALF = WGS == 1;
   static_assert(!WG || (F32 && GCI == 32 && GCO == 64 && FUSE_W1), "weights-from-global dgrad: fp32 SimpleCNN conv2");
   constexpr int CE = P::CE;
-  constexpr int NCT = WG ? 1 : 2;  // 16-wide input-channel tiles per wave
+  constexpr int NCT = HALF ? 1 : 2;  // 16-wide input-channel tiles per wave
   DDP_STAMP(STAMP_K_DGRAD, 0);
   DDP_GEOM_OVERRIDE();
   constexpr int CH = 64 * PXT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
-  const int ci_blk = WG ? by * 16 : by * 32;
+  const int ci_blk = HALF ? by * 16 : by * 32;
   const int KW = 9 * Cout, WS = KW + P::PAD, DS = Cout + P::PAD;  // row strides = 8 mod 16 dwords (conflict-free)
   const int XR = CH + 2 * W + 2;
   T* sWT = reinterpret_cast<T*>(smem);                   // [32 ci][9*Cout] (not WG)
@@ -537,7 +568,7 @@ __device__ __forceinline__ void dgrad_body(
   const long Pbase = P0 - W - 1;
   // conv1 channel group of this wave's mask work: WG - the half's two groups, waves
   // (w, w + 2) splitting the pixels; otherwise group = wave
-  const int mg = WG ? 2 * by + (wave & 1) : wave;
+  const int mg = HALF ? 2 * by + (wave & 1) : wave;
 
   // conv1 input values for the fused w1 gradient: loads issued before the staging
   // round so the dependent index -> image chain overlaps it
@@ -554,6 +585,16 @@ __device__ __forceinline__ void dgrad_body(
   const float x0_pre = (FUSE_W1 && (int)threadIdx.x < XR) ? x0_at(threadIdx.x) : 0.f;
   Conv1Group cg;
   if (A1X) cg = conv1_group_load(c1.w, c1.b, mg);  // lands during the staging round
+  // WG: tap 0's weight fragments, requested now so they land during the staging round
+  const T* wg = WT + (long)(ci_blk + (lane & 15)) * Cout + P::kofs(lane);
+  const long tstr = (long)Cin * Cout;
+  typename P::Frag an[WG ? 2 : 1][WG ? NCT : 1];
+  if constexpr (WG) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) an[k][t] = P::frag(wg + 16 * t * Cout + 32 * k);
+  }
   const int wc = KW / CE, cpc = Cout / CE;
   stage2<F32 ? 32 : 16>(WG ? 0 : 32 * wc,
           [&](int i) {
@@ -585,7 +626,7 @@ __device__ __forceinline__ void dgrad_body(
     // a1 recomputed from conv1 exactly as stored (bf16-rounded), channel group wave-uniform
     __syncthreads();
     const int g = mg;
-    for (int lp = lane + (WG ? 64 * (wave >> 1) : 0); lp < CH; lp += WG ? 128 : 64) {
+    for (int lp = lane + (HALF ? 64 * (wave >> 1) : 0); lp < CH; lp += HALF ? 128 : 64) {
       const long P = P0 + lp;
       unsigned m = 0;
       if (P < Ptot) {
@@ -663,21 +704,25 @@ __device__ __forceinline__ void dgrad_body(
       for (int t = 0; t < NCT; ++t) acc[pt][t] = P::mma(a[t], b[pt], acc[pt][t]);
   };
   if constexpr (WG) {
-    // A fragments from the global [tap][ci][co] copy: lane (row ci_blk + col, K offset kofs)
-    // reads 2 x 16 bytes per 32-wide K step; the next tap's are requested before this one's
-    // MFMAs (Cout == 64: two K steps per tap)
-    const T* wg = WT + (long)(ci_blk + col) * Cout + kofs;
-    const long tstr = (long)Cin * Cout;
-    typename P::Frag an[2] = {P::frag(wg), P::frag(wg + 32)};
+    // A fragments from the global [tap][ci][co] copy: lane (row ci + col, K offset kofs)
+    // reads 2 x 16 bytes per 32-wide K step and channel tile; tap 0's were requested before
+    // the staging round, every next tap's before this one's MFMAs (Cout == 64: two K steps
+    // per tap)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const typename P::Frag a0 = an[0], a1 = an[1];
+      typename P::Frag ac[2][NCT];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int t = 0; t < NCT; ++t) ac[k][t] = an[k][t];
       if (tap + 1 < 9) {
-        an[0] = P::frag(wg + (tap + 1) * tstr);
-        an[1] = P::frag(wg + (tap + 1) * tstr + 32);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int t = 0; t < NCT; ++t) an[k][t] = P::frag(wg + (tap + 1) * tstr + 16 * t * Cout + 32 * k);
       }
-      kstep(tap, 0, &a0);
-      kstep(tap, 32, &a1);
+      kstep(tap, 0, ac[0]);
+      kstep(tap, 32, ac[1]);
     }
   } else {
     const T* wrow = sWT + col * WS + kofs;
@@ -767,7 +812,7 @@ __device__ __forceinline__ void dgrad_body(
     __syncthreads();
     for (int i = threadIdx.x; i < 320; i += 256) {
       // WG: only this half's 16 channels (the other half-block writes the rest of the row)
-      if (WG && ((i < 288 ? i / 9 : i - 288) >> 4) != by) continue;
+      if (HALF && ((i < 288 ? i / 9 : i - 288) >> 4) != by) continue;
       st_wt(w1slab + (long)bx * 320 + i, ((s_w1[i] + s_w1[320 + i]) + s_w1[640 + i]) + s_w1[960 + i]);
     }
   }
@@ -1127,7 +1172,7 @@ __device__ __forceinline__ void fc_role_chunk(const BwdFc& fcr, const float* s_d
 }
 
 template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
-          bool FCR = false>
+          bool FCR = false, int DG = 1>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv3x3_bwd_kernel(
     const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
@@ -1157,26 +1202,35 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
     }
     if (f >= 0) cb -= fcr.nfc;
   }
-  // exact fp32 with the channel split: the dgrad role is split over input-channel halves too
-  // (weights from global: dgrad_body WG), two blocks per pixel chunk, paired 8 apart (same
-  // XCD, as the wgrad halves) - nd counts both halves
+  // exact fp32 with the channel split: the dgrad role reads its weights from global
+  // (dgrad_body WGS); DG == 2 also splits it over input-channel halves, two blocks per pixel
+  // chunk, paired 8 apart (same XCD, as the wgrad halves) - nd counts both halves
   constexpr bool WG = sizeof(T) == 4 && CS == 2;
-  if (cb < nd) {
-    int px = cb, hf = 0;
-    if constexpr (WG) {
+  constexpr int WGS = WG ? (DG == 2 ? 1 : 2) : 0;
+  const int nw = (red.nconv > 0 ? red.nconv : (int)gridDim.x) - nd;  // (nconv is always set by the launcher)
+  int rd = cb;  // role-local index: dgrad block rd (rd < nd) or wgrad block rd - nd
+  if (red.interleave) {
+    const int m = nd < nw ? nd : nw;
+    if (cb < 2 * m) rd = (cb & 1) ? nd + (cb >> 1) : (cb >> 1);
+    else rd = nd > nw ? cb - m : nd + (cb - m);
+  }
+  if (rd < nd) {
+    const int db = rd;
+    int px = db, hf = 0;
+    if constexpr (WGS == 1) {
       if (((nd >> 1) & 7) == 0) {
-        hf = (cb >> 3) & 1;
-        px = ((cb >> 4) << 3) | (cb & 7);
+        hf = (db >> 3) & 1;
+        px = ((db >> 4) << 3) | (db & 7);
       } else {
-        hf = cb & 1;
-        px = cb >> 1;
+        hf = db & 1;
+        px = db >> 1;
       }
     }
-    dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO, WG>(
+    dgrad_body<T, PXT, false, true, true, DA1X, GH, GW, GCI, GCO, WGS>(
         dY, nullptr, WT, DA1X ? nullptr : Xact, dX, B, H, W, Cin, Cout, c1.x, 1, c1.bi, w1slab, c1, smem, px, hf);
   } else {
     wgrad_body<T, false, WA1X, GH, GW, GCI, GCO, !WG, CS>(dY, nullptr, WA1X ? nullptr : Xact, slab, B, H,
-                                                         W, Cin, Cout, R, c1, smem, cb - nd, 0);
+                                                         W, Cin, Cout, R, c1, smem, rd - nd, 0);
   }
   if constexpr (FRED) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are out
@@ -1503,7 +1557,7 @@ using BwdKFn = void (*)(const T*, const T*, T*, float*, float*, int, int, int, i
 // query, so that query sees the exact kernel - its registers decide its residency).
 // cs == 2 and FCR: the bf16 SimpleCNN variants only (FCR: pxt 2, channel split).
 template <typename T, int PX, bool DA, bool WA>
-static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr) {
+static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr, int dg) {
   if (!g) return conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0, false>;
   if constexpr (sizeof(T) == 2) {
     if (cs == 2) {
@@ -1516,9 +1570,17 @@ static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr) {
                   : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2>;
     }
   } else {
-    // exact fp32, two blocks per CU (both roles channel-split): pxt 2, conv1 recomputed
+    // exact fp32, two blocks per CU (wgrad channel-split, dgrad weights from global, dgrad
+    // channel-split too when dg == 2): pxt 2, conv1 recomputed
     if constexpr (PX == 2 && DA && WA) {
       if (cs == 2) {
+        if (dg == 2) {
+          if (fcr)
+            return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true, 2>
+                        : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, true, 2>;
+          return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, false, 2>
+                      : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, false, 2>;
+        }
         if (fcr)
           return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true>
                       : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, true>;
@@ -1531,13 +1593,13 @@ static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr) {
               : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false>;
 }
 template <typename T>
-static BwdKFn<T> pick_bwd(int pxt, bool da, bool wa, bool g, bool fred, int cs, bool fcr) {
+static BwdKFn<T> pick_bwd(int pxt, bool da, bool wa, bool g, bool fred, int cs, bool fcr, int dg) {
   if (pxt == 2) {
-    if (da) return pick_bwd3<T, 2, true, true>(g, fred, cs, fcr);
-    return wa ? pick_bwd3<T, 2, false, true>(g, fred, cs, fcr) : pick_bwd3<T, 2, false, false>(g, fred, cs, fcr);
+    if (da) return pick_bwd3<T, 2, true, true>(g, fred, cs, fcr, dg);
+    return wa ? pick_bwd3<T, 2, false, true>(g, fred, cs, fcr, dg) : pick_bwd3<T, 2, false, false>(g, fred, cs, fcr, dg);
   }
-  if (da) return pick_bwd3<T, 1, true, true>(g, fred, cs, fcr);
-  return wa ? pick_bwd3<T, 1, false, true>(g, fred, cs, fcr) : pick_bwd3<T, 1, false, false>(g, fred, cs, fcr);
+  if (da) return pick_bwd3<T, 1, true, true>(g, fred, cs, fcr, dg);
+  return wa ? pick_bwd3<T, 1, false, true>(g, fred, cs, fcr, dg) : pick_bwd3<T, 1, false, false>(g, fred, cs, fcr, dg);
 }
 
 bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split) {
@@ -1555,7 +1617,12 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   // chunk, at two blocks per CU; otherwise one block each
   constexpr bool F32 = sizeof(T) == 4;
   const int cs = (csplit == 2 && g && (!F32 || (pxt == 2 && !Xact))) ? 2 : 1;
-  const int dcs = F32 && cs == 2 ? 2 : 1;
+  // exact fp32: dgrad channel split (DDP_AMD_F32_DSPLIT=1 keeps one dgrad block per chunk)
+  int dcs = 1;
+  if (F32 && cs == 2) {
+    const char* e = std::getenv("DDP_AMD_F32_DSPLIT");
+    dcs = (e && e[0] == '1') ? 1 : 2;
+  }
   const int nrows = conv3x3_wgrad_blocks(B, H, R);
   const int nd = conv3x3_dgrad_blocks(B, H, W, pxt) * dcs, nw = nrows * cs;
   size_t lds = conv3x3_bwd_lds(W, Cin, Cout, pxt, R, (int)sizeof(T), cs);
@@ -1582,6 +1649,11 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   }
   BwdReduce red;
   red.nconv = nd + nw;
+  {  // role order: interleaved for bf16 (+1.7-2.3 % in-call, profiles/r4_interleave), the
+     // fp32 split keeps dgrad-then-wgrad (neutral there); A/B knob DDP_AMD_BWD_INTERLEAVE=0|1
+    const char* e = std::getenv("DDP_AMD_BWD_INTERLEAVE");
+    red.interleave = e && e[0] ? (e[0] == '1') : !F32;
+  }
   if (fused) {
     // the reducer's 16-byte row loads need n >= 4; its summation order is grad_reduce's
     // 16-row-group one (deep slabs; shallow ones keep the separate kernel)
@@ -1594,7 +1666,7 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     // slower - their polling shares the CUs of the still-running wgrad blocks)
     // (channel split: the last nrows blocks - as many reducers as without the split).
     // Residency of the exact instantiation that will run.
-    const BwdKFn<T> kf = pick_bwd<T>(pxt, da, wa, g, true, cs, fc != nullptr);
+    const BwdKFn<T> kf = pick_bwd<T>(pxt, da, wa, g, true, cs, fc != nullptr, dcs);
     lds_optin(kf, lds);
     const int nr = (g && red_done) ? fused_reducers(kf, lds, nrows, exclusive) : 0;
     if (nr <= 0) fused = nullptr;  // the caller reduces with grad_reduce
@@ -1608,7 +1680,7 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");
   }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
-  const BwdKFn<T> k = pick_bwd<T>(pxt, da, wa, g, fused != nullptr, cs, fc != nullptr);
+  const BwdKFn<T> k = pick_bwd<T>(pxt, da, wa, g, fused != nullptr, cs, fc != nullptr, dcs);
   lds_optin(k, lds);
   hipLaunchKernelGGL(k, dim3(nd + nw + nfc), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R,
                      nd, c1, Xact, red, fcr);

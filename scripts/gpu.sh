@@ -14,6 +14,10 @@
 #                              1000-step runs; "so=<path>" as an env selects another _C.so
 #   resnet [bench args]        ResNet-18 bench (graph) + rocprofv3 stats
 #   pmc <counters> [bench args]  one PMC pass (<= 8 SQ counters) over a 200-step run
+#   roofline                   ResNet-18 per-layer roofline (scripts/resnet_roofline.py) -> roofline.md
+#   rehearse [n...]            N-rank rehearsal of the xGMI data plane on ONE GPU (gloo control
+#                              plane, bench.py --backend gloo --comm xgmi; default n = 4 8)
+#   calibrate [n]              fit the xGMI cost model on n same-GPU ranks (scripts/comm_calibrate.py)
 #   all                        tests + smoke + bench + stats + resnet (round-end evidence)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -67,6 +71,27 @@ run_pmc() {
       --warmup 20 --no_fp32 "$@" > /dev/null 2>> "$out/err.log"
 }
 
+run_roofline() {
+  T 400 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d "$out/rf" -- python \
+      scripts/resnet_roofline.py run --out "$out/calls.json" > "$out/roofline_run.log" 2>&1 &&
+    python scripts/resnet_roofline.py report "$out/rf" --calls "$out/calls.json" --md "$out/roofline.md" > /dev/null &&
+    head -40 "$out/roofline.md"
+}
+
+run_rehearse() {
+  export DDP_AMD_XGMI_GRID_CAP=${DDP_AMD_XGMI_GRID_CAP:-16} DDP_AMD_XGMI_TIMEOUT_S=${DDP_AMD_XGMI_TIMEOUT_S:-20}
+  for n in ${@:-4 8}; do
+    T 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
+      --master-port $((29500 + n)) bench.py --gpus $n --backend gloo --comm xgmi --steps 200 --warmup 20 \
+      --no_comm_calibration > "$out/bench_n$n.log" 2>&1 || { echo "n=$n failed"; return 1; }
+    tail -1 "$out/bench_n$n.log"
+  done
+}
+run_calibrate() {
+  T 300 python scripts/comm_calibrate.py --ranks ${1:-2} --out "$out/xgmi_calibration.json" > "$out/calibrate.log" 2>&1 &&
+    cat "$out/calibrate.log"
+}
+
 case $task in
   tests) run_tests "$@" ;;
   smoke) run_smoke ;;
@@ -76,6 +101,9 @@ case $task in
   ab) run_ab "$@" ;;
   resnet) run_resnet "$@" ;;
   pmc) run_pmc "$@" ;;
+  roofline) run_roofline ;;
+  rehearse) run_rehearse "$@" ;;
+  calibrate) run_calibrate "$@" ;;
   all) run_tests && run_smoke && run_bench && run_stats && run_resnet ;;
   *) echo "unknown task $task"; exit 2 ;;
 esac
