@@ -127,7 +127,7 @@ __host__ __device__ inline size_t fc_epi_lds(int pxt, int nof) { return sizeof(f
 // block's image(s), evaluate dL and write dZ2 for the block's own pixels (see FwdDz).
 constexpr unsigned long long FWD_DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 MHz clock
 #ifndef DDP_AMD_F32_FC_PREFETCH
-#define DDP_AMD_F32_FC_PREFETCH 1
+#define DDP_AMD_F32_FC_PREFETCH 0  // 1: measured neutral (block 22.6 vs 22.7 us, profiles/r4_fp32)
 #endif
 constexpr bool F32_FC_PREFETCH = DDP_AMD_F32_FC_PREFETCH;  // see conv3x3_fwd_kernel (DZ, fp32)
 
@@ -1643,7 +1643,11 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     // free first
     nfc = (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
-    fcr.fc0 = nd + nw;
+    // fc blocks after every conv block (default) or before them (A/B knob DDP_AMD_FC_FIRST=1:
+    // B = 32 838k vs 954k img/s in-call, B = 64 within the spread - profiles/r4_b64)
+    const char* ff = std::getenv("DDP_AMD_FC_FIRST");
+    const bool first = ff && ff[0] == '1';
+    fcr.fc0 = first ? 0 : nd + nw;
     if ((size_t)B * (FCDW_LD + 10) * sizeof(float) > lds)
       throw std::runtime_error("conv3x3_bwd: LDS too small for the fc role");
   }

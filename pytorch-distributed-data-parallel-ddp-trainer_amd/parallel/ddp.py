@@ -111,8 +111,12 @@ class _NativeReducer:
             from .bucket_model import XgmiCost
 
             # small buckets: the one-shot kernel (one cross-GPU barrier), below the cost
-            # model's crossover for this world size
-            lim = XgmiCost(dist.get_world_size()).oneshot_max_elems()
+            # model's crossover for this world size and the one-grid cap the engine uses
+            # (ONESHOT_MAX_ELEMS: each one-shot channel also holds 2 x its bucket of stage
+            # memory - uncapped, every ResNet-18 bucket got one at N <= 2, ~94 MB more)
+            from ..engine.fused_step import ONESHOT_MAX_ELEMS
+
+            lim = min(ONESHOT_MAX_ELEMS, XgmiCost.calibrated(dist.get_world_size()).oneshot_max_elems())
             oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
             # the bucket kernels run next to the backward: small spinning grid
             self.xgmi = create_xgmi(fs.grads, ranges, dist.get_rank(), dist.get_world_size(),
