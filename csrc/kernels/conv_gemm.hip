@@ -32,6 +32,10 @@
 namespace ddp_amd {
 
 constexpr int CG_KS = 32;  // K-step (channels of one tap)
+#ifndef DDP_AMD_CG_PIPE
+#define DDP_AMD_CG_PIPE 1  // 4: slower (512@7 fwd 102 -> 124 us: registers halve the occupancy that hid the latency; profiles/r4_resnet)
+#endif
+constexpr int CG_PIPE = DDP_AMD_CG_PIPE;  // K-steps of global-load lookahead (forward kernel)
 // LDS row stride (elements) of K-contiguous tiles.  40 (20 dwords) shows 4.9-5.3 bank-
 // conflict cycles per LDS instruction in the forward (PMC SQ_LDS_BANK_CONFLICT,
 // profiles/r1_resnet); the conflict-free 48 (24 dwords, == 8 mod 16) measured no faster
@@ -146,30 +150,41 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
 #pragma unroll
     for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 ra[BC * 4 / 256 > 0 ? BC * 4 / 256 : 1], rb[2];
-  if (kb < ke) {
-    load_k(kb, ra, rb);
-    store_k(0, ra, rb);
-  }
+  // K loop, software-pipelined CG_PIPE deep: the global loads of K-step ks + CG_PIPE are
+  // issued at the start of step ks into register set (ks - kb) % CG_PIPE (free: its step
+  // was stored to LDS one step earlier), so each load has CG_PIPE - 1 steps of MFMAs to land
+  // before the step that stores it.  With one step of lookahead every step waited out a
+  // full L2 / HBM round trip (~1-2 us against ~0.1 us of MFMAs: the ResNet-18 layers ran at
+  // 5-15 % of their roofline, profiles/r4_resnet/roofline.md).  LDS stays double-buffered.
+  constexpr int NA = BC * 4 / 256 > 0 ? BC * 4 / 256 : 1;
+  bf16x8 ra[CG_PIPE][NA], rb[CG_PIPE][2];
+#pragma unroll
+  for (int u = 0; u < CG_PIPE; ++u)
+    if (kb + u < ke) load_k(kb + u, ra[u], rb[u]);
+  if (kb < ke) store_k(0, ra[0], rb[0]);
   __syncthreads();
   const int kofs = 8 * (lane >> 4), col = lane & 15;
-  for (int ks = kb; ks < ke; ++ks) {
-    const int cur = (ks - kb) & 1;
-    const bool more = ks + 1 < ke;
-    if (more) load_k(ks + 1, ra, rb);  // in flight during this step's MFMAs
-    bf16x8 a[TCO], b[TPX];
+  for (int base = kb; base < ke; base += CG_PIPE) {
 #pragma unroll
-    for (int i = 0; i < TCO; ++i)
-      a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(wco * (BC / 2) + 16 * i + col) * CG_RS + kofs]);
+    for (int u = 0; u < CG_PIPE; ++u) {
+      const int ks = base + u;
+      if (ks >= ke) break;  // block-uniform
+      const int cur = (ks - kb) & 1;
+      if (ks + CG_PIPE < ke) load_k(ks + CG_PIPE, ra[u], rb[u]);  // set u was stored last step
+      bf16x8 a[TCO], b[TPX];
 #pragma unroll
-    for (int j = 0; j < TPX; ++j)
-      b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * (BP / 2) + 16 * j + col) * CG_RS + kofs]);
+      for (int i = 0; i < TCO; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(wco * (BC / 2) + 16 * i + col) * CG_RS + kofs]);
 #pragma unroll
-    for (int i = 0; i < TCO; ++i)
+      for (int j = 0; j < TPX; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * (BP / 2) + 16 * j + col) * CG_RS + kofs]);
 #pragma unroll
-      for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-    if (more) store_k(cur ^ 1, ra, rb);
-    __syncthreads();
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      if (ks + 1 < ke) store_k(cur ^ 1, ra[(u + 1) % CG_PIPE], rb[(u + 1) % CG_PIPE]);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue
@@ -346,36 +361,41 @@ __global__ __launch_bounds__(256) void conv_gemm_dgrad_kernel(ConvGeom g, const 
   for (int i = 0; i < TCI; ++i)
 #pragma unroll
     for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 ra[ACH], rb[2];
-  if (kb < ke) {
-    load_k(kb, ra, rb);
-    store_k(0, ra, rb);
-  }
+  // K loop pipelined CG_PIPE deep (see conv_gemm_fwd_kernel)
+  bf16x8 ra[CG_PIPE][ACH], rb[CG_PIPE][2];
+#pragma unroll
+  for (int u = 0; u < CG_PIPE; ++u)
+    if (kb + u < ke) load_k(kb + u, ra[u], rb[u]);
+  if (kb < ke) store_k(0, ra[0], rb[0]);
   __syncthreads();
   const int kofs = 8 * (lane >> 4), col = lane & 15;
   const int gq = lane >> 4, q = col >> 2, pq = col & 3;
   const int rlo = (4 * gq + q) * AS, rhi = (16 + 4 * gq + q) * AS;
-  for (int ks = kb; ks < ke; ++ks) {
-    const int cur = (ks - kb) & 1;
-    const bool more = ks + 1 < ke;
-    if (more) load_k(ks + 1, ra, rb);
-    bf16x8 a[TCI], b[TPX];
+  for (int base = kb; base < ke; base += CG_PIPE) {
 #pragma unroll
-    for (int i = 0; i < TCI; ++i) {
-      const int m = wci * (BC / 2) + 16 * i + 4 * pq;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sA[cur][rlo + m]);
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sA[cur][rhi + m]);
-      a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int u = 0; u < CG_PIPE; ++u) {
+      const int ks = base + u;
+      if (ks >= ke) break;  // block-uniform
+      const int cur = (ks - kb) & 1;
+      if (ks + CG_PIPE < ke) load_k(ks + CG_PIPE, ra[u], rb[u]);
+      bf16x8 a[TCI], b[TPX];
+#pragma unroll
+      for (int i = 0; i < TCI; ++i) {
+        const int m = wci * (BC / 2) + 16 * i + 4 * pq;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sA[cur][rlo + m]);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&sA[cur][rhi + m]);
+        a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TPX; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * (BP / 2) + 16 * j + col) * CG_RS + kofs]);
+#pragma unroll
+      for (int i = 0; i < TCI; ++i)
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      if (ks + 1 < ke) store_k(cur ^ 1, ra[(u + 1) % CG_PIPE], rb[(u + 1) % CG_PIPE]);
+      __syncthreads();
     }
-#pragma unroll
-    for (int j = 0; j < TPX; ++j)
-      b[j] = *reinterpret_cast<const bf16x8*>(&sB[cur][(wpx * (BP / 2) + 16 * j + col) * CG_RS + kofs]);
-#pragma unroll
-    for (int i = 0; i < TCI; ++i)
-#pragma unroll
-      for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-    if (more) store_k(cur ^ 1, ra, rb);
-    __syncthreads();
   }
   const long Ptot = (long)g.N * g.H * g.W;
 #pragma unroll
