@@ -132,8 +132,8 @@ constexpr unsigned long long FWD_DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 M
 constexpr bool F32_FC_PREFETCH = DDP_AMD_F32_FC_PREFETCH;  // see conv3x3_fwd_kernel (DZ, fp32)
 
 template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
-          bool DZ = false>
-__global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
+          bool DZ = false, int OCC = 1>
+__global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  // 2nd: waves per SIMD
     const T* __restrict__ X, const T* __restrict__ Wt, const float* __restrict__ bias,
     T* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
     const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1, FwdDz dzo) {
@@ -236,16 +236,31 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
   // fc weight prefetch (lands while the MFMAs run; issued before the staging it delayed
   // it - in-order vmcnt - by more than it saved); fp32 reads its FCFRAG-order fp32 weight in
   // the epilogue instead (160 more VGPRs would not fit next to the fp32 fragments)
-  uint2 wv[NOF > 0 && !F32 ? PXT : 1][4][NOF > 0 && !F32 ? NOF : 1];
-  if (NOF > 0 && !F32) {
+  // OCC 2 (level 3 at B > 32, two blocks per CU): no prefetch - the 80 VGPRs of bf16 weight
+  // pairs would hold the kernel at one block per CU; they are read where used (L2 hits),
+  // the other block of the CU hides that latency
+  constexpr bool PFW = NOF > 0 && !F32 && OCC == 1;
+  // (!PFW: buffer loads - one per-lane VGPR offset per pixel tile and a uniform (o, t) SGPR
+  // offset; flat loads kept 40 64-bit addresses live between the fc partials and dZ2)
+  const __amdgpu_buffer_rsrc_t rwfc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(wfc), (short)0, 0x7fffffff, 0x00020000);
+  auto fcw = [&](int pt, int t, int o) {
+    if constexpr (PFW)
+      return *reinterpret_cast<const uint2*>(
+          wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
+    const int vo = (((rem[pt] >> 4) * (Cout >> 4) + (co0 >> 4)) * 64 + lane) * 4 * (int)sizeof(T);
+    const int so = ((o * (HW >> 4) * (Cout >> 4) + t) * 64) * 4 * (int)sizeof(T);
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwfc, vo, so, 0));
+  };
+  uint2 wv[PFW ? PXT : 1][4][PFW ? NOF : 1];
+  if constexpr (PFW) {
 #pragma unroll
     for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o)
-          wv[pt][t][o] = *reinterpret_cast<const uint2*>(
-              wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
+          wv[pt][t][o] = fcw(pt, t, o);
   }
   // DZ, exact fp32: the fc weight quads are needed twice (fc partials, then dZ2) and held in
   // registers anyway - request them here too, so they land during the MFMA loop (the fp32
@@ -334,6 +349,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
     for (int o = 0; o < (NOF > 0 ? NOF : 1); ++o) fcs[o] = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      if constexpr (NOF > 0 && !PFW && !F32) __builtin_amdgcn_sched_barrier(0);  // 20 VGPRs of weights at a time
       const int co = co0 + 16 * t + 4 * (lane >> 4);
       const float4 bv = bq[t];
       float v0 = acc[pt][t][0] + bv.x, v1 = acc[pt][t][1] + bv.y;
@@ -368,10 +384,12 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
             // the stored bf16 pairs against the bf16 weight pairs: v_dot2c_f32_bf16 (exact
             // bf16 products, fp32 accumulate) - no unpacking of either operand
             const uint2 pk = pack4(v0, v1, v2, v3);
+            uint2 wo;
+            if constexpr (PFW) wo = wv[pt][t][o]; else wo = fcw(pt, t, o);
             s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, pk.x),
-                                                __builtin_bit_cast(bf16x2v, wv[pt][t][o].x), s, false);
+                                                __builtin_bit_cast(bf16x2v, wo.x), s, false);
             s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, pk.y),
-                                                __builtin_bit_cast(bf16x2v, wv[pt][t][o].y), s, false);
+                                                __builtin_bit_cast(bf16x2v, wo.y), s, false);
           }
           fcs[o] = valid[pt] ? s : 0.f;
         }
@@ -489,6 +507,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
       for (int o = 0; o < NOF; ++o) d[o] = dl[o];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
+        if constexpr (!PFW && !F32) __builtin_amdgcn_sched_barrier(0);
         float dz[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int o = 0; o < NOF; ++o) {
@@ -496,8 +515,10 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_fwd_kernel(
           if constexpr (F32) {
             const float4 wf = wq[pt][t][o];
             w4[0] = wf.x; w4[1] = wf.y; w4[2] = wf.z; w4[3] = wf.w;
-          } else {
+          } else if constexpr (PFW) {
             unpack4(wv[pt][t][o], w4);
+          } else {
+            unpack4(fcw(pt, t, o), w4);
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) dz[j] = fmaf(d[o], w4[j], dz[j]);
@@ -1302,9 +1323,20 @@ static void lds_optin(K kernel, size_t bytes) {
 }
 
 // the level-3 forward of SimpleCNN's conv2 (fc epilogue, conv1 recompute, pxt 1 / 2)
-template <typename T, int PX>
+template <typename T, int PX, int OCC = 1>
 static auto fwd_dz_kernel() {
-  return conv3x3_fwd_kernel<T, 1, 4 * PX, true, 10, true, 28, 28, 32, 64, true>;
+  return conv3x3_fwd_kernel<T, 1, 4 * PX, true, 10, true, 28, 28, 32, 64, true, OCC>;
+}
+
+// bf16 level-3 forward at two blocks per CU (OCC 2, no fc weight prefetch) when the grid
+// exceeds one block per CU (B > 32 at pxt 2); DDP_AMD_FWD_OCC2=0/1 forces it off/on
+static bool fwd_dz_occ2(unsigned grid) {
+  static const int env = [] { const char* e = getenv("DDP_AMD_FWD_OCC2"); return e ? atoi(e) : -1; }();
+  if (env >= 0) return env == 1;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  return cus > 0 && grid > (unsigned)cus;
 }
 
 template <typename T>
@@ -1356,6 +1388,14 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
         !dz->img_cnt || !dz->fc_bias)
       throw std::runtime_error("conv3x3_fwd: the level-3 dZ2 epilogue is the SimpleCNN forward with the fc "
                                "epilogue and the conv1 recompute");
+    if constexpr (sizeof(T) == 2) {
+      if (pxt == 2 && fwd_dz_occ2(grid.x)) {
+        auto k = fwd_dz_kernel<T, 2, 2>();
+        lds_optin(k, lds);
+        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo);
+        return;
+      }
+    }
     auto k = pxt == 2 ? fwd_dz_kernel<T, 2>() : fwd_dz_kernel<T, 1>();
     lds_optin(k, lds);
     hipLaunchKernelGGL(k, grid, dim3(256 * pxt), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo);
