@@ -18,6 +18,9 @@
 #   rehearse [n...]            N-rank rehearsal of the xGMI data plane on ONE GPU (gloo control
 #                              plane, bench.py --backend gloo --comm xgmi; default n = 4 8)
 #   calibrate [n]              fit the xGMI cost model on n same-GPU ranks (scripts/comm_calibrate.py)
+#   sweep <run>...             bench variants, each run "tag|ENV=v ENV2=w|bench args" (env and args
+#                              may be empty): 1000-step + driver-shaped json per tag, one line each
+#   stamps [stamps.py args]    in-kernel phase timeline (scripts/stamps.py --graph) -> stamps.txt
 #   all                        tests + smoke + bench + stats + resnet (round-end evidence)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -91,6 +94,15 @@ run_calibrate() {
   T 300 python scripts/comm_calibrate.py --ranks ${1:-2} --out "$out/xgmi_calibration.json" > "$out/calibrate.log" 2>&1 &&
     cat "$out/calibrate.log"
 }
+run_sweep() {
+  for spec in "$@"; do
+    IFS='|' read -r tag envs args <<< "$spec"
+    env $envs timeout -k 10 200 python bench.py $args > "$out/l_$tag.json" 2>> "$out/err.log" || return $?
+    env $envs timeout -k 10 200 python bench.py --steps 20 --warmup 5 $args > "$out/d_$tag.json" 2>> "$out/err.log" || return $?
+    echo "$tag: 1000 $(grep -o '"value": [0-9.]*' "$out/l_$tag.json") | driver $(grep -o '"value": [0-9.]*' "$out/d_$tag.json")"
+  done
+}
+run_stamps() { T 200 python scripts/stamps.py --graph "$@" > "$out/stamps.txt" 2>&1 && grep -v amdgpu.ids "$out/stamps.txt"; }
 
 case $task in
   tests) run_tests "$@" ;;
@@ -104,6 +116,8 @@ case $task in
   roofline) run_roofline ;;
   rehearse) run_rehearse "$@" ;;
   calibrate) run_calibrate "$@" ;;
+  sweep) run_sweep "$@" ;;
+  stamps) run_stamps "$@" ;;
   all) run_tests && run_smoke && run_bench && run_stats && run_resnet ;;
   *) echo "unknown task $task"; exit 2 ;;
 esac
