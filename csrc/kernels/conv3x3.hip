@@ -240,14 +240,12 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   // pairs would hold the kernel at one block per CU; they are read where used (L2 hits),
   // the other block of the CU hides that latency
   constexpr bool PFW = NOF > 0 && !F32 && OCC == 1;
-  // (!PFW: buffer loads - one per-lane VGPR offset per pixel tile and a uniform (o, t) SGPR
-  // offset; flat loads kept 40 64-bit addresses live between the fc partials and dZ2)
+  // buffer loads: one per-lane VGPR offset per pixel tile and a uniform (o, t) SGPR offset
+  // (flat loads: two 64-bit adds per load; without the prefetch (!PFW) the compiler kept 40
+  // 64-bit addresses live between the fc partials and dZ2 and spilled)
   const __amdgpu_buffer_rsrc_t rwfc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(wfc), (short)0, 0x7fffffff, 0x00020000);
   auto fcw = [&](int pt, int t, int o) {
-    if constexpr (PFW)
-      return *reinterpret_cast<const uint2*>(
-          wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
     const int vo = (((rem[pt] >> 4) * (Cout >> 4) + (co0 >> 4)) * 64 + lane) * 4 * (int)sizeof(T);
     const int so = ((o * (HW >> 4) * (Cout >> 4) + t) * 64) * 4 * (int)sizeof(T);
     return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwfc, vo, so, 0));
@@ -1681,6 +1679,9 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     // one 128-column chunk per wave (4 per block), blocks after every conv block: the first
     // take the resident slots the conv blocks leave free, the rest those the dgrad blocks
     // free first
+    // (two chunks per wave - 49 blocks, all resident from the start at B = 32 - measured
+    // slower: each fc wave's time doubles, 944k -> 935k in-call, B = 64 1.13M -> 1.05M;
+    // profiles/r4_fc_cpw)
     nfc = (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
     // fc blocks after every conv block (default) or before them (A/B knob DDP_AMD_FC_FIRST=1:
