@@ -32,7 +32,7 @@ constexpr int HL_MAXPX = 232;     // largest halo: (R+2) x (W+2) = 4 x 58 at W =
 // (BnAffine, bitwise bn_apply's value; the zero padding stays zero) - the producer's
 // bn_apply pass disappears.  The per-channel sc / sh table sits in LDS (4 KB).
 template <int BC, int BP, bool STATS, bool PART, bool AFF = false>
-__global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
+__global__ __launch_bounds__(256, 2) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ Wt,
                                                                  bf16_t* __restrict__ Y,
                                                                  float* __restrict__ stats,
@@ -132,43 +132,49 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
 #pragma unroll
     for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 ra[WCH], rh[HCH];
+  // Weights (one kernel row per barrier step) are loaded TWO steps ahead into alternating
+  // register sets: with one step of lookahead the ~600-cycle L2 latency of the next row
+  // was longer than a step's 24 MFMAs per wave (384 cycles) and every barrier waited for it.
+  // Step t = (chunk c_beg + t / 3, kernel row t % 3); set t & 1 holds step t's row.
+  bf16x8 ra[2][WCH], rh[HCH];
+  const int nsteps = 3 * (c_end - c_beg);
+  auto load_step = [&](int t, bf16x8* dst) { load_w(c_beg + t / 3, t % 3, dst); };
   if (c_beg < c_end) {
     load_halo(c_beg, rh);
-    load_w(c_beg, 0, ra);
+    load_step(0, ra[0]);
+    if (nsteps > 1) load_step(1, ra[1]);
     store_halo(0, rh, c_beg);
-    store_w(0, ra);
+    store_w(0, ra[0]);
   }
   __syncthreads();
-  int step = 0;
-  for (int ch = c_beg; ch < c_end; ++ch) {
+  auto body = [&](int t, const int u) {  // u = t & 1 (a constant in each unrolled half)
+    const int ch = c_beg + t / 3, kh = t - (t / 3) * 3;
     const int hb = (ch - c_beg) & 1;
     const bool next_chunk = ch + 1 < c_end;
-    for (int kh = 0; kh < 3; ++kh, ++step) {  // one kernel row (3 taps) per barrier
-      const int cur = step & 1;
-      const bool last = kh == 2;
-      const bool more = !last || next_chunk;
-      if (more) load_w(last ? ch + 1 : ch, last ? 0 : kh + 1, ra);
-      if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
+    if (t + 2 < nsteps) load_step(t + 2, ra[u]);  // set u: step t's row is already in LDS
+    if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int toff = kh * HW2 + kw;
-        bf16x8 a[TCO], b[TPX];
+    for (int kw = 0; kw < 3; ++kw) {
+      const int toff = kh * HW2 + kw;
+      bf16x8 a[TCO], b[TPX];
 #pragma unroll
-        for (int i = 0; i < TCO; ++i)
-          a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(kw * BC + wco * (BC / 2) + 16 * i + col) * HL_RS + kofs]);
+      for (int i = 0; i < TCO; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(&sA[u][(kw * BC + wco * (BC / 2) + 16 * i + col) * HL_RS + kofs]);
 #pragma unroll
-        for (int j = 0; j < TPX; ++j)
-          b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
+      for (int j = 0; j < TPX; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
 #pragma unroll
-        for (int i = 0; i < TCO; ++i)
+      for (int i = 0; i < TCO; ++i)
 #pragma unroll
-          for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
-      }
-      if (last && next_chunk) store_halo(hb ^ 1, rh, ch + 1);  // buffer hb^1 was last read a chunk ago
-      if (more) store_w(cur ^ 1, ra);
-      __syncthreads();
+        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     }
+    if (kh == 2 && next_chunk) store_halo(hb ^ 1, rh, ch + 1);  // buffer hb^1 was last read a chunk ago
+    if (t + 1 < nsteps) store_w(u ^ 1, ra[u ^ 1]);                // step t + 1's row (loaded a step ago)
+    __syncthreads();
+  };
+  for (int t = 0; t < nsteps; t += 2) {
+    body(t, 0);
+    if (t + 1 < nsteps) body(t + 1, 1);
   }
 
   // ---- epilogue (block-local pixel p -> output row oh0 + p / W, column p % W)
@@ -244,7 +250,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
 __device__ __forceinline__ int dtrk_pos(int k4) { return k4 < 4 ? 8 * k4 : 8 * (k4 - 4) + 4; }
 
 template <int BC, int BP, bool MASK_X, bool PART>
-__global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
+__global__ __launch_bounds__(256, 2) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                                    const bf16_t* __restrict__ Wt,
                                                                    const bf16_t* __restrict__ Xact,
                                                                    bf16_t* __restrict__ dX,
@@ -331,48 +337,51 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, c
 #pragma unroll
     for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 ra[WCH], rh[HCH];
+  // weight rows two steps ahead in alternating register sets (see the forward kernel)
+  bf16x8 ra[2][WCH], rh[HCH];
+  const int nsteps = 3 * (c_end - c_beg);
+  auto load_step = [&](int t, bf16x8* dst) { load_w(c_beg + t / 3, t % 3, dst); };
   if (c_beg < c_end) {
     load_halo(c_beg, rh);
-    load_w(c_beg, 0, ra);
+    load_step(0, ra[0]);
+    if (nsteps > 1) load_step(1, ra[1]);
     store_halo(0, rh);
-    store_w(0, ra);
+    store_w(0, ra[0]);
   }
   __syncthreads();
-  int step = 0;
-  for (int ch = c_beg; ch < c_end; ++ch) {
+  auto body = [&](int t, const int u) {  // u = t & 1 (a constant in each unrolled half)
+    const int ch = c_beg + t / 3, kh = t - (t / 3) * 3;
     const int hb = (ch - c_beg) & 1;
     const bool next_chunk = ch + 1 < c_end;
-    for (int kh = 0; kh < 3; ++kh, ++step) {
-      const int cur = step & 1;
-      const bool last = kh == 2;
-      const bool more = !last || next_chunk;
-      if (more) load_w(last ? ch + 1 : ch, last ? 0 : kh + 1, ra);
-      if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
+    if (t + 2 < nsteps) load_step(t + 2, ra[u]);
+    if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int toff = (2 - kh) * HW2 + (2 - kw);  // flipped tap
-        const bf16_t* wa = &sA[cur][kw * HL_KS * AS];
-        bf16x8 a[TCI], b[TPX];
+    for (int kw = 0; kw < 3; ++kw) {
+      const int toff = (2 - kh) * HW2 + (2 - kw);  // flipped tap
+      const bf16_t* wa = &sA[u][kw * HL_KS * AS];
+      bf16x8 a[TCI], b[TPX];
 #pragma unroll
-        for (int i = 0; i < TCI; ++i) {
-          const int m = wci * (BC / 2) + 16 * i + 4 * pq;
-          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(4 * gq + q) * AS + m]);
-          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(16 + 4 * gq + q) * AS + m]);
-          a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-#pragma unroll
-        for (int j = 0; j < TPX; ++j)
-          b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
-#pragma unroll
-        for (int i = 0; i < TCI; ++i)
-#pragma unroll
-          for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      for (int i = 0; i < TCI; ++i) {
+        const int m = wci * (BC / 2) + 16 * i + 4 * pq;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(4 * gq + q) * AS + m]);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(16 + 4 * gq + q) * AS + m]);
+        a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-      if (last && next_chunk) store_halo(hb ^ 1, rh);
-      if (more) store_w(cur ^ 1, ra);
-      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < TPX; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
+#pragma unroll
+      for (int i = 0; i < TCI; ++i)
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
     }
+    if (kh == 2 && next_chunk) store_halo(hb ^ 1, rh);
+    if (t + 1 < nsteps) store_w(u ^ 1, ra[u ^ 1]);
+    __syncthreads();
+  };
+  for (int t = 0; t < nsteps; t += 2) {
+    body(t, 0);
+    if (t + 1 < nsteps) body(t + 1, 1);
   }
 
   const long Ptot = (long)g.N * H * W;
@@ -494,14 +503,18 @@ size_t conv_halo_wgrad_lds() {
 // AFF: X is the producer conv's RAW output; the staging applies its BatchNorm + ReLU
 // (BnAffine) to the in-image halo positions - each thread's 8 input channels are fixed
 // (chunk c % (CIT / 8) == tid % (CIT / 8)), so its sc / sh are computed once.
-template <int CIT, bool AFF = false>
-__global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
+// WP: W rounded up to 8 (8 / 16 / 32 / 56 - ResNet-18's 7 / 14 / 28 / 56-wide layers), a
+// template constant so the slot -> (row, column) divisions and the tap offsets fold away
+// (one block per CU: the planner launches ~256 blocks, one per CU, so the register budget
+// is a whole SIMD's 512 - the pipelined K-steps below need ~270)
+template <int CIT, bool AFF, int WP>
+__global__ __launch_bounds__(256, 1) void conv3x3s1_halo_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                                       const bf16_t* __restrict__ X,
                                                                       float* __restrict__ out, int rows_per_chunk,
                                                                       int accum, BnAffine bn) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = g.H, W = g.W, Cin = g.Cin, Cout = g.Cout;
-  const int Wp = hwg_wp(W), R = HWG_SLOTS / Wp, XW = Wp + 2;
+  constexpr int Wp = WP, R = HWG_SLOTS / Wp, XW = Wp + 2;
   // segment = rows sharing one halo: a group of R rows of one image, or nimg stacked images
   const int Hs = H < R ? H : R, nimg = R / Hs, live = nimg * Hs;
   constexpr int XCP = CIT / 8, HWG_XC = hwg_xc<CIT>();        // 16-byte chunks per position / thread
@@ -521,13 +534,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
   // runtime Wp / XW / Hs + 2 were ~1.5k VALU instructions per group when done in load()):
   // dY chunk u -> packed (slot row rr | column col << 8); X chunk u -> packed (segment k |
   // halo row loc << 8 | halo column cc << 16 | channel chunk << 24), 0xff in k = past the halo
-  unsigned dgeo[HWG_DYC], xgeo[HWG_XC];
-#pragma unroll
-  for (int u = 0; u < HWG_DYC; ++u) {
-    const int slot = (tid + 256 * u) >> 3;
-    const int rr = slot / Wp;
-    dgeo[u] = (unsigned)rr | (unsigned)(slot - rr * Wp) << 8;
-  }
+  // (the dY chunk geometry is recomputed in load(): Wp is a constant, the divisions are
+  // multiplies - 7 VGPRs fewer across the MFMA loop)
+  unsigned xgeo[HWG_XC];
 #pragma unroll
   for (int u = 0; u < HWG_XC; ++u) {
     const int c = tid + 256 * u;
@@ -545,7 +554,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
     if constexpr (AFF) xin = 0;
 #pragma unroll
     for (int u = 0; u < HWG_DYC; ++u) {
-      const int rr = dgeo[u] & 0xff, col = dgeo[u] >> 8, ch = ((tid + 256 * u) & 7) * 8;
+      const int slot = (tid + 256 * u) >> 3;
+      const int rr = slot / Wp, col = slot - (slot / Wp) * Wp, ch = ((tid + 256 * u) & 7) * 8;
       vd[u] = (rr < cnt && col < W) ? ld8(dY + ((long)(r + rr) * W + col) * Cout + co0 + ch) : zero8();
     }
 #pragma unroll
@@ -587,6 +597,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
     for (int t = 0; t < 9; ++t) acc[c][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   lds_char* lsm = (lds_char*)smem;
   const int ldsX = HWG_SLOTS * HWG_DS;  // element offset of sX
+  // LDS operand offsets of the group's 7 K-steps - the same for every group, so computed
+  // once (the runtime divisions by Wp / Hs per K-step were a VALU chain in front of every
+  // step's LDS reads; at one wave per SIMD nothing hid it: ~576 cycles per 288-cycle step).
+  // The K-step loop is then fully unrolled so the next step's reads issue under this step's
+  // MFMAs.  Each accumulator still sees its K slots in the same order (bitwise unchanged).
+  constexpr int NKS = HWG_SLOTS / 32;
+  const int aA = (4 * gq + q) * HWG_DS + coT + 4 * p;  // + 32 * ks * HWG_DS (+ 16 rows: sB)
+  // halo position of K slot sl (Wp a constant: the divisions are multiplies): slot row r
+  // -> halo row r + 2 per preceding segment; rows past the live ones (dY 0) are clamped
+  // onto staged halo rows
+  auto xo = [&](int sl) {
+    const int r0 = min(sl / Wp, live - 1), c0 = sl - (sl / Wp) * Wp;
+    return ldsX + ((r0 + 2 * (r0 / Hs)) * XW + c0) * HWG_XS + ciT + 4 * p;
+  };
+  const int sL = 4 * gq + q;  // this lane's first K row of a step
   int r0 = rbeg, cnt = r0 < rend ? group_rows(r0) : 0;
   if (cnt > 0) load(r0, cnt);
   // (after the first group's loads are in flight: the parameters land behind them)
@@ -597,32 +622,57 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_wgrad_kernel(ConvGeom g
     const int r1 = r0 + cnt;
     const int cnt1 = r1 < rend ? group_rows(r1) : 0;
     if (cnt1 > 0) load(r1, cnt1);  // lands while this group's MFMAs run
-#pragma unroll 1
-    for (int s0 = 0; s0 < HWG_SLOTS; s0 += 32) {
-      const int sA = s0 + 4 * gq + q, sB = s0 + 16 + 4 * gq + q;  // this lane's K rows
-      bf16x8 a[NCT];
+    // step ks + 1's operand reads are issued under step ks's MFMAs: the a fragments double
+    // buffered, each tap's b fragment re-read for the next step right after its two MFMAs
+    bf16x8 a[2][NCT], b[9];
+    auto rd_a = [&](int ks, int u) {
 #pragma unroll
       for (int c = 0; c < NCT; ++c) {
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, sA * HWG_DS + coT + 16 * c + 4 * p));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, sB * HWG_DS + coT + 16 * c + 4 * p));
-        a[c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const int ao = aA + 32 * ks * HWG_DS + 16 * c;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, ao));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, ao + 16 * HWG_DS));
+        a[u][c] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-      // halo row of slot row r: r + 2 per preceding segment; rows past the live ones (dY 0)
-      // are clamped onto staged halo rows
-      const int rA0 = min(sA / Wp, live - 1), cA = sA - (sA / Wp) * Wp;
-      const int rB0 = min(sB / Wp, live - 1), cB = sB - (sB / Wp) * Wp;
-      const int rA = rA0 + 2 * (rA0 / Hs), rB = rB0 + 2 * (rB0 / Hs);
-      const int xA = ldsX + (rA * XW + cA) * HWG_XS + ciT + 4 * p;
-      const int xB = ldsX + (rB * XW + cB) * HWG_XS + ciT + 4 * p;
+    };
+    int xa = 0, xb = 0;  // the step's two halo offsets (recomputed per step: a few VALU under the MFMAs)
+    auto rd_b = [&](int tap) {
+      const int to = ((tap / 3) * XW + tap % 3) * HWG_XS;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xa + to));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xb + to));
+      b[tap] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    auto set_x = [&](int ks) {
+      xa = xo(32 * ks + sL);
+      xb = xo(32 * ks + sL + 16);
+    };
+    rd_a(0, 0);
+    set_x(0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) rd_b(tap);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int u = ks & 1;
+      if (ks + 1 < NKS) {
+        rd_a(ks + 1, u ^ 1);
+        set_x(ks + 1);
+      }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int to = ((tap / 3) * XW + tap % 3) * HWG_XS;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xA + to));
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(lds_ptr4(lsm, xB + to));
-        const bf16x8 b = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int c = 0; c < NCT; ++c) acc[c][tap] = mfma16(a[c], b, acc[c][tap]);
+        for (int c = 0; c < NCT; ++c) acc[c][tap] = mfma16(a[u][c], b[tap], acc[c][tap]);
+        if (ks + 1 < NKS) rd_b(tap);
       }
+      if (ks + 1 < NKS) {
+        // issue order: the next a reads, then per tap its MFMAs and the next b reads (left
+        // alone the scheduler hoisted all reads and kept two b sets live: spills)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NCT, 0);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NCT, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // no further hoisting of reads (registers)
     }
     __syncthreads();  // every wave is done with this group's tiles
     r0 = r1;
@@ -665,22 +715,30 @@ void conv_halo_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float
   const int chunks = (g.N * g.H + rows_per_chunk - 1) / rows_per_chunk;
   const dim3 grid(g.Cout / 64, g.Cin / cit, chunks);
   const size_t lds = conv_halo_wgrad_lds();
-  static bool opted = false;
-  if (!opted) {
-    for (const void* k : {reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<32, false>),
-                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<16, false>),
-                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<32, true>),
-                          reinterpret_cast<const void*>(conv3x3s1_halo_wgrad_kernel<16, true>)})
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    opted = true;
-  }
+  const int wp = hwg_wp(g.W);
+  if (wp != 8 && wp != 16 && wp != 32 && wp != 56) throw std::runtime_error("conv_halo_wgrad: W outside 7..56");
   const int acc = accum && chunks == 1 ? 1 : 0;
-  if (cit == 16)
-    { if (af) hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<16, true>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a);
-      else hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<16, false>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a); }
-  else
-    { if (af) hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<32, true>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a);
-      else hipLaunchKernelGGL((conv3x3s1_halo_wgrad_kernel<32, false>), grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a); }
+#define HWG_L(CIT, AF, WPV)                                                                                       \
+  do {                                                                                                           \
+    auto k = conv3x3s1_halo_wgrad_kernel<CIT, AF, WPV>;                                                          \
+    static bool opted = false;                                                                                   \
+    if (!opted) {                                                                                                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+      opted = true;                                                                                              \
+    }                                                                                                            \
+    hipLaunchKernelGGL(k, grid, dim3(256), lds, s, g, dY, X, out, rows_per_chunk, acc, a);                      \
+  } while (0)
+#define HWG_W(CIT, AF)                       \
+  do {                                       \
+    if (wp == 8) HWG_L(CIT, AF, 8);          \
+    else if (wp == 16) HWG_L(CIT, AF, 16);   \
+    else if (wp == 32) HWG_L(CIT, AF, 32);   \
+    else HWG_L(CIT, AF, 56);                 \
+  } while (0)
+  if (cit == 16) { if (af) HWG_W(16, true); else HWG_W(16, false); }
+  else { if (af) HWG_W(32, true); else HWG_W(32, false); }
+#undef HWG_W
+#undef HWG_L
 }
 
 }  // namespace ddp_amd

@@ -29,7 +29,6 @@ by the reducing kernel when allowed (:mod:`.direct_grad`), otherwise returned.
 """
 from __future__ import annotations
 
-import contextlib
 import os
 
 import torch
@@ -53,39 +52,9 @@ MASK_FROM_Y = os.environ.get("DDP_AMD_BN_MASK_FROM_Y", "1") != "0"
 # weight gradient; DDP_AMD_DEFER_BN=0 materialises them.  Needs MASK_FROM_Y (the output is
 # never stored).
 DEFER_BN = os.environ.get("DDP_AMD_DEFER_BN", "1") != "0" and MASK_FROM_Y
-# Weight gradients on a side stream (opt-in A/B knob DDP_AMD_WGRAD_STREAM=1): a conv's
-# wgrad (+ its split-K reduction) only feeds the optimizer, so it can run beside the
-# critical chain (BatchNorm backward -> data gradient -> the next layer down) instead of in
-# it.  Single process with direct gradients only (no bucket all-reduce may read a gradient
-# the side stream is still writing); the side stream forks from the current stream per
-# layer and is joined by join_side_streams() - FusedSGD.step() calls it - which also
-# releases the tensors kept alive for it.
-WGRAD_STREAM = os.environ.get("DDP_AMD_WGRAD_STREAM", "0") == "1"
-_side: dict = {}  # device index -> {"stream", "keep"}
-
-
-def _side_stream_ok(gw) -> bool:
-    if not WGRAD_STREAM or gw is None:
-        return False
-    import torch.distributed as dist
-
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
-
-
-def _side_state(dev):
-    st = _side.get(dev.index)
-    if st is None:
-        st = _side[dev.index] = {"stream": torch.cuda.Stream(device=dev), "keep": []}
-    return st
-
-
-def join_side_streams():
-    """Make each device's current stream wait for its weight-gradient side stream (no-op
-    when nothing ran there since the last join)."""
-    for idx, st in _side.items():
-        if st["keep"]:
-            torch.cuda.current_stream(idx).wait_stream(st["stream"])
-            st["keep"].clear()
+# (Weight gradients on a side stream - graph branches do overlap here, scripts/
+# graph_branch_probe.py - measured 5 % slower over 1000 steps: the side-stream wgrad
+# kernels share the CUs with the critical chain's own; profiles/r4_resnet/halo_pipe.)
 
 
 _configured = False
@@ -259,19 +228,12 @@ class _ConvBNAct(torch.autograd.Function):
         chunks = C.conv_gemm_wgrad_chunks(x, dy, KH, KW, stride, pad, ppc)
         row = w.numel()
         dw = gw if gw is not None else torch.empty(w.shape, device=dev)
-        side = _side_state(dev) if _side_stream_ok(gw) else None
-        if side is not None:
-            side["stream"].wait_stream(torch.cuda.current_stream(dev))
-            side["keep"] += [dy, x] + ([v for v in ctx.xbn if torch.is_tensor(v)] if ctx.xbn else [])
-        with torch.cuda.stream(side["stream"]) if side is not None else contextlib.nullcontext():
-            if chunks == 1:
-                C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, gw is not None, bn=ctx.xbn)
-            else:
-                slab = torch.empty(chunks, row, device=dev)
-                C.conv_gemm_wgrad(dy, x, slab, KH, KW, stride, pad, ppc, False, bn=ctx.xbn)
-                C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, gw is not None)])
-                if side is not None:
-                    side["keep"].append(slab)
+        if chunks == 1:
+            C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, gw is not None, bn=ctx.xbn)
+        else:
+            slab = torch.empty(chunks, row, device=dev)
+            C.conv_gemm_wgrad(dy, x, slab, KH, KW, stride, pad, ppc, False, bn=ctx.xbn)
+            C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, gw is not None)])
         rw = None if gw is not None else dw
         rg, rb = (None, None) if direct_bn else (dgamma, dbeta)
         if ctx.stash is not None:  # residual branch: hand the block-input gradient over

@@ -53,10 +53,6 @@ class FusedSGD:
     def step(self):
         g = self.param_groups[0]
         fs = self.flat
-        if fs.params.is_cuda:
-            from .resnet_fn import join_side_streams
-
-            join_side_streams()  # weight gradients still running on a side stream (opt-in)
         fs.reattach_grads()
         first = self.momentum_buffer is None
         if g["momentum"] != 0 and first:

@@ -705,52 +705,6 @@ def test_graphed_step_equals_eager():
         assert torch.equal(be, bf), n
 
 
-def test_wgrad_side_stream_bitwise(monkeypatch):
-    """Weight gradients on a side stream (resnet_fn.WGRAD_STREAM, joined by FusedSGD.step):
-    eager and graphed training steps give bit-identical parameters and buffers to the
-    single-stream steps."""
-    from ddp_amd.engine import GraphedStep
-    from ddp_amd.models import resnet18
-    from ddp_amd.ops import CrossEntropyLoss, FusedSGD, resnet_fn
-
-    xs = [torch.randn(4, 3, 64, 64, device=dev) for _ in range(2)]
-    ys = [torch.randint(0, 10, (4,), device=dev) for _ in range(2)]
-    torch.manual_seed(0)
-    base = resnet18(num_classes=10).to(dev)
-    order = [0, 0, 1, 0, 1]  # graphed: 2 warm-up steps on its static input (xs[0]), then replays
-    out = []
-    for side, graphed in ((False, False), (True, False), (True, True)):
-        monkeypatch.setattr(resnet_fn, "WGRAD_STREAM", side)
-        m = resnet18(num_classes=10).to(dev)
-        m.load_state_dict(base.state_dict())
-        opt = FusedSGD(m, lr=0.05, momentum=0.9, weight_decay=1e-4)
-        lossf = CrossEntropyLoss()
-
-        def step(x, y):
-            opt.zero_grad()
-            loss = lossf(m(x), y)
-            loss.backward()
-            opt.step()
-            return loss
-        if graphed:
-            g = GraphedStep(step, (xs[0], ys[0]), warmup=2)
-            for i in order[2:]:
-                loss = g(xs[i], ys[i])
-        else:
-            for i in order:
-                loss = step(xs[i], ys[i])
-        torch.cuda.synchronize()
-        assert not any(st["keep"] for st in resnet_fn._side.values())
-        out.append((loss.detach().clone(), [p.detach().clone() for p in m.parameters()],
-                    [b.clone() for b in m.buffers()]))
-    for o in out[1:]:
-        assert torch.equal(out[0][0], o[0])
-        for a, b in zip(out[0][1], o[1]):
-            assert torch.equal(a, b)
-        for a, b in zip(out[0][2], o[2]):
-            assert torch.equal(a, b)
-
-
 def test_image_gather_nhwc4_matches_cpu_pipeline():
     from ddp_amd.data import DeviceImages, synthetic_imagenet
 
