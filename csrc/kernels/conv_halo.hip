@@ -32,7 +32,7 @@ constexpr int HL_MAXPX = 232;     // largest halo: (R+2) x (W+2) = 4 x 58 at W =
 // (BnAffine, bitwise bn_apply's value; the zero padding stays zero) - the producer's
 // bn_apply pass disappears.  The per-channel sc / sh table sits in LDS (4 KB).
 template <int BC, int BP, bool STATS, bool PART, bool AFF = false>
-__global__ __launch_bounds__(256, 2) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
+__global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ Wt,
                                                                  bf16_t* __restrict__ Y,
                                                                  float* __restrict__ stats,
@@ -132,49 +132,43 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_fwd_kernel(ConvGeom g, 
 #pragma unroll
     for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // Weights (one kernel row per barrier step) are loaded TWO steps ahead into alternating
-  // register sets: with one step of lookahead the ~600-cycle L2 latency of the next row
-  // was longer than a step's 24 MFMAs per wave (384 cycles) and every barrier waited for it.
-  // Step t = (chunk c_beg + t / 3, kernel row t % 3); set t & 1 holds step t's row.
-  bf16x8 ra[2][WCH], rh[HCH];
-  const int nsteps = 3 * (c_end - c_beg);
-  auto load_step = [&](int t, bf16x8* dst) { load_w(c_beg + t / 3, t % 3, dst); };
+  bf16x8 ra[WCH], rh[HCH];
   if (c_beg < c_end) {
     load_halo(c_beg, rh);
-    load_step(0, ra[0]);
-    if (nsteps > 1) load_step(1, ra[1]);
+    load_w(c_beg, 0, ra);
     store_halo(0, rh, c_beg);
-    store_w(0, ra[0]);
+    store_w(0, ra);
   }
   __syncthreads();
-  auto body = [&](int t, const int u) {  // u = t & 1 (a constant in each unrolled half)
-    const int ch = c_beg + t / 3, kh = t - (t / 3) * 3;
+  int step = 0;
+  for (int ch = c_beg; ch < c_end; ++ch) {
     const int hb = (ch - c_beg) & 1;
     const bool next_chunk = ch + 1 < c_end;
-    if (t + 2 < nsteps) load_step(t + 2, ra[u]);  // set u: step t's row is already in LDS
-    if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
+    for (int kh = 0; kh < 3; ++kh, ++step) {  // one kernel row (3 taps) per barrier
+      const int cur = step & 1;
+      const bool last = kh == 2;
+      const bool more = !last || next_chunk;
+      if (more) load_w(last ? ch + 1 : ch, last ? 0 : kh + 1, ra);
+      if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int toff = kh * HW2 + kw;
-      bf16x8 a[TCO], b[TPX];
+      for (int kw = 0; kw < 3; ++kw) {
+        const int toff = kh * HW2 + kw;
+        bf16x8 a[TCO], b[TPX];
 #pragma unroll
-      for (int i = 0; i < TCO; ++i)
-        a[i] = *reinterpret_cast<const bf16x8*>(&sA[u][(kw * BC + wco * (BC / 2) + 16 * i + col) * HL_RS + kofs]);
+        for (int i = 0; i < TCO; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(&sA[cur][(kw * BC + wco * (BC / 2) + 16 * i + col) * HL_RS + kofs]);
 #pragma unroll
-      for (int j = 0; j < TPX; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
+        for (int j = 0; j < TPX; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
 #pragma unroll
-      for (int i = 0; i < TCO; ++i)
+        for (int i = 0; i < TCO; ++i)
 #pragma unroll
-        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+          for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      }
+      if (last && next_chunk) store_halo(hb ^ 1, rh, ch + 1);  // buffer hb^1 was last read a chunk ago
+      if (more) store_w(cur ^ 1, ra);
+      __syncthreads();
     }
-    if (kh == 2 && next_chunk) store_halo(hb ^ 1, rh, ch + 1);  // buffer hb^1 was last read a chunk ago
-    if (t + 1 < nsteps) store_w(u ^ 1, ra[u ^ 1]);                // step t + 1's row (loaded a step ago)
-    __syncthreads();
-  };
-  for (int t = 0; t < nsteps; t += 2) {
-    body(t, 0);
-    if (t + 1 < nsteps) body(t + 1, 1);
   }
 
   // ---- epilogue (block-local pixel p -> output row oh0 + p / W, column p % W)
@@ -250,7 +244,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_fwd_kernel(ConvGeom g, 
 __device__ __forceinline__ int dtrk_pos(int k4) { return k4 < 4 ? 8 * k4 : 8 * (k4 - 4) + 4; }
 
 template <int BC, int BP, bool MASK_X, bool PART>
-__global__ __launch_bounds__(256, 2) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
+__global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                                    const bf16_t* __restrict__ Wt,
                                                                    const bf16_t* __restrict__ Xact,
                                                                    bf16_t* __restrict__ dX,
@@ -337,51 +331,48 @@ __global__ __launch_bounds__(256, 2) void conv3x3s1_halo_dgrad_kernel(ConvGeom g
 #pragma unroll
     for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // weight rows two steps ahead in alternating register sets (see the forward kernel)
-  bf16x8 ra[2][WCH], rh[HCH];
-  const int nsteps = 3 * (c_end - c_beg);
-  auto load_step = [&](int t, bf16x8* dst) { load_w(c_beg + t / 3, t % 3, dst); };
+  bf16x8 ra[WCH], rh[HCH];
   if (c_beg < c_end) {
     load_halo(c_beg, rh);
-    load_step(0, ra[0]);
-    if (nsteps > 1) load_step(1, ra[1]);
+    load_w(c_beg, 0, ra);
     store_halo(0, rh);
-    store_w(0, ra[0]);
+    store_w(0, ra);
   }
   __syncthreads();
-  auto body = [&](int t, const int u) {  // u = t & 1 (a constant in each unrolled half)
-    const int ch = c_beg + t / 3, kh = t - (t / 3) * 3;
+  int step = 0;
+  for (int ch = c_beg; ch < c_end; ++ch) {
     const int hb = (ch - c_beg) & 1;
     const bool next_chunk = ch + 1 < c_end;
-    if (t + 2 < nsteps) load_step(t + 2, ra[u]);
-    if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
+    for (int kh = 0; kh < 3; ++kh, ++step) {
+      const int cur = step & 1;
+      const bool last = kh == 2;
+      const bool more = !last || next_chunk;
+      if (more) load_w(last ? ch + 1 : ch, last ? 0 : kh + 1, ra);
+      if (kh == 0 && next_chunk) load_halo(ch + 1, rh);
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int toff = (2 - kh) * HW2 + (2 - kw);  // flipped tap
-      const bf16_t* wa = &sA[u][kw * HL_KS * AS];
-      bf16x8 a[TCI], b[TPX];
+      for (int kw = 0; kw < 3; ++kw) {
+        const int toff = (2 - kh) * HW2 + (2 - kw);  // flipped tap
+        const bf16_t* wa = &sA[cur][kw * HL_KS * AS];
+        bf16x8 a[TCI], b[TPX];
 #pragma unroll
-      for (int i = 0; i < TCI; ++i) {
-        const int m = wci * (BC / 2) + 16 * i + 4 * pq;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(4 * gq + q) * AS + m]);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(16 + 4 * gq + q) * AS + m]);
-        a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        for (int i = 0; i < TCI; ++i) {
+          const int m = wci * (BC / 2) + 16 * i + 4 * pq;
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(4 * gq + q) * AS + m]);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)&wa[(16 + 4 * gq + q) * AS + m]);
+          a[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < TPX; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
+#pragma unroll
+        for (int i = 0; i < TCI; ++i)
+#pragma unroll
+          for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
       }
-#pragma unroll
-      for (int j = 0; j < TPX; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(&sH[hb][(hbase[j] + toff) * HL_RS + kofs]);
-#pragma unroll
-      for (int i = 0; i < TCI; ++i)
-#pragma unroll
-        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+      if (last && next_chunk) store_halo(hb ^ 1, rh);
+      if (more) store_w(cur ^ 1, ra);
+      __syncthreads();
     }
-    if (kh == 2 && next_chunk) store_halo(hb ^ 1, rh);
-    if (t + 1 < nsteps) store_w(u ^ 1, ra[u ^ 1]);
-    __syncthreads();
-  };
-  for (int t = 0; t < nsteps; t += 2) {
-    body(t, 0);
-    if (t + 1 < nsteps) body(t + 1, 1);
   }
 
   const long Ptot = (long)g.N * H * W;
