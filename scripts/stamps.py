@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--wgrad_split", type=int, default=None)
     ap.add_argument("--wgrad_rows", type=int, default=None)
     ap.add_argument("--store_a1", type=int, default=None)
+    ap.add_argument("--fuse_reduce", type=int, default=None)
+    ap.add_argument("--pxt_fwd", type=int, default=None)
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -44,7 +46,7 @@ def main():
     eo = EngineOptions(use_graph=a.graph, graph_steps=10, dtype=a.dtype)
     if a.fuse_level is not None:
         eo.fuse_level = a.fuse_level
-    for f in ("wgrad_split", "wgrad_rows", "store_a1"):
+    for f in ("wgrad_split", "wgrad_rows", "store_a1", "fuse_reduce", "pxt_fwd"):
         if getattr(a, f) is not None:
             setattr(eo, f, getattr(a, f))
     eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, dev, "synthetic"),
