@@ -83,6 +83,10 @@ struct BwdReduce {
   // of both roles instead of a dgrad phase followed by a wgrad phase (the reducers are the
   // last nr blocks whatever their role).  Set by the launcher (also without FRED).
   int interleave = 0;
+  // 1: the slab set's largest segment has 128 < rows <= 256 (exact fp32, bf16 at B = 64):
+  // the reducers take 2 chunks per pass with all 16 rows per group in flight
+  // (slab_fused_run16); 0: 3 chunks per pass, 8 rows per group (slab_fused_run)
+  int deep = 0;
 };
 
 // Geometry specialisation: kernels take <GH, GW, GCI, GCO>; non-zero values replace
@@ -1261,34 +1265,53 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
     // wait for; the host keeps nr within a quarter of the resident capacity)
     const int nblk = red.nconv > 0 ? red.nconv : (int)gridDim.x;
     const int w = cb - red.first_reducer, nw = nblk - red.first_reducer;
-    constexpr int J = 3;  // chunks per reducer pass (thread t < 64 * J finalises one output of chunk t >> 6)
-    SlabFusedPlan<J> pl;
-    slab_fused_plan<J>(red.ss, w, nw, red.nchunks, pl);  // index work + SGD operands before the wait
-    DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
-    if (threadIdx.x < 64) {  // wave 0 polls the 8 shards (sc1 loads), sleeping between polls
-      const int lane = threadIdx.x;
-      const int want = nblk;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (true) {
-        const int v = lane < 8 ? __hip_atomic_load(red.done + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        int tot = 0;
+    // (a lambda capturing only scalars: capturing the kernel argument put the SlabSet in scratch)
+    int* const done = red.done;
+    int* const errw = red.err;
+    auto wait_all = [done, errw, nblk]() {
+      if (threadIdx.x < 64) {  // wave 0 polls the 8 shards (sc1 loads), sleeping between polls
+        const int lane = threadIdx.x;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (true) {
+          const int v = lane < 8 ? __hip_atomic_load(done + 32 * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+          int tot = 0;
 #pragma unroll
-        for (int l = 0; l < 8; ++l) tot += __builtin_amdgcn_readlane(v, l);
-        if (tot >= want) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > DZ_WAIT_TICKS) {
-          if (lane == 0 && red.err) __hip_atomic_store(red.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
+          for (int l = 0; l < 8; ++l) tot += __builtin_amdgcn_readlane(v, l);
+          if (tot >= nblk) break;
+          if (__builtin_amdgcn_s_memrealtime() - t0 > DZ_WAIT_TICKS) {
+            if (lane == 0 && errw) __hip_atomic_store(errw, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_s_sleep(2);
       }
-    }
-    __syncthreads();
-    DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
+      __syncthreads();
+    };
     float* part = reinterpret_cast<float*>(smem);
-    slab_fused_run<J>(red.ss, pl, part);
-    for (long q0 = w + (long)J * nw; q0 < red.nchunks; q0 += (long)J * nw) {  // few wgrad blocks: more passes
-      slab_fused_plan<J>(red.ss, q0, nw, red.nchunks, pl);
+    if (red.deep) {
+      constexpr int J = 2;  // chunks per reducer pass (thread t < 64 * J finalises one output of chunk t >> 6)
+      SlabFusedPlan<J> pl;
+      slab_fused_plan<J>(red.ss, w, nw, red.nchunks, pl);  // index work + SGD operands before the wait
+      DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
+      wait_all();
+      DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
+      slab_fused_run16<J>(red.ss, pl, part);
+      for (long q0 = w + (long)J * nw; q0 < red.nchunks; q0 += (long)J * nw) {  // few wgrad blocks: more passes
+        slab_fused_plan<J>(red.ss, q0, nw, red.nchunks, pl);
+        slab_fused_run16<J>(red.ss, pl, part);
+      }
+    } else {
+      constexpr int J = 3;
+      SlabFusedPlan<J> pl;
+      slab_fused_plan<J>(red.ss, w, nw, red.nchunks, pl);
+      DDP_STAMP(STAMP_K_GRAD_REDUCE, 0);
+      wait_all();
+      DDP_STAMP(STAMP_K_GRAD_REDUCE, 1);
       slab_fused_run<J>(red.ss, pl, part);
+      for (long q0 = w + (long)J * nw; q0 < red.nchunks; q0 += (long)J * nw) {
+        slab_fused_plan<J>(red.ss, q0, nw, red.nchunks, pl);
+        slab_fused_run<J>(red.ss, pl, part);
+      }
     }
     if (w == 0 && threadIdx.x == 0 && red.ss.step_ctr) red.ss.step_ctr[0] += 1;
     DDP_STAMP(STAMP_K_GRAD_REDUCE, 2);
@@ -1720,6 +1743,14 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   if (fused) {
     red.ss = *fused;
     red.nchunks = slab_chunks(*fused);
+    {  // the largest segment's row count picks the reducer's load depth
+      int kmax = 0;
+      for (int k = 1; k < fused->count; ++k)
+        if (fused->s[k].n > fused->s[kmax].n) kmax = k;
+      const int rows = fused->s[kmax].rows;
+      const char* e = std::getenv("DDP_AMD_RED_DEEP");  // A/B knob: 0 forces the 8-row reducer
+      red.deep = (rows > 128 && rows <= 256 && !(e && e[0] == '0')) ? 1 : 0;
+    }
     red.done = red_done;
     red.err = red_err;
     if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");

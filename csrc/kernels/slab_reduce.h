@@ -231,11 +231,50 @@ __device__ __forceinline__ void slab_fused_plan(const SlabSet& ss, long q0, long
   }
 }
 
+// group sums acc (this thread's quad of group g) -> LDS -> the finalising threads combine
+// groups 0..15 in order, scale, store and apply the fused SGD
+template <int J>
+__device__ __forceinline__ void slab_fused_finish(const SlabSet& ss, const SlabFusedPlan<J>& pl, float* part,
+                                                  const float4* acc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cq = lane & 15, g = 4 * wave + (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < J; ++j) *reinterpret_cast<float4*>(part + (j * 16 + g) * 64 + 4 * cq) = acc[j];
+  __syncthreads();
+  DDP_STAMP(STAMP_K_GRAD_REDUCE, 4);  // group sums in LDS
+  // combine + epilogue: thread t < 64 * J finalises output t & 63 of chunk t >> 6
+  if (pl.own_live) {
+    const int j = wave, c = lane;
+    const long i = pl.own_i;
+    float gsum = part[(j * 16) * 64 + c];
+#pragma unroll
+    for (int qq = 1; qq < 16; ++qq) gsum += part[(j * 16 + qq) * 64 + c];
+    gsum *= pl.scale;
+    if (pl.accum) gsum += pl.dst[i];
+    if (ss.sys_store) st_sys(pl.dst + i, gsum);
+    else pl.dst[i] = gsum;
+    if (ss.sgd.update && pl.p) {
+      float m = pl.m0;
+      const float pn = sgd_one(pl.p0, gsum, &m, ss.sgd);
+      pl.p[i] = pn;
+      if (pl.m) pl.m[i] = m;
+      if (pl.shb) pl.shb[i] = f2bf(pn);
+      if (pl.sht || pl.sh32) {
+        const long per = (long)pl.t_taps * pl.t_ci;
+        const long co = i / per;
+        if (pl.sht) pl.sht[(i - co * per) * pl.t_co + co] = f2bf(pn);
+        if (pl.sh32) pl.sh32[(i - co * per) * pl.t_co + co] = pn;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // part: J * 16 * 64 floats of LDS.  Every thread of the block calls it.
 template <int J>
 __device__ __forceinline__ void slab_fused_run(const SlabSet& ss, const SlabFusedPlan<J>& pl, float* part) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int cq = lane & 15, g = 4 * wave + (lane >> 4);
+  const int g = 4 * wave + (lane >> 4);
   float4 a[J][8];
   // every chunk's first 8 rows per group in ONE straight-line block
 #pragma unroll
@@ -269,36 +308,50 @@ __device__ __forceinline__ void slab_fused_run(const SlabSet& ss, const SlabFuse
       acc[j] = t;
     }
   }
+  slab_fused_finish<J>(ss, pl, part, acc);
+}
+
+// Deep slab sets (128 < rows <= 256: the exact-fp32 step's 224 weight-gradient rows, bf16 at
+// B = 64: 256): all 16 rows of every group of the J chunks in flight at once.  The 8-row
+// variant above made one serial load round per further 128 rows and chunk - 1 + J rounds
+// after the arrival wait.  Same summation order (rows g, g + 16, ... sequentially).  Rows
+// past 256 (the fp32 w1 slab: one row per dgrad block) continue in serial 8-row rounds.
+template <int J>
+__device__ __forceinline__ void slab_fused_run16(const SlabSet& ss, const SlabFusedPlan<J>& pl, float* part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = 4 * wave + (lane >> 4);
+  float4 a[J][16];
 #pragma unroll
-  for (int j = 0; j < J; ++j) *reinterpret_cast<float4*>(part + (j * 16 + g) * 64 + 4 * cq) = acc[j];
-  __syncthreads();
-  DDP_STAMP(STAMP_K_GRAD_REDUCE, 4);  // group sums in LDS
-  // combine + epilogue: thread t < 64 * J finalises output t & 63 of chunk t >> 6
-  if (pl.own_live) {
-    const int j = wave, c = lane;
-    const long i = pl.own_i;
-    float gsum = part[(j * 16) * 64 + c];
+  for (int j = 0; j < J; ++j) {
+    const int rl = pl.rows[j] > 0 ? pl.rows[j] - 1 : 0;
 #pragma unroll
-    for (int qq = 1; qq < 16; ++qq) gsum += part[(j * 16 + qq) * 64 + c];
-    gsum *= pl.scale;
-    if (pl.accum) gsum += pl.dst[i];
-    if (ss.sys_store) st_sys(pl.dst + i, gsum);
-    else pl.dst[i] = gsum;
-    if (ss.sgd.update && pl.p) {
-      float m = pl.m0;
-      const float pn = sgd_one(pl.p0, gsum, &m, ss.sgd);
-      pl.p[i] = pn;
-      if (pl.m) pl.m[i] = m;
-      if (pl.shb) pl.shb[i] = f2bf(pn);
-      if (pl.sht || pl.sh32) {
-        const long per = (long)pl.t_taps * pl.t_ci;
-        const long co = i / per;
-        if (pl.sht) pl.sht[(i - co * per) * pl.t_co + co] = f2bf(pn);
-        if (pl.sh32) pl.sh32[(i - co * per) * pl.t_co + co] = pn;
+    for (int u = 0; u < 16; ++u) a[j][u] = slab_ld4_sc1(pl.base[j], pl.ic[j] + (long)min(g + 16 * u, rl) * pl.stride[j]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  DDP_STAMP(STAMP_K_GRAD_REDUCE, 3);  // loads issued
+  float4 acc[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) add4_if(acc[j], shift4(a[j][u], pl.sh[j]), g + 16 * u < pl.rows[j]);
+  }
+#pragma clang loop unroll(full)
+  for (int j = 0; j < J; ++j) {
+    if (pl.rows[j] > 16 * 16) {  // block-uniform
+      float4 t = acc[j];
+      for (int r0 = 16 * 16; r0 < pl.rows[j]; r0 += 8 * 16) {
+        float4 b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          b[u] = slab_ld4_sc1(pl.base[j], pl.ic[j] + (long)min(g + r0 + 16 * u, pl.rows[j] - 1) * pl.stride[j]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) add4_if(t, shift4(b[u], pl.sh[j]), g + r0 + 16 * u < pl.rows[j]);
       }
+      acc[j] = t;
     }
   }
-  __syncthreads();
+  slab_fused_finish<J>(ss, pl, part, acc);
 }
 
 // number of 64-output chunks of a SlabSet
