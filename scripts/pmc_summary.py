@@ -41,8 +41,9 @@ def main():
         d = sum(dur[name]) / len(dur[name])
         rows.append((d, name, avg))
     rows.sort(key=lambda t: -t[0] * len(dur[t[1]]))
-    print("| kernel | us/dispatch | MFMA TFLOP/s | LDS instr | LDS conflict cycles / instr | fetch GB/s | write GB/s |")
-    print("|---|---|---|---|---|---|---|")
+    print("| kernel | us/dispatch | MFMA TFLOP/s | LDS instr | LDS conflict cycles / instr | fetch GB/s | write GB/s "
+          "| VALU instr | MFMA instr | LDS-wait / wave cycles |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for d, name, c in rows[:a.top]:
         mf = c.get("SQ_INSTS_MFMA")
         tf = f"{mf * 16384 / (d * 1e-6) / 1e12:.0f}" if mf else "-"
@@ -50,8 +51,12 @@ def main():
         lc = f"{c['SQ_LDS_BANK_CONFLICT'] / li:.2f}" if li and "SQ_LDS_BANK_CONFLICT" in c else "-"
         fs = f"{c['FETCH_SIZE'] * 1024 / (d * 1e-6) / 1e9:.0f}" if "FETCH_SIZE" in c else "-"
         ws = f"{c['WRITE_SIZE'] * 1024 / (d * 1e-6) / 1e9:.0f}" if "WRITE_SIZE" in c else "-"
-        print(f"| `{name[:80]}` | {d:.1f} | {tf} | {li:.0f} | {lc} | {fs} | {ws} |" if li is not None else
-              f"| `{name[:80]}` | {d:.1f} | {tf} | - | {lc} | {fs} | {ws} |")
+        va = f"{c['SQ_INSTS_VALU']:.0f}" if "SQ_INSTS_VALU" in c else "-"
+        mi = f"{mf:.0f}" if mf else "-"
+        lw = (f"{c['SQ_WAIT_INST_LDS'] / c['SQ_WAVE_CYCLES']:.2f}"
+              if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_INST_LDS" in c else "-")
+        lis = f"{li:.0f}" if li is not None else "-"
+        print(f"| `{name[:80]}` | {d:.1f} | {tf} | {lis} | {lc} | {fs} | {ws} | {va} | {mi} | {lw} |")
 
 
 if __name__ == "__main__":
