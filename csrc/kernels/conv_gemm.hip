@@ -50,9 +50,26 @@ __device__ __forceinline__ int trk_pos(int k4) {  // LDS position of the 4-group
   return k4 < 4 ? 8 * k4 : 8 * (k4 - 4) + 4;
 }
 
+// Stem geometry as constants (SG = 1: ResNet-18's 7x7 / s2 / p3 stem on 224 x 224 inputs,
+// 112 x 112 outputs; SG = 0: runtime).  The stem kernels' per-K-step tap / pixel index math
+// was ~30 VALU instructions per MFMA with runtime divisors (profiles/r4_resnet/pmc).
+template <int SG>
+struct StemGeo {
+  static constexpr int KW = 0, S = 0, PAD = 0, H = 0, W = 0, OH = 0, OW = 0;
+};
+template <>
+struct StemGeo<1> {
+  static constexpr int KW = 7, S = 2, PAD = 3, H = 224, W = 224, OH = 112, OW = 112;
+};
+inline bool stem_geo_224(const ConvGeom& g) {
+  return g.Cin == 4 && g.KH == 7 && g.KW == 7 && g.stride == 2 && g.pad == 3 && g.H == 224 && g.W == 224 &&
+         g.OH == 112 && g.OW == 112;
+}
+#define SG_(f, rt) (StemGeo<SG>::f ? StemGeo<SG>::f : (rt))
+
 // STEM: Cin == 4 (3 real channels + 1 zero pad); a K-step covers 8 taps x 4 channels,
 // k = tap*4 + c, so the weight row [KH*KW*4] is still contiguous per K-step.
-template <int BP, int BC, bool RELU, bool STATS, bool STEM, bool PART>
+template <int BP, int BC, bool RELU, bool STATS, bool STEM, bool PART, int SG = 0>
 __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
                                                             const bf16_t* __restrict__ Wt,
                                                             const float* __restrict__ bias,
@@ -70,7 +87,7 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
   constexpr int TPR = 256 / BP;          // staging threads per pixel row
   constexpr int EPT = CG_KS / TPR;       // elements per thread (16 or 8)
   const int3 bk = xcd_block3();  // XCD-contiguous block order (pixel tiles share an L2)
-  const int OHW = g.OH * g.OW;
+  const int OWv = SG_(OW, g.OW), OHW = SG_(OH, g.OH) * OWv;
   const int Ptot = g.N * OHW;
   const int p0 = bk.x * BP;
   const int co0 = bk.y * BC;
@@ -87,8 +104,8 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
   if (pv) {
     n_ = P / OHW;
     const int r = P - n_ * OHW;
-    oh = r / g.OW;
-    ow = r - oh * g.OW;
+    oh = r / OWv;
+    ow = r - oh * OWv;
   }
   auto load_k = [&](int ks, bf16x8* ra, bf16x8* rb) {
     if (STEM) {
@@ -99,10 +116,11 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int tap = ks * 8 + bh / 4 + h2 * 2 + u;
-          const int kh = tap / g.KW, kw = tap - kh * g.KW;
-          const int ih = oh * g.stride - g.pad + kh, iw = ow * g.stride - g.pad + kw;
-          const bool ok = pv && tap < T && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-          two[u] = ok ? *reinterpret_cast<const uint2*>(X + (((long)n_ * g.H + ih) * g.W + iw) * 4)
+          const int KWv = SG_(KW, g.KW), Hv = SG_(H, g.H), Wv = SG_(W, g.W);
+          const int kh = tap / KWv, kw = tap - kh * KWv;
+          const int ih = oh * SG_(S, g.stride) - SG_(PAD, g.pad) + kh, iw = ow * SG_(S, g.stride) - SG_(PAD, g.pad) + kw;
+          const bool ok = pv && tap < T && (unsigned)ih < (unsigned)Hv && (unsigned)iw < (unsigned)Wv;
+          two[u] = ok ? *reinterpret_cast<const uint2*>(X + (((long)n_ * Hv + ih) * Wv + iw) * 4)
                       : make_uint2(0u, 0u);
         }
         uint4 q4 = make_uint4(two[0].x, two[0].y, two[1].x, two[1].y);
@@ -515,7 +533,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // K-along-lane MFMA fragments are read with the hardware transpose.
 // STEM (Cin == 4 in X, BN = 64): the block's 64 columns are 16 taps x 4 channels (tap
 // group blockIdx.y); the output keeps only the 3 real channels: [Cout][T][3].
-template <int BM, int BN, bool STEM, int KS>
+template <int BM, int BN, bool STEM, int KS, int SG = 0>  // SG: see StemGeo
 __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                               const bf16_t* __restrict__ X,
                                                               float* __restrict__ out, int px_per_chunk,
@@ -536,7 +554,7 @@ __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const 
   const int ci0 = STEM ? 0 : (bk.y - tap * (g.Cin / BN)) * BN;
   const int kh = tap / g.KW, kw = tap - kh * g.KW;
   const int tg0 = STEM ? bk.y * 16 : 0;  // first tap of this block (STEM)
-  const int OHW = g.OH * g.OW;
+  const int OWv = SG_(OW, g.OW), OHW = SG_(OH, g.OH) * OWv;
   const int Ptot = g.N * OHW;
   const int pbeg = bk.z * px_per_chunk;
   const int pend = min(Ptot, pbeg + px_per_chunk);
@@ -557,16 +575,17 @@ __global__ __launch_bounds__(256) void conv_gemm_wgrad_kernel(ConvGeom g, const 
       if (P < pend) {
         const int n_ = P / OHW;
         const int r = P - n_ * OHW;
-        const int oh = r / g.OW, ow = r - oh * g.OW;
+        const int oh = r / OWv, ow = r - oh * OWv;
         if (STEM) {
           uint2 two[2];
+          const int KWv = SG_(KW, g.KW), Hv = SG_(H, g.H), Wv = SG_(W, g.W);
 #pragma unroll
           for (int v = 0; v < 2; ++v) {
             const int t = tg0 + sc / 4 + v;
-            const int th = t / g.KW, tw = t - th * g.KW;
-            const int ih = oh * g.stride - g.pad + th, iw = ow * g.stride - g.pad + tw;
-            two[v] = (t < T && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-                         ? *reinterpret_cast<const uint2*>(X + (((long)n_ * g.H + ih) * g.W + iw) * 4)
+            const int th = t / KWv, tw = t - th * KWv;
+            const int ih = oh * SG_(S, g.stride) - SG_(PAD, g.pad) + th, iw = ow * SG_(S, g.stride) - SG_(PAD, g.pad) + tw;
+            two[v] = (t < T && (unsigned)ih < (unsigned)Hv && (unsigned)iw < (unsigned)Wv)
+                         ? *reinterpret_cast<const uint2*>(X + (((long)n_ * Hv + ih) * Wv + iw) * 4)
                          : make_uint2(0u, 0u);
           }
           vx[u] = __builtin_bit_cast(bf16x8, make_uint4(two[0].x, two[0].y, two[1].x, two[1].y));
@@ -827,9 +846,16 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
   const int kp = pl.ks_per;
   const BnFin f = (fin && pl.splits <= 1) ? *fin : BnFin{};
   if (g.Cin == 4) {  // stem: 8 taps x 4 channels per K-step (host enforces Cout % 64)
-    if (stats) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, false, true, true, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f);
-    else if (relu) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, true, false, true, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f);
-    else hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, false, false, true, false>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f);
+    const bool s224 = stem_geo_224(g);
+#define CGS(RL, ST)                                                                                                  \
+  do {                                                                                                               \
+    if (s224) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 1>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f); \
+    else hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 0>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f); \
+  } while (0)
+    if (stats) CGS(false, true);
+    else if (relu) CGS(true, false);
+    else CGS(false, false);
+#undef CGS
     return;
   }
 #define CGF(BP, BC, RL, ST, PT) hipLaunchKernelGGL((conv_gemm_fwd_kernel<BP, BC, RL, ST, false, PT>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f)
@@ -985,7 +1011,12 @@ void conv_gemm_wgrad(const ConvGeom& g, const bf16_t* dY, const bf16_t* X, float
   if (ks != 32 && ks != 64) ks = 32;
   if (g.Cin == 4) {
     const dim3 grid(g.Cout / bm, (g.KH * g.KW + 15) / 16, ch);
-#define CGWS(M, K) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, 64, true, K>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc)
+    const bool s224 = stem_geo_224(g);
+#define CGWS(M, K)                                                                                                   \
+  do {                                                                                                               \
+    if (s224) hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, 64, true, K, 1>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc); \
+    else hipLaunchKernelGGL((conv_gemm_wgrad_kernel<M, 64, true, K, 0>), grid, dim3(256), 0, s, g, dY, X, out, px_per_chunk, acc); \
+  } while (0)
     if (bm == 128) { if (ks == 64) CGWS(128, 64); else CGWS(128, 32); }
     else { if (ks == 64) CGWS(64, 64); else CGWS(64, 32); }
 #undef CGWS

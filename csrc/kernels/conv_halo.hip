@@ -31,7 +31,10 @@ constexpr int HL_MAXPX = 232;     // largest halo: (R+2) x (W+2) = 4 x 58 at W =
 // AFF: X is the producer conv's RAW output; the halo staging applies its BatchNorm + ReLU
 // (BnAffine, bitwise bn_apply's value; the zero padding stays zero) - the producer's
 // bn_apply pass disappears.  The per-channel sc / sh table sits in LDS (4 KB).
-template <int BC, int BP, bool STATS, bool PART, bool AFF = false>
+// GW: the image width as a template constant (56 / 28 / 14 for ResNet-18's layers; 0 =
+// runtime) - the halo index divisions and the tap offsets then fold (the per-dispatch SQ
+// counters showed ~10 VALU instructions per MFMA in this kernel, profiles/r4_resnet/pmc)
+template <int BC, int BP, bool STATS, bool PART, bool AFF = false, int GW = 0>
 __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
                                                                  const bf16_t* __restrict__ Wt,
                                                                  bf16_t* __restrict__ Y,
@@ -45,7 +48,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
   __shared__ __attribute__((aligned(16))) bf16_t sH[2][HL_MAXPX * HL_RS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wco = wave >> 1, wpx = wave & 1;
-  const int W = g.W, H = g.H, Cin = g.Cin;
+  const int W = GW ? GW : g.W, H = g.H, Cin = g.Cin;
   const int RG = (H + R - 1) / R;
   const int3 bk = xcd_block3();  // XCD-contiguous block order
   const int n_ = bk.x / RG, rg = bk.x - n_ * RG;
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
 // (dtrk_pos, as conv_gemm_dgrad_kernel does for its gathered tile).
 __device__ __forceinline__ int dtrk_pos(int k4) { return k4 < 4 ? 8 * k4 : 8 * (k4 - 4) + 4; }
 
-template <int BC, int BP, bool MASK_X, bool PART>
+template <int BC, int BP, bool MASK_X, bool PART, int GW = 0>  // GW: see the forward kernel
 __global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, const bf16_t* __restrict__ dY,
                                                                    const bf16_t* __restrict__ Wt,
                                                                    const bf16_t* __restrict__ Xact,
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_dgrad_kernel(ConvGeom g, c
   __shared__ __attribute__((aligned(16))) bf16_t sH[2][HL_MAXPX * HL_RS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wci = wave >> 1, wpx = wave & 1;
-  const int W = g.W, H = g.H, Cout = g.Cout;
+  const int W = GW ? GW : g.W, H = g.H, Cout = g.Cout;
   const int RG = (H + R - 1) / R;
   const int3 bk = xcd_block3();  // XCD-contiguous block order
   const int n_ = bk.x / RG, rg = bk.x - n_ * RG;
@@ -410,7 +413,16 @@ void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t
   const int nch = g.Cout / HL_KS;
   const int cps = (nch + splits - 1) / splits;
   const dim3 grid(g.N * RG, g.Cin / bc, splits);
-#define HLD(BC, BP, MX, PT) hipLaunchKernelGGL((conv3x3s1_halo_dgrad_kernel<BC, BP, MX, PT>), grid, dim3(256), 0, s, g, dY, Wt, Xact, dX, part, R, cps)
+  const int gw = g.W == 56 ? 56 : g.W == 28 ? 28 : g.W == 14 ? 14 : 0;  // (see conv_halo_fwd)
+#define HLD_W(BC, BP, MX, PT, GWV) \
+  hipLaunchKernelGGL((conv3x3s1_halo_dgrad_kernel<BC, BP, MX, PT, GWV>), grid, dim3(256), 0, s, g, dY, Wt, Xact, dX, part, R, cps)
+#define HLD(BC, BP, MX, PT)                                              \
+  do {                                                                   \
+    if (BC != 64 || gw == 0) HLD_W(BC, BP, MX, PT, 0);                   \
+    else if (gw == 56) HLD_W(BC, BP, MX, PT, (BC == 64 ? 56 : 0));       \
+    else if (gw == 28) HLD_W(BC, BP, MX, PT, (BC == 64 ? 28 : 0));       \
+    else HLD_W(BC, BP, MX, PT, (BC == 64 ? 14 : 0));                     \
+  } while (0)
 #define HLD_BP(BC, BP)                                  \
   if (splits > 1) HLD(BC, BP, false, true);             \
   else if (Xact) HLD(BC, BP, true, false);              \
@@ -419,6 +431,7 @@ void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t
   else { if (bc == 128) { HLD_BP(128, 64) } else { HLD_BP(64, 64) } }
 #undef HLD_BP
 #undef HLD
+#undef HLD_W
 }
 
 // bp: pixel columns of the block's MFMA tile (128 or 64); R = bp / W full rows per block
@@ -442,10 +455,19 @@ void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* 
   const int nch = g.Cin / HL_KS;
   const int cps = (nch + splits - 1) / splits;
   const dim3 grid(g.N * RG, g.Cout / bc, splits);
-#define HLF(BC, BP, ST, PT)                                                                                     \
+  // the 64-channel tiles ResNet-18's planner picks get a width-specialised build
+  const int gw = g.W == 56 ? 56 : g.W == 28 ? 28 : g.W == 14 ? 14 : 0;
+#define HLF_W(BC, BP, ST, PT, GWV)                                                                              \
   do {                                                                                                          \
-    if (af) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, true>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
-    else hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, false>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
+    if (af) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, true, GWV>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
+    else hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, false, GWV>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
+  } while (0)
+#define HLF(BC, BP, ST, PT)                                              \
+  do {                                                                   \
+    if (BC != 64 || gw == 0) HLF_W(BC, BP, ST, PT, 0);                   \
+    else if (gw == 56) HLF_W(BC, BP, ST, PT, (BC == 64 ? 56 : 0));       \
+    else if (gw == 28) HLF_W(BC, BP, ST, PT, (BC == 64 ? 28 : 0));       \
+    else HLF_W(BC, BP, ST, PT, (BC == 64 ? 14 : 0));                     \
   } while (0)
 #define HLF_BP(BC, BP)                                  \
   if (splits > 1) HLF(BC, BP, false, true);             \
@@ -455,6 +477,7 @@ void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* 
   else { if (bc == 128) { HLF_BP(128, 64) } else { HLF_BP(64, 64) } }
 #undef HLF_BP
 #undef HLF
+#undef HLF_W
 }
 
 

@@ -184,12 +184,12 @@ def test_conv_halo_wgrad(C, N, H, Cin, Cout, rpc, cit):
         C.conv_gemm_wgrad_set_halo(1)
 
 
-def test_stem_conv_7x7_s2():
+@pytest.mark.parametrize("N,H", [(2, 32), (1, 224)])  # 224: the constant-geometry stem kernels (StemGeo<1>)
+def test_stem_conv_7x7_s2(N, H):
     from ddp_amd import native
     from ddp_amd.ops.resnet_fn import to_nhwc4
 
     C = native.require()
-    N, H = 2, 32
     img = torch.randn(N, 3, H, H, device=dev)
     x4 = to_nhwc4(img)
     w3 = torch.randn(64, 7, 7, 3) * 0.05
