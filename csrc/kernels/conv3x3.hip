@@ -359,11 +359,16 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
       if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
       float q[4] = {v0, v1, v2, v3};  // the values actually stored (what backward re-reads)
       if constexpr (F32) {
-        if (valid[pt]) st_wt(reinterpret_cast<float4*>(Y + Pp[pt] * Cout + co), make_float4(v0, v1, v2, v3));
+        // (DZ: stored after the partial logits are published - see the dZ2 section)
+        if constexpr (!DZ) {
+          if (valid[pt]) st_wt(reinterpret_cast<float4*>(Y + Pp[pt] * Cout + co), make_float4(v0, v1, v2, v3));
+        }
         if constexpr (DZ) a2q[pt][t] = make_float4(v0, v1, v2, v3);
       } else {
         const uint2 pk = pack4(v0, v1, v2, v3);
-        if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
+        if constexpr (!DZ) {
+          if (valid[pt]) st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), pk);  // a2: write-through
+        }
         unpack4(pk, q);
         if constexpr (DZ) a2pk[pt][t] = pk;
       }
@@ -441,7 +446,21 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     const int nimg = (int)(plast / HWi) - img0 + 1;  // 1 or 2 (CH <= HW)
     float* s_lg = s_fc + NW * PXT * 4 * NOF;          // [2][NOF] logits
     float* s_dl = s_lg + 2 * NOF;                     // [2][NOF] dL
+    // the stored a2 (write-through; the conv backward reads it): deferred out of the epilogue
+    // so that wave 0's drain before its arrival add waits for the partial logits only
+    auto store_a2 = [&]() {
+#pragma unroll
+      for (int pt = 0; pt < PXT; ++pt)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int co = co0 + 16 * t + 4 * (lane >> 4);
+          if (!valid[pt]) continue;
+          if constexpr (F32) st_wt(reinterpret_cast<float4*>(Y + Pp[pt] * Cout + co), a2q[pt][t]);
+          else st_wt(reinterpret_cast<uint2*>(Y + Pp[pt] * Cout + co), a2pk[pt][t]);
+        }
+    };
     DDP_STAMP(STAMP_K_FWD_DZ, 0);
+    if (wave != 0) store_a2();
     if (wave == 0) {
       int label = 0;
       if (lane < 2 * NOF) {  // the label of this thread's row, requested before the wait
@@ -453,6 +472,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
       if (lane < nimg)
         __hip_atomic_fetch_add(dzo.img_cnt + (img0 + lane) * FWD_DZ_CNT_STRIDE, 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+      store_a2();  // wave 0's a2 stores: after the drain above (it waited only for the partials)
       {
         const int im = img0 + (lane < nimg ? lane : 0);
         const int kb0 = im * HWi / CH, kb1 = (im * HWi + HWi - 1) / CH;
