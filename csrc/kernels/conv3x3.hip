@@ -181,6 +181,9 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
                return (Pq >= 0 && Pq < Ptot) ? ld16(X + Pq * Cin + c) : zero8();
              },
              [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * CE; st16(sX + r * XS + c, v); });
+  // level 3: wave 0's label (of its dL row, see the DZ section), loaded here so that its
+  // dependent-load chain (step counter -> index -> label) is not ahead of the drain there
+  int dz_label = 0;
   if (A1X) {
     // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), then a1 (conv1 recompute).
     // The block also writes its own pixels (and the labels of images starting in them)
@@ -188,6 +191,12 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     float* sxx = reinterpret_cast<float*>(sX + XR * XS);
     const int NXX = XR + 2 * W + 2;
     const int base = c1.bi.base();
+    if constexpr (DZ) {
+      if (wave == 0 && lane < 2 * NOF) {
+        const int im = (int)(P0 / HW) + (lane >= NOF ? 1 : 0);
+        if (im < B) dz_label = c1.labels[c1.bi.row(im, base)];
+      }
+    }
     for (int r = threadIdx.x; r < NXX; r += NT) {
       const long Pq = Pbase - W - 1 + r;
       float v = 0.f;
@@ -462,11 +471,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     DDP_STAMP(STAMP_K_FWD_DZ, 0);
     if (wave != 0) store_a2();
     if (wave == 0) {
-      int label = 0;
-      if (lane < 2 * NOF) {  // the label of this thread's row, requested before the wait
-        const int im = img0 + (lane >= NOF ? 1 : 0);
-        if (im < B) label = c1.labels[c1.bi.row(im, c1.bi.base())];
-      }
+      const int label = dz_label;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial-logit stores are out
       DDP_STAMP(STAMP_K_FWD_DZ, 1);
       if (lane < nimg)
