@@ -181,9 +181,6 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
                return (Pq >= 0 && Pq < Ptot) ? ld16(X + Pq * Cin + c) : zero8();
              },
              [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * CE; st16(sX + r * XS + c, v); });
-  // level 3: wave 0's label (of its dL row, see the DZ section), loaded here so that its
-  // dependent-load chain (step counter -> index -> label) is not ahead of the drain there
-  int dz_label = 0;
   if (A1X) {
     // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), then a1 (conv1 recompute).
     // The block also writes its own pixels (and the labels of images starting in them)
@@ -191,12 +188,6 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     float* sxx = reinterpret_cast<float*>(sX + XR * XS);
     const int NXX = XR + 2 * W + 2;
     const int base = c1.bi.base();
-    if constexpr (DZ) {
-      if (wave == 0 && lane < 2 * NOF) {
-        const int im = (int)(P0 / HW) + (lane >= NOF ? 1 : 0);
-        if (im < B) dz_label = c1.labels[c1.bi.row(im, base)];
-      }
-    }
     for (int r = threadIdx.x; r < NXX; r += NT) {
       const long Pq = Pbase - W - 1 + r;
       float v = 0.f;
@@ -253,6 +244,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   // pairs would hold the kernel at one block per CU; they are read where used (L2 hits),
   // the other block of the CU hides that latency
   constexpr bool PFW = NOF > 0 && !F32 && OCC == 1;
+  if constexpr (DZ) DDP_STAMP(STAMP_K_FWD_DZ, 6);  // (pixel index math done)
   // buffer loads: one per-lane VGPR offset per pixel tile and a uniform (o, t) SGPR offset
   // (flat loads: two 64-bit adds per load; without the prefetch (!PFW) the compiler kept 40
   // 64-bit addresses live between the fc partials and dZ2 and spilled)
@@ -288,6 +280,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
           wq[pt][t][o] = *reinterpret_cast<const float4*>(
               wfc + ((((long)o * (HW >> 4) + (rem[pt] >> 4)) * (Cout >> 4) + (co0 >> 4) + t) * 64 + lane) * 4);
   }
+  if constexpr (DZ) DDP_STAMP(STAMP_K_FWD_DZ, 7);  // (fc weight prefetch issued)
   // LDS-only barrier: the fc weight prefetch stays in flight through the MFMA loop
   // (__syncthreads drained it here: ~2 us per block, stamps s5 -> s2)
   lds_barrier();
@@ -471,7 +464,13 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     DDP_STAMP(STAMP_K_FWD_DZ, 0);
     if (wave != 0) store_a2();
     if (wave == 0) {
-      const int label = dz_label;
+      int label = 0;
+      if (lane < 2 * NOF) {  // the label of this thread's row, requested before the wait (its
+        // dependent-load chain overlaps the store drain below; loading it in the prologue
+        // instead measured -0.6 %: it delayed the x staging loads, profiles/r4_label)
+        const int im = img0 + (lane >= NOF ? 1 : 0);
+        if (im < B) label = c1.labels[c1.bi.row(im, c1.bi.base())];
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial-logit stores are out
       DDP_STAMP(STAMP_K_FWD_DZ, 1);
       if (lane < nimg)
