@@ -133,7 +133,10 @@ constexpr unsigned long long FWD_DZ_WAIT_TICKS = 2000000;  // 20 ms of the 100 M
 #ifndef DDP_AMD_F32_FC_PREFETCH
 #define DDP_AMD_F32_FC_PREFETCH 0  // 1: measured neutral (block 22.6 vs 22.7 us, profiles/r4_fp32)
 #endif
-constexpr bool F32_FC_PREFETCH = DDP_AMD_F32_FC_PREFETCH;  // see conv3x3_fwd_kernel (DZ, fp32)
+constexpr bool F32_FC_PREFETCH = DDP_AMD_F32_FC_PREFETCH;
+#ifndef DDP_AMD_FWD_PF_SPLIT
+#define DDP_AMD_FWD_PF_SPLIT 1
+#endif  // see conv3x3_fwd_kernel (DZ, fp32)
 
 template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
           bool DZ = false, int OCC = 1>
@@ -256,7 +259,20 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwfc, vo, so, 0));
   };
   uint2 wv[PFW ? PXT : 1][4][PFW ? NOF : 1];
-  if constexpr (PFW) {
+  // PF_SPLIT: the prefetch is issued in slices between the MFMA loop's taps instead of all
+  // ahead of it (80 b64 loads per wave, 327 KB per block: the CU's vector-memory path needs
+  // ~1.2 us to take them - stamps, profiles/r4_diag - time the MFMAs can cover)
+  constexpr bool PF_SPLIT = PFW && DDP_AMD_FWD_PF_SPLIT;
+  constexpr int NPF = PXT * 4 * (NOF > 0 ? NOF : 1);
+  auto wv_slice = [&](int tap) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i)
+      if (i * 9 / NPF == tap) {
+        const int pt = i / (4 * NOF), t = (i / NOF) % 4, o = i % NOF;
+        wv[pt][t][o] = fcw(pt, t, o);
+      }
+  };
+  if constexpr (PFW && !PF_SPLIT) {
 #pragma unroll
     for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
@@ -336,6 +352,11 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
       for (int pt = 0; pt < PXT; ++pt)
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[pt][t] = P::mma(a[t], b[pt], acc[pt][t]);
+    }
+    if constexpr (PF_SPLIT) {
+      __builtin_amdgcn_sched_barrier(0);
+      wv_slice(tap);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
