@@ -23,7 +23,10 @@
 // The data gradient reads the OHWI weight itself: its A operand (rows ci, K = co) is the
 // transpose of the stored layout, so the [32 co][BC ci] weight tile is staged as stored
 // and the MFMA fragments are read with ds_read_b64_tr_b16 (no transposed weight copy).
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "kernels/bn_tail.h"
 #include "kernels/common.h"
@@ -275,6 +278,183 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
       st_wt(dst + g.Cout + co0 + c, s_st[0][1][c] + s_st[1][1][c]);
     }
     if (fin.tickets) bn_stats_tail(fin, stats, bk.x, bk.y, co0, BC, reinterpret_cast<float*>(&sA[0][0]));
+  }
+}
+
+// ---------------------------------------------------------------- stem forward, halo form
+// The 7x7 / s2 / p3 stem on 224 x 224 x 4 inputs (StemGeo<1>), same block -> pixel map,
+// MFMA tiling and epilogue as conv_gemm_fwd_kernel<128, 64, ..., STEM, ..., 1>, but the
+// block's input rows are staged into LDS ONCE and its weight fragments are read ONCE into
+// registers: the gathered form waited out a global round trip per K-step (7 per block, ~1 us
+// each against 8 MFMAs per wave; 47 us per launch at B = 32, profiles/r4_final).
+// 128 consecutive output pixels of one image (12544 = 98 x 128: blocks never straddle
+// images) lie in at most 3 output rows oh0..oh0+2, i.e. input rows 2*oh0-3 .. 2*oh0+7 (11).
+// K-step = one kernel row kh: k = kw * 4 + c for kw = 0..7 (kw = 7: zero weight), so a
+// lane's 8 K values are taps 2q, 2q+1 of one input row = 2 adjacent pixels x 4 channels =
+// 16 contiguous bytes of the staged row (LDS column j = iw + 3, even for every read).
+constexpr int STEM_ROWS = 11, STEM_COLS = 232;  // staged input rows / columns (j = iw + 3)
+template <bool RELU, bool STATS>
+__global__ __launch_bounds__(256, 2) void conv_stem_halo_fwd_kernel(ConvGeom g, const bf16_t* __restrict__ X,
+                                                                 const bf16_t* __restrict__ Wt,
+                                                                 const float* __restrict__ bias,
+                                                                 bf16_t* __restrict__ Y,
+                                                                 float* __restrict__ stats, int ntiles) {
+  using SGeo = StemGeo<1>;
+  constexpr int BP = 128, BC = 64, TCO = 2, TPX = 4;
+  constexpr int OHW = SGeo::OH * SGeo::OW, KWC = 49 * 4, RS = STEM_COLS * 4;  // RS: elements per row
+  constexpr int NPAIR = STEM_ROWS * (SGeo::W / 2), XPT = (NPAIR + 255) / 256;  // 16-B pieces per thread
+  __shared__ __attribute__((aligned(16))) bf16_t sX[2][STEM_ROWS * RS];
+  __shared__ float s_st[2][2][BC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wco = wave >> 1, wpx = wave & 1;
+  const int3 bk = xcd_block3();
+  const int Ptot = g.N * OHW;
+  const int co0 = bk.y * BC;
+  const int kofs = 8 * (lane >> 4), col = lane & 15, q = lane >> 4;
+  // a contiguous range of 128-pixel tiles per block (neighbouring tiles share input rows;
+  // xcd_block3 keeps neighbouring blocks on one XCD): weights once, inputs double-buffered
+  const int t_beg = (int)((long)bk.x * ntiles / gridDim.x), t_end = (int)((long)(bk.x + 1) * ntiles / gridDim.x);
+
+  // weight fragments: a[kh][i] = taps 2q, 2q+1 of kernel row kh, output channel
+  // co0 + wco*32 + 16i + col
+  bf16x8 a[7][TCO];
+#pragma unroll
+  for (int i = 0; i < TCO; ++i) {
+    const bf16_t* wr = Wt + (long)(co0 + wco * 32 + 16 * i + col) * KWC;
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      const uint2 t0 = *reinterpret_cast<const uint2*>(wr + (kh * 7 + 2 * q) * 4);
+      const uint2 t1 = q < 3 ? *reinterpret_cast<const uint2*>(wr + (kh * 7 + 2 * q + 1) * 4) : make_uint2(0u, 0u);
+      a[kh][i] = __builtin_bit_cast(bf16x8, make_uint4(t0.x, t0.y, t1.x, t1.y));
+    }
+  }
+  // the zero columns of both buffers: j = 0..2 (iw = -3..-1) and j = 227..231 (iw >= 224)
+  for (int e = tid; e < 2 * STEM_ROWS * 8; e += 256) {
+    const int bf = e / (STEM_ROWS * 8), r = (e >> 3) % STEM_ROWS, k = e & 7;
+    const int j = k < 3 ? k : 224 + k;
+    *reinterpret_cast<uint2*>(&sX[bf][r * RS + j * 4]) = make_uint2(0u, 0u);
+  }
+  // input rows of tile t: pairs of input columns (16 B) -> LDS columns j, j + 1 (j odd).
+  // Tile t + 1 is requested when tile t starts (a second tile of lookahead, in a second
+  // register set, measured no faster: 34.8 vs 34.5 us per launch at B = 32)
+  uint4 xr[2][XPT];
+  auto load_x = [&](int t, uint4* xs) {
+    const int p0 = t * BP, n_ = p0 / OHW, oh0 = (p0 - n_ * OHW) / SGeo::OW;
+    const bf16_t* xim = X + (long)n_ * SGeo::H * SGeo::W * 4;
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) {
+      const int e = tid + 256 * u;
+      const int r = e / (SGeo::W / 2), c2 = e - r * (SGeo::W / 2);
+      const int ih = 2 * oh0 - 3 + r;
+      xs[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (e < NPAIR && (unsigned)ih < (unsigned)SGeo::H)
+        xs[u] = *reinterpret_cast<const uint4*>(xim + ((long)ih * SGeo::W + 2 * c2) * 4);
+    }
+  };
+  auto store_x = [&](int bf, const uint4* xs) {
+#pragma unroll
+    for (int u = 0; u < XPT; ++u) {
+      const int e = tid + 256 * u;
+      if (e < NPAIR) {
+        const int r = e / (SGeo::W / 2), c2 = e - r * (SGeo::W / 2);
+        bf16_t* d = &sX[bf][r * RS + (2 * c2 + 3) * 4];
+        *reinterpret_cast<uint2*>(d) = make_uint2(xs[u].x, xs[u].y);
+        *reinterpret_cast<uint2*>(d + 4) = make_uint2(xs[u].z, xs[u].w);
+      }
+    }
+  };
+  if (t_beg < t_end) {
+    load_x(t_beg, xr[0]);
+    store_x(0, xr[0]);
+  }
+  __syncthreads();
+  // tile t: LDS buffer and register set cur = (t - t_beg) & 1 (a compile-time constant)
+  auto tile = [&](int t, auto CUR) {
+    constexpr int cur = decltype(CUR)::value;
+    if (t + 1 < t_end) load_x(t + 1, xr[cur ^ 1]);  // lands during this tile's MFMAs and epilogue
+    const int p0 = t * BP, n_ = p0 / OHW, oh0 = (p0 - n_ * OHW) / SGeo::OW;
+    f32x4 acc[TCO][TPX];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int j = 0; j < TPX; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    int hb[TPX];  // the lane's LDS element offset at kh = 0, per px tile
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) {
+      const int P = p0 + wpx * (BP / 2) + 16 * j + col;
+      const int rr = (P < Ptot ? P : p0) - n_ * OHW;
+      const int oh = rr / SGeo::OW, ow = rr - oh * SGeo::OW;
+      hb[j] = 2 * (oh - oh0) * RS + (2 * ow) * 4 + kofs;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      bf16x8 b[TPX];
+#pragma unroll
+      for (int j = 0; j < TPX; ++j) b[j] = *reinterpret_cast<const bf16x8*>(&sX[cur][hb[j] + kh * RS]);
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int j = 0; j < TPX; ++j) acc[i][j] = mfma16(a[kh][i], b[j], acc[i][j]);
+    }
+
+    // ---- epilogue (conv_gemm_fwd_kernel's, unsplit; stats row = tile)
+    float csum[TCO][4], csq[TCO][4];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) csum[i][r] = csq[i][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < TPX; ++j) {
+      const int Pj = p0 + wpx * (BP / 2) + 16 * j + col;
+      const bool ok = Pj < Ptot;
+#pragma unroll
+      for (int i = 0; i < TCO; ++i) {
+        const int co = co0 + wco * (BC / 2) + 16 * i + 4 * (lane >> 4);
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[i][j][r] + (bias ? bias[co + r] : 0.f);
+          if (RELU) v[r] = fmaxf(v[r], 0.f);
+        }
+        const uint2 pk = pack4(v[0], v[1], v[2], v[3]);
+        if (ok) *reinterpret_cast<uint2*>(Y + (long)Pj * g.Cout + co) = pk;
+        if (STATS) {
+          float qv[4];
+          unpack4(pk, qv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = ok ? qv[r] : 0.f;
+            csum[i][r] += x;
+            csq[i][r] = fmaf(x, x, csq[i][r]);
+          }
+        }
+      }
+    }
+    if (STATS) {
+#pragma unroll
+      for (int i = 0; i < TCO; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sa = sum16(csum[i][r]), sb = sum16(csq[i][r]);
+          if (col == 0) {
+            const int cl = wco * (BC / 2) + 16 * i + 4 * (lane >> 4) + r;
+            s_st[wpx][0][cl] = sa;
+            s_st[wpx][1][cl] = sb;
+          }
+        }
+      __syncthreads();
+      for (int c = tid; c < BC; c += 256) {
+        float* dst = stats + (long)t * 2 * g.Cout;
+        st_wt(dst + co0 + c, s_st[0][0][c] + s_st[1][0][c]);
+        st_wt(dst + g.Cout + co0 + c, s_st[0][1][c] + s_st[1][1][c]);
+      }
+    }
+    if (t + 1 < t_end) store_x(cur ^ 1, xr[cur ^ 1]);  // tile t + 1 (buffer cur ^ 1 was last read a tile ago)
+    __syncthreads();
+  };
+  for (int t = t_beg; t < t_end; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < t_end) tile(t + 1, std::integral_constant<int, 1>{});
   }
 }
 
@@ -847,6 +1027,24 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
   const BnFin f = (fin && pl.splits <= 1) ? *fin : BnFin{};
   if (g.Cin == 4) {  // stem: 8 taps x 4 channels per K-step (host enforces Cout % 64)
     const bool s224 = stem_geo_224(g);
+    // the 224 x 224 stem: staged-halo kernel (DDP_AMD_STEM_HALO=0: the gathered K loop)
+    static const int stem_halo = [] { const char* e = getenv("DDP_AMD_STEM_HALO"); return e ? atoi(e) : 1; }();
+    if (s224 && stem_halo && !f.tickets && pl.splits <= 1 && grid.x * 128 >= (unsigned)(g.N * 112 * 112)) {
+      // persistent: two blocks per CU, each over a contiguous range of the 128-pixel tiles
+      static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 256;
+        return n > 0 ? n : 256;
+      }();
+      const int ntiles = (int)grid.x;
+      const dim3 sg(std::min(ntiles, 2 * cus), grid.y, 1);
+#define CSH(RL, ST) hipLaunchKernelGGL((conv_stem_halo_fwd_kernel<RL, ST>), sg, dim3(256), 0, s, g, X, Wt, bias, Y, stats, ntiles)
+      if (stats) CSH(false, true);
+      else if (relu) CSH(true, false);
+      else CSH(false, false);
+#undef CSH
+      return;
+    }
 #define CGS(RL, ST)                                                                                                  \
   do {                                                                                                               \
     if (s224) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 1>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f); \

@@ -106,6 +106,10 @@ def setup(rank: int, world_size: int, backend: str | None = None, verbose: bool 
           timeout_s: float | None = None, device: str | None = None) -> str:
     """Join the process group; returns the backend used (see :func:`resolve_backend`)."""
     backend = resolve_backend(backend, device)
+    # a single process with no launcher-given port needs no TCP rendezvous: an in-process
+    # store avoids the free-port race (a port picked here can be taken before TCPStore binds
+    # it - seen as EADDRINUSE on a GPU box between back-to-back runs)
+    own_store = world_size == 1 and "MASTER_PORT" not in os.environ
     ensure_master_env()
     if backend == "nccl":
         if not torch.cuda.is_available():
@@ -116,6 +120,8 @@ def setup(rank: int, world_size: int, backend: str | None = None, verbose: bool 
               timeout=datetime.timedelta(seconds=t))
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", local_rank(rank))
+    if own_store:
+        kw["store"] = dist.HashStore()
     dist.init_process_group(**kw)
     if verbose:
         print(f"Rank: {rank} has initialized its process group with world size {world_size}",

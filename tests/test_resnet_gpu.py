@@ -200,6 +200,15 @@ def test_stem_conv_7x7_s2(N, H):
     ref = F.conv2d(x4[..., :3].float().permute(0, 3, 1, 2), w4[..., :3].float().permute(0, 3, 1, 2),
                    stride=2, padding=3).permute(0, 2, 3, 1)
     assert relerr(y, ref) < 1e-2
+    # with the BatchNorm statistics slab (per-block sum / sum of squares of the stored bf16 y)
+    rows = C.conv_gemm_plan(x4, y, 7, 7, 2, 3)[3]
+    stats = torch.empty(rows, 2, 64, device=dev)
+    y2 = torch.empty_like(y)
+    C.conv_gemm_fwd(x4, w4, None, y2, 7, 7, 2, 3, False, stats)
+    assert torch.equal(y2, y)
+    yf = y.float().view(-1, 64)
+    assert relerr(stats[:, 0].sum(0), yf.sum(0)) < 1e-4
+    assert relerr(stats[:, 1].sum(0), (yf * yf).sum(0)) < 1e-4
     dy = rnd(N, OH, OH, 64, seed=5)
     rdw = torch.nn.grad.conv2d_weight(x4[..., :3].float().permute(0, 3, 1, 2), (64, 3, 7, 7),
                                       dy.float().permute(0, 3, 1, 2), stride=2, padding=3)
