@@ -11,6 +11,7 @@
 // last block, which also writes dgamma / dbeta straight into the parameter
 // gradients; then the per-element input gradient.  All float reductions are
 // fixed-order (the only atomics are integer tickets).
+#include <type_traits>
 #include <stdexcept>
 #include <string>
 
@@ -252,21 +253,57 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     }
   };
   int p = p0 + tp;
-  // four pixels' loads in flight (a block streams ~150 KB at layer1; with two in flight
-  // the pass was latency-bound at ~2.2 TB/s), then two, then one - the per-thread
-  // summation order is still pixel order
-  for (; p + 96 < p1; p += 128) {
-    bf16x8 d[4], xx[4], r[4];
+  // groups of four pixels (a block streams ~150 KB at layer1; with two in flight the pass
+  // was latency-bound at ~2.2 TB/s), software-pipelined: group k + 1's loads (dout2's
+  // too) are issued before group k is summed, so a block waits out about one memory round
+  // trip instead of one per group (256 blocks = one 4-wave block per CU: nothing else
+  // hides it).  Then two, then one pixel - the per-thread summation order is pixel order.
+  bf16x8 gd[2][4], gx[2][4], gr[2][4], g2[2][4];
+  auto load_g = [&](int pp, auto SET) {
+    constexpr int st = decltype(SET)::value;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const long o = (long)(p + 32 * u) * C + c0;
-      d[u] = ld8(dout + o);
-      xx[u] = ld8(x + o);
-      r[u] = MSK == 1 ? ld8(out + o) : zero8();
+      const long o = (long)(pp + 32 * u) * C + c0;
+      gd[st][u] = ld8(dout + o);
+      gx[st][u] = ld8(x + o);
+      gr[st][u] = MSK == 1 ? ld8(out + o) : zero8();
+      g2[st][u] = dout2 ? ld8(dout2 + o) : zero8();
     }
+  };
+  auto sum_g = [&](auto SET) {
+    constexpr int st = decltype(SET)::value;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc8(d[u], (long)(p + 32 * u) * C + c0, xx[u], r[u]);
+    for (int u = 0; u < 4; ++u) {
+      float d[8], xv[8];
+      unpack8(gd[st][u], d);
+      if (dout2) {  // unpack8_sum's add, on the prefetched second gradient
+        float t[8];
+        unpack8(g2[st][u], t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = bf16_round(d[j] + t[j]);
+      }
+      unpack8(gx[st][u], xv);
+      bn_mask8<MSK>(gr[st][u], xv, msc, msh, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += d[j];
+        q[j] = fmaf(d[j], (xv[j] - mu[j]) * is[j], q[j]);
+      }
+    }
+  };
+  const int n4 = p1 - p - 96 > 0 ? (p1 - p - 96 + 127) / 128 : 0;  // groups with p + 96 < p1
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (n4 > 0) load_g(p, S0{});
+  for (int k = 0; k < n4; k += 2) {
+    if (k + 1 < n4) load_g(p + 128 * (k + 1), S1{});
+    sum_g(S0{});
+    if (k + 1 < n4) {
+      if (k + 2 < n4) load_g(p + 128 * (k + 2), S0{});
+      sum_g(S1{});
+    }
   }
+  p += 128 * n4;
   for (; p + 32 < p1; p += 64) {  // two pixels' loads in flight
     const long o0 = (long)p * C + c0, o1 = o0 + 32L * C;
     const bf16x8 d0 = ld8(dout + o0), x0 = ld8(x + o0), d1 = ld8(dout + o1), x1 = ld8(x + o1);
@@ -824,6 +861,8 @@ static int g_bn_bwd_px = 392;
 void bn_bwd_set_px_per_block(int px) { g_bn_bwd_px = px < 32 ? 32 : px; }
 
 int bn_bwd_rows(long P, int C, int* rpb) {
+  // (a floor of ~256 blocks for the deep layers' few pixels measured 0.9 % slower: more
+  // partial rows for the last block to sum, profiles/r4_resnet/bn_bwd)
   (void)C;
   long R = P / g_bn_bwd_px;
   if (R > 256) R = 256;
