@@ -99,7 +99,8 @@ __device__ __forceinline__ void fc_bwd_bias_loss(const FcBwdExtras& ex, const fl
   const int lane = threadIdx.x & 63;
   if (ex.dbias && lane < NO) {
     float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += s_dl[b * NO + lane];
+#pragma unroll 16
+    for (int b = 0; b < B; ++b) acc += s_dl[b * NO + lane];  // (unrolled: the reads go out together)
     const float g = acc * ex.dbias_scale;
     if (ex.sys_store) st_sys(ex.dbias + lane, g);
     else ex.dbias[lane] = g;
@@ -111,13 +112,23 @@ __device__ __forceinline__ void fc_bwd_bias_loss(const FcBwdExtras& ex, const fl
       if (ex.m_b) ex.m_b[lane] = m;
     }
   }
-  if ((XENT || ex.loss_rows) && ex.loss_out && lane == 63) {
+  if ((XENT || ex.loss_rows) && ex.loss_out) {
+    // (every caller runs this with a whole wave) one load per lane, then the same
+    // sequential b = 0, 1, ... sum through v_readlane: the loop of dependent-address-free
+    // but serially waited loads on one lane took ~12 us at B = 64 (profiles/r4_b64/final_sweep)
     const float* lr = XENT ? s_loss : ex.loss_rows;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += lr[b];
     const int at = ex.step_ctr ? *ex.step_ctr : 0;
-    ex.loss_out[at] = acc / (float)B;
-    if (last && ex.step_inc) *ex.step_inc = at + 1;  // ex.step_inc == ex.step_ctr (read just above)
+    float acc = 0.f;
+    for (int b0 = 0; b0 < B; b0 += 64) {
+      const float v = b0 + lane < B ? lr[b0 + lane] : 0.f;
+      const int nb = B - b0 < 64 ? B - b0 : 64;
+      for (int k = 0; k < nb; ++k)
+        acc += __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+    }
+    if (lane == 63) {
+      ex.loss_out[at] = acc / (float)B;
+      if (last && ex.step_inc) *ex.step_inc = at + 1;  // ex.step_inc == ex.step_ctr (read just above)
+    }
   }
   if (ex.zero_i32 && (last || !ex.last_ctr))  // (block 0 when there is no last-block count)
     for (int i = lane; i < ex.n_zero; i += 64) ex.zero_i32[(long)i * ex.zero_stride] = 0;
