@@ -443,12 +443,18 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     if ((int)threadIdx.x < 2 * NOF) {
       const int slot = threadIdx.x / NOF, o = threadIdx.x - (threadIdx.x / NOF) * NOF;
       const long img = P0 / HW + slot;
+      // every read unconditional and unrolled (the reads go out together; a branch per tile
+      // kept them one LDS round trip apart), the other image's tiles added as +0.0f - an
+      // exact no-op for a sum that starts at +0.0f, so the same bits as skipping them
       float acc_o = 0.f;
+#pragma unroll
       for (int tile = 0; tile < NW * PXT; ++tile) {
         const long tp = P0 + tile * 16;
-        if (tp < Ptot && tp / HW == img) {
+        const bool in = tp < Ptot && tp / HW == img;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) acc_o += s_fc[(tile * 4 + g) * NOF + o];
+        for (int g = 0; g < 4; ++g) {
+          const float v = s_fc[(tile * 4 + g) * NOF + o];
+          acc_o += in ? v : 0.f;
         }
       }
       float* dst = fc_part + ((long)blockIdx.x * 2 + slot) * NOF + o;
