@@ -71,19 +71,58 @@ def _free_port() -> int:
 
 
 def _child_json(cmd, env, timeout):
-    """Run one launcher child; return (its last JSON stdout line or None, reason)."""
+    """Run one launcher child; return (its last JSON stdout line or None, reason).
+
+    The child (torch.distributed.run) leads its own process group: on a timeout it first
+    gets SIGTERM so the elastic agent can stop its workers, then, after a grace period, the
+    whole group is SIGKILLed - hung workers (spinning in an xGMI or in-launch wait) must not
+    survive into the next fallback attempt on the same GPUs.  Returns only once
+    every process of the group has exited."""
+    import signal
+
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True,
+                         start_new_session=True)
     try:
-        p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True,
-                           timeout=timeout)
-    except subprocess.TimeoutExpired as e:
-        out = e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
-        sys.stdout.write(out)
+        out, _ = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        _kill_group(p, signal)
+        out, _ = p.communicate()
+        sys.stdout.write(out or "")
         return None, f"timed out after {timeout:.0f} s"
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    _reap_group(p.pid, signal)  # workers the agent left behind (it exited abnormally)
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     if p.returncode != 0 or not lines:
-        sys.stdout.write(p.stdout)
+        sys.stdout.write(out)
         return None, f"rc={p.returncode}"
     return json.loads(lines[-1]), None
+
+
+def _kill_group(p, signal, grace: float = 20.0):
+    """SIGTERM the child's process group, wait up to ``grace`` s, then SIGKILL the group."""
+    try:
+        os.killpg(p.pid, signal.SIGTERM)
+    except ProcessLookupError:
+        return
+    try:
+        p.wait(timeout=grace)
+    except subprocess.TimeoutExpired:
+        pass
+    _reap_group(p.pid, signal)
+
+
+def _reap_group(pgid: int, signal, wait_s: float = 30.0):
+    """SIGKILL whatever is left in process group ``pgid`` and wait until it is empty."""
+    try:
+        os.killpg(pgid, signal.SIGKILL)
+    except (ProcessLookupError, PermissionError):
+        return
+    t0 = time.time()
+    while time.time() - t0 < wait_s:
+        try:
+            os.killpg(pgid, 0)
+        except ProcessLookupError:
+            return
+        time.sleep(0.1)
 
 
 # What the parent retries with when an N-rank child fails or times out (VERDICT r3 #3b):
@@ -240,6 +279,17 @@ def main():
                     help="skip the exact-fp32 (reference precision) run after the bf16 headline")
     ap.add_argument("--no_comm_calibration", action="store_true",
                     help="N>1: skip the post-run sweep that refits the xGMI all-reduce cost model")
+    ap.add_argument("--force_allreduce", action="store_true",
+                    help="N=1: run the multi-GPU step chain anyway (fc weight gradient kernel, bucket "
+                         "all-reduces on the --comm plane at world size 1) - times the dist chain on one GPU")
+    ap.add_argument("--plan_world", type=int, default=None,
+                    help="bucket plan as for this many ranks (default: the world size; --force_allreduce: 8)")
+    ap.add_argument("--dist_fork", type=int, default=None, choices=[0, 1],
+                    help="N>1, level 3: fc weight gradient + fc bucket all-reduce on a branch forked after the "
+                         "forward (1, default) or in front of the conv backward (0, the round-4 order)")
+    ap.add_argument("--no_breakdown", action="store_true",
+                    help="N>1 / --force_allreduce: skip the comm-free local run that splits the step into "
+                         "local compute and exposed communication (config.step_breakdown)")
     ap.add_argument("--no_chain_check", action="store_true",
                     help="N>1: skip the start-up check that the production kernel chain gives the "
                          "conservative chain's bits across the ranks")
@@ -288,7 +338,8 @@ def main():
     dev = torch.device("cuda", lrank)
     comm = None
     ranks_seen, rccl_nranks = 1, None
-    if ws > 1:
+    force = bool(args.force_allreduce) and ws == 1
+    if ws > 1 or force:
         setup(rank, ws, backend=args.backend, verbose=False)
         ranks_seen = dist.get_world_size()
         assert ranks_seen == ws == args.gpus, (ranks_seen, ws, args.gpus)
@@ -302,6 +353,23 @@ def main():
     imgs, labels = synthetic_mnist()
     data = DeviceMNIST(imgs, labels, dev, "synthetic")
 
+    # at N > 1 fit the xGMI cost model on this node's real bucket kernels
+    # BEFORE the engine is built (untimed, a few ms) and plan the buckets with it; on real
+    # peers the fit is also stored (xgmi/<N>, with provenance) for later runs
+    calib = None
+    if ws > 1 and args.comm != "rccl" and not args.no_comm_calibration:
+        from ddp_amd.parallel.comm_calibration import calibrate, save, topology
+
+        calib = calibrate(rank, ws, dev)
+        if calib is not None:
+            calib["topology"] = topology(ws, rank=rank)
+            if calib["topology"] == "xgmi" and rank == 0:
+                try:
+                    save({k: v for k, v in calib.items() if k != "topology"}, ws, "xgmi",
+                         extra={"source": "bench.py pre-engine calibration"})
+                except OSError as e:
+                    print(f"[bench] could not store the xGMI fit ({e})", file=sys.stderr)
+
     def barrier():
         if ws > 1:
             if args.backend == "nccl":
@@ -310,14 +378,16 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize()
 
-    def timed_run(dtype):
+    def timed_run(dtype, local=False):
         """Build the engine for ``dtype`` (fresh seeded model, rank-0 init broadcast), warm up,
         time exactly ``args.steps`` steps between barrier + synchronize brackets; returns
-        (seconds = MAX over ranks, engine, flat space, model, graph chunk)."""
+        (seconds = MAX over ranks, engine, flat space, model, graph chunk).  ``local``: the
+        same config as a comm-free one-rank engine on every rank at once (the step-breakdown
+        reference: what the step costs without any collective)."""
         torch.manual_seed(0)
         model = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
         fs = flat_space(model)
-        if ws > 1:
+        if ws > 1 and not local:
             if args.backend == "nccl":
                 dist.broadcast(fs.params, src=0)  # DDP construction semantics (rank-0 init)
             else:
@@ -336,14 +406,22 @@ def main():
                            bucket_plan=args.bucket_plan)
         eo.comm = args.comm
         for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role",
-                  "fuse_reduce"):
+                  "fuse_reduce", "dist_fork"):
             if getattr(args, f) is not None and not (dtype == "fp32" and f == "store_a1"):
                 setattr(eo, f, getattr(args, f))
         if dtype == "fp32":
             eo.store_a1 = 0  # the exact-fp32 chains recompute conv1 (engine.cpp launch_step_f32)
-        eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
+            eo.fuse_level = max(int(eo.fuse_level), 1)  # (no level-0 fp32 chain: --fuse_level 0 times level 1)
+        eo.force_allreduce = force and not local
+        if not local:
+            eo.plan_world = args.plan_world or (8 if force else None)
+            eo.cost_fit = calib
+        if local:
+            eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, 1, 0, None, eo)
+        else:
+            eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
         eng.refresh()
-        if ws > 1 and not args.no_chain_check:
+        if (ws > 1 or force) and not local and not args.no_chain_check:
             eng.verify_chain()  # untimed: production vs conservative chain, bitwise, all ranks
         if not args.no_graph:
             eng.run_steps(0)           # uploads epoch 0's indices
@@ -366,18 +444,25 @@ def main():
     dt, eng, fs, model, k, eo = timed_run(args.dtype)
     ms = dt * 1000.0 / args.steps
     img_s = ws * args.batch_size * args.steps / dt
-    bucket_us = eng.measure_bucket_allreduce() if ws > 1 else None  # after the timed region
-    # refit the xGMI cost model on this node's real kernels: a few ms, untimed
-    calib = None
-    if ws > 1 and eng.comm_kind.startswith("xgmi") and not args.no_comm_calibration:
-        from ddp_amd.parallel.comm_calibration import calibrate, topology
-
-        calib = calibrate(rank, ws, dev)
-        if calib is not None:
-            calib["topology"] = topology(ws, rank=rank)
+    bucket_us = eng.measure_bucket_allreduce() if (ws > 1 or force) else None  # after the timed region
+    # what the multi-GPU step costs over the one-GPU step.  Every rank times the
+    # same config as a comm-free local engine (the ws=1 chain: 2 kernels, fc role fused) right
+    # after the headline, untimed for the metric; the difference is the exposed communication
+    # (+ the dist chain's extra kernels), the rest is local compute.
+    breakdown = None
+    if (ws > 1 or force) and not args.no_breakdown:
+        dtl, engl, _, _, _, _ = timed_run(args.dtype, local=True)
+        loc_us = dtl * 1e6 / args.steps
+        step_us = dt * 1e6 / args.steps
+        breakdown = {"step_us": round(step_us, 2), "local_step_us": round(loc_us, 2),
+                     "exposed_comm_us": round(step_us - loc_us, 2),
+                     "dist_over_local": round(step_us / loc_us, 4),
+                     "local_kernels_per_step": (2 if engl.eng.last_fc_role else 3) if engl.eng.last_level3 else None,
+                     "bucket_allreduce_isolated_us": bucket_us}
+        del engl
     from ddp_amd.parallel.bucket_model import describe
 
-    plan = describe(eng.buckets, fs, eng.cost) if ws > 1 else None
+    plan = describe(eng.buckets, fs, eng.cost, ranges=eng.ranges) if (ws > 1 or force) else None
     finite = bool(torch.isfinite(fs.params).all().item())
     level3 = bool(eng.eng.last_level3)
     kps = (2 if eng.eng.last_fc_role else 3) if level3 else None
@@ -431,16 +516,19 @@ def main():
                        "rccl_nranks": rccl_nranks, "backend": args.backend if ws > 1 else None,
                        "scaling_efficiency": None, "tuned_planes_us": eng.allreduce_us,
                        "bucket_plan": {"rule": args.bucket_plan, "buckets": plan,
+                                       "cost_source": eng.cost.source if (ws > 1 or force) else None,
+                                       "plan_world": eo.plan_world,
                                        "pred_last_allreduce_done_us": (round(eng.pred_comm_us, 2)
                                                                        if ws > 1 and eng.pred_comm_us else None)},
                        "chain_check": eng.chain_check, "downgrades": getattr(eng, "downgrades", []),
+                       "force_allreduce": force, "step_breakdown": breakdown,
                        "comm_calibration": calib,
                        "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
                        "fp32_level3": fp32["level3"] if fp32 else None,
                        "fp32_kernels_per_step": fp32["kernels_per_step"] if fp32 else None,
                        "fp32_ms_per_step": fp32["ms_per_step"] if fp32 else None},
         }), flush=True)
-    if ws > 1:
+    if ws > 1 or force:
         barrier()
         dist.destroy_process_group()
 

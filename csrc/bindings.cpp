@@ -838,6 +838,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              check_cuda(t, "tensor");
              c.all_reduce(t.data_ptr(), t.numel(), dtype_code(t), op, stream_or_current(stream));
            }, py::arg("tensor"), py::arg("op") = 0, py::arg("stream") = 0)
+      .def("all_reduce_premul", [](Comm& c, Tensor& t, double scale, uint64_t stream) {
+             check_cuda(t, "tensor");
+             TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous(), "all_reduce_premul: contiguous fp32");
+             c.all_reduce_premul(t.data_ptr<float>(), t.numel(), (float)scale, stream_or_current(stream));
+           }, py::arg("tensor"), py::arg("scale"), py::arg("stream") = 0)
       .def("broadcast", [](Comm& c, Tensor& t, int root, uint64_t stream) {
              check_cuda(t, "tensor");
              c.broadcast(t.data_ptr(), t.numel(), dtype_code(t), root, stream_or_current(stream));
@@ -925,6 +930,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? cfgd["fuse_reduce"].cast<int>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
+             c.dist_fork = cfgd.contains("dist_fork") ? cfgd["dist_fork"].cast<int>() : 1;
              TORCH_CHECK(c.l3_fc_role == 0 || c.l3_fc_role == 1, "engine: l3_fc_role must be 0 or 1");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;

@@ -37,38 +37,11 @@
 // the result wrong (detected by the host) instead of hanging the GPU.
 #include "kernels/common.h"
 #include "kernels/launchers.h"
+#include "kernels/shadow.h"
 
 namespace ddp_amd {
 
 
-
-// bf16 shadows of one updated parameter (flat index j), same layouts as sgd_kernel
-__device__ __forceinline__ void shadow_one(const ShadowSet& sh, long j, float v) {
-#pragma unroll
-  for (int r = 0; r < MAX_SHADOWS; ++r) {
-    if (r >= sh.count) break;
-    const long k = j - sh.r[r].off;
-    if (k < 0 || k >= sh.r[r].n) continue;
-    const bf16_t b = f2bf(v);
-    if (sh.r[r].kind == SHADOW_BF16) {
-      sh.r[r].dst[k] = b;
-    } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
-      sh.r[r].dst[fcfrag_index((int)k, sh.r[r].a, sh.r[r].b)] = b;
-    } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
-      sh.r[r].dst32[fcfrag_index((int)k, sh.r[r].a, sh.r[r].b)] = v;
-    } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {  // [..][3] -> [..][4], 4th stays zero
-      sh.r[r].dst[(k / 3) * 4 + k % 3] = b;
-    } else if (sh.r[r].kind == SHADOW_F32_TAPT) {  // exact fp32 [tap][ci][co] copy
-      const long per = (long)sh.r[r].b * sh.r[r].c;
-      const long co = k / per;
-      sh.r[r].dst32[(k - co * per) * sh.r[r].a + co] = v;
-    } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
-      const long per = (long)sh.r[r].b * sh.r[r].c;
-      const long co = k / per;
-      sh.r[r].dst[(k - co * per) * sh.r[r].a + co] = b;
-    }
-  }
-}
 
 // Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
 // has signalled `target` to us.  Caller guarantees every wave drained its stores.
@@ -168,31 +141,34 @@ __device__ __forceinline__ void sgd_elem(const XgmiArgs& a, long k, float g) {
   shadow_one(a.sh, j, pn);
 }
 // quad q (elements 4q.., below lim) of the reduced bucket times scale -> my gradient
-// buffer; without SGD when `sgd` is false (the caller runs sgd4 afterwards)
+// buffer and, with the fused optimizer (a.sgd.update), the parameters / momentum / shadows.
+// Whole quads of a 4-aligned bucket are 16-byte accesses (sgd_quad / shadow_quad: the
+// same writers as sgd_kernel); a partial last quad goes element by element.
 __device__ __forceinline__ float4 scale4(const XgmiArgs& a, float4 v) {
   return make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
 }
-__device__ __forceinline__ void store4(const XgmiArgs& a, long q, float4 v, long lim) {
-  float* d = a.data[a.rank] + a.off + 4 * q;
-  if (4 * q + 3 < lim) {
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-  } else {
-    const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (4 * q + j < lim) d[j] = e[j];
+__device__ __forceinline__ void finish_quad(const XgmiArgs& a, long q, float4 v, long lim) {
+  if (4 * q + 3 < lim && (a.off & 3) == 0) {
+    const long j = a.off + 4 * q;
+    *reinterpret_cast<float4*>(a.data[a.rank] + j) = v;
+    if (a.sgd.update) {
+      const float4 pm = ld_quad(a.params, j);
+      const float4 mm = a.sgd.momentum != 0.f ? ld_quad(a.mbuf, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sgd_quad_apply(a.params, a.mbuf, j, v, pm, mm, a.sgd, a.sh);
+    }
+    return;
   }
-}
-__device__ __forceinline__ void sgd4(const XgmiArgs& a, long q, float4 v, long lim) {
+  float* d = a.data[a.rank] + a.off + 4 * q;
   const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (4 * q + j < lim) sgd_elem(a, 4 * q + j, e[j]);
+  for (int j = 0; j < 4; ++j) {
+    if (4 * q + j >= lim) continue;
+    d[j] = e[j];
+    if (a.sgd.update) sgd_elem(a, 4 * q + j, e[j]);
+  }
 }
 __device__ __forceinline__ void finish4(const XgmiArgs& a, long q, float4 v, long lim) {
-  v = scale4(a, v);
-  store4(a, q, v, lim);
-  if (a.sgd.update) sgd4(a, q, v, lim);
+  finish_quad(a, q, scale4(a, v), lim);
 }
 
 __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
@@ -306,26 +282,39 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a
     __amdgpu_buffer_rsrc_t st[XGMI_MAX_RANKS];
 #pragma unroll
     for (int p = 0; p < XGMI_MAX_RANKS; ++p) st[p] = sys_rsrc((p < N ? a.stage[p] : a.stage[r]) + par);
+    // every load of the iteration (N reduced quads over xGMI, and with the fused optimizer
+    // the N local parameter / momentum quads) is issued before the first store
+    const bool vec = (a.off & 3) == 0;
+    const bool mom = a.sgd.momentum != 0.f;
     for (long q = q0; q < sq; q += G) {
-      float4 v[XGMI_MAX_RANKS];
+      float4 v[XGMI_MAX_RANKS], pv[XGMI_MAX_RANKS], mv[XGMI_MAX_RANKS];
 #pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p)
-        v[p] = (p < N && (long)p * slice + 4 * q < a.n) ? ld4_sys(st[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p)
-        if (p < N && (long)p * slice + 4 * q < a.n) store4(a, (long)p * sq + q, scale4(a, v[p]), a.n);
-      if (a.sgd.update) {
-        // the optimizer per peer slice from the quads just stored (this thread's own
-        // plain stores: coherent), keeping one copy of the SGD + shadow code
+      for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
+        const long qq = (long)p * sq + q;
+        const bool ok = p < N && 4 * qq < a.n;
+        v[p] = ok ? ld4_sys(st[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool whole = ok && vec && 4 * qq + 3 < a.n;
+        pv[p] = whole && a.sgd.update ? ld_quad(a.params, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        mv[p] = whole && a.sgd.update && mom ? ld_quad(a.mbuf, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      // finish one peer's quad per trip (the finishing code once, not N times: unrolled N
+      // ways it made the kernel too large to unroll); the trip's registers are picked from
+      // the arrays by a select chain on the (uniform) peer index - constant array indices only
 #pragma unroll 1
-        for (int p = 0; p < N; ++p) {
-          const long qq = (long)p * sq + q;
-          if (4 * qq >= a.n) break;
-          const float* d = a.data[r] + a.off + 4 * qq;
-          float t[4];
+      for (int p = 0; p < N; ++p) {
+        const long qq = (long)p * sq + q;
+        if (4 * qq >= a.n) break;
+        float4 vv = v[0], pp = pv[0], mm = mv[0];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) t[j] = 4 * qq + j < a.n ? d[j] : 0.f;
-          sgd4(a, qq, make_float4(t[0], t[1], t[2], t[3]), a.n);
+        for (int u = 1; u < XGMI_MAX_RANKS; ++u)
+          if (p == u) { vv = v[u]; pp = pv[u]; mm = mv[u]; }
+        const float4 d = scale4(a, vv);
+        if (vec && 4 * qq + 3 < a.n) {
+          const long j = a.off + 4 * qq;
+          *reinterpret_cast<float4*>(a.data[r] + j) = d;
+          if (a.sgd.update) sgd_quad_apply(a.params, a.mbuf, j, d, pp, mm, a.sgd, a.sh);
+        } else {
+          finish_quad(a, qq, d, a.n);
         }
       }
     }

@@ -12,6 +12,7 @@
 // gradient-bucket views, prescaled by 1/world_size (DDP averaging).
 #include "kernels/common.h"
 #include "kernels/launchers.h"
+#include "kernels/shadow.h"
 #include "kernels/slab_reduce.h"
 
 namespace ddp_amd {
@@ -38,55 +39,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
       reinterpret_cast<float4*>(p)[q] = v;
       if (a.momentum != 0.f) reinterpret_cast<float4*>(mbuf)[q] = m;
     }
-#pragma unroll
-    for (int r = 0; r < MAX_SHADOWS; ++r) {
-      if (r < sh.count) {
-        const long j = i - sh.r[r].off;
-        if (j + 3 >= 0 && j < sh.r[r].n) {
-          const float e[4] = {v.x, v.y, v.z, v.w};
-          const bool whole = j >= 0 && j + 3 < sh.r[r].n && ((sh.r[r].off & 3) == 0);
-          if (sh.r[r].kind == SHADOW_BF16 && whole) {
-            *reinterpret_cast<uint2*>(sh.r[r].dst + j) = pack4(e[0], e[1], e[2], e[3]);
-          } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG && whole) {
-            // C % 4 == 0: the quad is 4 consecutive channels of one (o, hw) -> 8 contiguous bytes
-            *reinterpret_cast<uint2*>(sh.r[r].dst + fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)) =
-                pack4(e[0], e[1], e[2], e[3]);
-          } else if (sh.r[r].kind == SHADOW_F32_FCFRAG && whole) {
-            *reinterpret_cast<float4*>(sh.r[r].dst32 + fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)) =
-                make_float4(e[0], e[1], e[2], e[3]);
-          } else {
-            // element by element (a unit-stride quad straddling the region, or a transposed
-            // layout); four explicit calls, not a loop over e[u]: the dynamic index put the
-            // quad in scratch (68 bytes per lane, utils/kernel_resources.py)
-            auto put = [&](long jj, float ev) {
-              if (jj < 0 || jj >= sh.r[r].n) return;
-              if (sh.r[r].kind == SHADOW_BF16) {
-                sh.r[r].dst[jj] = f2bf(ev);
-              } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
-                sh.r[r].dst[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = f2bf(ev);
-              } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
-                sh.r[r].dst32[fcfrag_index((int)jj, sh.r[r].a, sh.r[r].b)] = ev;
-              } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
-                sh.r[r].dst[(jj / 3) * 4 + jj % 3] = f2bf(ev);
-              } else if (sh.r[r].kind == SHADOW_F32_TAPT) {
-                const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
-                const long co = jj / ((long)T * Ci);
-                sh.r[r].dst32[(jj - co * T * Ci) * Co + co] = ev;
-              } else {  // SHADOW_BF16_TAPT: OHWI [co][tap][ci] -> [tap][ci][co]
-                const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
-                const long co = jj / ((long)T * Ci);
-                const long rr = jj - co * T * Ci;
-                sh.r[r].dst[rr * Co + co] = f2bf(ev);
-              }
-            };
-            put(j, v.x);
-            put(j + 1, v.y);
-            put(j + 2, v.z);
-            put(j + 3, v.w);
-          }
-        }
-      }
-    }
+    shadow_quad(sh, i, v);
   }
   // scalar tail
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
@@ -98,29 +51,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
       p[i] = v;
       if (a.momentum != 0.f) mbuf[i] = m;
     }
-#pragma unroll
-    for (int r = 0; r < MAX_SHADOWS; ++r) {  // (constant trip count: a loop to sh.count indexed the
-      if (r >= sh.count) break;              //  by-value ShadowSet dynamically -> scratch)
-      const long j = i - sh.r[r].off;
-      if (j < 0 || j >= sh.r[r].n) continue;
-      if (sh.r[r].kind == SHADOW_BF16) {
-        sh.r[r].dst[j] = f2bf(v);
-      } else if (sh.r[r].kind == SHADOW_BF16_FCFRAG) {
-        sh.r[r].dst[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = f2bf(v);
-      } else if (sh.r[r].kind == SHADOW_F32_FCFRAG) {
-        sh.r[r].dst32[fcfrag_index((int)j, sh.r[r].a, sh.r[r].b)] = v;
-      } else if (sh.r[r].kind == SHADOW_BF16_PAD4) {
-        sh.r[r].dst[(j / 3) * 4 + j % 3] = f2bf(v);
-      } else if (sh.r[r].kind == SHADOW_F32_TAPT) {
-        const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
-        const long co = j / ((long)T * Ci);
-        sh.r[r].dst32[(j - co * T * Ci) * Co + co] = v;
-      } else {
-        const int Co = sh.r[r].a, T = sh.r[r].b, Ci = sh.r[r].c;
-        const long co = j / ((long)T * Ci);
-        sh.r[r].dst[(j - co * T * Ci) * Co + co] = f2bf(v);
-      }
-    }
+    shadow_one(sh, i, v);
   }
   if (step_ctr && blockIdx.x == 0 && threadIdx.x == 0) step_ctr[0] += 1;
   DDP_STAMP(STAMP_K_SGD, 1);

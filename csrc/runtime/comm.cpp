@@ -53,7 +53,27 @@ Comm::Comm(const std::string& uid, int rank, int world, int device) : rank_(rank
 }
 
 Comm::~Comm() {
-  if (comm_ && !process_exiting()) ncclCommDestroy(comm_);
+  if (comm_ && !process_exiting()) {
+    for (auto& kv : premul_) ncclRedOpDestroy(kv.second, comm_);
+    ncclCommDestroy(comm_);
+  }
+}
+
+void Comm::all_reduce_premul(float* buf, size_t count, float scale, hipStream_t s) {
+  ncclRedOp_t op{};
+  bool have = false;
+  for (auto& kv : premul_)
+    if (kv.first == scale) {
+      op = kv.second;
+      have = true;
+    }
+  if (!have) {
+    // the scalar is captured by value (host-immediate), so the op stays valid inside
+    // captured graphs; it lives as long as the communicator
+    DDP_NCCL_CHECK(ncclRedOpCreatePreMulSum(&op, &scale, ncclFloat32, ncclScalarHostImmediate, comm_));
+    premul_.emplace_back(scale, op);
+  }
+  DDP_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, op, comm_, s));
 }
 
 void Comm::all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t s) {

@@ -15,10 +15,11 @@
 //                 gradient + SGD of the fc weight and bias, the loss, the step counter)
 //                 and the in-launch fixed-order slab reduction + SGD of the conv weights
 //
-// At world size > 1 the fc weight gradient is its own light kernel between the two
-// (fc_bwd without dX, dL given), so the fc bucket's all-reduce - the direct xGMI kernels
-// with SGD fused into their all-gather, or RCCL + one SGD pass - overlaps the conv
-// backward on the comm stream; the conv bucket's all-reduce follows the conv backward.
+// At world size > 1 the fc weight gradient is its own light kernel (fc_bwd without dX, dL
+// given) on the comm stream, forked after the forward beside the conv backward, followed by
+// the fc bucket's all-reduce - the direct xGMI kernels with SGD fused into their
+// all-gather, or RCCL + one SGD pass; the conv bucket's all-reduce follows the conv
+// backward (schedule_backward).
 //
 // Older chains stay selectable (tests pin them bit for bit against each other):
 //   level 0: 8 kernels (conv1_fwd, conv3x3_fwd, xent, fc_bwd, dgrad, wgrad, grad_reduce,
@@ -66,7 +67,7 @@ SimpleCNNEngine::SimpleCNNEngine(const EngineConfig& cfg, const EngineBuffers& b
   xch_.assign(buckets_.size(), -1);
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
   DDP_HIP_CHECK(hipStreamCreateWithFlags(&ms_, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_})
+  for (hipEvent_t* e : {&e_b0_, &e_b1_, &e_d0_, &e_d1_, &e_fwd_, &e_fc_})
     DDP_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   l3_fits_.assign(cfg_.max_batch + 1, -1);
   // the in-launch wait-timeout word lives in coherent host memory: a kernel that times out
@@ -88,7 +89,7 @@ SimpleCNNEngine::~SimpleCNNEngine() {
   if (process_exiting()) return;
   if (cs_) hipStreamSynchronize(cs_);
   destroy_graph();
-  for (hipEvent_t e : {e_b0_, e_b1_, e_d0_, e_d1_}) hipEventDestroy(e);
+  for (hipEvent_t e : {e_b0_, e_b1_, e_d0_, e_d1_, e_fwd_, e_fc_}) hipEventDestroy(e);
   if (err_host_) hipHostFree(err_host_);
 }
 
@@ -257,6 +258,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   }
   // (fused optimizer: the fc weight gradient is consumed in registers and not stored)
   BwdFc fcr;  // the conv backward's fc role (fc_role)
+  std::function<void(hipStream_t)> fc_launch;  // the fc weight-gradient kernel, when not a role
   if (l3) {
     // level 3: no dZ2 and no cross-entropy prologue here (the forward wrote dZ2, dL, losses)
     ex.part = nullptr;
@@ -281,23 +283,26 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       fcr.ex = ex;
     } else {
       ex.sh_plain = nullptr;
-      fc_bwd(b_.dlogits, b_.a2, nullptr, nullptr, fopt ? nullptr : G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
-             /*mask=*/true, cs_, ex);
+      fc_launch = [&](hipStream_t s) {
+        fc_bwd(b_.dlogits, b_.a2, nullptr, nullptr, fopt ? nullptr : G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
+               /*mask=*/true, s, ex);
+      };
     }
     plain_stale_ = true;
   } else {
-    fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
-           (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+    fc_launch = [&](hipStream_t s) {
+      fc_bwd(b_.dlogits, b_.a2, b_.wfc_bf16, b_.dz2, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
+             (long)HW * C2, NO, /*mask=*/true, s, ex);
+    };
   }
-  // every bf16 shadow; a bucket's fused SGD refreshes the ones inside its range
+  // every bf16 shadow the chain reads; a bucket's fused SGD refreshes the ones inside its
+  // range (level 3 never reads the plain fc shadow: plain_stale_ re-derives it on a switch)
   ShadowSet sh_all{};
   sh_all.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
   sh_all.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
-  sh_all.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
-  sh_all.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
-  sh_all.count = 4;
-  // fc-only buckets: all-reduce (and, over xGMI, the fused SGD) overlaps the conv backward
-  if (dist) launch_buckets(0, use_x, sa, M, sh_all);
+  sh_all.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+  sh_all.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
+  sh_all.count = l3 ? 3 : 4;
   // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
   SlabSet ss{};
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
@@ -332,27 +337,28 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   }
   ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
   bool reduced = false;  // the conv backward launch also did grad_reduce's work
-  if (f1) {
-    // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
-    reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
-                          cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
-                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
-                          fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
-  } else {
-    conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
-                  b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
-    conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
-  }
-  if (!reduced) grad_reduce(ss, cs_);
+  auto conv_launch = [&]() {
+    if (f1) {
+      // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
+      reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
+                            cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
+                            fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
+                            fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
+    } else {
+      conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
+                    b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
+      conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
+    }
+    if (!reduced) grad_reduce(ss, cs_);
+  };
+  // fc buckets overlap the conv backward; at level 3 the fc weight gradient itself forks
+  // off the compute stream after the forward (dist_fork)
+  schedule_backward(dist, dist && l3 && cfg_.dist_fork, use_x, fc_launch, conv_launch, sa, M, sh_all);
   last_fused_reduce_ = reduced;
   last_level3_ = l3;
   last_fc_role_ = fc_role;
   if (fopt) return;
-  if (dist) {
-    launch_buckets(1, use_x, sa, M, sh_all);
-    join_buckets();
-    if (use_x) return;  // the optimizer ran inside the all-reduces
-  }
+  if (dist && use_x) return;  // the optimizer ran inside the all-reduces
   // ---- optimizer + bf16 shadows + next batch window
   sgd_step(P, G, M, b_.n_params, sa, sh_all, b_.step_ctr, cs_);
 }
@@ -362,15 +368,71 @@ void SimpleCNNEngine::launch_buckets(int stage, bool use_x, const SgdArgs& sa, f
   hipEvent_t ready = stage == 0 ? e_b0_ : e_b1_;
   DDP_HIP_CHECK(hipEventRecord(ready, cs_));
   DDP_HIP_CHECK(hipStreamWaitEvent(ms_, ready, 0));
+  enqueue_buckets(stage, use_x, ms_, sa, M, sh);
+  DDP_HIP_CHECK(hipEventRecord(stage == 0 ? e_d0_ : e_d1_, ms_));
+}
+
+void SimpleCNNEngine::enqueue_buckets(int stage, bool use_x, hipStream_t s, const SgdArgs& sa, float* M,
+                                      const ShadowSet& sh) {
   for (int b = 0; b < (int)buckets_.size(); ++b) {
     if (stage_[b] != stage) continue;
     if (use_x) {
-      xgmi_->all_reduce_sgd(xch_[b], ms_, sa, b_.params, M, sh, b == last_bucket_ ? b_.step_ctr : nullptr);
+      xgmi_->all_reduce_sgd(xch_[b], s, sa, b_.params, M, sh, b == last_bucket_ ? b_.step_ctr : nullptr);
     } else {
-      comm_->all_reduce(b_.grads + buckets_[b].off, (size_t)buckets_[b].n, 0, 0, ms_);
+      comm_->all_reduce(b_.grads + buckets_[b].off, (size_t)buckets_[b].n, 0, 0, s);
     }
   }
-  DDP_HIP_CHECK(hipEventRecord(stage == 0 ? e_d0_ : e_d1_, ms_));
+}
+
+// World size > 1 (or forced), dist_fork, level 3 - the forward already wrote dL and dZ2, so
+// the fc weight gradient depends on the forward alone:
+//
+//   cs_: forward -> conv backward (+ fused slab reduction) -> [xGMI] conv buckets -> join
+//   ms_:         `-> fc_bwd -> fc buckets' all-reduce (+ fused SGD) -----------------'
+//
+// a two-branch graph: the conv backward starts right behind the forward instead of behind
+// fc_bwd (DDP's bucket 0 fires while the conv backward
+// still runs).  Over xGMI the conv buckets stay on the compute stream (no event hop after
+// the conv backward; each bucket has its own channel, so the two branches' all-reduces
+// never share flags); they wait for fc_bwd first, which reads the step counter that the
+// last bucket advances.  RCCL keeps every collective on ms_ (one communicator: the ranks
+// must issue its calls in one order).
+void SimpleCNNEngine::schedule_backward(bool dist, bool fork, bool use_x, const std::function<void(hipStream_t)>& fc,
+                                        const std::function<void()>& conv, const SgdArgs& sa, float* M,
+                                        const ShadowSet& sh) {
+  if (!dist) {
+    if (fc) fc(cs_);
+    conv();
+    return;
+  }
+  if (!fork || !fc) {  // the round-4 order
+    if (fc) fc(cs_);
+    launch_buckets(0, use_x, sa, M, sh);
+    conv();
+    launch_buckets(1, use_x, sa, M, sh);
+    join_buckets();
+    return;
+  }
+  DDP_HIP_CHECK(hipEventRecord(e_fwd_, cs_));
+  DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_fwd_, 0));
+  fc(ms_);
+  DDP_HIP_CHECK(hipEventRecord(e_fc_, ms_));
+  if (stage_used_[0]) enqueue_buckets(0, use_x, ms_, sa, M, sh);
+  DDP_HIP_CHECK(hipEventRecord(e_d0_, ms_));
+  conv();
+  if (use_x) {
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_fc_, 0));
+    if (stage_used_[1]) enqueue_buckets(1, use_x, cs_, sa, M, sh);
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d0_, 0));
+  } else {
+    if (stage_used_[1]) {
+      DDP_HIP_CHECK(hipEventRecord(e_b1_, cs_));
+      DDP_HIP_CHECK(hipStreamWaitEvent(ms_, e_b1_, 0));
+      enqueue_buckets(1, use_x, ms_, sa, M, sh);
+    }
+    DDP_HIP_CHECK(hipEventRecord(e_d1_, ms_));
+    DDP_HIP_CHECK(hipStreamWaitEvent(cs_, e_d1_, 0));
+  }
 }
 
 void SimpleCNNEngine::join_buckets() {
@@ -471,6 +533,7 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     ex.frag_C = C2;
   }
   BwdFc fcr;
+  std::function<void(hipStream_t)> fc_launch;  // the fc weight-gradient kernel, when not a role
   if (fc_role) {
     // inside the conv backward launch: block 0 of the fc role owns the fc bias, the loss and
     // the step counter (nothing else in the launch reads them)
@@ -486,17 +549,20 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     fcr.K = (long)HW * C2;
     fcr.ex = ex;
   } else if (l3) {
-    fc_bwd(b_.dlogits, b_.a2_f32, nullptr, nullptr, fopt ? nullptr : G + b_.off_wfc, inv_ws, B, (long)HW * C2, NO,
-           /*mask=*/true, cs_, ex);
+    fc_launch = [&](hipStream_t s) {
+      fc_bwd(b_.dlogits, b_.a2_f32, nullptr, nullptr, fopt ? nullptr : G + b_.off_wfc, inv_ws, B, (long)HW * C2,
+             NO, /*mask=*/true, s, ex);
+    };
   } else {
-    fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
-           (long)HW * C2, NO, /*mask=*/true, cs_, ex);
+    fc_launch = [&](hipStream_t s) {
+      fc_bwd(b_.dlogits, b_.a2_f32, P + b_.off_wfc, b_.dz2_f32, fopt ? nullptr : G + b_.off_wfc, inv_ws, B,
+             (long)HW * C2, NO, /*mask=*/true, s, ex);
+    };
   }
   ShadowSet sh1{};
   sh1.r[0] = ShadowRegion{b_.off_w2, n_w2, nullptr, SHADOW_F32_TAPT, C2, 9, C1, b_.w2t_f32};
   sh1.r[1] = ShadowRegion{b_.off_wfc, n_fc, nullptr, SHADOW_F32_FCFRAG, HW, C2, 0, b_.wfc_frag32};
   sh1.count = 2;
-  if (dist) launch_buckets(0, use_x, sa, M, sh1);
   // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
   SlabSet ss{};
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);
@@ -527,20 +593,20 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     ss.sgd = sa;
   }
   ss.sys_store = use_x ? 1 : 0;
-  const bool reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2,
-                                   cfg_.pxt_dgrad, cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr),
-                                   false, cs_, fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
-                                   fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
-  if (!reduced) grad_reduce(ss, cs_);
+  bool reduced = false;
+  auto conv_launch = [&]() {
+    reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
+                          cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr), false, cs_,
+                          fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
+                          fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
+    if (!reduced) grad_reduce(ss, cs_);
+  };
+  schedule_backward(dist, dist && l3 && cfg_.dist_fork, use_x, fc_launch, conv_launch, sa, M, sh1);
   last_fused_reduce_ = reduced;
   last_level3_ = l3;
   last_fc_role_ = fc_role;
   if (fopt) return;
-  if (dist) {
-    launch_buckets(1, use_x, sa, M, sh1);
-    join_buckets();
-    if (use_x) return;
-  }
+  if (dist && use_x) return;
   sgd_step(P, G, M, b_.n_params, sa, sh1, b_.step_ctr, cs_);
 }
 

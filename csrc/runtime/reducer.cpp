@@ -74,9 +74,12 @@ void Reducer::launch_bucket(int b, hipStream_t compute) {
     xgmi_->all_reduce(xch_[b], comm_stream_, 1.f, true, prescale_ ? 1.f : inv);
     ++calls_;
   } else if (comm_ && comm_->world() > 1) {
-    // prescale by 1/world on the comm stream (one pass over the bucket), then SUM
-    if (!prescale_) scale_copy(flat_ + bucket_off_[b], flat_ + bucket_off_[b], bucket_num_[b], inv, comm_stream_);
-    comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
+    // DDP's prescale by 1/world folded into the reduction (RCCL pre-multiplied SUM: no
+    // separate read + write pass over the bucket); producers that prescaled already SUM
+    if (prescale_)
+      comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
+    else
+      comm_->all_reduce_premul(flat_ + bucket_off_[b], (size_t)bucket_num_[b], inv, comm_stream_);
     ++calls_;
   }
   DDP_HIP_CHECK(hipEventRecord(done_[b], comm_stream_));

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -54,10 +55,14 @@ class Comm {
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s);
   void all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t s);
   void reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s);
+  // fp32 SUM of every rank's buffer times `scale` (RCCL's pre-multiplied sum: the multiply
+  // happens inside the reduction - DDP's prescale-by-1/world without a separate pass)
+  void all_reduce_premul(float* buf, size_t count, float scale, hipStream_t s);
 
  private:
   ncclComm_t comm_ = nullptr;
   int rank_ = 0, world_ = 1;
+  std::vector<std::pair<float, ncclRedOp_t>> premul_;  // one op per scale, destroyed with the comm
 };
 
 // ---------------------------------------------------------------- direct xGMI all-reduce
@@ -242,6 +247,12 @@ struct EngineConfig {
   // 2: the fused conv backward's wgrad role runs two blocks per slab row, one per half of
   //    conv2's input channels (bf16; bit-identical slabs); 1: one block per row
   int wgrad_split = 1;
+  // world size > 1, level 3: 1 = the fc weight-gradient kernel and the fc buckets'
+  //    all-reduces run on the comm stream, forked right after the forward (a graph branch
+  //    beside the conv backward), and the conv buckets' xGMI all-reduces follow the conv
+  //    backward on the compute stream; 0 = the round-4 order (fc_bwd on the compute stream
+  //    in front of the conv backward, every all-reduce on the comm stream)
+  int dist_fork = 1;
 };
 
 // Gradient bucket of the engine's data plane: a [off, off + n) range of the flat gradient
@@ -298,6 +309,14 @@ class SimpleCNNEngine {
   void launch_buckets(int stage, bool use_x, const SgdArgs& sa, float* M, const ShadowSet& sh);
   // compute stream waits for every launched stage
   void join_buckets();
+  // the buckets of `stage` on stream s (no cross-stream ordering)
+  void enqueue_buckets(int stage, bool use_x, hipStream_t s, const SgdArgs& sa, float* M, const ShadowSet& sh);
+  // backward of a step whose forward is queued on cs_: the fc weight-gradient kernel `fc`
+  // (may be empty: the fc role runs inside the conv backward), the conv backward `conv`
+  // and, at world size > 1, the bucket all-reduces, ordered for the chain in use
+  // (dist_fork); returns with every part of the step joined into cs_
+  void schedule_backward(bool dist, bool fork, bool use_x, const std::function<void(hipStream_t)>& fc,
+                         const std::function<void()>& conv, const SgdArgs& sa, float* M, const ShadowSet& sh);
   EngineConfig cfg_;
   EngineBuffers b_;
   std::shared_ptr<Comm> comm_;
@@ -308,7 +327,7 @@ class SimpleCNNEngine {
   int last_bucket_ = -1;    // the step's last collective (advances the step counter)
   bool stage_used_[2] = {false, false};
   hipStream_t cs_ = nullptr, ms_ = nullptr;
-  hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_;
+  hipEvent_t e_b0_, e_b1_, e_d0_, e_d1_, e_fwd_, e_fc_;
   std::vector<signed char> l3_fits_;  // per batch size: -1 unknown, 0 / 1
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;

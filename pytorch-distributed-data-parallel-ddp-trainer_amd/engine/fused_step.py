@@ -34,10 +34,9 @@ from ..parallel.ddp import bucket_plan, bucket_ranges
 # buckets up to this many fp32 elements may get a one-shot xGMI channel: the bucket must
 # fit one kernel grid (1024 x 256); below it the cost model's crossover decides
 # (parallel/bucket_model.py: SimpleCNN's 75 KB conv bucket is one-shot at every N; the
-# 2 MB fc bucket (501,770 elements) is above this cap, so it is always two-shot - the
-# cost model's N = 2 one-shot crossover for it is not applied).  The module path (ddp.py)
-# uses the same cap.
-ONESHOT_MAX_ELEMS = 1024 * 256
+# 2 MB fc bucket (501,770 elements) is above this cap, so it is always two-shot).  The
+# module path (ddp.py), the planner and describe() use the same cap.
+from ..parallel.bucket_model import ONESHOT_MAX_ELEMS  # noqa: E402
 
 BF16 = torch.bfloat16
 
@@ -110,6 +109,16 @@ class EngineOptions:
     # for fp32 the dgrad role is split the same way (weights read from global) so both roles
     # run at two blocks per CU; 1 = one block per row (fp32: the round-3 kernels, 1 block/CU)
     wgrad_split: int = 2
+    # world size > 1, level 3: 1 = fc_bwd + the fc buckets' all-reduces on a graph branch
+    # forked after the forward, beside the conv backward (engine.cpp schedule_backward);
+    # 0 = the round-4 serial order (fc_bwd in front of the conv backward).  Bitwise equal.
+    dist_fork: int = 1
+    # bucket plan as for this many ranks (None: the real world size) - forced all-reduces
+    # at world size 1 (--force_allreduce) then run the multi-GPU plan's buckets
+    plan_world: int | None = None
+    # a comm_calibration fit (dict: launch_us, barrier_us, link_eff, topology, ...) measured by
+    # this job; the bucket plan and the one-shot choice are made with it
+    cost_fit: dict | None = None
 
 
 def agree(store, key: str, rank: int, world: int, ok: bool) -> bool:
@@ -138,9 +147,17 @@ class FusedSimpleCNNEngine:
         # final (fc-only buckets right after fc_bwd, overlapping the conv backward)
         from ..parallel.bucket_model import XgmiCost, engine_plan
 
-        self.cost = XgmiCost.calibrated(world_size)
+        pw = self.opts.plan_world or world_size
+        # the cost model's constants: a fit measured by this job before the engine was built
+        # (bench.py at N > 1: comm_calibration.calibrate), else a stored fit for this world
+        # size, else the defaults (XgmiCost.source records which)
+        if self.opts.cost_fit is not None:
+            self.cost = XgmiCost.from_fit(pw, self.opts.cost_fit,
+                                          source=f"fit:{self.opts.cost_fit.get('topology', 'job')}")
+        else:
+            self.cost = XgmiCost.calibrated(pw)
         if self.opts.bucket_plan == "model":
-            self.buckets, self.pred_comm_us = engine_plan(fs, world_size, self.cost)
+            self.buckets, self.pred_comm_us = engine_plan(fs, pw, self.cost)
         elif self.opts.bucket_plan == "torch":
             self.buckets, self.pred_comm_us = bucket_plan(fs, self.opts.bucket_cap_mb, self.opts.first_bucket_mb), None
         else:
@@ -206,7 +223,7 @@ class FusedSimpleCNNEngine:
                    fuse_level=self._fuse_level_ok(world_size), fuse_opt=bool(self.opts.fuse_opt),
                    store_a1=int(self.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
                    epoch_order=bool(self.opts.epoch_order), wgrad_split=int(self.opts.wgrad_split),
-                   l3_fc_role=int(self.opts.l3_fc_role))
+                   l3_fc_role=int(self.opts.l3_fc_role), dist_fork=int(self.opts.dist_fork))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
@@ -217,7 +234,7 @@ class FusedSimpleCNNEngine:
             from ..parallel.xgmi import channel_plan, create_xgmi, pick_data_plane
 
             # small buckets also get a one-shot channel (one cross-GPU barrier instead of two)
-            lim = min(ONESHOT_MAX_ELEMS, self.cost.oneshot_max_elems())
+            lim = self.cost.oneshot_cap_elems()
             oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
             self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size, oneshot=oneshot)
             if self.xgmi is not None and self.opts.comm in ("xgmi1", "xgmi2"):
@@ -238,6 +255,10 @@ class FusedSimpleCNNEngine:
                     self.xgmi, comm, fs.grads, ranges, rank, oneshot=oneshot, rccl_variants=variants)
                 if plan.startswith("rccl"):
                     comm = chosen  # the tuned communicator (algorithm / protocol) becomes the plane
+                # the candidates that lost are destroyed now (ncclCommDestroy, local), not kept
+                # with their buffers and channels for the rest of the run
+                variants = {k: c for k, c in variants.items() if c is comm}
+                del variants
             if self.xgmi is not None:
                 self.xgmi_plan = plan
                 if plan.startswith("rccl"):
@@ -300,11 +321,17 @@ class FusedSimpleCNNEngine:
         B = self.B
 
         def restore(e):
+            # the copies (and start_epoch's index / epoch-order copies before them) are queued
+            # on the production engine's stream, but engine e runs on its own: drain the device
+            # before e derives its shadows and steps, or e could read the production run's
+            # parameters / step counter
             with torch.cuda.stream(self.stream):
                 for k in keys:
                     t[k].copy_(snap[k])
+            torch.cuda.synchronize()
             e.set_momentum_started(started)
             e.refresh_shadows()
+            torch.cuda.synchronize()
 
         def run(e):
             """nsteps on engine e from the snapshot -> (params, momentum, losses) or an error."""

@@ -35,6 +35,14 @@ import torch
 import torch.nn as nn
 
 
+# Largest bucket (fp32 elements) a one-shot channel can take: the whole bucket must fit one
+# kernel grid (1024 x 256, kernels/launchers.h XGMI_MAX_BLOCKS x XGMI_THREADS) - larger
+# buckets always run two-shot, whatever the model's crossover says.  The engine (fused_step.py), the
+# module path (ddp.py), the planner and describe() all apply it, so a plan is priced with
+# the kernel that will actually run it.
+ONESHOT_MAX_ELEMS = 1024 * 256
+
+
 @dataclasses.dataclass
 class XgmiCost:
     world: int
@@ -42,6 +50,10 @@ class XgmiCost:
     link_eff: float = 0.7     # achievable share with system-scope 4-byte pulls
     barrier_us: float = 3.0   # one cross-GPU barrier
     launch_us: float = 1.5    # one more bucket kernel on the comm stream (graph node + event)
+    # where the constants came from: "default" (guesses), "stored:<key>" (a fit measured on
+    # real peers earlier, xgmi_calibration.json) or "fit:<topology>" (measured by this job,
+    # before its engine was built - bench.py at N > 1)
+    source: str = dataclasses.field(default="default", compare=False)
 
     @classmethod
     def calibrated(cls, world: int, path: str | None = None) -> "XgmiCost":
@@ -52,8 +64,13 @@ class XgmiCost:
         rec = load(path or CAL_PATH).get(f"xgmi/{world}")
         if not rec:
             return cls(world)
-        return cls(world, link_gbps=rec.get("link_gbps", 153.0), link_eff=rec["link_eff"],
-                   barrier_us=rec["barrier_us"], launch_us=rec["launch_us"])
+        return cls.from_fit(world, rec, source=f"stored:xgmi/{world}")
+
+    @classmethod
+    def from_fit(cls, world: int, fit: dict, source: str = "fit") -> "XgmiCost":
+        """The model with a fit's constants (comm_calibration.fit_cost / calibrate)."""
+        return cls(world, link_gbps=fit.get("link_gbps", 153.0), link_eff=fit["link_eff"],
+                   barrier_us=fit["barrier_us"], launch_us=fit["launch_us"], source=source)
 
     def _link_us(self, nbytes: float) -> float:
         return nbytes / (self.link_gbps * self.link_eff * 1e3)  # bytes / (GB/s) -> us
@@ -69,9 +86,18 @@ class XgmiCost:
         return self.launch_us + self.barrier_us + self._link_us(nbytes)
 
     def allreduce(self, nbytes: float) -> tuple[float, str]:
-        """(predicted us, kernel) of one bucket all-reduce."""
-        a, b = self.one_shot_us(nbytes), self.two_shot_us(nbytes)
+        """(predicted us, kernel) of one bucket all-reduce - the kernel the engine runs for it:
+        one-shot only up to :meth:`oneshot_cap_elems`."""
+        b = self.two_shot_us(nbytes)
+        if nbytes / 4 > self.oneshot_cap_elems():
+            return b, "twoshot"
+        a = self.one_shot_us(nbytes)
         return (a, "oneshot") if a <= b else (b, "twoshot")
+
+    def oneshot_cap_elems(self) -> int:
+        """Largest bucket that gets a one-shot channel: the model's crossover, capped by the
+        kernel's grid limit (ONESHOT_MAX_ELEMS)."""
+        return min(ONESHOT_MAX_ELEMS, self.oneshot_max_elems())
 
     def oneshot_max_elems(self) -> int:
         """Largest fp32 bucket for which the one-shot kernel is predicted faster: one barrier
@@ -212,11 +238,18 @@ def engine_plan(fs, world: int, cost: XgmiCost | None = None, fc_ready_us: float
     return [fs.names[i:j] for i, j in bounds], finish
 
 
-def describe(buckets, fs, cost: XgmiCost) -> list[dict]:
-    """Per-bucket record for logs / bench config: size, kernel, predicted us."""
+def describe(buckets, fs, cost: XgmiCost, ranges=None) -> list[dict]:
+    """Per-bucket record for logs / bench config: size, the kernel that runs it (one-shot
+    only within :meth:`XgmiCost.oneshot_cap_elems`, as the engine decides - by the bucket's
+    range in the flat buffer when ``ranges`` is given), predicted us, and where the cost
+    constants came from."""
     out = []
-    for b in buckets:
+    cap = cost.oneshot_cap_elems()
+    for i, b in enumerate(buckets):
         nbytes = sum(fs.numels[n] * 4 for n in b)
-        us, kind = cost.allreduce(nbytes)
-        out.append({"params": len(b), "bytes": nbytes, "kernel": kind, "pred_us": round(us, 2)})
+        n_elems = ranges[i][1] if ranges is not None else nbytes // 4
+        kind = "oneshot" if n_elems <= cap else "twoshot"
+        us = cost.one_shot_us(nbytes) if kind == "oneshot" else cost.two_shot_us(nbytes)
+        out.append({"params": len(b), "bytes": nbytes, "elems": int(n_elems), "kernel": kind,
+                    "pred_us": round(us, 2), "cost_source": cost.source})
     return out

@@ -17,8 +17,10 @@ link).  Its three free constants were guesses in round 3.  This module measures 
 
 ``XgmiCost.calibrated(world)`` uses a stored fit of the SAME world size measured on real
 peers ("xgmi"); same-GPU fits are kept as a record only (their "links" are one GPU's own
-memory).  ``bench.py`` at N > 1 sweeps and fits after its timed region and reports the fit
-(``config.comm_calibration``), so the first 8-GPU run refits the model on real xGMI links.
+memory).  ``bench.py`` at N > 1 sweeps and fits BEFORE it builds the engine (untimed),
+plans the buckets with that fit (``XgmiCost.from_fit``: ``config.bucket_plan`` records
+``cost_source = "fit:<topology>"``), reports it (``config.comm_calibration``) and, on real
+xGMI peers, stores it under ``xgmi/<N>`` with its provenance for later runs.
 """
 from __future__ import annotations
 
@@ -94,9 +96,23 @@ def sweep_xgmi(rank: int, world: int, device, elems=SWEEP_ELEMS, iters: int = 20
             e1.record()
             e1.synchronize()
             out.append((4 * int(n), kind, e0.elapsed_time(e1) * 1000.0 / iters))
-    if x.error_flags():
-        return []
-    return out
+    bad = x.error_flags() != 0
+    # every rank finished its kernels before any rank drops its channels (the peers' last
+    # all-gathers read this rank's stage buffers)
+    torch.cuda.synchronize()
+    if store is not None or world > 1:
+        import torch.distributed as dist
+
+        st = store or dist.distributed_c10d._get_default_store()
+        key = f"ddp_amd/cal_sweep_done/{next(_sweep_gen)}"
+        st.set(f"{key}/{rank}", b"1")
+        for r in range(world):
+            st.get(f"{key}/{r}")
+    del x
+    return [] if bad else out
+
+
+_sweep_gen = iter(range(1 << 30))
 
 
 def topology(world: int, store=None, rank: int = 0) -> str:

@@ -20,7 +20,9 @@ MI355X-first differences: parameters and gradients live in one flat fp32 buffer
 each (``FlatSpace``), so buckets are plain slices (no pack / unpack copies,
 ``gradient_as_bucket_view`` always on).  On GPUs the bucket all-reduces are
 issued by the native C++ reducer (``csrc/runtime/reducer.cpp``) on its own HIP
-stream through our RCCL communicator (ncclAvg); on CPU/gloo a Python reducer
+stream through our RCCL communicator (a pre-multiplied SUM: every rank's bucket times
+1/ws inside the reduction, ``Comm::all_reduce_premul``) or the direct xGMI kernels (1/ws
+in their publish pass, fixed rank-order SUM); on CPU/gloo a Python reducer
 with async c10d work handles implements the same protocol.
 """
 from __future__ import annotations
@@ -112,11 +114,9 @@ class _NativeReducer:
 
             # small buckets: the one-shot kernel (one cross-GPU barrier), below the cost
             # model's crossover for this world size and the one-grid cap the engine uses
-            # (ONESHOT_MAX_ELEMS: each one-shot channel also holds 2 x its bucket of stage
-            # memory - uncapped, every ResNet-18 bucket got one at N <= 2, ~94 MB more)
-            from ..engine.fused_step import ONESHOT_MAX_ELEMS
-
-            lim = min(ONESHOT_MAX_ELEMS, XgmiCost.calibrated(dist.get_world_size()).oneshot_max_elems())
+            # (bucket_model.ONESHOT_MAX_ELEMS: each one-shot channel also holds 2 x its bucket
+            # of stage memory - uncapped, every ResNet-18 bucket got one at N <= 2, ~94 MB more)
+            lim = XgmiCost.calibrated(dist.get_world_size()).oneshot_cap_elems()
             oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
             # the bucket kernels run next to the backward: small spinning grid
             self.xgmi = create_xgmi(fs.grads, ranges, dist.get_rank(), dist.get_world_size(),

@@ -200,10 +200,28 @@ def rccl_candidate_comms(rank: int, world: int, store=None, candidates=RCCL_CAND
         saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO")}
         os.environ["NCCL_ALGO"], os.environ["NCCL_PROTO"] = algo, proto
         comm = None
+        # vote BEFORE the collective init: a rank that cannot even start this
+        # candidate must not leave the others blocked inside ncclCommInitRank
+        uid = b""
         try:
             if rank == 0:
-                store.set(key, C.Comm.new_unique_id())
-            comm = C.Comm(store.get(key), rank, world, torch.cuda.current_device())
+                try:
+                    uid = C.Comm.new_unique_id()
+                finally:
+                    store.set(key, uid)
+            uid = store.get(key)
+        except Exception as e:  # noqa: BLE001
+            print(f"[ddp_amd] rank {rank}: RCCL {algo}/{proto} id exchange failed ({e})", file=sys.stderr)
+            uid = b""
+        if not agree(store, key + "/ready", rank, world, len(uid) > 0):
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            continue
+        try:
+            comm = C.Comm(uid, rank, world, torch.cuda.current_device())
         except Exception as e:  # noqa: BLE001 - an unsupported combination on this node
             print(f"[ddp_amd] rank {rank}: RCCL {algo}/{proto} communicator failed ({e})", file=sys.stderr)
             comm = None

@@ -82,3 +82,36 @@ def test_self_launch_falls_back_on_failing_child():
     assert rec["config"]["fallback"] == "conservative chain", rec
     assert rec["fuse_level"] == 1 and rec["comm"] == "xgmi"
     assert rec["config"]["failed_attempts"][0]["attempt"] == "production"
+
+
+def test_child_timeout_kills_the_whole_group(tmp_path):
+    """a launcher child that times out is torn down WITH its workers (its process
+    group: SIGTERM, grace, SIGKILL) before the next fallback attempt starts - a hung worker
+    must not keep the GPUs busy.  The child here spawns a grandchild that ignores SIGTERM and
+    would outlive a plain subprocess.run timeout; both must be gone when _child_json returns."""
+    import importlib.util
+    import time
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    pidfile = tmp_path / "grandchild.pid"
+    script = (
+        "import os, signal, subprocess, sys, time\n"
+        "g = subprocess.Popen([sys.executable, '-c', 'import signal, time; "
+        "signal.signal(signal.SIGTERM, signal.SIG_IGN); time.sleep(600)'])\n"
+        f"open({str(pidfile)!r}, 'w').write(str(g.pid))\n"
+        "time.sleep(600)\n")
+    t0 = time.time()
+    rec, why = bench._child_json([sys.executable, "-c", script], dict(os.environ), timeout=3)
+    assert rec is None and "timed out" in why
+    assert time.time() - t0 < 60
+    gpid = int(pidfile.read_text())
+    for _ in range(50):
+        try:
+            os.kill(gpid, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("the grandchild survived the timeout")

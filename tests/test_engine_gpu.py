@@ -387,8 +387,8 @@ def test_engine_xgmi_world1_beside_fused_reduce(fuse_level, use_graph):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("corrupt", [False, True])
-def test_verify_chain_world1_forced(corrupt):
+@pytest.mark.parametrize("corrupt,stall", [(False, False), (True, False), (False, True)])
+def test_verify_chain_world1_forced(corrupt, stall):
     """VERDICT r3 #3a on one GPU: the start-up chain check (production = level 3 + fused
     slab reduction + the xGMI kernels forced at world size 1; conservative = level 1 +
     grad_reduce over the same plane) passes bitwise and restores its snapshot exactly (the
@@ -414,6 +414,18 @@ def test_verify_chain_world1_forced(corrupt):
                                      EngineOptions(graph_steps=5, force_allreduce=True, comm="xgmi"))
             assert e.level3 and e.comm_kind.startswith("xgmi")
             e.refresh()
+            if check and stall:
+                # a long kernel queued on the production stream in front of every
+                # snapshot restore - the conservative engine (its own stream) must still start
+                # from the restored state, not race the copies
+                orig = e.start_epoch
+
+                def slow_start(ep, _orig=orig, _e=e):
+                    with torch.cuda.stream(_e.stream):
+                        torch.cuda._sleep(40_000_000)
+                    _orig(ep)
+
+                e.start_epoch = slow_start
             if check:
                 kept = e.verify_chain(_corrupt_rank=0 if corrupt else None)
                 assert e.chain_check["ran"]
@@ -469,5 +481,90 @@ def test_comm_tune_rccl_candidates_world1():
             e.synchronize()
             out.append(e.fs.params.clone())
         assert torch.equal(out[0], out[1])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("plane,dtype", [("xgmi", "bf16"), ("xgmi", "fp32"), ("rccl", "bf16")])
+def test_dist_fork_chain_bitwise_world1(plane, dtype):
+    """the multi-GPU chain with fc_bwd + the fc bucket's all-reduce on a graph
+    branch forked after the forward (dist_fork 1, engine.cpp schedule_backward) trains to the
+    same bits as the round-4 serial dist chain (dist_fork 0) and as the comm-free one-GPU
+    chain, at world size 1 with the all-reduces forced and the 8-rank bucket plan (fc bucket
+    two-shot, conv bucket one-shot), eager and graph-replayed, with momentum (the fused SGD
+    of the xGMI all-gather updates the momentum buffer too) and a ragged last batch."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import free_port, native_comm
+
+    if plane == "rccl":
+        dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}",
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}")
+    try:
+        comm = native_comm() if plane == "rccl" else None
+        imgs, labels = synthetic_mnist(1000)  # 31 full batches + a ragged one of 8
+        data = DeviceMNIST(imgs, labels, dev)
+        out = {}
+        for tag, force, fork in (("local", False, 1), ("serial", True, 0), ("fork", True, 1)):
+            torch.manual_seed(0)
+            m = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
+            e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, comm,
+                                     EngineOptions(graph_steps=5, force_allreduce=force, comm=plane,
+                                                   dist_fork=fork, plan_world=8 if force else None,
+                                                   dtype=dtype))
+            if force:
+                assert e.comm_kind.startswith(plane), e.comm_kind
+                assert len(e.ranges) == 2  # the 8-rank plan: [fc], [conv]
+            assert e.level3
+            e.refresh()
+            e.run_epoch(0)
+            e.synchronize()
+            assert e.eng.sync_error == 0 and e.eng.last_level3
+            out[tag] = (e.fs.params.clone(), e.opt.momentum_buffer.clone())
+        for tag in ("serial", "fork"):
+            assert torch.equal(out[tag][0], out["local"][0]), tag
+            assert torch.equal(out[tag][1], out["local"][1]), tag
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_premul_sum_world1_eager_and_graph():
+    """the module-path reducer's RCCL plane folds DDP's 1/ws prescale into the
+    reduction (RCCL pre-multiplied SUM, Comm::all_reduce_premul) instead of a separate
+    scale pass; at world size 1 the result is exactly x * scale (fp32 multiply), eagerly and
+    replayed from a captured graph (the host-immediate scalar is captured by value)."""
+    import torch.distributed as dist
+
+    from ddp_amd.parallel import free_port, native_comm
+
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}",
+                            device_id=torch.device("cuda", 0))
+    try:
+        comm = native_comm()
+        x = torch.randn(100_003, device=dev)
+        s = 1.0 / 3.0
+        want = x * torch.tensor(s, dtype=torch.float32, device=dev)
+        y = x.clone()
+        comm.all_reduce_premul(y, s)
+        torch.cuda.synchronize()
+        assert torch.equal(y, want)
+        z = x.clone()
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g):
+                comm.all_reduce_premul(z, s)
+        torch.cuda.current_stream().wait_stream(side)
+        z.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(z, want)
     finally:
         dist.destroy_process_group()

@@ -51,10 +51,10 @@ def parse_args(argv=None):
     p.add_argument("--num_workers", type=int, default=2, help="CPU DataLoader workers")
     p.add_argument("--max_steps", type=int, default=None, help="cap steps per epoch (module/CPU path)")
     p.add_argument("--metrics_json", default=None, help="append per-epoch img/s records (rank 0)")
-    p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1, 2, 3],
+    p.add_argument("--fuse_level", type=int, default=None, choices=[0, 1, 3],
                    help="fused engine: 0 = a1 materialised, separate conv1/xent/dgrad/wgrad/SGD kernels; "
-                        "1 = 3 kernels/step; 2 = fc + conv backward in one launch (opt-in); 3 = dZ2 in the "
-                        "forward, fc weight gradient inside the conv backward: 2 kernels/step (default)")
+                        "1 = 3 kernels/step; 3 = dZ2 in the forward, fc weight gradient inside the conv "
+                        "backward: 2 kernels/step (default)")
     p.add_argument("--comm", choices=["auto", "tune", "xgmi", "xgmi1", "xgmi2", "rccl"], default="auto",
                    help="bucket all-reduce data plane at world size > 1. Fused engine: auto = the direct xGMI "
                         "kernels (one-shot for the small bucket; RCCL if their self-test fails) - deterministic, "
