@@ -284,9 +284,12 @@ def main():
                          "all-reduces on the --comm plane at world size 1) - times the dist chain on one GPU")
     ap.add_argument("--plan_world", type=int, default=None,
                     help="bucket plan as for this many ranks (default: the world size; --force_allreduce: 8)")
-    ap.add_argument("--dist_fork", type=int, default=None, choices=[0, 1],
-                    help="N>1, level 3: fc weight gradient + fc bucket all-reduce on a branch forked after the "
-                         "forward (1, default) or in front of the conv backward (0, the round-4 order)")
+    ap.add_argument("--dist_mode", type=int, default=None, choices=[0, 1, 2],
+                    help="N>1, level 3: 2 = bucket all-reduces inside the conv backward launch (xGMI, default); "
+                         "1 = fc weight gradient + fc bucket all-reduce on a graph branch forked after the "
+                         "forward; 0 = the round-4 serial order")
+    ap.add_argument("--xar_blocks", type=int, default=None,
+                    help="dist_mode 2: most blocks per bucket channel (in-launch all-reduce role)")
     ap.add_argument("--no_breakdown", action="store_true",
                     help="N>1 / --force_allreduce: skip the comm-free local run that splits the step into "
                          "local compute and exposed communication (config.step_breakdown)")
@@ -406,7 +409,7 @@ def main():
                            bucket_plan=args.bucket_plan)
         eo.comm = args.comm
         for f in ("fuse_level", "pxt_fwd", "pxt_dgrad", "wgrad_rows", "store_a1", "wgrad_split", "l3_fc_role",
-                  "fuse_reduce", "dist_fork"):
+                  "fuse_reduce", "dist_mode", "xar_blocks"):
             if getattr(args, f) is not None and not (dtype == "fp32" and f == "store_a1"):
                 setattr(eo, f, getattr(args, f))
         if dtype == "fp32":
@@ -465,7 +468,10 @@ def main():
     plan = describe(eng.buckets, fs, eng.cost, ranges=eng.ranges) if (ws > 1 or force) else None
     finite = bool(torch.isfinite(fs.params).all().item())
     level3 = bool(eng.eng.last_level3)
-    kps = (2 if eng.eng.last_fc_role else 3) if level3 else None
+    # kernels per step of the chain that ran: 2 on one GPU and with the in-launch all-reduce;
+    # otherwise fc_bwd and one all-reduce kernel per bucket come on top
+    kps = ((2 if eng.eng.last_fc_role else 3) + (0 if eng.eng.last_xar or eng.comm_kind == "none"
+                                                  else len(eng.ranges))) if level3 else None
     same = True
     if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
         pd = dev if args.backend == "nccl" else "cpu"
@@ -522,6 +528,7 @@ def main():
                                                                        if ws > 1 and eng.pred_comm_us else None)},
                        "chain_check": eng.chain_check, "downgrades": getattr(eng, "downgrades", []),
                        "force_allreduce": force, "step_breakdown": breakdown,
+                       "inlaunch_allreduce": bool(eng.eng.last_xar),
                        "comm_calibration": calib,
                        "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
                        "fp32_level3": fp32["level3"] if fp32 else None,

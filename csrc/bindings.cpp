@@ -930,7 +930,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? cfgd["fuse_reduce"].cast<int>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
-             c.dist_fork = cfgd.contains("dist_fork") ? cfgd["dist_fork"].cast<int>() : 1;
+             c.dist_mode = cfgd.contains("dist_mode") ? cfgd["dist_mode"].cast<int>() : 2;
+             TORCH_CHECK(c.dist_mode >= 0 && c.dist_mode <= 2, "engine: dist_mode must be 0, 1 or 2");
              TORCH_CHECK(c.l3_fc_role == 0 || c.l3_fc_role == 1, "engine: l3_fc_role must be 0 or 1");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;
@@ -1024,6 +1025,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("last_fused_reduce", &SimpleCNNEngine::last_fused_reduce)
       .def_property_readonly("last_level3", &SimpleCNNEngine::last_level3)
       .def_property_readonly("last_fc_role", &SimpleCNNEngine::last_fc_role)
+      .def_property_readonly("last_xar", &SimpleCNNEngine::last_xar)
       .def("level3_active", &SimpleCNNEngine::level3_active, py::arg("batch"))
       .def_property_readonly("sync_error", &SimpleCNNEngine::sync_error)
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)

@@ -35,291 +35,15 @@
 // uncached memory; every spin is bounded (XgmiArgs::timeout_ticks of the 100 MHz clock):
 // on timeout the block sets the error word and stops waiting, so a broken peer makes
 // the result wrong (detected by the host) instead of hanging the GPU.
-#include "kernels/common.h"
-#include "kernels/launchers.h"
-#include "kernels/shadow.h"
+#include "kernels/xgmi_body.h"
 
 namespace ddp_amd {
 
-
-
-// Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
-// has signalled `target` to us.  Caller guarantees every wave drained its stores.
-// On a timeout the FIRST stalled wait is recorded in the error word (xgmi_error_code:
-// block, peer, barrier); the word stays non-zero (sticky) for every later call.
-__device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target, unsigned* s_fail, int phase) {
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < a.world && !*s_fail) {
-    unsigned* dst = a.sig[t] + XGMI_FLAG_OFF + blockIdx.x * XGMI_MAX_RANKS + a.rank;
-    // release at system scope: everything this block stored (the caller drained its
-    // waves) is visible to the peers before they can see the flag
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store(dst, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned* src = a.sig[a.rank] + XGMI_FLAG_OFF + blockIdx.x * XGMI_MAX_RANKS + t;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int)(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-        unsigned expected = 0u;
-        __hip_atomic_compare_exchange_strong(a.sig[a.rank] + XGMI_ERR_OFF, &expected,
-                                             xgmi_error_code((int)blockIdx.x, t, phase), __ATOMIC_RELAXED,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        *s_fail = 1u;
-        break;
-      }
-    }
-    // acquire at system scope: no later load of this block may hit a cache line older
-    // than the peer's release (invalidates this CU's L1 and the non-coherent L2 lines)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  }
-  __syncthreads();
-}
-
-// Data movement is in 16-byte quads (4 floats): thread t of block b handles quad
-// q = b * XGMI_THREADS + t, then q + G, q + 2G, ... (G = grid x XGMI_THREADS quads), two
-// quads at a time, with all N ranks' loads of both in flight at once - 32 B x N per lane,
-// so a small grid (XGMI_GRID_CAP blocks, leaving most CUs to the concurrent backward)
-// still keeps megabytes in flight over the 7 links.  Peer memory is read with
-// system-scope (sc0 sc1) buffer loads, stage buffers written with system-scope stores.
-// Two-shot slices are whole quads (XgmiComm rounds the slice up to a multiple of 4), so
-// every rank's slice starts on a quad; the bucket's last quad may be partial and takes
-// the per-element path.
-constexpr int SYS_CPOL = 1 | 16;  // sc0 | sc1: system scope
-typedef __attribute__((ext_vector_type(4))) int ar_i32x4;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ float4 ld4_sys(__amdgpu_buffer_rsrc_t r, long q) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(q * 16), 0, SYS_CPOL));
-}
-__device__ __forceinline__ void st4_sys(__amdgpu_buffer_rsrc_t r, long q, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ar_i32x4, v), r, (int)(q * 16), 0, SYS_CPOL);
-}
-__device__ __forceinline__ float4 add4(float4 x, float4 y) {
-  return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
-}
-
-// fixed rank-order (0..N-1) sum of quad q of every rank's source
-__device__ __forceinline__ float4 rank_sum4(const __amdgpu_buffer_rsrc_t* src, long q, int N) {
-  float4 v[XGMI_MAX_RANKS];
-#pragma unroll
-  for (int p = 0; p < XGMI_MAX_RANKS; ++p) v[p] = p < N ? ld4_sys(src[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 sum = v[0];
-#pragma unroll
-  for (int p = 1; p < XGMI_MAX_RANKS; ++p)
-    if (p < N) sum = add4(sum, v[p]);
-  return sum;
-}
-// the same for the elements [4q, lim) of a partial last quad (element loads)
-__device__ __forceinline__ float4 rank_sum_tail(float* const* src, long q, long lim, int N) {
-  float e[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const long k = 4 * q + j;
-    float sum = 0.f;
-    if (k < lim) {
-      sum = ld_sys(src[0] + k);
-#pragma unroll
-      for (int p = 1; p < XGMI_MAX_RANKS; ++p)
-        if (p < N) sum += ld_sys(src[p] + k);
-    }
-    e[j] = sum;
-  }
-  return make_float4(e[0], e[1], e[2], e[3]);
-}
-
-// the fused optimizer on flat bucket element k with reduced gradient g: same update on
-// every rank, so parameters stay bitwise identical
-__device__ __forceinline__ void sgd_elem(const XgmiArgs& a, long k, float g) {
-  const long j = a.off + k;
-  float m = a.mbuf ? a.mbuf[j] : 0.f;
-  const float pn = sgd_one(a.params[j], g, &m, a.sgd);
-  a.params[j] = pn;
-  if (a.mbuf) a.mbuf[j] = m;
-  shadow_one(a.sh, j, pn);
-}
-// quad q (elements 4q.., below lim) of the reduced bucket times scale -> my gradient
-// buffer and, with the fused optimizer (a.sgd.update), the parameters / momentum / shadows.
-// Whole quads of a 4-aligned bucket are 16-byte accesses (sgd_quad / shadow_quad: the
-// same writers as sgd_kernel); a partial last quad goes element by element.
-__device__ __forceinline__ float4 scale4(const XgmiArgs& a, float4 v) {
-  return make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
-}
-__device__ __forceinline__ void finish_quad(const XgmiArgs& a, long q, float4 v, long lim) {
-  if (4 * q + 3 < lim && (a.off & 3) == 0) {
-    const long j = a.off + 4 * q;
-    *reinterpret_cast<float4*>(a.data[a.rank] + j) = v;
-    if (a.sgd.update) {
-      const float4 pm = ld_quad(a.params, j);
-      const float4 mm = a.sgd.momentum != 0.f ? ld_quad(a.mbuf, j) : make_float4(0.f, 0.f, 0.f, 0.f);
-      sgd_quad_apply(a.params, a.mbuf, j, v, pm, mm, a.sgd, a.sh);
-    }
-    return;
-  }
-  float* d = a.data[a.rank] + a.off + 4 * q;
-  const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (4 * q + j >= lim) continue;
-    d[j] = e[j];
-    if (a.sgd.update) sgd_elem(a, 4 * q + j, e[j]);
-  }
-}
-__device__ __forceinline__ void finish4(const XgmiArgs& a, long q, float4 v, long lim) {
-  finish_quad(a, q, scale4(a, v), lim);
-}
-
 __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
-  __shared__ unsigned s_epoch, s_fail;
-  const int N = a.world, r = a.rank;
-  unsigned* my = a.sig[r];
-  // sticky failure: after any timeout every later call skips its barriers at once
-  // (the host raises on the error word; a broken run must not cost timeouts per step)
-  const bool failed_before = __hip_atomic_load(my + XGMI_ERR_OFF, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
-  if (threadIdx.x == 0) {
-    // per-block call counter (only this block of this rank touches it); every call of a
-    // channel uses the same grid, so the counters of all blocks stay equal
-    const unsigned e = my[XGMI_SEQ_OFF + blockIdx.x] + 1u;
-    my[XGMI_SEQ_OFF + blockIdx.x] = e;
-    s_epoch = e;
-    s_fail = failed_before ? 1u : 0u;
-  }
-  __syncthreads();
-  const unsigned e = s_epoch;
-  const long G = (long)gridDim.x * XGMI_THREADS;     // quads per grid stride
-  const long q0 = (long)blockIdx.x * XGMI_THREADS + threadIdx.x;
-
-  if (a.oneshot) {
-    // ---- publish my whole bucket, one barrier, sum every rank's copy in rank order
-    const long n = a.n, nq = (n + 3) / 4, fq = n / 4;  // quads, full quads
-    const long par1 = (long)(e & 1u) * ((nq * 4 + 3) & ~3L);
-    const float* mine = a.data[r] + a.off;
-    const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par1);
-    for (long q = q0; q < nq; q += G) {
-      float4 v;
-      const float ps = a.prescale;
-      if (q < fq) {
-        v = make_float4(mine[4 * q] * ps, mine[4 * q + 1] * ps, mine[4 * q + 2] * ps, mine[4 * q + 3] * ps);
-      } else {
-        float t[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = 4 * q + j < n ? mine[4 * q + j] * ps : 0.f;
-        v = make_float4(t[0], t[1], t[2], t[3]);
-      }
-      st4_sys(mystage, q, v);  // the stage holds whole quads (zero-padded tail)
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_ONESHOT);
-    if (!s_fail) {
-      __amdgpu_buffer_rsrc_t src[XGMI_MAX_RANKS];
-#pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) src[p] = sys_rsrc(p < N ? a.stage[p] + par1 : a.stage[r]);
-      long q = q0;
-      for (; q + G < nq; q += 2 * G) {
-        const float4 s0 = rank_sum4(src, q, N), s1 = rank_sum4(src, q + G, N);
-        finish4(a, q, s0, n);
-        finish4(a, q + G, s1, n);
-      }
-      if (q < nq) finish4(a, q, rank_sum4(src, q, N), n);
-    }
-    if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
-    return;
-  }
-  const long slice = a.slice;  // elements per rank slice, a multiple of 4 (the last rank's may be shorter)
-  const long sq = slice / 4;
-  const long par = (long)(e & 1u) * slice;
-  if (a.publish) {
-    // the peers' block b reads quad q of every slice of my bucket for exactly this
-    // block's q: make those elements system-visible (write-through) before arriving.
-    // Slice-relative quads, the same thread <-> quad map as RS / AG below: the AG's
-    // reduced value must land after (program order) this re-store of the local value.
-    float* mine = a.data[r] + a.off;
-    const __amdgpu_buffer_rsrc_t rm = sys_rsrc(mine);
-    const float ps = a.prescale;  // (x * 1.f == x: the plain re-store when not prescaling)
-    for (int p = 0; p < N; ++p) {
-      const long lim = min(slice, a.n - (long)p * slice);
-      for (long q = q0; 4 * q < lim; q += G) {
-        const long k = (long)p * slice + 4 * q;
-        if (4 * q + 3 < lim) {
-          st4_sys(rm, k / 4, make_float4(mine[k] * ps, mine[k + 1] * ps, mine[k + 2] * ps, mine[k + 3] * ps));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (4 * q + j < lim) st_sys(mine + k + j, mine[k + j] * ps);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_B0);  // B0
-  if (!s_fail) {
-    // ---- RS: quads of my slice, fixed-order sum over ranks 0..N-1
-    float* srcp[XGMI_MAX_RANKS];
-    __amdgpu_buffer_rsrc_t src[XGMI_MAX_RANKS];
-#pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
-      srcp[p] = (p < N ? a.data[p] : a.data[r]) + a.off + (long)r * slice;
-      src[p] = sys_rsrc(srcp[p]);
-    }
-    const long lim = min(slice, a.n - (long)r * slice);  // my slice's real length (may be <= 0)
-    const long fq = lim > 0 ? lim / 4 : 0, nq = lim > 0 ? (lim + 3) / 4 : 0;
-    const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par);
-    long q = q0;
-    for (; q + G < fq; q += 2 * G) {
-      const float4 s0 = rank_sum4(src, q, N), s1 = rank_sum4(src, q + G, N);
-      st4_sys(mystage, q, s0);
-      st4_sys(mystage, q + G, s1);
-    }
-    for (; q < nq; q += G) st4_sys(mystage, q, q < fq ? rank_sum4(src, q, N) : rank_sum_tail(srcp, q, lim, N));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  xgmi_barrier(a, 2u * e + 1u, &s_fail, XGMI_PHASE_B1);  // B1
-  if (!s_fail) {
-    // ---- AG: quad q of every rank's reduced slice into my gradient buffer
-    __amdgpu_buffer_rsrc_t st[XGMI_MAX_RANKS];
-#pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p) st[p] = sys_rsrc((p < N ? a.stage[p] : a.stage[r]) + par);
-    // every load of the iteration (N reduced quads over xGMI, and with the fused optimizer
-    // the N local parameter / momentum quads) is issued before the first store
-    const bool vec = (a.off & 3) == 0;
-    const bool mom = a.sgd.momentum != 0.f;
-    for (long q = q0; q < sq; q += G) {
-      float4 v[XGMI_MAX_RANKS], pv[XGMI_MAX_RANKS], mv[XGMI_MAX_RANKS];
-#pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
-        const long qq = (long)p * sq + q;
-        const bool ok = p < N && 4 * qq < a.n;
-        v[p] = ok ? ld4_sys(st[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool whole = ok && vec && 4 * qq + 3 < a.n;
-        pv[p] = whole && a.sgd.update ? ld_quad(a.params, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
-        mv[p] = whole && a.sgd.update && mom ? ld_quad(a.mbuf, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      // finish one peer's quad per trip (the finishing code once, not N times: unrolled N
-      // ways it made the kernel too large to unroll); the trip's registers are picked from
-      // the arrays by a select chain on the (uniform) peer index - constant array indices only
-#pragma unroll 1
-      for (int p = 0; p < N; ++p) {
-        const long qq = (long)p * sq + q;
-        if (4 * qq >= a.n) break;
-        float4 vv = v[0], pp = pv[0], mm = mv[0];
-#pragma unroll
-        for (int u = 1; u < XGMI_MAX_RANKS; ++u)
-          if (p == u) { vv = v[u]; pp = pv[u]; mm = mv[u]; }
-        const float4 d = scale4(a, vv);
-        if (vec && 4 * qq + 3 < a.n) {
-          const long j = a.off + 4 * qq;
-          *reinterpret_cast<float4*>(a.data[r] + j) = d;
-          if (a.sgd.update) sgd_quad_apply(a.params, a.mbuf, j, d, pp, mm, a.sgd, a.sh);
-        } else {
-          finish_quad(a, qq, d, a.n);
-        }
-      }
-    }
-  }
-  if (a.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
+  __shared__ unsigned s_sh[2];
+  DDP_STAMP(STAMP_K_XGMI, 0);
+  xgmi_allreduce_body(a, (int)blockIdx.x, (int)gridDim.x, s_sh);
+  DDP_STAMP(STAMP_K_XGMI, 7);
 }
 
 long xgmi_slice(long n, int world) { return (((n + world - 1) / world) + 3) & ~3L; }
@@ -334,5 +58,7 @@ int xgmi_blocks(long n, int world, bool oneshot) {
 void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s) {
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(blocks), dim3(XGMI_THREADS), 0, s, a);
 }
+
+DDP_STAMPS_SETTER(stamps_set_allreduce)
 
 }  // namespace ddp_amd

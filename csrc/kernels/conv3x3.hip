@@ -37,6 +37,7 @@
 #include "kernels/fc_bwd_body.h"
 #include "kernels/launchers.h"
 #include "kernels/slab_reduce.h"
+#include "kernels/xgmi_body.h"
 
 namespace ddp_amd {
 
@@ -1245,15 +1246,82 @@ __device__ __forceinline__ void fc_role_chunk(const BwdFc& fcr, const float* s_d
   else fc_dw_wave_chunk<BFC_MAXB>(s_dl, a2, fcr.dW, fcr.scale, B, fcr.K, fcr.ex, q * 128);
 }
 
+// Spin until *cnt >= want (wave 0 polls with sleeps between polls, so the waiting block
+// takes few issue slots from the conv waves sharing its CU); false on a timeout, after
+// setting *err = code.  Then every thread of the block acquires at agent scope.
+__device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, int code) {
+  __shared__ int s_ok;
+  if (threadIdx.x < 64) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > DZ_WAIT_TICKS) {
+        if (threadIdx.x == 0 && err) __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return s_ok != 0;
+}
+
+// this block's global stores are out (each wave drained), then one count: the release that
+// wait_count's acquire pairs with
+__device__ __forceinline__ void count_done(int* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
-          bool FCR = false, int DG = 1>
+          bool FCR = false, int DG = 1, bool XAR = false>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv3x3_bwd_kernel(
     const T* __restrict__ dY, const T* __restrict__ WT, T* __restrict__ dX,
     float* __restrict__ w1slab, float* __restrict__ slab, int B, int H, int W, int Cin, int Cout,
-    int R, int nd, C1Src c1, const T* __restrict__ Xact, BwdReduce red, BwdFc fcr) {
+    int R, int nd, C1Src c1, const T* __restrict__ Xact, BwdReduce red, BwdFc fcr, BwdXar xar) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // conv-role index: the fc-role blocks [fc0, fc0 + nfc) are cut out of the grid order
+  // conv-role index: the in-launch all-reduce blocks (XAR, the grid's head) and the fc-role
+  // blocks [fc0, fc0 + nfc) are cut out of the grid order
   int cb = (int)blockIdx.x;
+  if constexpr (XAR) {
+    static_assert(FCR && FRED, "the in-launch all-reduce waits for the fc role and the fused reduction");
+    // multi-GPU level-3 step (BwdXar): the bucket all-reduces run here, each as soon as its
+    // gradients are final - the fc bucket while the conv roles still run (SURVEY.md §2.6 I6:
+    // DDP's bucket 0 overlapping the rest of the backward), the conv bucket right behind the
+    // last fused reducer.  These blocks come first in the grid, so they are dispatched
+    // before every block they wait for (in-order dispatch: no deadlock whatever the grid's
+    // residency); each waits only for this launch's producers and for the same role block of
+    // its peers (which is at the head of their grids too).
+    const int nx = xar.nblk0 + xar.nblk1;
+    if (cb < nx) {
+      unsigned* s_sh = reinterpret_cast<unsigned*>(smem);
+      if (cb < xar.nblk0) {
+        if (wait_count(xar.fc_done, xar.fc_expect, xar.err, XAR_ERR))
+          xgmi_allreduce_body(xar.args[0], cb, xar.nblk0, s_sh);
+      } else {
+        if (wait_count(xar.fc_done, xar.fc_expect, xar.err, XAR_ERR) &&
+            wait_count(xar.red_done, xar.red_expect, xar.err, XAR_ERR))
+          xgmi_allreduce_body(xar.args[1], cb - xar.nblk0, xar.nblk1, s_sh);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        // the step's last work item advances the batch window (the fc role read it before
+        // counting itself into fc_done, which every role block waited for)
+        const int old = __hip_atomic_fetch_add(xar.xar_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nx - 1 && xar.step_ctr) xar.step_ctr[0] += 1;
+      }
+      return;
+    }
+    cb -= nx;
+  }
   if constexpr (FCR) {
     const int f = cb - fcr.fc0;
     if (f >= 0 && f < fcr.nfc) {
@@ -1272,6 +1340,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
       const int q = f * 4 + (threadIdx.x >> 6);
       if (q < nch) fc_role_chunk<T>(fcr, s_dl, B, q);
       DDP_STAMP(STAMP_K_FC_BWD, 4);
+      if constexpr (XAR) count_done(xar.fc_done);  // the fc bucket's gradient rows are out
       return;
     }
     if (f >= 0) cb -= fcr.nfc;
@@ -1366,6 +1435,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
     }
     if (w == 0 && threadIdx.x == 0 && red.ss.step_ctr) red.ss.step_ctr[0] += 1;
     DDP_STAMP(STAMP_K_GRAD_REDUCE, 2);
+    if constexpr (XAR) count_done(xar.red_done);  // this reducer's conv gradients are out
   }
 }
 
@@ -1663,17 +1733,20 @@ static int fused_reducers(K kernel, size_t lds, int nblocks, bool exclusive) {
 
 template <typename T>
 using BwdKFn = void (*)(const T*, const T*, T*, float*, float*, int, int, int, int, int, int, int, C1Src, const T*,
-                        BwdReduce, BwdFc);
+                        BwdReduce, BwdFc, BwdXar);
 
 // The conv backward instantiation a launch runs (chosen BEFORE the fused reduction's residency
 // query, so that query sees the exact kernel - its registers decide its residency).
 // cs == 2 and FCR: the bf16 SimpleCNN variants only (FCR: pxt 2, channel split).
+// xar: the in-launch all-reduce variant (FCR + FRED only: bf16 pxt 2 channel split, or the
+// exact-fp32 double split) - callers check xar_ok first
 template <typename T, int PX, bool DA, bool WA>
-static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr, int dg) {
+static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr, int dg, bool xar = false) {
   if (!g) return conv3x3_bwd_kernel<T, PX, DA, WA, 0, 0, 0, 0, false>;
   if constexpr (sizeof(T) == 2) {
     if (cs == 2) {
       if constexpr (PX == 2) {
+        if (xar && fcr && fred) return conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true, 1, true>;
         if (fcr)
           return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true>
                       : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, true>;
@@ -1687,6 +1760,7 @@ static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr, int dg) {
     if constexpr (PX == 2 && DA && WA) {
       if (cs == 2) {
         if (dg == 2) {
+          if (xar && fcr && fred) return conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true, 2, true>;
           if (fcr)
             return fred ? conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, true, 2, true, 2>
                         : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false, 2, true, 2>;
@@ -1705,9 +1779,9 @@ static BwdKFn<T> pick_bwd3(bool g, bool fred, int cs, bool fcr, int dg) {
               : conv3x3_bwd_kernel<T, PX, DA, WA, 28, 28, 32, 64, false>;
 }
 template <typename T>
-static BwdKFn<T> pick_bwd(int pxt, bool da, bool wa, bool g, bool fred, int cs, bool fcr, int dg) {
+static BwdKFn<T> pick_bwd(int pxt, bool da, bool wa, bool g, bool fred, int cs, bool fcr, int dg, bool xar = false) {
   if (pxt == 2) {
-    if (da) return pick_bwd3<T, 2, true, true>(g, fred, cs, fcr, dg);
+    if (da) return pick_bwd3<T, 2, true, true>(g, fred, cs, fcr, dg, xar);
     return wa ? pick_bwd3<T, 2, false, true>(g, fred, cs, fcr, dg) : pick_bwd3<T, 2, false, false>(g, fred, cs, fcr, dg);
   }
   if (da) return pick_bwd3<T, 1, true, true>(g, fred, cs, fcr, dg);
@@ -1722,7 +1796,8 @@ template <typename T>
 static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* slab, int B, int H, int W,
                        int Cin, int Cout, int pxt, int R, const C1Src& c1, const T* Xact,
                        bool wgrad_load_a1, hipStream_t s, const SlabSet* fused, int* red_done, int* red_err,
-                       int csplit, const BwdFc* fc, bool exclusive) {
+                       int csplit, const BwdFc* fc, bool exclusive, const BwdXar* xar, bool* xar_used) {
+  if (xar_used) *xar_used = false;
   const bool g = simplecnn_geom(H, W, Cin, Cout);
   // the channel split (SimpleCNN geometry): bf16 - two wgrad blocks per slab row; exact fp32
   // (pxt 2, conv1 recomputed) - two wgrad blocks per row AND two dgrad blocks per pixel
@@ -1759,9 +1834,10 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     nfc = (int)((fc->K + 127) / 128 + 3) / 4;
     fcr.nfc = nfc;
     // fc blocks after every conv block (default) or before them (A/B knob DDP_AMD_FC_FIRST=1:
-    // B = 32 838k vs 954k img/s in-call, B = 64 within the spread - profiles/r4_b64)
+    // B = 32 838k vs 954k img/s in-call, B = 64 within the spread - profiles/r4_b64); with
+    // the in-launch all-reduce always first: the fc bucket's all-reduce waits for them
     const char* ff = std::getenv("DDP_AMD_FC_FIRST");
-    const bool first = ff && ff[0] == '1';
+    const bool first = (ff && ff[0] == '1') || xar != nullptr;
     fcr.fc0 = first ? 0 : nd + nw;
     if ((size_t)B * (FCDW_LD + 10) * sizeof(float) > lds)
       throw std::runtime_error("conv3x3_bwd: LDS too small for the fc role");
@@ -1785,7 +1861,7 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     // slower - their polling shares the CUs of the still-running wgrad blocks)
     // (channel split: the last nrows blocks - as many reducers as without the split).
     // Residency of the exact instantiation that will run.
-    const BwdKFn<T> kf = pick_bwd<T>(pxt, da, wa, g, true, cs, fc != nullptr, dcs);
+    const BwdKFn<T> kf = pick_bwd<T>(pxt, da, wa, g, true, cs, fc != nullptr, dcs, xar != nullptr);
     lds_optin(kf, lds);
     const int nr = (g && red_done) ? fused_reducers(kf, lds, nrows, exclusive) : 0;
     if (nr <= 0) fused = nullptr;  // the caller reduces with grad_reduce
@@ -1806,27 +1882,43 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     red.err = red_err;
     if (lds < sizeof(float) * 3 * 16 * 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the reducer");
   }
+  // the in-launch bucket all-reduce (BwdXar): needs the fc role and the fused reduction in
+  // this launch (its waits count their blocks); otherwise the caller runs the bucket kernels
+  BwdXar xv;
+  int nx = 0;
+  const bool use_xar = xar && fc && fused && pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, true) !=
+                                                pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, false);
+  if (use_xar) {
+    xv = *xar;
+    xv.fc_expect = nfc;
+    xv.red_expect = nd + nw - red.first_reducer;  // the reducers
+    nx = xv.nblk0 + xv.nblk1;
+    if (xv.nblk1 <= 0 || !xv.args || !xv.fc_done || !xv.red_done || !xv.xar_done)
+      throw std::runtime_error("conv3x3_bwd: in-launch all-reduce needs a conv bucket and its counters");
+    if (lds < 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the all-reduce role");
+    if (xar_used) *xar_used = true;
+  }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32
-  const BwdKFn<T> k = pick_bwd<T>(pxt, da, wa, g, fused != nullptr, cs, fc != nullptr, dcs);
+  const BwdKFn<T> k = pick_bwd<T>(pxt, da, wa, g, fused != nullptr, cs, fc != nullptr, dcs, use_xar);
   lds_optin(k, lds);
-  hipLaunchKernelGGL(k, dim3(nd + nw + nfc), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, R,
-                     nd, c1, Xact, red, fcr);
+  hipLaunchKernelGGL(k, dim3(nx + nd + nw + nfc), dim3(256), lds, s, dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout,
+                     R, nd, c1, Xact, red, fcr, xv);
   return fused != nullptr;
 }
 
 bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
-                 int wgrad_split, const BwdFc* fc, bool exclusive) {
+                 int wgrad_split, const BwdFc* fc, bool exclusive, const BwdXar* xar, bool* xar_used) {
   return bwd_launch<bf16_t>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                     fused_reduce, red_done, red_err, wgrad_split, fc, exclusive);
+                     fused_reduce, red_done, red_err, wgrad_split, fc, exclusive, xar, xar_used);
 }
 bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, float* slab, int B,
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce, int* red_done, int* red_err,
-                 int wgrad_split, const BwdFc* fc, bool exclusive) {
+                 int wgrad_split, const BwdFc* fc, bool exclusive, const BwdXar* xar, bool* xar_used) {
   return bwd_launch<float>(dY, WT, dX, w1slab, slab, B, H, W, Cin, Cout, pxt, R, c1, Xact, wgrad_load_a1, s,
-                    fused_reduce, red_done, red_err, wgrad_split, fc, exclusive);
+                    fused_reduce, red_done, red_err, wgrad_split, fc, exclusive, xar, xar_used);
 }
 
 DDP_STAMPS_SETTER(stamps_set_conv3x3)

@@ -78,6 +78,7 @@ int conv3x3_dgrad_blocks(int B, int H, int W, int pxt);
 // blocks per slab row, one per half of the input channels (bit-identical slabs).
 struct SlabSet;
 struct BwdFc;
+struct BwdXar;
 constexpr int SYNC_RED_INTS = 256;  // ints of the 8 arrival counters (32 apart) of red_done
 // fc != null (fuse level 3, single process): the same launch also runs the fc weight
 // gradient + fused SGD as a third role (conv3x3_bwd_fc_role_ok shapes only; BwdFc below)
@@ -85,7 +86,7 @@ bool conv3x3_bwd(const bf16_t* dY, const bf16_t* WT, bf16_t* dX, float* w1slab, 
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const bf16_t* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
                  int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr,
-                 bool exclusive = false);
+                 bool exclusive = false, const BwdXar* xar = nullptr, bool* xar_used = nullptr);
 bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split);
 // exact fp32: wgrad_split 2 (pxt 2, conv1 recomputed) splits both roles over input-channel
 // halves at two blocks per CU (dgrad weights read from global); bit-identical to split 1
@@ -93,7 +94,7 @@ bool conv3x3_bwd(const float* dY, const float* WT, float* dX, float* w1slab, flo
                  int H, int W, int Cin, int Cout, int pxt, int R, const C1Src& c1, const float* Xact,
                  bool wgrad_load_a1, hipStream_t s, const SlabSet* fused_reduce = nullptr,
                  int* red_done = nullptr, int* red_err = nullptr, int wgrad_split = 1, const BwdFc* fc = nullptr,
-                 bool exclusive = false);
+                 bool exclusive = false, const BwdXar* xar = nullptr, bool* xar_used = nullptr);
 size_t conv3x3_bwd_lds(int W, int Cin, int Cout, int pxt, int R, int es = 2, int cs = 1);
 int conv3x3_wgrad_blocks(int B, int H, int R);
 size_t conv3x3_wgrad_lds(int W, int Cin, int Cout, int R, bool a1x = false, int es = 2);
@@ -403,5 +404,27 @@ struct XgmiArgs {
 long xgmi_slice(long n, int world);  // two-shot slice: n / world rounded up to whole quads
 int xgmi_blocks(long n, int world, bool oneshot = false);
 void xgmi_allreduce(const XgmiArgs& a, int blocks, hipStream_t s);
+
+// In-launch bucket all-reduce of the multi-GPU level-3 step (engine dist_mode 2,
+// conv3x3.hip XAR): role blocks at the HEAD of the conv backward grid run the direct xGMI
+// all-reduce + fused SGD (xgmi_body.h) of each gradient bucket as soon as its gradients are
+// final inside the same launch - bucket 0 (the fc bucket) once every fc-role block has
+// counted itself into fc_done, bucket 1 (the conv bucket) once every fused slab reducer has
+// counted itself into red_done (and the fc role too: a single bucket may hold both).  No
+// kernel boundary and no cross-stream edge separates a gradient from its all-reduce.
+struct BwdXar {
+  // [0] / [1]: the stage-0 / stage-1 bucket's arguments (XgmiComm::make_args, step_ctr null)
+  // in DEVICE memory - held in the kernel-argument struct, the compiler copied the whole
+  // struct to scratch for the body's rank-indexed peer pointers
+  const XgmiArgs* args = nullptr;
+  int nblk0 = 0, nblk1 = 0;   // role blocks = the channel's grid (XgmiComm::blocks); 0 = none
+  int* fc_done = nullptr;     // completion counters, zeroed by the step's forward
+  int* red_done = nullptr;
+  int* xar_done = nullptr;    // role blocks done: the last one advances step_ctr
+  int fc_expect = 0, red_expect = 0;  // (set by the launcher)
+  int* step_ctr = nullptr;
+  int* err = nullptr;         // 4: a completion wait timed out
+};
+constexpr int XAR_ERR = 4;
 
 }  // namespace ddp_amd

@@ -153,12 +153,14 @@ void stamps_set_conv1(void*);
 void stamps_set_conv3x3(void*);
 void stamps_set_linear(void*);
 void stamps_set_xent(void*);
+void stamps_set_allreduce(void*);
 void stamps_set(void* p) {
   stamps_set_optim(p);
   stamps_set_conv1(p);
   stamps_set_conv3x3(p);
   stamps_set_linear(p);
   stamps_set_xent(p);
+  stamps_set_allreduce(p);
 }
 
 }  // namespace ddp_amd

@@ -35,6 +35,7 @@
 // bucket plan works (stage 0 = fc-only buckets, stage 1 = the rest).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "runtime/runtime.h"
 
@@ -90,6 +91,7 @@ SimpleCNNEngine::~SimpleCNNEngine() {
   if (cs_) hipStreamSynchronize(cs_);
   destroy_graph();
   for (hipEvent_t e : {e_b0_, e_b1_, e_d0_, e_d1_, e_fwd_, e_fc_}) hipEventDestroy(e);
+  for (XarArgs& e : xar_cache_) hipFree(const_cast<XgmiArgs*>(e.dev));
   if (err_host_) hipHostFree(err_host_);
 }
 
@@ -105,10 +107,12 @@ void SimpleCNNEngine::synchronize() {
   DDP_HIP_CHECK(hipStreamSynchronize(cs_));
   if (const int e = sync_error()) {
     throw std::runtime_error(std::string("engine: an in-launch hand-off wait timed out (") +
-                             (e == 2 ? "fused slab reduction" : "level-3 forward dZ2") +
+                             (e == 2 ? "fused slab reduction" : e == XAR_ERR ? "in-launch all-reduce" : "level-3 forward dZ2") +
                              "); results invalid");
   }
 }
+
+bool SimpleCNNEngine::sync_ok_for_xar() const { return b_.sync_flags != nullptr && b_.sync_err != nullptr; }
 
 bool SimpleCNNEngine::level3_active(int batch) {
   if (cfg_.fuse_level < 3 || !b_.sync_flags || !b_.sync_err) return false;
@@ -203,7 +207,10 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // level 3, single process: the fc weight gradient runs as a third role of the conv
   // backward launch (2 kernels per step); at world size > 1 it runs as its own light kernel
   // before it (the fc bucket's all-reduce then overlaps the conv backward)
-  const bool fc_role = l3 && !dist && cfg_.l3_fc_role &&
+  // dist_mode 2 (xGMI): the same fc role inside the conv backward at world size > 1, its
+  // gradient all-reduced in-launch (make_xar / BwdXar)
+  const bool xar_mode = dist && use_x && l3 && cfg_.dist_mode == 2 && xar_plan_ok_;
+  const bool fc_role = l3 && (!dist || xar_mode) && cfg_.l3_fc_role &&
                        conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
   const C1Src* pc1 = f1 ? &c1 : nullptr;
   BatchIdx bid{nullptr, nullptr, 0, 0};
@@ -337,26 +344,36 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   }
   ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
   bool reduced = false;  // the conv backward launch also did grad_reduce's work
+  BwdXar xa;
+  const bool want_xar = xar_mode && fc_role && fred && make_xar(xa, sa, M, sh_all);
+  bool xar_used = false;
   auto conv_launch = [&]() {
     if (f1) {
       // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
       reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                             cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
                             fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
-                            fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
+                            fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2, want_xar ? &xa : nullptr,
+                            &xar_used);
     } else {
       conv3x3_dgrad(b_.dz2, nullptr, b_.w2t_bf16, b_.a1, b_.dz1, B, H, W, C1, C2, b_.images, true, bi,
                     b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
       conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
     }
     if (!reduced) grad_reduce(ss, cs_);
+    if (xar_mode && !xar_used) {  // the in-launch all-reduce did not apply: bucket kernels behind it
+      enqueue_buckets(0, use_x, cs_, sa, M, sh_all);
+      enqueue_buckets(1, use_x, cs_, sa, M, sh_all);
+    }
   };
-  // fc buckets overlap the conv backward; at level 3 the fc weight gradient itself forks
-  // off the compute stream after the forward (dist_fork)
-  schedule_backward(dist, dist && l3 && cfg_.dist_fork, use_x, fc_launch, conv_launch, sa, M, sh_all);
+  // fc buckets overlap the conv backward: in-launch (dist_mode 2), or the fc weight gradient
+  // forks off the compute stream after the forward (dist_mode 1)
+  if (xar_mode) conv_launch();
+  else schedule_backward(dist, dist && l3 && cfg_.dist_mode == 1, use_x, fc_launch, conv_launch, sa, M, sh_all);
   last_fused_reduce_ = reduced;
   last_level3_ = l3;
   last_fc_role_ = fc_role;
+  last_xar_ = xar_used;
   if (fopt) return;
   if (dist && use_x) return;  // the optimizer ran inside the all-reduces
   // ---- optimizer + bf16 shadows + next batch window
@@ -384,7 +401,45 @@ void SimpleCNNEngine::enqueue_buckets(int stage, bool use_x, hipStream_t s, cons
   }
 }
 
-// World size > 1 (or forced), dist_fork, level 3 - the forward already wrote dL and dZ2, so
+bool SimpleCNNEngine::make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh) {
+  if (!xgmi_ || !xar_plan_ok_) return false;
+  XgmiArgs pair[2] = {};
+  for (int b = 0; b < (int)buckets_.size(); ++b) {
+    // the bucket's fused optimizer; the in-launch roles advance the step counter themselves
+    pair[stage_[b]] = xgmi_->make_args(xch_[b], sa, b_.params, M, sh, nullptr);
+    (stage_[b] == 0 ? xa.nblk0 : xa.nblk1) = xgmi_->blocks(xch_[b]);
+  }
+  // the pair lives in device memory, one immutable copy per distinct content (a captured
+  // graph keeps pointing at the copy it was captured with): the momentum-init step's and
+  // the steady state's, a few more if the learning rate changes
+  const XgmiArgs* dev = nullptr;
+  for (const XarArgs& e : xar_cache_)
+    if (std::memcmp(e.host, pair, sizeof(pair)) == 0) dev = e.dev;
+  if (!dev) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    DDP_HIP_CHECK(hipStreamIsCapturing(cs_, &st));
+    if (st != hipStreamCaptureStatusNone)
+      throw std::runtime_error("engine: new in-launch all-reduce arguments during graph capture");
+    XarArgs e;
+    std::memcpy(e.host, pair, sizeof(pair));
+    XgmiArgs* d = nullptr;
+    DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), sizeof(pair)));
+    DDP_HIP_CHECK(hipMemcpy(d, pair, sizeof(pair), hipMemcpyHostToDevice));
+    e.dev = d;
+    xar_cache_.push_back(e);
+    dev = d;
+  }
+  xa.args = dev;
+  // three counters of the step's zeroed hand-off words (the forward clears [0, L3_IMG_OFF))
+  xa.fc_done = b_.sync_flags + SYNC_RED_INTS + 8;
+  xa.red_done = b_.sync_flags + SYNC_RED_INTS + 16;
+  xa.xar_done = b_.sync_flags + SYNC_RED_INTS + 24;
+  xa.step_ctr = b_.step_ctr;
+  xa.err = b_.sync_err;
+  return true;
+}
+
+// World size > 1 (or forced), dist_mode 1, level 3 - the forward already wrote dL and dZ2, so
 // the fc weight gradient depends on the forward alone:
 //
 //   cs_: forward -> conv backward (+ fused slab reduction) -> [xGMI] conv buckets -> join
@@ -496,7 +551,8 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     dzo.dl_out = b_.dlogits;
     dzo.loss_rows = b_.loss_rows;
   }
-  const bool fc_role = l3 && !dist && cfg_.l3_fc_role &&
+  const bool xar_mode = dist && use_x && l3 && cfg_.dist_mode == 2 && xar_plan_ok_;
+  const bool fc_role = l3 && (!dist || xar_mode) && cfg_.l3_fc_role &&
                        conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
 
   // ---- forward: conv1 (recomputed) + conv2 + bias + ReLU -> a2, fused fc partial logits
@@ -594,17 +650,27 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   }
   ss.sys_store = use_x ? 1 : 0;
   bool reduced = false;
+  BwdXar xa;
+  const bool want_xar = xar_mode && fc_role && fred && make_xar(xa, sa, M, sh1);
+  bool xar_used = false;
   auto conv_launch = [&]() {
     reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                           cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr), false, cs_,
                           fred ? &ss : nullptr, b_.sync_flags, b_.sync_err, cfg_.wgrad_split,
-                          fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2);
+                          fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2, want_xar ? &xa : nullptr,
+                          &xar_used);
     if (!reduced) grad_reduce(ss, cs_);
+    if (xar_mode && !xar_used) {
+      enqueue_buckets(0, use_x, cs_, sa, M, sh1);
+      enqueue_buckets(1, use_x, cs_, sa, M, sh1);
+    }
   };
-  schedule_backward(dist, dist && l3 && cfg_.dist_fork, use_x, fc_launch, conv_launch, sa, M, sh1);
+  if (xar_mode) conv_launch();
+  else schedule_backward(dist, dist && l3 && cfg_.dist_mode == 1, use_x, fc_launch, conv_launch, sa, M, sh1);
   last_fused_reduce_ = reduced;
   last_level3_ = l3;
   last_fc_role_ = fc_role;
+  last_xar_ = xar_used;
   if (fopt) return;
   if (dist && use_x) return;
   sgd_step(P, G, M, b_.n_params, sa, sh1, b_.step_ctr, cs_);
@@ -625,6 +691,18 @@ void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> cha
   destroy_graph();
   xgmi_ = std::move(x);
   xch_ = xgmi_ ? channels : std::vector<int>(buckets_.size(), -1);
+  // the in-launch all-reduce (dist_mode 2) takes at most one bucket per stage, a conv-stage
+  // bucket, and few role blocks (they wait at the head of the grid: <= 64 of its >= 256
+  // resident slots, next to the fused reducers' half)
+  xar_plan_ok_ = false;
+  if (xgmi_ && sync_ok_for_xar()) {
+    int per[2] = {0, 0}, nb = 0;
+    for (int b = 0; b < (int)buckets_.size(); ++b) {
+      ++per[stage_[b]];
+      nb += xgmi_->blocks(xch_[b]);
+    }
+    xar_plan_ok_ = per[0] <= 1 && per[1] == 1 && nb <= 64;
+  }
 }
 
 void SimpleCNNEngine::step(int batch, int batch_stride) {

@@ -93,6 +93,10 @@ class XgmiComm {
   void all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
                       const ShadowSet& sh, int* step_ctr, float scale = 1.f, bool publish = false,
                       float prescale = 1.f);
+  // the kernel arguments all_reduce_sgd would launch with (the in-launch all-reduce role of
+  // the conv backward runs the same body from them, with blocks(channel) blocks)
+  XgmiArgs make_args(int channel, const SgdArgs& sgd, float* params, float* mbuf, const ShadowSet& sh,
+                     int* step_ctr, float scale = 1.f, bool publish = false, float prescale = 1.f) const;
   // != 0: a barrier timed out (result invalid) - the first failed channel's error word
   // (xgmi_error_code: block, peer, barrier)
   unsigned error_flags() const;
@@ -247,12 +251,17 @@ struct EngineConfig {
   // 2: the fused conv backward's wgrad role runs two blocks per slab row, one per half of
   //    conv2's input channels (bf16; bit-identical slabs); 1: one block per row
   int wgrad_split = 1;
-  // world size > 1, level 3: 1 = the fc weight-gradient kernel and the fc buckets'
-  //    all-reduces run on the comm stream, forked right after the forward (a graph branch
-  //    beside the conv backward), and the conv buckets' xGMI all-reduces follow the conv
-  //    backward on the compute stream; 0 = the round-4 order (fc_bwd on the compute stream
-  //    in front of the conv backward, every all-reduce on the comm stream)
-  int dist_fork = 1;
+  // world size > 1, level 3 - how the backward meets the bucket all-reduces:
+  //  2 = in-launch (xGMI, at most one bucket per stage): the fc weight gradient runs as the
+  //      conv backward's fc role, and role blocks at the head of that same launch all-reduce
+  //      each bucket (+ fused SGD) as soon as its gradients are final (BwdXar) - 2 kernels
+  //      per step, no cross-stream edge; falls back to the bucket kernels on the compute
+  //      stream when a condition fails (RCCL: mode 1)
+  //  1 = fork: fc_bwd and the fc buckets' all-reduces on the comm stream, forked after the
+  //      forward beside the conv backward (a graph branch), the conv buckets' all-reduces
+  //      behind the conv backward
+  //  0 = the round-4 order (fc_bwd in front of the conv backward, all-reduces on ms_)
+  int dist_mode = 2;
 };
 
 // Gradient bucket of the engine's data plane: a [off, off + n) range of the flat gradient
@@ -292,6 +301,8 @@ class SimpleCNNEngine {
   bool last_level3() const { return last_level3_; }
   // ... and whether its fc weight gradient ran as a role of the conv backward launch
   bool last_fc_role() const { return last_fc_role_; }
+  // ... and whether its bucket all-reduces ran inside the conv backward launch (dist_mode 2)
+  bool last_xar() const { return last_xar_; }
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
   // bucket b; set before capturing a graph
@@ -314,9 +325,13 @@ class SimpleCNNEngine {
   // backward of a step whose forward is queued on cs_: the fc weight-gradient kernel `fc`
   // (may be empty: the fc role runs inside the conv backward), the conv backward `conv`
   // and, at world size > 1, the bucket all-reduces, ordered for the chain in use
-  // (dist_fork); returns with every part of the step joined into cs_
+  // (dist_mode 0 / 1); returns with every part of the step joined into cs_
   void schedule_backward(bool dist, bool fork, bool use_x, const std::function<void(hipStream_t)>& fc,
                          const std::function<void()>& conv, const SgdArgs& sa, float* M, const ShadowSet& sh);
+  // dist_mode 2 with this bucket plan / data plane: the in-launch all-reduce's arguments for
+  // this step (false: not applicable - the caller uses the bucket kernels)
+  bool make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh);
+  bool sync_ok_for_xar() const;
   EngineConfig cfg_;
   EngineBuffers b_;
   std::shared_ptr<Comm> comm_;
@@ -336,6 +351,13 @@ class SimpleCNNEngine {
   bool last_fused_reduce_ = false;
   bool last_level3_ = false;
   bool last_fc_role_ = false;
+  bool last_xar_ = false;
+  bool xar_plan_ok_ = false;  // set_xgmi: the bucket plan fits the in-launch all-reduce
+  struct XarArgs {
+    XgmiArgs host[2];
+    const XgmiArgs* dev = nullptr;
+  };
+  std::vector<XarArgs> xar_cache_;  // make_xar: device copies of the in-launch arguments
   bool plain_stale_ = false;  // level-3 steps skipped the plain bf16 fc shadow
   int* err_host_ = nullptr;  // coherent host word behind b_.sync_err
 };

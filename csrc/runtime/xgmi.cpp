@@ -144,9 +144,8 @@ void XgmiComm::all_reduce(int channel, hipStream_t s, float scale, bool publish,
   all_reduce_sgd(channel, s, SgdArgs{}, nullptr, nullptr, ShadowSet{}, nullptr, scale, publish, prescale);
 }
 
-void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params,
-                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale, bool publish,
-                              float prescale) {
+XgmiArgs XgmiComm::make_args(int channel, const SgdArgs& sgd, float* params, float* mbuf, const ShadowSet& sh,
+                              int* step_ctr, float scale, bool publish, float prescale) const {
   if (!imported_) throw std::runtime_error("xgmi: import_handles first");
   if (channel < 0 || channel >= (int)ch_.size()) throw std::runtime_error("xgmi: bad channel");
   const Channel& c = ch_[channel];
@@ -174,7 +173,14 @@ void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, fl
   a.sh = sh;
   a.step_ctr = step_ctr;
   if (sgd.update && !params) throw std::runtime_error("xgmi: fused SGD needs the parameter buffer");
-  xgmi_allreduce(a, c.blocks, s);
+  return a;
+}
+
+void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, float* params,
+                              float* mbuf, const ShadowSet& sh, int* step_ctr, float scale, bool publish,
+                              float prescale) {
+  const XgmiArgs a = make_args(channel, sgd, params, mbuf, sh, step_ctr, scale, publish, prescale);
+  xgmi_allreduce(a, ch_[channel].blocks, s);
   DDP_HIP_CHECK(hipGetLastError());
 }
 

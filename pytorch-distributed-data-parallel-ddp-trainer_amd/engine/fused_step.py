@@ -109,10 +109,17 @@ class EngineOptions:
     # for fp32 the dgrad role is split the same way (weights read from global) so both roles
     # run at two blocks per CU; 1 = one block per row (fp32: the round-3 kernels, 1 block/CU)
     wgrad_split: int = 2
-    # world size > 1, level 3: 1 = fc_bwd + the fc buckets' all-reduces on a graph branch
-    # forked after the forward, beside the conv backward (engine.cpp schedule_backward);
-    # 0 = the round-4 serial order (fc_bwd in front of the conv backward).  Bitwise equal.
-    dist_fork: int = 1
+    # world size > 1, level 3 - how the backward meets the bucket all-reduces (all bitwise
+    # equal): 2 = in-launch (xGMI plane): the fc weight gradient is the conv backward's fc
+    # role and role blocks at the head of that launch all-reduce each bucket (+ fused SGD) as
+    # soon as it is final - 2 kernels per step, as on one GPU (engine.cpp make_xar, conv3x3.hip
+    # XAR); 1 = fc_bwd + the fc buckets' all-reduces on a graph branch forked after the
+    # forward (schedule_backward); 0 = the round-4 serial order
+    dist_mode: int = 2
+    # dist_mode 2: the most blocks of a bucket's xGMI channel (its role blocks wait at the
+    # head of the conv backward grid; the engine takes the in-launch path while the channels'
+    # blocks total <= 64)
+    xar_blocks: int = 40
     # bucket plan as for this many ranks (None: the real world size) - forced all-reduces
     # at world size 1 (--force_allreduce) then run the multi-GPU plan's buckets
     plan_world: int | None = None
@@ -223,7 +230,7 @@ class FusedSimpleCNNEngine:
                    fuse_level=self._fuse_level_ok(world_size), fuse_opt=bool(self.opts.fuse_opt),
                    store_a1=int(self.store_a1), f32=f32, fuse_reduce=self._fuse_reduce_ok(world_size),
                    epoch_order=bool(self.opts.epoch_order), wgrad_split=int(self.opts.wgrad_split),
-                   l3_fc_role=int(self.opts.l3_fc_role), dist_fork=int(self.opts.dist_fork))
+                   l3_fc_role=int(self.opts.l3_fc_role), dist_mode=int(self.opts.dist_mode))
         self.dtype = "fp32" if f32 else "bf16"
         use_comm = world_size > 1 or self.opts.force_allreduce
         self.xgmi = None
@@ -236,7 +243,10 @@ class FusedSimpleCNNEngine:
             # small buckets also get a one-shot channel (one cross-GPU barrier instead of two)
             lim = self.cost.oneshot_cap_elems()
             oneshot = tuple(b for b, (_, n) in enumerate(ranges) if n <= lim)
-            self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size, oneshot=oneshot)
+            from ..parallel.xgmi import ENGINE_GRID_CAP
+
+            cap = int(self.opts.xar_blocks) if self.opts.dist_mode == 2 else ENGINE_GRID_CAP
+            self.xgmi = create_xgmi(fs.grads, ranges, rank, world_size, oneshot=oneshot, grid_cap=cap)
             if self.xgmi is not None and self.opts.comm in ("xgmi1", "xgmi2"):
                 plan = "xgmi1" if self.opts.comm == "xgmi1" else "xgmi"  # forced (tests, sweeps)
             elif self.xgmi is not None and self.opts.comm in ("auto", "xgmi"):

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 NAMES = {0: "conv3x3_fwd", 1: "fc_bwd", 2: "conv3x3_dgrad", 3: "conv3x3_wgrad",
-         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging", 8: "fwd-dZ2"}
+         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging", 8: "fwd-dZ2", 9: "xgmi"}
 
 
 def main():
@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--store_a1", type=int, default=None)
     ap.add_argument("--fuse_reduce", type=int, default=None)
     ap.add_argument("--pxt_fwd", type=int, default=None)
+    ap.add_argument("--force_allreduce", action="store_true",
+                    help="the multi-GPU chain at world size 1 (bucket all-reduces of the 8-rank plan)")
+    ap.add_argument("--comm", default="xgmi", help="with --force_allreduce: xgmi | rccl")
+    ap.add_argument("--dist_mode", type=int, default=None)
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -44,13 +48,26 @@ def main():
     opt = FusedSGD(model, lr=0.01)
     imgs, labels = synthetic_mnist()
     eo = EngineOptions(use_graph=a.graph, graph_steps=10, dtype=a.dtype)
+    comm = None
+    if a.force_allreduce:
+        import torch.distributed as dist
+
+        from ddp_amd.parallel import free_port, native_comm
+
+        dist.init_process_group("nccl" if a.comm == "rccl" else "gloo", rank=0, world_size=1,
+                                init_method=f"tcp://127.0.0.1:{free_port()}",
+                                **({"device_id": dev} if a.comm == "rccl" else {}))
+        comm = native_comm() if a.comm == "rccl" else None
+        eo.force_allreduce, eo.comm, eo.plan_world = True, a.comm, 8
+    if a.dist_mode is not None:
+        eo.dist_mode = a.dist_mode
     if a.fuse_level is not None:
         eo.fuse_level = a.fuse_level
     for f in ("wgrad_split", "wgrad_rows", "store_a1", "fuse_reduce", "pxt_fwd"):
         if getattr(a, f) is not None:
             setattr(eo, f, getattr(a, f))
     eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, dev, "synthetic"),
-                               a.batch_size, 1, 0, None, eo)
+                               a.batch_size, 1, 0, comm, eo)
     eng.refresh()
     eng.run_steps(10 if a.graph else 3)
     eng.synchronize()

@@ -486,13 +486,13 @@ def test_comm_tune_rccl_candidates_world1():
 
 
 @pytest.mark.parametrize("plane,dtype", [("xgmi", "bf16"), ("xgmi", "fp32"), ("rccl", "bf16")])
-def test_dist_fork_chain_bitwise_world1(plane, dtype):
-    """the multi-GPU chain with fc_bwd + the fc bucket's all-reduce on a graph
-    branch forked after the forward (dist_fork 1, engine.cpp schedule_backward) trains to the
-    same bits as the round-4 serial dist chain (dist_fork 0) and as the comm-free one-GPU
-    chain, at world size 1 with the all-reduces forced and the 8-rank bucket plan (fc bucket
-    two-shot, conv bucket one-shot), eager and graph-replayed, with momentum (the fused SGD
-    of the xGMI all-gather updates the momentum buffer too) and a ragged last batch."""
+def test_dist_chains_bitwise_world1(plane, dtype):
+    """every multi-GPU step chain trains to the same bits as the comm-free
+    one-GPU chain, at world size 1 with the all-reduces forced and the 8-rank bucket plan (fc
+    bucket two-shot, conv bucket one-shot), graph-replayed, with momentum (the fused SGD of
+    the xGMI all-gather updates the momentum buffer too) and a ragged last batch:
+    dist_mode 2 - the in-launch all-reduce (xGMI; 2 kernels per step, engine.cpp make_xar),
+    1 - fc_bwd + the fc bucket forked beside the conv backward, 0 - the round-4 serial order."""
     import torch.distributed as dist
 
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -511,12 +511,13 @@ def test_dist_fork_chain_bitwise_world1(plane, dtype):
         imgs, labels = synthetic_mnist(1000)  # 31 full batches + a ragged one of 8
         data = DeviceMNIST(imgs, labels, dev)
         out = {}
-        for tag, force, fork in (("local", False, 1), ("serial", True, 0), ("fork", True, 1)):
+        modes = (("local", False, 2), ("serial", True, 0), ("fork", True, 1), ("inlaunch", True, 2))
+        for tag, force, mode in modes:
             torch.manual_seed(0)
             m = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
             e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, comm,
                                      EngineOptions(graph_steps=5, force_allreduce=force, comm=plane,
-                                                   dist_fork=fork, plan_world=8 if force else None,
+                                                   dist_mode=mode, plan_world=8 if force else None,
                                                    dtype=dtype))
             if force:
                 assert e.comm_kind.startswith(plane), e.comm_kind
@@ -526,8 +527,10 @@ def test_dist_fork_chain_bitwise_world1(plane, dtype):
             e.run_epoch(0)
             e.synchronize()
             assert e.eng.sync_error == 0 and e.eng.last_level3
+            # the in-launch all-reduce ran (xGMI) - the ragged last step included
+            assert e.eng.last_xar == (tag == "inlaunch" and plane == "xgmi"), tag
             out[tag] = (e.fs.params.clone(), e.opt.momentum_buffer.clone())
-        for tag in ("serial", "fork"):
+        for tag, _, _ in modes[1:]:
             assert torch.equal(out[tag][0], out["local"][0]), tag
             assert torch.equal(out[tag][1], out["local"][1]), tag
     finally:

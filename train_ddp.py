@@ -78,6 +78,9 @@ def parse_args(argv=None):
                    help="simulate a crash (os._exit) at that step; re-run to auto-resume")
     p.add_argument("--stall_at", default=None, metavar="EPOCH:RANK:SECONDS",
                    help="simulate a slow rank: it sleeps before that epoch's first step")
+    p.add_argument("--force_allreduce", action="store_true",
+                   help="rehearsal on one GPU: run the multi-GPU fused step chain at world size 1 (forked "
+                        "fc branch, bucket all-reduces of the 8-rank plan on the --comm plane, chain check)")
     p.add_argument("--verify_replicas", action="store_true",
                    help="after every epoch check that all ranks' parameters and momentum are bitwise equal")
     return p.parse_args(argv)
@@ -96,6 +99,7 @@ def main(argv=None):
                         comm=a.comm, model=a.model, image_size=a.image_size,
                         num_classes=a.num_classes, dataset_size=a.dataset_size,
                         graph_module=a.graph_module, verify_replicas=a.verify_replicas,
+                        force_allreduce=a.force_allreduce,
                         stall=tuple(float(v) for v in a.stall_at.split(":")) if a.stall_at else None,
                         fault=tuple(int(v) for v in a.fault_at.split(":")) if a.fault_at else None)
     launch(ddp_train, a.world_size, args=(a.epochs, a.batch_size, opts))
