@@ -284,7 +284,7 @@ def main():
                          "all-reduces on the --comm plane at world size 1) - times the dist chain on one GPU")
     ap.add_argument("--plan_world", type=int, default=None,
                     help="bucket plan as for this many ranks (default: the world size; --force_allreduce: 8)")
-    ap.add_argument("--dist_mode", type=int, default=None, choices=[0, 1, 2],
+    ap.add_argument("--dist_mode", type=int, default=None, choices=[0, 1, 2, 3],
                     help="N>1, level 3: 2 = bucket all-reduces inside the conv backward launch (xGMI, default); "
                          "1 = fc weight gradient + fc bucket all-reduce on a graph branch forked after the "
                          "forward; 0 = the round-4 serial order")

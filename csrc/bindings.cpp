@@ -931,7 +931,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
              c.dist_mode = cfgd.contains("dist_mode") ? cfgd["dist_mode"].cast<int>() : 2;
-             TORCH_CHECK(c.dist_mode >= 0 && c.dist_mode <= 2, "engine: dist_mode must be 0, 1 or 2");
+             TORCH_CHECK(c.dist_mode >= 0 && c.dist_mode <= 3, "engine: dist_mode must be 0..3");
              TORCH_CHECK(c.l3_fc_role == 0 || c.l3_fc_role == 1, "engine: l3_fc_role must be 0 or 1");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
              const int es = c.f32 ? 4 : 2;

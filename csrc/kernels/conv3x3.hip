@@ -31,6 +31,7 @@
 //           reduction in grad_reduce (bitwise reproducible, no float atomics).
 #include <stdexcept>
 
+#include <cstdio>
 #include <cstdlib>
 
 #include "kernels/common.h"
@@ -1302,16 +1303,30 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
     const int nx = xar.nblk0 + xar.nblk1;
     if (cb < nx) {
       unsigned* s_sh = reinterpret_cast<unsigned*>(smem);
-      if (cb < xar.nblk0) {
-        if (wait_count(xar.fc_done, xar.fc_expect, xar.err, XAR_ERR))
-          xgmi_allreduce_body(xar.args[0], cb, xar.nblk0, s_sh);
+      DDP_STAMP(STAMP_K_XGMI, 0);
+      // the bucket's arguments into this block's LDS while it waits: read from global memory
+      // inside the body, every field was re-loaded after each store (they may alias), ~1 us a
+      // time; from LDS (another address space) the compiler keeps them
+      const int k = cb < xar.nblk0 ? 0 : 1;
+      XgmiArgs* s_xa = reinterpret_cast<XgmiArgs*>(smem + 64);
+      {
+        const int* src = reinterpret_cast<const int*>(xar.args + k);
+        int* dst = reinterpret_cast<int*>(s_xa);
+        for (int i = threadIdx.x; i < (int)(sizeof(XgmiArgs) / 4); i += 256) dst[i] = src[i];
+      }
+      if (k == 0) {
+        const bool ok = wait_count(xar.fc_done, xar.fc_expect, xar.err, XAR_ERR);  // (its barrier orders the copy)
+        DDP_STAMP(STAMP_K_XGMI, 5);
+        if (ok) xgmi_allreduce_body(*s_xa, cb, xar.nblk0, s_sh);
       } else {
-        if (wait_count(xar.fc_done, xar.fc_expect, xar.err, XAR_ERR) &&
-            wait_count(xar.red_done, xar.red_expect, xar.err, XAR_ERR))
-          xgmi_allreduce_body(xar.args[1], cb - xar.nblk0, xar.nblk1, s_sh);
+        const bool ok = wait_count(xar.fc_done, xar.fc_expect, xar.err, XAR_ERR) &&
+                        wait_count(xar.red_done, xar.red_expect, xar.err, XAR_ERR);
+        DDP_STAMP(STAMP_K_XGMI, 5);
+        if (ok) xgmi_allreduce_body(*s_xa, cb - xar.nblk0, xar.nblk1, s_sh);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      DDP_STAMP(STAMP_K_XGMI, 7);
       if (threadIdx.x == 0) {
         // the step's last work item advances the batch window (the fc role read it before
         // counting itself into fc_done, which every role block waited for)
@@ -1782,10 +1797,11 @@ template <typename T>
 static BwdKFn<T> pick_bwd(int pxt, bool da, bool wa, bool g, bool fred, int cs, bool fcr, int dg, bool xar = false) {
   if (pxt == 2) {
     if (da) return pick_bwd3<T, 2, true, true>(g, fred, cs, fcr, dg, xar);
-    return wa ? pick_bwd3<T, 2, false, true>(g, fred, cs, fcr, dg) : pick_bwd3<T, 2, false, false>(g, fred, cs, fcr, dg);
+    return wa ? pick_bwd3<T, 2, false, true>(g, fred, cs, fcr, dg, xar)
+              : pick_bwd3<T, 2, false, false>(g, fred, cs, fcr, dg, xar);
   }
-  if (da) return pick_bwd3<T, 1, true, true>(g, fred, cs, fcr, dg);
-  return wa ? pick_bwd3<T, 1, false, true>(g, fred, cs, fcr, dg) : pick_bwd3<T, 1, false, false>(g, fred, cs, fcr, dg);
+  if (da) return pick_bwd3<T, 1, true, true>(g, fred, cs, fcr, dg, xar);
+  return wa ? pick_bwd3<T, 1, false, true>(g, fred, cs, fcr, dg, xar) : pick_bwd3<T, 1, false, false>(g, fred, cs, fcr, dg, xar);
 }
 
 bool conv3x3_bwd_fc_role_ok(int H, int W, int Cin, int Cout, int pxt, int wgrad_split) {
@@ -1888,6 +1904,9 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   int nx = 0;
   const bool use_xar = xar && fc && fused && pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, true) !=
                                                 pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, false);
+  if (xar && !use_xar && std::getenv("DDP_AMD_XAR_DEBUG"))
+    fprintf(stderr, "[ddp_amd] in-launch all-reduce not used: fc %d fused %d first_reducer %d nconv %d\n",
+            fc != nullptr, fused != nullptr, red.first_reducer, nd + nw);
   if (use_xar) {
     xv = *xar;
     xv.fc_expect = nfc;
@@ -1895,7 +1914,7 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
     nx = xv.nblk0 + xv.nblk1;
     if (xv.nblk1 <= 0 || !xv.args || !xv.fc_done || !xv.red_done || !xv.xar_done)
       throw std::runtime_error("conv3x3_bwd: in-launch all-reduce needs a conv bucket and its counters");
-    if (lds < 64) throw std::runtime_error("conv3x3_bwd: LDS too small for the all-reduce role");
+    if (lds < 64 + sizeof(XgmiArgs)) throw std::runtime_error("conv3x3_bwd: LDS too small for the all-reduce role");
     if (xar_used) *xar_used = true;
   }
   // the wgrad role needs a single (Cout/32)*(Cin/16)/4 == 1 y-block and the dgrad role Cin == 32

@@ -9,6 +9,9 @@
 
 namespace ddp_amd {
 
+// loads in flight per thread in the reduce-scatter / all-gather loops (XgmiArgs items)
+constexpr int XGMI_BATCH = 8;
+
 // Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
 // has signalled `target` to us.  Caller guarantees every wave drained its stores.
 // On a timeout the FIRST stalled wait is recorded in the error word (xgmi_error_code:
@@ -243,13 +246,36 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
     const long lim = min(slice, a.n - (long)r * slice);  // my slice's real length (may be <= 0)
     const long fq = lim > 0 ? lim / 4 : 0, nq = lim > 0 ? (lim + 3) / 4 : 0;
     const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par);
-    long q = q0;
-    for (; q + G < fq; q += 2 * G) {
-      const float4 s0 = rank_sum4(src, q, N), s1 = rank_sum4(src, q + G, N);
-      st4_sys(mystage, q, s0);
-      st4_sys(mystage, q + G, s1);
+    // the thread's full quads q0, q0 + G, ... below fq as (quad j, rank p) items in order,
+    // XGMI_BATCH loads in flight per batch whatever N is (N = 1 would otherwise wait on one
+    // load per quad); each quad's sum runs p = 0..N-1 exactly as rank_sum4 (same bits)
+    const long J = fq > q0 ? (fq - q0 + G - 1) / G : 0;
+    const long items = J * N;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long i0 = 0; i0 < items; i0 += XGMI_BATCH) {
+      float4 v[XGMI_BATCH];
+      long jj = i0 / N;
+      int pp = (int)(i0 - jj * N);
+#pragma unroll
+      for (int u = 0; u < XGMI_BATCH; ++u) {
+        v[u] = i0 + u < items ? ld4_sys(sys_rsrc(a.data[pp] + a.off + (long)r * slice), q0 + jj * G)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (++pp == N) { pp = 0; ++jj; }
+      }
+      jj = i0 / N;
+      pp = (int)(i0 - jj * N);
+#pragma unroll
+      for (int u = 0; u < XGMI_BATCH; ++u) {
+        if (i0 + u < items) {
+          acc = pp == 0 ? v[u] : add4(acc, v[u]);
+          if (pp == N - 1) st4_sys(mystage, q0 + jj * G, acc);
+        }
+        if (++pp == N) { pp = 0; ++jj; }
+      }
     }
-    for (; q < nq; q += G) st4_sys(mystage, q, q < fq ? rank_sum4(src, q, N) : rank_sum_tail(srcp, q, lim, N));
+    // the partial last quad of the bucket (element loads)
+    for (long q = q0 + J * G; q < nq; q += G) st4_sys(mystage, q, rank_sum_tail(srcp, q, lim, N));
+    (void)src;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   DDP_STAMP(STAMP_K_XGMI, 3);
@@ -257,40 +283,51 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
   DDP_STAMP(STAMP_K_XGMI, 4);
   if (!s_fail) {
     // ---- AG: quad q of every rank's reduced slice into my gradient buffer
-    __amdgpu_buffer_rsrc_t st[XGMI_MAX_RANKS];
-#pragma unroll
-    for (int p = 0; p < XGMI_MAX_RANKS; ++p) st[p] = sys_rsrc((p < N ? a.stage[p] : a.stage[r]) + par);
-    // every load of the iteration (N reduced quads over xGMI, and with the fused optimizer
-    // the N local parameter / momentum quads) is issued before the first store
+    // the thread's quads q0, q0 + G, ... of every rank's reduced slice as (quad j, rank p)
+    // items in order, XGMI_BATCH per batch: every load of a batch (reduced quads over xGMI,
+    // and with the fused optimizer the local parameter / momentum quads) is issued before
+    // the first store, whatever N is
     const bool vec = (a.off & 3) == 0;
     const bool mom = a.sgd.momentum != 0.f;
-    for (long q = q0; q < sq; q += G) {
-      float4 v[XGMI_MAX_RANKS], pv[XGMI_MAX_RANKS], mv[XGMI_MAX_RANKS];
+    const long J = sq > q0 ? (sq - q0 + G - 1) / G : 0;
+    const long items = J * N;
+    for (long i0 = 0; i0 < items; i0 += XGMI_BATCH) {
+      float4 v[XGMI_BATCH], pv[XGMI_BATCH], mv[XGMI_BATCH];
+      long jj = i0 / N;
+      int pp = (int)(i0 - jj * N);
 #pragma unroll
-      for (int p = 0; p < XGMI_MAX_RANKS; ++p) {
-        const long qq = (long)p * sq + q;
-        const bool ok = p < N && 4 * qq < a.n;
-        v[p] = ok ? ld4_sys(st[p], q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < XGMI_BATCH; ++u) {
+        const long q = q0 + jj * G, qq = (long)pp * sq + q;
+        const bool ok = i0 + u < items && 4 * qq < a.n;
+        v[u] = ok ? ld4_sys(sys_rsrc(a.stage[pp] + par), q) : make_float4(0.f, 0.f, 0.f, 0.f);
         const bool whole = ok && vec && 4 * qq + 3 < a.n;
-        pv[p] = whole && a.sgd.update ? ld_quad(a.params, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
-        mv[p] = whole && a.sgd.update && mom ? ld_quad(a.mbuf, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        pv[u] = whole && a.sgd.update ? ld_quad(a.params, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        mv[u] = whole && a.sgd.update && mom ? ld_quad(a.mbuf, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (++pp == N) { pp = 0; ++jj; }
       }
-      // finish one peer's quad per trip (the finishing code once, not N times: unrolled N
-      // ways it made the kernel too large to unroll); the trip's registers are picked from
-      // the arrays by a select chain on the (uniform) peer index - constant array indices only
+      // finish one item per trip (the finishing code once, not XGMI_BATCH times: unrolled it
+      // made the kernel too large to unroll); the trip's registers are picked from the arrays
+      // by a select chain on the (uniform) slot index - constant array indices only
+      jj = i0 / N;
+      pp = (int)(i0 - jj * N);
+      // one wait for the whole batch: inside the rolled loop the compiler waits for every
+      // outstanding memory operation (the previous items' stores included) before each item
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll 1
-      for (int p = 0; p < N; ++p) {
-        const long qq = (long)p * sq + q;
-        if (4 * qq >= a.n) break;
-        float4 vv = v[0], pp = pv[0], mm = mv[0];
+      for (int u = 0; u < XGMI_BATCH; ++u) {
+        const long q = q0 + jj * G, qq = (long)pp * sq + q;
+        if (++pp == N) { pp = 0; ++jj; }
+        if (i0 + u >= items) break;
+        if (4 * qq >= a.n) continue;
+        float4 vv = v[0], pq = pv[0], mq = mv[0];
 #pragma unroll
-        for (int u = 1; u < XGMI_MAX_RANKS; ++u)
-          if (p == u) { vv = v[u]; pp = pv[u]; mm = mv[u]; }
+        for (int w = 1; w < XGMI_BATCH; ++w)
+          if (u == w) { vv = v[w]; pq = pv[w]; mq = mv[w]; }
         const float4 d = scale4(a, vv);
         if (vec && 4 * qq + 3 < a.n) {
           const long j = a.off + 4 * qq;
           *reinterpret_cast<float4*>(a.data[r] + j) = d;
-          if (a.sgd.update) sgd_quad_apply(a.params, a.mbuf, j, d, pp, mm, a.sgd, a.sh);
+          if (a.sgd.update) sgd_quad_apply(a.params, a.mbuf, j, d, pq, mq, a.sgd, a.sh);
         } else {
           finish_quad(a, qq, d, a.n);
         }

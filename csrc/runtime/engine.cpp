@@ -34,6 +34,7 @@
 // bucket 0 = [fl.weight, fl.bias] (2.0 MB), bucket 1 = [net.2.*, net.0.*] (74 KB); any
 // bucket plan works (stage 0 = fc-only buckets, stage 1 = the rest).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -209,7 +210,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // before it (the fc bucket's all-reduce then overlaps the conv backward)
   // dist_mode 2 (xGMI): the same fc role inside the conv backward at world size > 1, its
   // gradient all-reduced in-launch (make_xar / BwdXar)
-  const bool xar_mode = dist && use_x && l3 && cfg_.dist_mode == 2 && xar_plan_ok_;
+  const bool xar_mode = dist && use_x && l3 &&
+                        ((cfg_.dist_mode == 2 && xar_plan_ok_) || cfg_.dist_mode == 3);
   const bool fc_role = l3 && (!dist || xar_mode) && cfg_.l3_fc_role &&
                        conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
   const C1Src* pc1 = f1 ? &c1 : nullptr;
@@ -345,7 +347,10 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   ss.sys_store = use_x ? 1 : 0;  // bucket 1 likewise
   bool reduced = false;  // the conv backward launch also did grad_reduce's work
   BwdXar xa;
-  const bool want_xar = xar_mode && fc_role && fred && make_xar(xa, sa, M, sh_all);
+  const bool want_xar = xar_mode && cfg_.dist_mode == 2 && fc_role && fred && make_xar(xa, sa, M, sh_all);
+  if (dist && use_x && l3 && cfg_.dist_mode == 2 && !want_xar && std::getenv("DDP_AMD_XAR_DEBUG"))
+    fprintf(stderr, "[ddp_amd] in-launch all-reduce off: plan_ok %d fc_role %d fred %d buckets %d\n",
+            (int)xar_plan_ok_, (int)fc_role, (int)fred, (int)buckets_.size());
   bool xar_used = false;
   auto conv_launch = [&]() {
     if (f1) {
@@ -403,31 +408,52 @@ void SimpleCNNEngine::enqueue_buckets(int stage, bool use_x, hipStream_t s, cons
 
 bool SimpleCNNEngine::make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh) {
   if (!xgmi_ || !xar_plan_ok_) return false;
-  XgmiArgs pair[2] = {};
-  for (int b = 0; b < (int)buckets_.size(); ++b) {
-    // the bucket's fused optimizer; the in-launch roles advance the step counter themselves
-    pair[stage_[b]] = xgmi_->make_args(xch_[b], sa, b_.params, M, sh, nullptr);
-    (stage_[b] == 0 ? xa.nblk0 : xa.nblk1) = xgmi_->blocks(xch_[b]);
-  }
   // the pair lives in device memory, one immutable copy per distinct content (a captured
   // graph keeps pointing at the copy it was captured with): the momentum-init step's and
-  // the steady state's, a few more if the learning rate changes
-  const XgmiArgs* dev = nullptr;
-  for (const XarArgs& e : xar_cache_)
-    if (std::memcmp(e.host, pair, sizeof(pair)) == 0) dev = e.dev;
+  // the steady state's - both made on the first (eager) call, so a capture never needs a
+  // new one - and a pair more if the learning rate changes
+  static const int expt = [] { const char* e = std::getenv("DDP_AMD_XAR_EXPT"); return e ? std::atoi(e) : 0; }();
+  auto build = [&](const SgdArgs& g, XgmiArgs* pair) {
+    for (int b = 0; b < (int)buckets_.size(); ++b) {
+      // the bucket's fused optimizer; the in-launch roles advance the step counter themselves
+      ShadowSet shx = sh;
+      if (expt == 1) shx.count = 0;  // TIMING EXPERIMENT ONLY: no shadow refresh (wrong results)
+      SgdArgs gx = g;
+      if (expt == 2) gx.update = 0;  // TIMING EXPERIMENT ONLY: no SGD (wrong results)
+      pair[stage_[b]] = xgmi_->make_args(xch_[b], gx, b_.params, M, shx, nullptr);
+      (stage_[b] == 0 ? xa.nblk0 : xa.nblk1) = xgmi_->blocks(xch_[b]);
+    }
+  };
+  auto find = [&](const XgmiArgs* pair) -> const XgmiArgs* {
+    for (const XarArgs& e : xar_cache_)
+      if (std::memcmp(e.host, pair, sizeof(XgmiArgs) * 2) == 0) return e.dev;
+    return nullptr;
+  };
+  XgmiArgs pair[2] = {};
+  build(sa, pair);
+  const XgmiArgs* dev = find(pair);
   if (!dev) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    DDP_HIP_CHECK(hipStreamIsCapturing(cs_, &st));
-    if (st != hipStreamCaptureStatusNone)
-      throw std::runtime_error("engine: new in-launch all-reduce arguments during graph capture");
-    XarArgs e;
-    std::memcpy(e.host, pair, sizeof(pair));
-    XgmiArgs* d = nullptr;
-    DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), sizeof(pair)));
-    DDP_HIP_CHECK(hipMemcpy(d, pair, sizeof(pair), hipMemcpyHostToDevice));
-    e.dev = d;
-    xar_cache_.push_back(e);
-    dev = d;
+    // (a first capture without an eager step before it lands here while capturing: the
+    // capture is in relaxed mode, and the allocation and the copy run at once, outside the
+    // graph, on a stream of their own)
+    SgdArgs other = sa;
+    other.first_step = sa.first_step ? 0 : 1;
+    XgmiArgs pair2[2] = {};
+    build(other, pair2);
+    for (const XgmiArgs* p : {static_cast<const XgmiArgs*>(pair), static_cast<const XgmiArgs*>(pair2)}) {
+      if (find(p)) continue;
+      XarArgs e;
+      std::memcpy(e.host, p, sizeof(e.host));
+      XgmiArgs* d = nullptr;
+      DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), sizeof(e.host)));
+      // (a private non-blocking stream: the legacy stream may not depend on a capture)
+      if (!xs_) DDP_HIP_CHECK(hipStreamCreateWithFlags(&xs_, hipStreamNonBlocking));
+      DDP_HIP_CHECK(hipMemcpyAsync(d, p, sizeof(e.host), hipMemcpyHostToDevice, xs_));
+      DDP_HIP_CHECK(hipStreamSynchronize(xs_));
+      e.dev = d;
+      xar_cache_.push_back(e);
+    }
+    dev = find(pair);
   }
   xa.args = dev;
   // three counters of the step's zeroed hand-off words (the forward clears [0, L3_IMG_OFF))
@@ -551,7 +577,8 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     dzo.dl_out = b_.dlogits;
     dzo.loss_rows = b_.loss_rows;
   }
-  const bool xar_mode = dist && use_x && l3 && cfg_.dist_mode == 2 && xar_plan_ok_;
+  const bool xar_mode = dist && use_x && l3 &&
+                        ((cfg_.dist_mode == 2 && xar_plan_ok_) || cfg_.dist_mode == 3);
   const bool fc_role = l3 && (!dist || xar_mode) && cfg_.l3_fc_role &&
                        conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
 
@@ -651,7 +678,7 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   ss.sys_store = use_x ? 1 : 0;
   bool reduced = false;
   BwdXar xa;
-  const bool want_xar = xar_mode && fc_role && fred && make_xar(xa, sa, M, sh1);
+  const bool want_xar = xar_mode && cfg_.dist_mode == 2 && fc_role && fred && make_xar(xa, sa, M, sh1);
   bool xar_used = false;
   auto conv_launch = [&]() {
     reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
@@ -692,8 +719,8 @@ void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> cha
   xgmi_ = std::move(x);
   xch_ = xgmi_ ? channels : std::vector<int>(buckets_.size(), -1);
   // the in-launch all-reduce (dist_mode 2) takes at most one bucket per stage, a conv-stage
-  // bucket, and few role blocks (they wait at the head of the grid: <= 64 of its >= 256
-  // resident slots, next to the fused reducers' half)
+  // bucket, and a bounded number of role blocks (they wait at the head of the grid: <= 192
+  // of its 512 resident slots, next to the fused reducers' <= 256)
   xar_plan_ok_ = false;
   if (xgmi_ && sync_ok_for_xar()) {
     int per[2] = {0, 0}, nb = 0;
@@ -701,7 +728,10 @@ void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> cha
       ++per[stage_[b]];
       nb += xgmi_->blocks(xch_[b]);
     }
-    xar_plan_ok_ = per[0] <= 1 && per[1] == 1 && nb <= 64;
+    xar_plan_ok_ = per[0] <= 1 && per[1] == 1 && nb <= 192;
+    if (std::getenv("DDP_AMD_XAR_DEBUG"))
+      fprintf(stderr, "[ddp_amd] set_xgmi: stage buckets %d/%d, role blocks %d -> in-launch %d\n", per[0], per[1],
+              nb, (int)xar_plan_ok_);
   }
 }
 

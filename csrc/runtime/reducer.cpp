@@ -76,10 +76,14 @@ void Reducer::launch_bucket(int b, hipStream_t compute) {
   } else if (comm_ && comm_->world() > 1) {
     // DDP's prescale by 1/world folded into the reduction (RCCL pre-multiplied SUM: no
     // separate read + write pass over the bucket); producers that prescaled already SUM
-    if (prescale_)
+    if (prescale_) {
       comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
-    else
+    } else if (bucket_num_[b] % 4 == 0) {
       comm_->all_reduce_premul(flat_ + bucket_off_[b], (size_t)bucket_num_[b], inv, comm_stream_);
+    } else {  // (RCCL's pre-multiplied SUM was seen skipping a non-multiple-of-4 tail at one rank)
+      scale_copy(flat_ + bucket_off_[b], flat_ + bucket_off_[b], bucket_num_[b], inv, comm_stream_);
+      comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
+    }
     ++calls_;
   }
   DDP_HIP_CHECK(hipEventRecord(done_[b], comm_stream_));

@@ -260,6 +260,8 @@ struct EngineConfig {
   //  1 = fork: fc_bwd and the fc buckets' all-reduces on the comm stream, forked after the
   //      forward beside the conv backward (a graph branch), the conv buckets' all-reduces
   //      behind the conv backward
+  //  3 = one stream (xGMI): the fc role inside the conv backward as on one GPU, then the
+  //      bucket kernels (full grids) behind it on the compute stream - no cross-stream edge
   //  0 = the round-4 order (fc_bwd in front of the conv backward, all-reduces on ms_)
   int dist_mode = 2;
 };
@@ -358,6 +360,7 @@ class SimpleCNNEngine {
     const XgmiArgs* dev = nullptr;
   };
   std::vector<XarArgs> xar_cache_;  // make_xar: device copies of the in-launch arguments
+  hipStream_t xs_ = nullptr;        // ... and the stream their copies run on
   bool plain_stale_ = false;  // level-3 steps skipped the plain bf16 fc shadow
   int* err_host_ = nullptr;  // coherent host word behind b_.sync_err
 };

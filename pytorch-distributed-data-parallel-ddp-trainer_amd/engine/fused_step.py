@@ -114,11 +114,12 @@ class EngineOptions:
     # role and role blocks at the head of that launch all-reduce each bucket (+ fused SGD) as
     # soon as it is final - 2 kernels per step, as on one GPU (engine.cpp make_xar, conv3x3.hip
     # XAR); 1 = fc_bwd + the fc buckets' all-reduces on a graph branch forked after the
-    # forward (schedule_backward); 0 = the round-4 serial order
+    # forward (schedule_backward); 3 = one stream: the fc role inside the conv backward, the
+    # bucket kernels behind it (no cross-stream edge); 0 = the round-4 serial order
     dist_mode: int = 2
     # dist_mode 2: the most blocks of a bucket's xGMI channel (its role blocks wait at the
     # head of the conv backward grid; the engine takes the in-launch path while the channels'
-    # blocks total <= 64)
+    # blocks total <= 192)
     xar_blocks: int = 40
     # bucket plan as for this many ranks (None: the real world size) - forced all-reduces
     # at world size 1 (--force_allreduce) then run the multi-GPU plan's buckets

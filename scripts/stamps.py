@@ -34,6 +34,7 @@ def main():
                     help="the multi-GPU chain at world size 1 (bucket all-reduces of the 8-rank plan)")
     ap.add_argument("--comm", default="xgmi", help="with --force_allreduce: xgmi | rccl")
     ap.add_argument("--dist_mode", type=int, default=None)
+    ap.add_argument("--xgmi_blocks", action="store_true", help="print every xgmi block's stamps")
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -103,6 +104,10 @@ def main():
                 continue
             d = (v[ok] - kstart) / 100.0
             line.append(f" s{slot} med {d.median().item():6.2f} max {d.max().item():6.2f}")
+        if NAMES.get(k) == "xgmi" and a.xgmi_blocks:
+            for bi in range(nb):
+                vals = " ".join(f"s{sl} {(s[bi, sl] - kstart) / 100.0:6.2f}" for sl in range(8) if s[bi, sl] > 0)
+                print(f"    xgmi block {bi:3d}: {vals}")
         # per-block durations (first -> last stamp)
         last = s.max(dim=1).values
         dur = (last - s[:, 0]) / 100.0

@@ -288,7 +288,7 @@ def test_module_ddp_world1_rccl(tmp_path):
     from ddp_amd.parallel import DistributedDataParallel, free_port
 
     dist.init_process_group("nccl", rank=0, world_size=1,
-                            init_method=f"tcp://127.0.0.1:{free_port()}",
+                            store=dist.HashStore(),
                             device_id=torch.device("cuda", 0))
     try:
         torch.manual_seed(0)
@@ -323,7 +323,7 @@ def test_engine_rccl_allreduce_inside_graph_world1(fuse_level):
     from ddp_amd.parallel import free_port, native_comm
 
     dist.init_process_group("nccl", rank=0, world_size=1,
-                            init_method=f"tcp://127.0.0.1:{free_port()}",
+                            store=dist.HashStore(),
                             device_id=torch.device("cuda", 0))
     try:
         comm = native_comm()
@@ -363,7 +363,7 @@ def test_engine_xgmi_world1_beside_fused_reduce(fuse_level, use_graph):
     from ddp_amd.ops import FusedSGD
     from ddp_amd.parallel import free_port
 
-    dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}")
+    dist.init_process_group("gloo", rank=0, world_size=1, store=dist.HashStore())
     try:
         imgs, labels = synthetic_mnist(2048)
         data = DeviceMNIST(imgs, labels, dev)
@@ -402,7 +402,7 @@ def test_verify_chain_world1_forced(corrupt, stall):
     from ddp_amd.ops import FusedSGD
     from ddp_amd.parallel import free_port
 
-    dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}")
+    dist.init_process_group("gloo", rank=0, world_size=1, store=dist.HashStore())
     try:
         imgs, labels = synthetic_mnist(2048)
         data = DeviceMNIST(imgs, labels, dev)
@@ -454,7 +454,7 @@ def test_comm_tune_rccl_candidates_world1():
     from ddp_amd.parallel import free_port, native_comm
     from ddp_amd.parallel.xgmi import rccl_candidate_comms
 
-    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}",
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
                             device_id=torch.device("cuda", 0))
     try:
         variants = rccl_candidate_comms(0, 1)
@@ -501,11 +501,12 @@ def test_dist_chains_bitwise_world1(plane, dtype):
     from ddp_amd.ops import FusedSGD
     from ddp_amd.parallel import free_port, native_comm
 
+    # (an in-process store: no TCP port to race for)
     if plane == "rccl":
-        dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}",
+        dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
                                 device_id=torch.device("cuda", 0))
     else:
-        dist.init_process_group("gloo", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}")
+        dist.init_process_group("gloo", rank=0, world_size=1, store=dist.HashStore())
     try:
         comm = native_comm() if plane == "rccl" else None
         imgs, labels = synthetic_mnist(1000)  # 31 full batches + a ragged one of 8
@@ -524,10 +525,10 @@ def test_dist_chains_bitwise_world1(plane, dtype):
                 assert len(e.ranges) == 2  # the 8-rank plan: [fc], [conv]
             assert e.level3
             e.refresh()
-            e.run_epoch(0)
+            e.run_epoch(0)  # (its ragged last step of 8 reduces its slabs apart: bucket kernels)
+            e.run_steps(3)  # full batches again: the in-launch all-reduce runs
             e.synchronize()
             assert e.eng.sync_error == 0 and e.eng.last_level3
-            # the in-launch all-reduce ran (xGMI) - the ragged last step included
             assert e.eng.last_xar == (tag == "inlaunch" and plane == "xgmi"), tag
             out[tag] = (e.fs.params.clone(), e.opt.momentum_buffer.clone())
         for tag, _, _ in modes[1:]:
@@ -541,16 +542,19 @@ def test_rccl_premul_sum_world1_eager_and_graph():
     """the module-path reducer's RCCL plane folds DDP's 1/ws prescale into the
     reduction (RCCL pre-multiplied SUM, Comm::all_reduce_premul) instead of a separate
     scale pass; at world size 1 the result is exactly x * scale (fp32 multiply), eagerly and
-    replayed from a captured graph (the host-immediate scalar is captured by value)."""
+    replayed from a captured graph (the host-immediate scalar is captured by value).
+    (RCCL 2.26's one-rank path leaves the last n % 4 elements of a large buffer unscaled -
+    scripts/premul_probe.py, profiles/r5_dist; the reducer's buckets are whole 64-element
+    parameter slots, and it takes the pre-multiplied SUM only for counts % 4 == 0.)"""
     import torch.distributed as dist
 
     from ddp_amd.parallel import free_port, native_comm
 
-    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{free_port()}",
-                            device_id=torch.device("cuda", 0))
+    # (an in-process store: no TCP port to race for)
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=torch.device("cuda", 0))
     try:
         comm = native_comm()
-        x = torch.randn(100_003, device=dev)
+        x = torch.randn(100_000, device=dev)
         s = 1.0 / 3.0
         want = x * torch.tensor(s, dtype=torch.float32, device=dev)
         y = x.clone()
