@@ -285,9 +285,9 @@ def main():
     ap.add_argument("--plan_world", type=int, default=None,
                     help="bucket plan as for this many ranks (default: the world size; --force_allreduce: 8)")
     ap.add_argument("--dist_mode", type=int, default=None, choices=[0, 1, 2, 3],
-                    help="N>1, level 3: 2 = bucket all-reduces inside the conv backward launch (xGMI, default); "
-                         "1 = fc weight gradient + fc bucket all-reduce on a graph branch forked after the "
-                         "forward; 0 = the round-4 serial order")
+                    help="N>1, level 3: 3 = both bucket all-reduces in one launch behind the conv backward "
+                         "(xGMI, default); 2 = inside the conv backward launch; 1 = fc weight gradient + fc "
+                         "bucket all-reduce on a graph branch forked after the forward; 0 = the round-4 serial order")
     ap.add_argument("--xar_blocks", type=int, default=None,
                     help="dist_mode 2: most blocks per bucket channel (in-launch all-reduce role)")
     ap.add_argument("--no_breakdown", action="store_true",
@@ -468,10 +468,11 @@ def main():
     plan = describe(eng.buckets, fs, eng.cost, ranges=eng.ranges) if (ws > 1 or force) else None
     finite = bool(torch.isfinite(fs.params).all().item())
     level3 = bool(eng.eng.last_level3)
-    # kernels per step of the chain that ran: 2 on one GPU and with the in-launch all-reduce;
-    # otherwise fc_bwd and one all-reduce kernel per bucket come on top
-    kps = ((2 if eng.eng.last_fc_role else 3) + (0 if eng.eng.last_xar or eng.comm_kind == "none"
-                                                  else len(eng.ranges))) if level3 else None
+    # kernels per step of the chain that ran: 2 on one GPU and with the in-launch all-reduce,
+    # 3 with both buckets' all-reduces in one launch (dist_mode 3); otherwise fc_bwd and one
+    # all-reduce kernel per bucket come on top
+    nar = 0 if eng.eng.last_xar or eng.comm_kind == "none" else 1 if eng.eng.last_pair else len(eng.ranges)
+    kps = ((2 if eng.eng.last_fc_role else 3) + nar) if level3 else None
     same = True
     if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
         pd = dev if args.backend == "nccl" else "cpu"
@@ -529,6 +530,7 @@ def main():
                        "chain_check": eng.chain_check, "downgrades": getattr(eng, "downgrades", []),
                        "force_allreduce": force, "step_breakdown": breakdown,
                        "inlaunch_allreduce": bool(eng.eng.last_xar),
+                       "pair_allreduce": bool(eng.eng.last_pair),
                        "comm_calibration": calib,
                        "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
                        "fp32_level3": fp32["level3"] if fp32 else None,

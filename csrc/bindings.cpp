@@ -930,7 +930,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.fuse_reduce = cfgd.contains("fuse_reduce") ? cfgd["fuse_reduce"].cast<int>() : 1;
              c.wgrad_split = cfgd.contains("wgrad_split") ? cfgd["wgrad_split"].cast<int>() : 1;
              c.l3_fc_role = cfgd.contains("l3_fc_role") ? cfgd["l3_fc_role"].cast<int>() : 1;
-             c.dist_mode = cfgd.contains("dist_mode") ? cfgd["dist_mode"].cast<int>() : 2;
+             c.dist_mode = cfgd.contains("dist_mode") ? cfgd["dist_mode"].cast<int>() : 3;
              TORCH_CHECK(c.dist_mode >= 0 && c.dist_mode <= 3, "engine: dist_mode must be 0..3");
              TORCH_CHECK(c.l3_fc_role == 0 || c.l3_fc_role == 1, "engine: l3_fc_role must be 0 or 1");
              TORCH_CHECK(c.wgrad_split == 1 || c.wgrad_split == 2, "engine: wgrad_split must be 1 or 2");
@@ -1026,6 +1026,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("last_level3", &SimpleCNNEngine::last_level3)
       .def_property_readonly("last_fc_role", &SimpleCNNEngine::last_fc_role)
       .def_property_readonly("last_xar", &SimpleCNNEngine::last_xar)
+      .def_property_readonly("last_pair", &SimpleCNNEngine::last_pair)
       .def("level3_active", &SimpleCNNEngine::level3_active, py::arg("batch"))
       .def_property_readonly("sync_error", &SimpleCNNEngine::sync_error)
       .def("set_momentum_started", &SimpleCNNEngine::set_momentum_started)

@@ -41,9 +41,46 @@ namespace ddp_amd {
 
 __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_kernel(XgmiArgs a) {
   __shared__ unsigned s_sh[2];
+  // the arguments into LDS first: the body indexes the peer pointers by rank, which made the
+  // compiler copy the by-value struct to scratch
+  __shared__ __attribute__((aligned(16))) int s_raw[sizeof(XgmiArgs) / 4];
+  {
+    const int* src = reinterpret_cast<const int*>(&a);
+    for (int i = threadIdx.x; i < (int)(sizeof(XgmiArgs) / 4); i += XGMI_THREADS) s_raw[i] = src[i];
+  }
+  __syncthreads();
   DDP_STAMP(STAMP_K_XGMI, 0);
-  xgmi_allreduce_body(a, (int)blockIdx.x, (int)gridDim.x, s_sh);
+  xgmi_allreduce_body(*reinterpret_cast<const XgmiArgs*>(s_raw), (int)blockIdx.x, (int)gridDim.x, s_sh);
   DDP_STAMP(STAMP_K_XGMI, 7);
+}
+
+// dist_mode 3: both buckets in one launch (BwdXar arguments in device memory, copied to LDS:
+// from global memory inside the body every field was re-loaded after each store)
+__global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_pair_kernel(BwdXar x) {
+  __shared__ unsigned s_sh[2];
+  __shared__ __attribute__((aligned(16))) int s_raw[sizeof(XgmiArgs) / 4];  // XgmiArgs has initializers
+  const int nx = x.nblk0 + x.nblk1;
+  const int k = (int)blockIdx.x < x.nblk0 ? 0 : 1;
+  {
+    const int* src = reinterpret_cast<const int*>(x.args + k);
+    for (int i = threadIdx.x; i < (int)(sizeof(XgmiArgs) / 4); i += XGMI_THREADS) s_raw[i] = src[i];
+  }
+  __syncthreads();
+  const XgmiArgs& s_xa = *reinterpret_cast<const XgmiArgs*>(s_raw);
+  DDP_STAMP(STAMP_K_XGMI, 0);
+  if (k == 0) xgmi_allreduce_body(s_xa, (int)blockIdx.x, x.nblk0, s_sh);
+  else xgmi_allreduce_body(s_xa, (int)blockIdx.x - x.nblk0, x.nblk1, s_sh);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  DDP_STAMP(STAMP_K_XGMI, 7);
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(x.xar_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nx - 1 && x.step_ctr) x.step_ctr[0] += 1;
+  }
+}
+
+void xgmi_allreduce_pair(const BwdXar& x, hipStream_t s) {
+  hipLaunchKernelGGL(xgmi_allreduce_pair_kernel, dim3(x.nblk0 + x.nblk1), dim3(XGMI_THREADS), 0, s, x);
 }
 
 long xgmi_slice(long n, int world) { return (((n + world - 1) / world) + 3) & ~3L; }

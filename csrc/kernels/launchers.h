@@ -426,5 +426,10 @@ struct BwdXar {
   int* err = nullptr;         // 4: a completion wait timed out
 };
 constexpr int XAR_ERR = 4;
+// Both buckets' all-reduces in ONE launch (engine dist_mode 3, behind the conv backward on
+// the compute stream): blocks [0, nblk0) run bucket 0, [nblk0, nblk0 + nblk1) bucket 1,
+// concurrently; the waits / expected counts of BwdXar are unused, the last block advances
+// step_ctr (xar_done).
+void xgmi_allreduce_pair(const BwdXar& x, hipStream_t s);
 
 }  // namespace ddp_amd

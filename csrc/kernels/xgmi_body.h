@@ -21,9 +21,12 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
   const int t = threadIdx.x;
   if (t < a.world && !*s_fail) {
     unsigned* dst = a.sig[t] + XGMI_FLAG_OFF + blk * XGMI_MAX_RANKS + a.rank;
-    // release at system scope: everything this block stored (the caller drained its
-    // waves) is visible to the peers before they can see the flag
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    // No fences: everything a peer reads (gradient buckets, stage buffers) is written with
+    // system-scope write-through stores that every wave drained (s_waitcnt vmcnt(0)) before
+    // this flag store, and read with system-scope loads that bypass the caches - so a
+    // release (write-back of the whole L2) and an acquire (invalidation of L1 / L2, after
+    // which this block's own parameter loads missed) only cost time.  Producers with plain
+    // stores go through the publish pass (a.publish), which re-stores write-through.
     __hip_atomic_store(dst, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned* src = a.sig[a.rank] + XGMI_FLAG_OFF + blk * XGMI_MAX_RANKS + t;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -38,9 +41,6 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
         break;
       }
     }
-    // acquire at system scope: no later load of this block may hit a cache line older
-    // than the peer's release (invalidates this CU's L1 and the non-coherent L2 lines)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
 }
@@ -279,20 +279,37 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   DDP_STAMP(STAMP_K_XGMI, 3);
+  // ---- AG: quad q of every rank's reduced slice into my gradient buffer
+  // the thread's quads q0, q0 + G, ... of every rank's reduced slice as (quad j, rank p)
+  // items in order, XGMI_BATCH per batch: every load of a batch (reduced quads over xGMI,
+  // and with the fused optimizer the local parameter / momentum quads) is issued before
+  // the first store, whatever N is.  The first batch's parameter / momentum loads (local,
+  // independent of the reduction) go out before B1, their latency under the barrier's.
+  const bool vec = (a.off & 3) == 0;
+  const bool mom = a.sgd.momentum != 0.f;
+  const long Jg = sq > q0 ? (sq - q0 + G - 1) / G : 0;
+  const long items_g = Jg * N;
+  float4 pv[XGMI_BATCH], mv[XGMI_BATCH];
+  auto load_pm = [&](long i0) {
+    long jj = i0 / N;
+    int pp = (int)(i0 - jj * N);
+#pragma unroll
+    for (int u = 0; u < XGMI_BATCH; ++u) {
+      const long qq = (long)pp * sq + q0 + jj * G;
+      const bool whole = i0 + u < items_g && vec && 4 * qq + 3 < a.n && a.sgd.update;
+      pv[u] = whole ? ld_quad(a.params, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+      mv[u] = whole && mom ? ld_quad(a.mbuf, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (++pp == N) { pp = 0; ++jj; }
+    }
+  };
+  load_pm(0);
   xgmi_barrier(a, 2u * e + 1u, &s_fail, XGMI_PHASE_B1, blk);  // B1
   DDP_STAMP(STAMP_K_XGMI, 4);
   if (!s_fail) {
-    // ---- AG: quad q of every rank's reduced slice into my gradient buffer
-    // the thread's quads q0, q0 + G, ... of every rank's reduced slice as (quad j, rank p)
-    // items in order, XGMI_BATCH per batch: every load of a batch (reduced quads over xGMI,
-    // and with the fused optimizer the local parameter / momentum quads) is issued before
-    // the first store, whatever N is
-    const bool vec = (a.off & 3) == 0;
-    const bool mom = a.sgd.momentum != 0.f;
-    const long J = sq > q0 ? (sq - q0 + G - 1) / G : 0;
-    const long items = J * N;
+    const long items = items_g;
     for (long i0 = 0; i0 < items; i0 += XGMI_BATCH) {
-      float4 v[XGMI_BATCH], pv[XGMI_BATCH], mv[XGMI_BATCH];
+      float4 v[XGMI_BATCH];
+      if (i0 > 0) load_pm(i0);
       long jj = i0 / N;
       int pp = (int)(i0 - jj * N);
 #pragma unroll
@@ -300,9 +317,6 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
         const long q = q0 + jj * G, qq = (long)pp * sq + q;
         const bool ok = i0 + u < items && 4 * qq < a.n;
         v[u] = ok ? ld4_sys(sys_rsrc(a.stage[pp] + par), q) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const bool whole = ok && vec && 4 * qq + 3 < a.n;
-        pv[u] = whole && a.sgd.update ? ld_quad(a.params, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
-        mv[u] = whole && a.sgd.update && mom ? ld_quad(a.mbuf, a.off + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
         if (++pp == N) { pp = 0; ++jj; }
       }
       // finish one item per trip (the finishing code once, not XGMI_BATCH times: unrolled it

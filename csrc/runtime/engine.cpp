@@ -351,7 +351,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   if (dist && use_x && l3 && cfg_.dist_mode == 2 && !want_xar && std::getenv("DDP_AMD_XAR_DEBUG"))
     fprintf(stderr, "[ddp_amd] in-launch all-reduce off: plan_ok %d fc_role %d fred %d buckets %d\n",
             (int)xar_plan_ok_, (int)fc_role, (int)fred, (int)buckets_.size());
-  bool xar_used = false;
+  bool xar_used = false, pair_used = false;
   auto conv_launch = [&]() {
     if (f1) {
       // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
@@ -366,9 +366,18 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
       conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
     }
     if (!reduced) grad_reduce(ss, cs_);
-    if (xar_mode && !xar_used) {  // the in-launch all-reduce did not apply: bucket kernels behind it
-      enqueue_buckets(0, use_x, cs_, sa, M, sh_all);
-      enqueue_buckets(1, use_x, cs_, sa, M, sh_all);
+    if (xar_mode && !xar_used) {
+      // dist_mode 3 (or the in-launch all-reduce did not apply): the bucket all-reduces behind
+      // the conv backward on the compute stream - both in one launch when the plan allows
+      BwdXar pr;
+      if (cfg_.dist_mode == 3 && make_xar(pr, sa, M, sh_all)) {
+        xgmi_allreduce_pair(pr, cs_);
+        pair_used = true;
+        DDP_HIP_CHECK(hipGetLastError());
+      } else {
+        enqueue_buckets(0, use_x, cs_, sa, M, sh_all);
+        enqueue_buckets(1, use_x, cs_, sa, M, sh_all);
+      }
     }
   };
   // fc buckets overlap the conv backward: in-launch (dist_mode 2), or the fc weight gradient
@@ -379,6 +388,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   last_level3_ = l3;
   last_fc_role_ = fc_role;
   last_xar_ = xar_used;
+  last_pair_ = pair_used;
   if (fopt) return;
   if (dist && use_x) return;  // the optimizer ran inside the all-reduces
   // ---- optimizer + bf16 shadows + next batch window
@@ -407,20 +417,15 @@ void SimpleCNNEngine::enqueue_buckets(int stage, bool use_x, hipStream_t s, cons
 }
 
 bool SimpleCNNEngine::make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh) {
-  if (!xgmi_ || !xar_plan_ok_) return false;
+  if (!xgmi_ || !(cfg_.dist_mode == 3 ? pair_plan_ok_ : xar_plan_ok_)) return false;
   // the pair lives in device memory, one immutable copy per distinct content (a captured
   // graph keeps pointing at the copy it was captured with): the momentum-init step's and
   // the steady state's - both made on the first (eager) call, so a capture never needs a
   // new one - and a pair more if the learning rate changes
-  static const int expt = [] { const char* e = std::getenv("DDP_AMD_XAR_EXPT"); return e ? std::atoi(e) : 0; }();
   auto build = [&](const SgdArgs& g, XgmiArgs* pair) {
     for (int b = 0; b < (int)buckets_.size(); ++b) {
-      // the bucket's fused optimizer; the in-launch roles advance the step counter themselves
-      ShadowSet shx = sh;
-      if (expt == 1) shx.count = 0;  // TIMING EXPERIMENT ONLY: no shadow refresh (wrong results)
-      SgdArgs gx = g;
-      if (expt == 2) gx.update = 0;  // TIMING EXPERIMENT ONLY: no SGD (wrong results)
-      pair[stage_[b]] = xgmi_->make_args(xch_[b], gx, b_.params, M, shx, nullptr);
+      // the bucket's fused optimizer; the all-reduce roles advance the step counter themselves
+      pair[stage_[b]] = xgmi_->make_args(xch_[b], g, b_.params, M, sh, nullptr);
       (stage_[b] == 0 ? xa.nblk0 : xa.nblk1) = xgmi_->blocks(xch_[b]);
     }
   };
@@ -679,7 +684,7 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   bool reduced = false;
   BwdXar xa;
   const bool want_xar = xar_mode && cfg_.dist_mode == 2 && fc_role && fred && make_xar(xa, sa, M, sh1);
-  bool xar_used = false;
+  bool xar_used = false, pair_used = false;
   auto conv_launch = [&]() {
     reduced = conv3x3_bwd(b_.dz2_f32, b_.w2t_f32, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                           cfg_.wgrad_rows, c1b, static_cast<const float*>(nullptr), false, cs_,
@@ -688,8 +693,17 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
                           &xar_used);
     if (!reduced) grad_reduce(ss, cs_);
     if (xar_mode && !xar_used) {
-      enqueue_buckets(0, use_x, cs_, sa, M, sh1);
-      enqueue_buckets(1, use_x, cs_, sa, M, sh1);
+      // dist_mode 3 (or the in-launch all-reduce did not apply): the bucket all-reduces behind
+      // the conv backward on the compute stream - both in one launch when the plan allows
+      BwdXar pr;
+      if (cfg_.dist_mode == 3 && make_xar(pr, sa, M, sh1)) {
+        xgmi_allreduce_pair(pr, cs_);
+        pair_used = true;
+        DDP_HIP_CHECK(hipGetLastError());
+      } else {
+        enqueue_buckets(0, use_x, cs_, sa, M, sh1);
+        enqueue_buckets(1, use_x, cs_, sa, M, sh1);
+      }
     }
   };
   if (xar_mode) conv_launch();
@@ -698,6 +712,7 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   last_level3_ = l3;
   last_fc_role_ = fc_role;
   last_xar_ = xar_used;
+  last_pair_ = pair_used;
   if (fopt) return;
   if (dist && use_x) return;
   sgd_step(P, G, M, b_.n_params, sa, sh1, b_.step_ctr, cs_);
@@ -722,6 +737,7 @@ void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> cha
   // bucket, and a bounded number of role blocks (they wait at the head of the grid: <= 192
   // of its 512 resident slots, next to the fused reducers' <= 256)
   xar_plan_ok_ = false;
+  pair_plan_ok_ = false;
   if (xgmi_ && sync_ok_for_xar()) {
     int per[2] = {0, 0}, nb = 0;
     for (int b = 0; b < (int)buckets_.size(); ++b) {
@@ -729,6 +745,7 @@ void SimpleCNNEngine::set_xgmi(std::shared_ptr<XgmiComm> x, std::vector<int> cha
       nb += xgmi_->blocks(xch_[b]);
     }
     xar_plan_ok_ = per[0] <= 1 && per[1] == 1 && nb <= 192;
+    pair_plan_ok_ = per[0] <= 1 && per[1] == 1;
     if (std::getenv("DDP_AMD_XAR_DEBUG"))
       fprintf(stderr, "[ddp_amd] set_xgmi: stage buckets %d/%d, role blocks %d -> in-launch %d\n", per[0], per[1],
               nb, (int)xar_plan_ok_);

@@ -260,10 +260,15 @@ struct EngineConfig {
   //  1 = fork: fc_bwd and the fc buckets' all-reduces on the comm stream, forked after the
   //      forward beside the conv backward (a graph branch), the conv buckets' all-reduces
   //      behind the conv backward
-  //  3 = one stream (xGMI): the fc role inside the conv backward as on one GPU, then the
-  //      bucket kernels (full grids) behind it on the compute stream - no cross-stream edge
+  //  3 = one stream (xGMI, the default): the fc role inside the conv backward as on one GPU,
+  //      then ONE launch running both buckets' all-reduces (+ fused SGD) side by side on
+  //      full grids (xgmi_allreduce_pair; the bucket kernels one by one when the plan has
+  //      more buckets per stage) - 3 kernels per step, no cross-stream edge.  Fastest
+  //      measured (forced world 1: 639k img/s vs 444k in-launch, 416k fork;
+  //      profiles/r5_dist/README.md): the in-launch roles get too few blocks, a graph
+  //      branch costs two cross-stream edges
   //  0 = the round-4 order (fc_bwd in front of the conv backward, all-reduces on ms_)
-  int dist_mode = 2;
+  int dist_mode = 3;
 };
 
 // Gradient bucket of the engine's data plane: a [off, off + n) range of the flat gradient
@@ -305,6 +310,8 @@ class SimpleCNNEngine {
   bool last_fc_role() const { return last_fc_role_; }
   // ... and whether its bucket all-reduces ran inside the conv backward launch (dist_mode 2)
   bool last_xar() const { return last_xar_; }
+  // ... or behind it in one launch for both buckets (dist_mode 3, xgmi_allreduce_pair)
+  bool last_pair() const { return last_pair_; }
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
   // bucket b; set before capturing a graph
@@ -354,7 +361,9 @@ class SimpleCNNEngine {
   bool last_level3_ = false;
   bool last_fc_role_ = false;
   bool last_xar_ = false;
+  bool last_pair_ = false;
   bool xar_plan_ok_ = false;  // set_xgmi: the bucket plan fits the in-launch all-reduce
+  bool pair_plan_ok_ = false;  // ... and the one-launch pair of bucket kernels (dist_mode 3)
   struct XarArgs {
     XgmiArgs host[2];
     const XgmiArgs* dev = nullptr;

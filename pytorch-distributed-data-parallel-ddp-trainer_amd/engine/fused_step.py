@@ -116,7 +116,7 @@ class EngineOptions:
     # XAR); 1 = fc_bwd + the fc buckets' all-reduces on a graph branch forked after the
     # forward (schedule_backward); 3 = one stream: the fc role inside the conv backward, the
     # bucket kernels behind it (no cross-stream edge); 0 = the round-4 serial order
-    dist_mode: int = 2
+    dist_mode: int = 3
     # dist_mode 2: the most blocks of a bucket's xGMI channel (its role blocks wait at the
     # head of the conv backward grid; the engine takes the in-launch path while the channels'
     # blocks total <= 192)

@@ -1,2 +1,5 @@
 set -o pipefail
-scripts/gpu.sh sweep r5_modes "base||--no_fp32" "m1||--no_fp32 --force_allreduce --comm xgmi --dist_mode 1" "m2||--no_fp32 --force_allreduce --comm xgmi --dist_mode 2" "m2b||--no_fp32 --force_allreduce --comm xgmi --dist_mode 2 --xar_blocks 128" "m3||--no_fp32 --force_allreduce --comm xgmi --dist_mode 3" "r1||--no_fp32 --force_allreduce --comm rccl --dist_mode 1" "r0||--no_fp32 --force_allreduce --comm rccl --dist_mode 0"
+out=gpurun_out/r5_pair2; mkdir -p $out
+timeout -k 10 200 python scripts/stamps.py --force_allreduce --comm xgmi > $out/stamps_m3.txt 2>&1 && grep "^xgmi\|grad_reduce\|fc_bwd" $out/stamps_m3.txt | cut -c1-330 &&
+scripts/gpu.sh tests r5_pair2/t "dist_chains or verify_chain or xgmi_world1 or dist_chain or premul" &&
+scripts/gpu.sh sweep r5_pair2 "m3||--force_allreduce --comm xgmi"

@@ -491,8 +491,10 @@ def test_dist_chains_bitwise_world1(plane, dtype):
     one-GPU chain, at world size 1 with the all-reduces forced and the 8-rank bucket plan (fc
     bucket two-shot, conv bucket one-shot), graph-replayed, with momentum (the fused SGD of
     the xGMI all-gather updates the momentum buffer too) and a ragged last batch:
-    dist_mode 2 - the in-launch all-reduce (xGMI; 2 kernels per step, engine.cpp make_xar),
-    1 - fc_bwd + the fc bucket forked beside the conv backward, 0 - the round-4 serial order."""
+    dist_mode 3 (default) - both buckets' all-reduces in one launch behind the conv backward
+    (xGMI; 3 kernels per step, xgmi_allreduce_pair), 2 - the in-launch all-reduce (xGMI; 2
+    kernels per step, engine.cpp make_xar), 1 - fc_bwd + the fc bucket forked beside the conv
+    backward, 0 - the round-4 serial order."""
     import torch.distributed as dist
 
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -512,7 +514,8 @@ def test_dist_chains_bitwise_world1(plane, dtype):
         imgs, labels = synthetic_mnist(1000)  # 31 full batches + a ragged one of 8
         data = DeviceMNIST(imgs, labels, dev)
         out = {}
-        modes = (("local", False, 2), ("serial", True, 0), ("fork", True, 1), ("inlaunch", True, 2))
+        modes = (("local", False, 3), ("serial", True, 0), ("fork", True, 1), ("inlaunch", True, 2),
+                 ("pair", True, 3))
         for tag, force, mode in modes:
             torch.manual_seed(0)
             m = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
@@ -530,6 +533,7 @@ def test_dist_chains_bitwise_world1(plane, dtype):
             e.synchronize()
             assert e.eng.sync_error == 0 and e.eng.last_level3
             assert e.eng.last_xar == (tag == "inlaunch" and plane == "xgmi"), tag
+            assert e.eng.last_pair == (tag == "pair" and plane == "xgmi"), tag
             out[tag] = (e.fs.params.clone(), e.opt.momentum_buffer.clone())
         for tag, _, _ in modes[1:]:
             assert torch.equal(out[tag][0], out["local"][0]), tag
