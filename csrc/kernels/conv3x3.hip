@@ -1504,24 +1504,37 @@ static bool fwd_dz_fits(int B, int H, int W, int pxt) {
   if (per_blk > H * W || P >= (1L << 31)) return false;
   const long grid = (P + per_blk - 1) / per_blk;
   const size_t lds = conv3x3_fwd_lds(W, 32, pxt, true, (int)sizeof(T));
+  // the kernel fwd_launch will pick for this grid (bf16 pxt 2 beyond one block per CU: OCC 2)
+  bool occ2 = false;
   const void* k = pxt == 2 ? reinterpret_cast<const void*>(fwd_dz_kernel<T, 2>())
                            : reinterpret_cast<const void*>(fwd_dz_kernel<T, 1>());
-  lds_optin(pxt == 2 ? fwd_dz_kernel<T, 2>() : fwd_dz_kernel<T, 1>(), lds);
+  if constexpr (sizeof(T) == 2) {  // (no fp32 OCC 2 instantiation)
+    occ2 = pxt == 2 && fwd_dz_occ2((unsigned)grid);
+    if (occ2) {
+      k = reinterpret_cast<const void*>(fwd_dz_kernel<T, 2, 2>());
+      lds_optin(fwd_dz_kernel<T, 2, 2>(), lds);
+    }
+  }
+  if (!occ2) lds_optin(pxt == 2 ? fwd_dz_kernel<T, 2>() : fwd_dz_kernel<T, 1>(), lds);
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256 * pxt, lds) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, occ2 ? 512 : 256 * pxt, lds) != hipSuccess) return false;
   // Every block spins on the other blocks of its image (a window of <= 8 consecutive block
-  // indices: a block covers 64 * pxt <= H*W pixels).  The grid need NOT be resident at once
-  // (B = 64: 392 blocks on 256 slots): workgroups are dispatched in index order round-robin
-  // over the XCDs, so on the XCD with the lowest dispatch frontier F the oldest resident block
-  // b satisfies b + 8 < F whenever that XCD holds >= 3 resident blocks (they sit 8 indices
-  // apart) - every block of b's image is dispatched (lower frontiers nowhere), b's image
-  // completes and frees a slot; an XCD with a free slot dispatches its next block.  So the
-  // forward cannot deadlock while every XCD holds >= 3 of these blocks; 8 per XCD is asked
-  // (the launch runs alone on its stream - a step's kernels are stream-ordered).
-  (void)grid;
-  return (long)occ * cus >= 64;
+  // indices: a block covers 64 * pxt <= H*W pixels).  Default: the whole grid must fit the
+  // GPU at once (bf16 B = 64 does, with the OCC 2 forward: 392 blocks on 512 slots), so no
+  // dispatch-order assumption is needed; otherwise the level-1 chain runs.
+  if ((long)occ * cus >= grid) return true;
+  // Opt-in (DDP_AMD_L3_INORDER=1): a grid larger than the GPU, relying on workgroups being
+  // dispatched in index order round-robin over the XCDs - then on the XCD with the lowest
+  // dispatch frontier F the oldest resident block b satisfies b + 8 < F whenever that XCD
+  // holds >= 3 resident blocks (they sit 8 indices apart): every block of b's image is
+  // dispatched, b's image completes and frees a slot.  The hardware does not promise this
+  // order and a concurrent stream's kernels can hold the slots; the failure mode is the
+  // bounded wait (FWD_DZ_WAIT_TICKS) setting the step's error word - the engine's
+  // synchronize() raises and the start-up chain check downgrades to level 1.
+  static const bool inorder = [] { const char* e = getenv("DDP_AMD_L3_INORDER"); return e && e[0] == '1'; }();
+  return inorder && (long)occ * cus >= 64;
 }
 bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt, int es) {
   return es == 4 ? fwd_dz_fits<float>(B, H, W, pxt) : fwd_dz_fits<bf16_t>(B, H, W, pxt);

@@ -147,3 +147,40 @@ def test_torchrun_entrypoint_gpu(tmp_path):
     out2 = torchrun("--epochs", "2", "--max_steps", "30")
     assert "Resumed from" in out2 and "Rank 0: Starting epoch 1" in out2 and "Starting epoch 0" not in out2
     assert sorted(os.listdir(tmp_path / "checkpoints")) == ["epoch_0.pt", "epoch_1.pt"]
+
+
+def _bench(*args, timeout=240):
+    import json
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-u", os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    assert p.returncode == 0, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_fuse_level0_keeps_the_fp32_record():
+    """``--fuse_level 0`` is an advertised choice; the exact-fp32 run after
+    the bf16 headline has no level-0 chain and times level 1 instead of failing the bench."""
+    r = _bench("--steps", "4", "--warmup", "1", "--fuse_level", "0")
+    c = r["config"]
+    assert r["n_gpus"] == 1 and r["value"] > 0 and c["fuse_level"] == 0
+    assert c["fp32_images_per_sec"] and c["fp32_images_per_sec"] > 0
+
+
+def test_bench_forced_dist_record():
+    """the multi-GPU chain timed on one GPU (``--force_allreduce``: world size
+    1, the 8-rank bucket plan over the xGMI kernels) reports the default one-stream chain
+    with both buckets' all-reduces in one launch (3 kernels per step), the per-step
+    breakdown against the comm-free engine, and the plan's cost source."""
+    r = _bench("--steps", "20", "--warmup", "5", "--force_allreduce", "--no_fp32")
+    c = r["config"]
+    assert c["force_allreduce"] and c["bucket_allreduce"].startswith("xgmi")
+    assert c["pair_allreduce"] and not c["inlaunch_allreduce"] and c["kernels_per_step"] == 3
+    b = c["step_breakdown"]
+    assert b["step_us"] > 0 and b["local_step_us"] > 0 and b["local_kernels_per_step"] == 2
+    assert c["bucket_plan"]["cost_source"]
+    assert c["params_finite"]
