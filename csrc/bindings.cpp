@@ -385,7 +385,7 @@ void op_conv_gemm_fwd(const Tensor& X, const Tensor& Wt, std::optional<Tensor> b
   }
   const BnAffine aff = bn_affine_of(bn, g.Cin);
   TORCH_CHECK(!aff.mean || (pl.halo && g.Cin <= 512), "conv_gemm_fwd: an input BatchNorm affine needs the halo plan");
-  conv_gemm_fwd(g, pl, cbf(X), cbf(Wt), bp_, bf(Y), relu, st, pt, cur_stream(), nullptr, &aff);
+  conv_gemm_fwd(g, pl, cbf(X), cbf(Wt), bp_, bf(Y), relu, st, pt, cur_stream(), &aff);
   kcheck();
 }
 
@@ -428,56 +428,6 @@ void op_conv_gemm_wgrad(const Tensor& dY, const Tensor& X, Tensor& out, int KH, 
   TORCH_CHECK(!aff.mean || conv_gemm_wgrad_uses_halo(g, ppc),
               "conv_gemm_wgrad: an input BatchNorm affine needs the halo weight gradient");
   conv_gemm_wgrad(g, cbf(dY), cbf(X), out.data_ptr<float>(), ppc, accum, cur_stream(), ks, &aff);
-  kcheck();
-}
-
-// conv_gemm_fwd (default plan, no bias / ReLU) whose stats-producing launch also finalises
-// the training BatchNorm (kernels/bn_tail.h): mean / invstd / running stats / batches
-// tracked without a bn_finalize launch.  ws: [bn_tail_groups(rows)][2][Cout].
-void op_conv_bn_fwd(const Tensor& X, const Tensor& Wt, Tensor& Y, int KH, int KW, int stride, int pad,
-                    Tensor& stats, std::optional<Tensor> part, Tensor& ws, double count, double eps,
-                    double momentum, std::optional<Tensor> rmean, std::optional<Tensor> rvar, Tensor& mean,
-                    Tensor& invstd, std::optional<Tensor> nbt) {
-  check(X, "X", at::kBFloat16); check(Wt, "Wt", at::kBFloat16); check(Y, "Y", at::kBFloat16);
-  const ConvGeom g = geom_of(X, Y, KH, KW, stride, pad);
-  TORCH_CHECK(g.Cin % 32 == 0 || (g.Cin == 4 && g.Cout % 64 == 0), "conv_bn_fwd: Cin % 32 (or stem Cin=4)");
-  TORCH_CHECK(g.Cout % 64 == 0 && g.Cout <= 512, "conv_bn_fwd: Cout % 64, <= 512");
-  TORCH_CHECK(Wt.numel() == (long)g.Cout * KH * KW * g.Cin, "conv_bn_fwd: weight shape");
-  const ConvPlan pl = plan_of(g, false, 0, 0, 0, -1, -1);
-  const int rows = conv_gemm_stat_rows(g, pl);
-  check(stats, "stats", at::kFloat); check(ws, "ws", at::kFloat);
-  check(mean, "mean", at::kFloat); check(invstd, "invstd", at::kFloat);
-  TORCH_CHECK(stats.numel() >= (long)rows * 2 * g.Cout, "stats slab too small");
-  TORCH_CHECK(ws.numel() >= (long)bn_tail_groups(rows) * 2 * g.Cout, "conv_bn_fwd: ws too small");
-  TORCH_CHECK(mean.numel() == g.Cout && invstd.numel() == g.Cout, "mean / invstd size");
-  float* pt = nullptr;
-  if (pl.splits > 1) {
-    TORCH_CHECK(part.has_value(), "conv_bn_fwd: split plan needs the fp32 `part` workspace");
-    check(*part, "part", at::kFloat);
-    TORCH_CHECK(part->numel() >= (long)pl.splits * g.N * g.OH * g.OW * g.Cout, "part workspace too small");
-    pt = part->data_ptr<float>();
-  }
-  BnFin f;
-  f.rows = rows;
-  f.C = g.Cout;
-  f.count = (float)count;
-  f.eps = (float)eps;
-  f.momentum = (float)momentum;
-  if (rmean) {
-    check(*rmean, "running_mean", at::kFloat); check(*rvar, "running_var", at::kFloat);
-    TORCH_CHECK(rmean->numel() == g.Cout && rvar->numel() == g.Cout, "running stats size");
-    f.running_mean = rmean->data_ptr<float>();
-    f.running_var = rvar->data_ptr<float>();
-  }
-  f.save_mean = mean.data_ptr<float>();
-  f.save_invstd = invstd.data_ptr<float>();
-  if (nbt) {
-    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "num_batches_tracked");
-    f.nbt = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
-  }
-  f.ws = ws.data_ptr<float>();
-  f.tickets = bn_ticket_slots(conv_gemm_stat_colblocks(g, pl) * (bn_tail_groups(rows) + 1));
-  conv_gemm_fwd(g, pl, cbf(X), cbf(Wt), nullptr, bf(Y), false, stats.data_ptr<float>(), pt, cur_stream(), &f);
   kcheck();
 }
 
@@ -784,11 +734,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stride"), py::arg("pad"), py::arg("dgrad") = false, py::arg("bp") = 0, py::arg("bc") = 0,
         py::arg("splits") = 0, py::arg("parity") = -1, py::arg("halo") = -1);
   m.def("bn_finalize", &op_bn_finalize);
-  m.def("conv_bn_fwd", &op_conv_bn_fwd, py::arg("X"), py::arg("W"), py::arg("Y"), py::arg("KH"), py::arg("KW"),
-        py::arg("stride"), py::arg("pad"), py::arg("stats"), py::arg("part"), py::arg("ws"), py::arg("count"),
-        py::arg("eps"), py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("mean"),
-        py::arg("invstd"), py::arg("nbt"));
-  m.def("bn_tail_groups", &bn_tail_groups);
   // host-side wait policy of the device (before torch creates its context): 1 =
   // hipDeviceScheduleSpin - synchronize() polls the completion signal instead of sleeping
   m.def("hip_set_device_flags", [](int dev, unsigned flags) {
@@ -804,9 +749,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dgamma"), py::arg("dbeta"), py::arg("accum"), py::arg("dx"), py::arg("dres"),
         py::arg("dout2") = py::none(), py::arg("mask_beta") = py::none());
   m.def("bn_bwd_set_px_per_block", &bn_bwd_set_px_per_block);
-  m.def("bn_bwd_set_fused", &bn_bwd_set_fused);
-  m.def("bn_bwd_fused_ok", &bn_bwd_fused_ok);
-  m.def("bn_bwd_fused_error", &bn_bwd_fused_error, py::arg("reset") = true);
   m.def("maxpool_fwd", &op_maxpool_fwd, py::arg("x"), py::arg("y"), py::arg("amax"), py::arg("bn") = py::none());
   m.def("maxpool_bwd", &op_maxpool_bwd, py::arg("dy"), py::arg("amax"), py::arg("dx"),
         py::arg("dy2") = py::none());

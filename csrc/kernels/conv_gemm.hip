@@ -28,7 +28,6 @@
 #include <stdexcept>
 #include <type_traits>
 
-#include "kernels/bn_tail.h"
 #include "kernels/common.h"
 #include "kernels/launchers.h"
 
@@ -78,8 +77,7 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
                                                             const float* __restrict__ bias,
                                                             bf16_t* __restrict__ Y,
                                                             float* __restrict__ stats,
-                                                            float* __restrict__ part, int ks_per,
-                                                            BnFin fin) {
+                                                            float* __restrict__ part, int ks_per) {
   static_assert(!STEM || (BP == 128 && !PART), "stem: 128-pixel tile, unsplit");
   __shared__ __attribute__((aligned(16))) bf16_t sA[2][BC * CG_RS];
   __shared__ __attribute__((aligned(16))) bf16_t sB[2][BP * CG_RS];
@@ -271,13 +269,12 @@ __global__ __launch_bounds__(256) void conv_gemm_fwd_kernel(ConvGeom g, const bf
         }
       }
     __syncthreads();
-    // stats slab: [blocks_x][2][Cout] (write-through: the BatchNorm tail reads it)
+    // stats slab: [blocks_x][2][Cout]
     for (int c = tid; c < BC; c += 256) {
       float* dst = stats + (long)bk.x * 2 * g.Cout;
       st_wt(dst + co0 + c, s_st[0][0][c] + s_st[1][0][c]);
       st_wt(dst + g.Cout + co0 + c, s_st[0][1][c] + s_st[1][1][c]);
     }
-    if (fin.tickets) bn_stats_tail(fin, stats, bk.x, bk.y, co0, BC, reinterpret_cast<float*>(&sA[0][0]));
   }
 }
 
@@ -637,7 +634,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             int C, int rpb,
                                                             const bf16_t* __restrict__ Xact,
                                                             bf16_t* __restrict__ out,
-                                                            float* __restrict__ stats, BnFin fin) {
+                                                            float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) float sred[];  // [pl][2][C]
   const int cg = C / 8, pl = 256 / cg;
   const int tg = threadIdx.x % cg, tp = threadIdx.x / cg;
@@ -698,8 +695,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     st_wt(stats + (long)blockIdx.x * 2 * C + c, a);
     st_wt(stats + (long)blockIdx.x * 2 * C + C + c, b);
   }
-  // (the [pl][2][C] LDS partials are dead: >= 2C + 512 floats for C <= 512)
-  if (fin.tickets) bn_stats_tail(fin, stats, blockIdx.x, 0, 0, C, sred);
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -989,47 +984,33 @@ int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl) {
 }
 
 static void splitk_reduce(const float* part, int S, long P, int C, const bf16_t* Xact, bf16_t* out,
-                          float* stats, hipStream_t s, const BnFin* fin = nullptr) {
+                          float* stats, hipStream_t s) {
   int rpb;
   const int nb = splitk_rows(P, C, &rpb);
-  size_t lds = stats ? sizeof(float) * (256 / (C / 8)) * 2 * C : 0;
-  BnFin f;
-  if (stats && fin) {
-    f = *fin;
-    if (f.rows != nb) throw std::runtime_error("splitk_reduce: BatchNorm tail rows != stats rows");
-    const size_t need = sizeof(float) * (2 * C + 512);
-    if (lds < need) lds = need;
-  }
-#define SKR(M, ST) hipLaunchKernelGGL((splitk_reduce_kernel<M, ST>), dim3(nb), dim3(256), lds, s, part, S, (int)P, C, rpb, Xact, out, stats, f)
+  const size_t lds = stats ? sizeof(float) * (256 / (C / 8)) * 2 * C : 0;
+#define SKR(M, ST) hipLaunchKernelGGL((splitk_reduce_kernel<M, ST>), dim3(nb), dim3(256), lds, s, part, S, (int)P, C, rpb, Xact, out, stats)
   if (Xact) { if (stats) SKR(true, true); else SKR(true, false); }
   else { if (stats) SKR(false, true); else SKR(false, false); }
 #undef SKR
 }
 
-int conv_gemm_stat_colblocks(const ConvGeom& g, const ConvPlan& pl) {
-  return pl.splits > 1 ? 1 : g.Cout / pl.bc;
-}
-
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,
                    const float* bias, bf16_t* Y, bool relu, float* stats, float* part, hipStream_t s,
-                   const BnFin* fin, const BnAffine* aff) {
-  if (fin && (!stats || fin->rows != conv_gemm_stat_rows(g, pl) || fin->C != g.Cout))
-    throw std::runtime_error("conv_gemm_fwd: BatchNorm tail needs the stats slab of this plan");
+                   const BnAffine* aff) {
   if (aff && aff->mean && !pl.halo)
     throw std::runtime_error("conv_gemm_fwd: an input BatchNorm affine needs the halo plan");
   if (pl.halo) {  // no bias / ReLU epilogue on this path (the host plans it off then)
-    conv_halo_fwd(g, pl.bp, pl.bc, pl.splits, X, Wt, Y, stats, part, s, pl.splits > 1 ? nullptr : fin, aff);
-    if (pl.splits > 1) splitk_reduce(part, pl.splits, (long)g.N * g.OH * g.OW, g.Cout, nullptr, Y, stats, s, fin);
+    conv_halo_fwd(g, pl.bp, pl.bc, pl.splits, X, Wt, Y, stats, part, s, aff);
+    if (pl.splits > 1) splitk_reduce(part, pl.splits, (long)g.N * g.OH * g.OW, g.Cout, nullptr, Y, stats, s);
     return;
   }
   const dim3 grid(pl.grid_x, pl.grid_y, pl.splits);
   const int kp = pl.ks_per;
-  const BnFin f = (fin && pl.splits <= 1) ? *fin : BnFin{};
   if (g.Cin == 4) {  // stem: 8 taps x 4 channels per K-step (host enforces Cout % 64)
     const bool s224 = stem_geo_224(g);
     // the 224 x 224 stem: staged-halo kernel (DDP_AMD_STEM_HALO=0: the gathered K loop)
     static const int stem_halo = [] { const char* e = getenv("DDP_AMD_STEM_HALO"); return e ? atoi(e) : 1; }();
-    if (s224 && stem_halo && !f.tickets && pl.splits <= 1 && grid.x * 128 >= (unsigned)(g.N * 112 * 112)) {
+    if (s224 && stem_halo && pl.splits <= 1 && grid.x * 128 >= (unsigned)(g.N * 112 * 112)) {
       // persistent: two blocks per CU, each over a contiguous range of the 128-pixel tiles
       static const int cus = [] {
         int dev = 0, n = 0;
@@ -1047,8 +1028,8 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
     }
 #define CGS(RL, ST)                                                                                                  \
   do {                                                                                                               \
-    if (s224) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 1>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f); \
-    else hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 0>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f); \
+    if (s224) hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 1>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp); \
+    else hipLaunchKernelGGL((conv_gemm_fwd_kernel<128, 64, RL, ST, true, false, 0>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp); \
   } while (0)
     if (stats) CGS(false, true);
     else if (relu) CGS(true, false);
@@ -1056,7 +1037,7 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
 #undef CGS
     return;
   }
-#define CGF(BP, BC, RL, ST, PT) hipLaunchKernelGGL((conv_gemm_fwd_kernel<BP, BC, RL, ST, false, PT>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp, f)
+#define CGF(BP, BC, RL, ST, PT) hipLaunchKernelGGL((conv_gemm_fwd_kernel<BP, BC, RL, ST, false, PT>), grid, dim3(256), 0, s, g, X, Wt, bias, Y, stats, part, kp)
 #define CGF_BP(BP, BC)                                                           \
   if (pl.splits > 1) CGF(BP, BC, false, false, true);                            \
   else if (stats) { if (relu) CGF(BP, BC, true, true, false); else CGF(BP, BC, false, true, false); } \
@@ -1067,7 +1048,7 @@ void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const
 #undef CGF
   if (pl.splits > 1) {
     // bias / ReLU of the split path: only the BatchNorm use (no bias, no ReLU) is split
-    splitk_reduce(part, pl.splits, (long)g.N * g.OH * g.OW, g.Cout, nullptr, Y, stats, s, fin);
+    splitk_reduce(part, pl.splits, (long)g.N * g.OH * g.OW, g.Cout, nullptr, Y, stats, s);
   }
 }
 

@@ -17,7 +17,6 @@
 #include <stdexcept>
 
 #include "kernels/bn_affine.h"
-#include "kernels/bn_tail.h"
 #include "kernels/common.h"
 #include "kernels/launchers.h"
 
@@ -40,7 +39,7 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
                                                                  bf16_t* __restrict__ Y,
                                                                  float* __restrict__ stats,
                                                                  float* __restrict__ part, int R,
-                                                                 int chunks_per_split, BnFin fin, BnAffine bn) {
+                                                                 int chunks_per_split, BnAffine bn) {
   constexpr int TCO = BC / 32, TPX = BP / 32;
   constexpr int HCH = (HL_MAXPX * 4 + 255) / 256;  // 16-B halo chunks per thread
   // weights of one kernel row (3 taps) per K-step: 3 MFMA K-steps between barriers
@@ -232,8 +231,6 @@ __global__ __launch_bounds__(256) void conv3x3s1_halo_fwd_kernel(ConvGeom g, con
       st_wt(dst + co0 + c, s_st[0][0][c] + s_st[1][0][c]);
       st_wt(dst + g.Cout + co0 + c, s_st[0][1][c] + s_st[1][1][c]);
     }
-    // (the halo buffers are dead too: the BatchNorm tail's LDS)
-    if (fin.tickets) bn_stats_tail(fin, stats, bk.x, bk.y, co0, BC, reinterpret_cast<float*>(&sH[0][0]));
   }
 }
 
@@ -445,8 +442,7 @@ bool conv_halo_fits(const ConvGeom& g, int bp) {
 int conv_halo_rows(const ConvGeom& g, int bp) { return bp / g.W; }
 
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
-                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin, const BnAffine* aff) {
-  const BnFin f = (fin && stats && splits <= 1) ? *fin : BnFin{};
+                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnAffine* aff) {
   const bool af = aff && aff->mean;
   if (af && g.Cin > 512) throw std::runtime_error("conv_halo_fwd: input BatchNorm affine needs Cin <= 512");
   const BnAffine a = af ? *aff : BnAffine{};
@@ -459,8 +455,8 @@ void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* 
   const int gw = g.W == 56 ? 56 : g.W == 28 ? 28 : g.W == 14 ? 14 : 0;
 #define HLF_W(BC, BP, ST, PT, GWV)                                                                              \
   do {                                                                                                          \
-    if (af) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, true, GWV>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
-    else hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, false, GWV>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, f, a); \
+    if (af) hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, true, GWV>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, a); \
+    else hipLaunchKernelGGL((conv3x3s1_halo_fwd_kernel<BC, BP, ST, PT, false, GWV>), grid, dim3(256), 0, s, g, X, Wt, Y, stats, part, R, cps, a); \
   } while (0)
 #define HLF(BC, BP, ST, PT)                                              \
   do {                                                                   \

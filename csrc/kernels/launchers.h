@@ -118,20 +118,6 @@ struct BnAffine {
   const float* gamma = nullptr;
   const float* beta = nullptr;
 };
-// BatchNorm finalisation folded into the stats-producing launch (kernels/bn_tail.h):
-// tickets == nullptr means "stats only" (a separate bn_finalize follows)
-struct BnFin {
-  int rows = 0, C = 0;
-  float count = 1.f, eps = 1e-5f, momentum = 0.1f;
-  float* running_mean = nullptr;
-  float* running_var = nullptr;
-  float* save_mean = nullptr;
-  float* save_invstd = nullptr;
-  long long* nbt = nullptr;
-  float* ws = nullptr;     // [groups][2][C], groups = ceil(rows / 32)
-  int* tickets = nullptr;  // [column blocks][groups + 1], zero (self-resetting)
-};
-int bn_tail_groups(int rows);
 int* bn_ticket_slots(int n);  // zeroed, self-resetting ticket words (round-robin pool)
 // launch plan: pixel tile bp (64/128), channel tile bc (64/128), K splits (grid.z)
 struct ConvPlan {
@@ -157,17 +143,14 @@ void conv_gemm_wgrad_set_halo(int halo, int target, int cit = 0);  // cit 0 = au
 // whole-row chunks for the halo kernel
 bool conv_gemm_wgrad_ppc_ok(const ConvGeom& g, int ppc);
 void conv_halo_fwd(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* X, const bf16_t* Wt,
-                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnFin* fin = nullptr,
-                   const BnAffine* aff = nullptr);
+                   bf16_t* Y, float* stats, float* part, hipStream_t s, const BnAffine* aff = nullptr);
 void conv_halo_dgrad(const ConvGeom& g, int bp, int bc, int splits, const bf16_t* dY, const bf16_t* Wt,
                      const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s);
 int conv_gemm_stat_rows(const ConvGeom& g, const ConvPlan& pl);  // BN stats slab rows (fwd)
 // splits > 1: `part` = fp32 workspace [splits][P][C]; no bias / ReLU on the split path
 void conv_gemm_fwd(const ConvGeom& g, const ConvPlan& pl, const bf16_t* X, const bf16_t* Wt,
                    const float* bias, bf16_t* Y, bool relu, float* stats, float* part, hipStream_t s,
-                   const BnFin* fin = nullptr, const BnAffine* aff = nullptr);  // aff: halo plans only
-// column blocks of the stats producer (its ticket strips) for a BnFin of this plan
-int conv_gemm_stat_colblocks(const ConvGeom& g, const ConvPlan& pl);
+                   const BnAffine* aff = nullptr);  // aff: halo plans only
 // W: the OHWI forward weight itself (read transposed through LDS)
 void conv_gemm_dgrad(const ConvGeom& g, const ConvPlan& pl, const bf16_t* dY, const bf16_t* W,
                      const bf16_t* Xact, bf16_t* dX, float* part, hipStream_t s);
@@ -192,9 +175,6 @@ void bn_apply(const bf16_t* x, long P, int C, const float* mean, const float* in
               const float* gamma, const float* beta, const bf16_t* res, bool relu, bf16_t* y,
               hipStream_t s);
 void bn_bwd_set_px_per_block(int px);
-void bn_bwd_set_fused(int on);                        // 0: always the two-launch backward
-bool bn_bwd_fused_ok(long P, int C, bool relu);       // this shape runs as one launch
-int bn_bwd_fused_error(bool reset);                   // 1 after a timed-out in-launch wait
 int bn_bwd_rows(long P, int C, int* rpb);  // ws of bn_bwd: [rows][2][C]
 // dout2 (optional): a second upstream gradient of the same tensor, summed on load
 // (bf16-rounded, == autograd's add) - the ResNet block input's two consumers

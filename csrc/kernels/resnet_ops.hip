@@ -199,22 +199,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 // block sums ws[0..R) in fixed order into sums[2C] = [sum dy | sum dy*xhat] and the
 // affine gradients (dbeta = sum dy, dgamma = sum dy*xhat; `accum` adds to them).
 //
-// FUSED (one launch per BatchNorm backward): every block then waits for its strip's
-// finished sums (the last block raises the strip flag) and applies pass 2 to the same
-// pixels it reduced - they are still in L2 / MALL.  Needs the whole grid co-resident
-// (the launcher checks the occupancy); the wait is bounded (err word) and a second
-// arrival count re-arms the flag for the next launch / graph replay.
-struct BnBwdFused {
-  const float* gamma = nullptr;
-  float count = 1.f;
-  bf16_t* dx = nullptr;
-  bf16_t* dres = nullptr;
-  int* flags = nullptr;  // [strips] strip flags, then [strips] second-arrival tickets (zero)
-  int* err = nullptr;    // set to 1 when a wait times out
-};
-constexpr unsigned long long BN_WAIT_TICKS = 20000000;  // 200 ms of the 100 MHz clock
-
-template <int MSK, bool FUSED>
+// (A one-launch variant - every block applying pass 2 to its own pixels after an in-launch
+// wait for the strip's sums - measured slower at every ResNet-18 layer and was removed in
+// round 5: profiles/r3_bn_fusion.)
+template <int MSK>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
                                                             const bf16_t* __restrict__ dout2,
                                                             const bf16_t* __restrict__ out,
@@ -225,7 +213,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             float* __restrict__ sums,
                                                             float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta, int accum,
-                                                            BnBwdFused fz, const float* __restrict__ mgamma,
+                                                            const float* __restrict__ mgamma,
                                                             const float* __restrict__ mbeta) {
   __shared__ float sred[32][2][64];
   __shared__ float sfin[8][128];
@@ -328,9 +316,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     for (int t = 0; t < 32; ++t) a += sred[t][which][cc];
     st_wt(ws + ((long)blockIdx.y * 2 + which) * C + cb + cc, a);
   }
-  const bool last = last_arrival(&tickets[blockIdx.x], R, &s_last);
-  if (!FUSED && !last) return;
-  if (last) {
+  if (!last_arrival(&tickets[blockIdx.x], R, &s_last)) return;
   // Fixed-order sum of the R partial rows: thread = 4 of the strip's 128 values (float4)
   // x one of 8 row phases, up to 8 rows in flight.  Plain loads are coherent here: the
   // rows were stored write-through and no block of this kernel read them before.
@@ -362,73 +348,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 #pragma unroll
     for (int k = 1; k < 8; ++k) tot += sfin[k][v];
     const int c = cb + cc;
-    if (FUSED) st_wt(sums + which * C + c, tot);
-    else sums[which * C + c] = tot;
+    sums[which * C + c] = tot;
     float* dst = which ? dgamma : dbeta;
     if (dst) dst[c] = accum ? dst[c] + tot : tot;
   }
-  }  // last
-  if (!FUSED) return;
-  // ---- pass 2 on this block's pixels, after the strip's sums are published
-  int* flag = fz.flags + blockIdx.x;
-  if (last) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the st_wt sums are out
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (threadIdx.x < 64) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > BN_WAIT_TICKS) {
-        if (threadIdx.x == 0) __hip_atomic_store(fz.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  {
-    float k[8], sd[8], sq[8];
-    ld8f(fz.gamma + c0, k);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      k[j] = k[j] * is[j] / fz.count;
-      sd[j] = ld_agent(sums + c0 + j);
-      sq[j] = ld_agent(sums + C + c0 + j);
-    }
-    auto apply8 = [&](long o, bf16x8 gd, bf16x8 gx, bf16x8 go) {
-      float d[8], xv[8], r[8];
-      unpack8_sum(gd, dout2, o, d);
-      unpack8(gx, xv);
-      bn_mask8<MSK>(go, xv, msc, msh, d);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (xv[j] - mu[j]) * is[j];
-        r[j] = k[j] * (fz.count * d[j] - sd[j] - xh * sq[j]);
-      }
-      *reinterpret_cast<uint4*>(fz.dx + o) = pack8(r);
-      if (fz.dres) *reinterpret_cast<uint4*>(fz.dres + o) = pack8(d);
-    };
-    int pp = p0 + tp;
-    for (; pp + 96 < p1; pp += 128) {  // four pixels' loads in flight (one block per CU here)
-      bf16x8 d[4], xx[4], r[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long o = (long)(pp + 32 * u) * C + c0;
-        d[u] = ld8(dout + o);
-        xx[u] = ld8(x + o);
-        r[u] = MSK == 1 ? ld8(out + o) : zero8();
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) apply8((long)(pp + 32 * u) * C + c0, d[u], xx[u], r[u]);
-    }
-    for (; pp < p1; pp += 32) {
-      const long o = (long)pp * C + c0;
-      apply8(o, ld8(dout + o), ld8(x + o), MSK == 1 ? ld8(out + o) : zero8());
-    }
-  }
-  // re-arm: the strip's last block through here lowers the flag
-  if (last_arrival(fz.flags + gridDim.x + blockIdx.x, R, &s_last) && threadIdx.x == 0)
-    __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Backward pass 2: dx = gamma*invstd/count * (count*dy - sum_dy - xhat*sum_dyxh); also
@@ -804,8 +727,6 @@ static unsigned grid_for(long n, int per_thread = 1) {
 
 // Ticket words for last_arrival: one zeroed pool per device, handed out round-robin
 // (every kernel resets the tickets it used, so a slot is clean when it comes round).
-int bn_tail_groups(int rows) { return (rows + BN_TAIL_GROUP - 1) / BN_TAIL_GROUP; }
-
 int* bn_ticket_slots(int n) {
   constexpr int kSlots = 1 << 16;
   static int* pool[64] = {};
@@ -872,62 +793,6 @@ int bn_bwd_rows(long P, int C, int* rpb) {
   return (int)((P + r - 1) / r);
 }
 
-// Single-launch backward (FUSED): used when enabled (bn_bwd_set_fused(1)) and the whole
-// grid fits half the device's resident capacity for the kernel (occupancy x CUs).  Off by
-// default: measured slower than the two launches at every ResNet-18 layer (B=32: 14.4 vs
-// 13.6 us at 7x7x512, 40.6 vs 30.8 us at 56x56x64 - its pass 2 runs on the reduce grid's
-// few fat blocks, profiles/r3_bn_fusion).
-static int g_bn_bwd_fused = 0;
-void bn_bwd_set_fused(int on) { g_bn_bwd_fused = on; }
-
-static int* bn_err_word() {
-  static int* w[64] = {};
-  int dev = 0;
-  RN_CHECK(hipGetDevice(&dev));
-  dev &= 63;
-  if (!w[dev]) {
-    RN_CHECK(hipMalloc(reinterpret_cast<void**>(&w[dev]), sizeof(int)));
-    RN_CHECK(hipMemset(w[dev], 0, sizeof(int)));
-    RN_CHECK(hipDeviceSynchronize());
-  }
-  return w[dev];
-}
-
-int bn_bwd_fused_error(bool reset) {
-  int* w = bn_err_word();
-  int v = 0;
-  RN_CHECK(hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost));
-  if (reset && v) RN_CHECK(hipMemset(w, 0, sizeof(int)));
-  return v;
-}
-
-template <int MSK>
-static long bn_bwd_fused_capacity() {
-  static long cap[64] = {};
-  int dev = 0;
-  RN_CHECK(hipGetDevice(&dev));
-  dev &= 63;
-  if (!cap[dev]) {
-    int per_cu = 0, cus = 0;
-    RN_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bn_bwd_reduce_kernel<MSK, true>, 256, 0));
-    RN_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    cap[dev] = (long)per_cu * cus;
-    if (cap[dev] <= 0) cap[dev] = -1;
-  }
-  return cap[dev];
-}
-
-static long bn_bwd_capacity(int msk) {
-  return msk == 1 ? bn_bwd_fused_capacity<1>() : msk == 2 ? bn_bwd_fused_capacity<2>() : bn_bwd_fused_capacity<0>();
-}
-
-bool bn_bwd_fused_ok(long P, int C, bool relu) {
-  if (!g_bn_bwd_fused) return false;
-  const long blocks = (long)(C / 64) * bn_bwd_rows(P, C, nullptr);
-  // half the resident capacity: other streams' kernels (bucket all-reduces) may hold CUs
-  return blocks <= bn_bwd_capacity(relu ? 1 : 0) / 2;
-}
-
 void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int C, const float* mean,
             const float* invstd, const float* gamma, float count, float* ws, float* sums,
             float* dgamma, float* dbeta, bool accum, bf16_t* dx, bf16_t* dres, hipStream_t s,
@@ -938,19 +803,8 @@ void bn_bwd(const bf16_t* dout, const bf16_t* out, const bf16_t* x, long P, int 
   int* tk = bn_ticket_slots(C / 64);
   // ReLU mask: the saved output, or (no output given, mask_beta given) recomputed from x
   const int msk = out ? 1 : (mask_beta ? 2 : 0);
-  BnBwdFused fz;
-#define BNR(M, F) hipLaunchKernelGGL((bn_bwd_reduce_kernel<M, F>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, fz, gamma, mask_beta)
-  if (g_bn_bwd_fused && (long)(C / 64) * R <= bn_bwd_capacity(msk) / 2) {
-    fz.gamma = gamma;
-    fz.count = count;
-    fz.dx = dx;
-    fz.dres = dres;
-    fz.flags = bn_ticket_slots(2 * (C / 64));
-    fz.err = bn_err_word();
-    if (msk == 1) BNR(1, true); else if (msk == 2) BNR(2, true); else BNR(0, true);
-    return;
-  }
-  if (msk == 1) BNR(1, false); else if (msk == 2) BNR(2, false); else BNR(0, false);
+#define BNR(M) hipLaunchKernelGGL((bn_bwd_reduce_kernel<M>), grid, dim3(256), 0, s, dout, dout2, out, x, (int)P, C, mean, invstd, rpb, ws, tk, sums, dgamma, dbeta, (int)accum, gamma, mask_beta)
+  if (msk == 1) BNR(1); else if (msk == 2) BNR(2); else BNR(0);
 #undef BNR
   const unsigned g = grid_for(P * C, 8);
 #define BNA(M) hipLaunchKernelGGL(bn_bwd_apply_kernel<M>, dim3(g), dim3(256), 0, s, dout, dout2, out, x, P * C / 8, C, mean, invstd, gamma, sums, count, dx, dres, mask_beta)

@@ -37,13 +37,9 @@ from .. import native
 from . import direct_grad
 
 BF16 = torch.bfloat16
-# Opt-in launch-count reductions of the BatchNorm (measured SLOWER on MI355X, so off by
-# default - profiles/r3_bn_fusion): DDP_AMD_BN_TAIL=1 finalises the statistics inside the
-# stats-producing conv launch (kernels/bn_tail.h; -20 bn_finalize launches, but every
-# producer block then pays a write-through drain + ticket round trip while holding its CU:
-# 13.7k vs 14.2k img/s); DDP_AMD_BN_BWD_FUSED=1 runs the BatchNorm backward as one launch
-# (resnet_ops.hip FUSED; pass 2 after an in-launch strip wait: 13.7k vs 14.2k img/s).
-BN_TAIL = os.environ.get("DDP_AMD_BN_TAIL", "0") == "1"
+# (Round 3 measured two BatchNorm launch-count reductions - the statistics finalised inside
+# the stats-producing conv launch, and a one-launch BatchNorm backward - both slower on
+# MI355X: 13.7k vs 14.2k img/s, profiles/r3_bn_fusion; removed in round 5.)
 # BatchNorm backward of a ReLU without a residual add: the mask recomputed from the BN input
 # (no read of the saved output in either pass); DDP_AMD_BN_MASK_FROM_Y=0 reads the output
 MASK_FROM_Y = os.environ.get("DDP_AMD_BN_MASK_FROM_Y", "1") != "0"
@@ -57,17 +53,8 @@ DEFER_BN = os.environ.get("DDP_AMD_DEFER_BN", "1") != "0" and MASK_FROM_Y
 # kernels share the CUs with the critical chain's own; profiles/r4_resnet/halo_pipe.)
 
 
-_configured = False
-
-
 def _C():
-    global _configured
-    C = native.require()
-    if not _configured:
-        # one-launch BatchNorm backward (resnet_ops.hip FUSED): opt-in, see BN_TAIL above
-        C.bn_bwd_set_fused(1 if os.environ.get("DDP_AMD_BN_BWD_FUSED", "0") == "1" else 0)
-        _configured = True
-    return C
+    return native.require()
 
 
 def to_nhwc4(x: torch.Tensor) -> torch.Tensor:
@@ -145,8 +132,7 @@ class _ConvBNAct(torch.autograd.Function):
         xbn = getattr(x, "_ddp_amd_bn", None)
         if xbn is not None:
             ppc = C.conv_gemm_wgrad_ppc(x, y, KH, KW, stride, pad)
-            if not (halo == 1 and not (training and BN_TAIL)
-                    and C.conv_gemm_wgrad_uses_halo(x, y, KH, KW, stride, pad, ppc)):
+            if not (halo == 1 and C.conv_gemm_wgrad_uses_halo(x, y, KH, KW, stride, pad, ppc)):
                 xm = torch.empty_like(x)
                 C.bn_apply(x, xbn[0], xbn[1], xbn[2], xbn[3], None, True, xm)
                 x, xbn = xm, None
@@ -155,20 +141,14 @@ class _ConvBNAct(torch.autograd.Function):
         if training:
             mean = torch.empty(Cout, device=x.device)
             invstd = torch.empty(Cout, device=x.device)
-        if training and BN_TAIL:
-            # the stats-producing launch finalises the BatchNorm itself (no bn_finalize)
-            ws = torch.empty(C.bn_tail_groups(rows), 2, Cout, device=x.device)
-            C.conv_bn_fwd(x, wk, y, KH, KW, stride, pad, stats, part, ws, float(P), eps, momentum,
-                          running_mean, running_var, mean, invstd, nbt)
+        C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part, bn=xbn)
+        if training:
+            ws = torch.empty(C.bn_finalize_groups(rows), 2, Cout, device=x.device)
+            C.bn_finalize(stats, rows, Cout, float(P), eps, momentum, running_mean, running_var,
+                          mean, invstd, nbt, ws)
         else:
-            C.conv_gemm_fwd(x, wk, None, y, KH, KW, stride, pad, False, stats, part, bn=xbn)
-            if training:
-                ws = torch.empty(C.bn_finalize_groups(rows), 2, Cout, device=x.device)
-                C.bn_finalize(stats, rows, Cout, float(P), eps, momentum, running_mean, running_var,
-                              mean, invstd, nbt, ws)
-            else:
-                mean = running_mean.float().contiguous()
-                invstd = torch.rsqrt(running_var.float() + eps).contiguous()
+            mean = running_mean.float().contiguous()
+            invstd = torch.rsqrt(running_var.float() + eps).contiguous()
         if defer:
             # the consumer applies BN + ReLU while loading (BnAffine); the returned tensor
             # holds the RAW conv output, tagged with the affine, and stands for relu(bn(y))

@@ -32,7 +32,7 @@ PEAK_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X
 PEAK_TBPS = 8.0       # HBM3E
 
 # native calls wrapped: name -> pass label
-WRAP = {"conv_gemm_fwd": "fwd", "conv_bn_fwd": "fwd", "conv_gemm_dgrad": "dgrad", "conv_gemm_wgrad": "wgrad",
+WRAP = {"conv_gemm_fwd": "fwd", "conv_gemm_dgrad": "dgrad", "conv_gemm_wgrad": "wgrad",
         "grad_reduce": "wgrad-reduce", "bn_finalize": "bn", "bn_apply": "bn", "bn_bwd": "bn-bwd",
         "maxpool_fwd": "pool", "maxpool_bwd": "pool", "avgpool_fwd": "pool", "avgpool_bwd": "pool",
         "sgemm": "head", "sgd": "sgd"}
@@ -74,7 +74,7 @@ def run(a):
     def shape_of(args, name):
         # conv calls: (x, w, ..., KH, KW, stride, pad ...) or dgrad (dy, w, Xact, dx, KH, ...)
         try:
-            if name in ("conv_gemm_fwd", "conv_bn_fwd"):
+            if name == "conv_gemm_fwd":
                 x, w, y, KH, KW, st = args[0], args[1], args[3 if name == "conv_gemm_fwd" else 2], args[4 if name == "conv_gemm_fwd" else 3], args[5 if name == "conv_gemm_fwd" else 4], args[6 if name == "conv_gemm_fwd" else 5]
                 N, H, W_, Cin = x.shape
                 return dict(N=N, H=H, W=W_, Cin=Cin, Cout=y.shape[3], OH=y.shape[1], OW=y.shape[2], KH=KH, KW=KW, s=st)
