@@ -74,7 +74,11 @@ __global__ __launch_bounds__(XGMI_THREADS) void xgmi_allreduce_pair_kernel(BwdXa
   __syncthreads();
   DDP_STAMP(STAMP_K_XGMI, 7);
   if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(x.xar_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed: the count only finds the last block (the step counter it advances is read by
+    // later kernels).  An agent-scope acq_rel here compiled to buffer_wbl2 sc1 + buffer_inv
+    // sc1 - an L2 write-back and invalidate of the XCD for each of the 275 blocks, ~3-5 us
+    // at the end of every multi-GPU step.
+    const int old = __hip_atomic_fetch_add(x.xar_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == nx - 1 && x.step_ctr) x.step_ctr[0] += 1;
   }
 }

@@ -1249,7 +1249,10 @@ __device__ __forceinline__ void fc_role_chunk(const BwdFc& fcr, const float* s_d
 
 // Spin until *cnt >= want (wave 0 polls with sleeps between polls, so the waiting block
 // takes few issue slots from the conv waves sharing its CU); false on a timeout, after
-// setting *err = code.  Then every thread of the block acquires at agent scope.
+// setting *err = code.  No acquire fence: everything the in-launch all-reduce reads after
+// the wait was stored write-through by its producers and is read with system-scope loads
+// (an agent-scope acquire is `buffer_inv sc1`, invalidating the XCD's L2 under the conv
+// roles sharing it).
 __device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, int code) {
   __shared__ int s_ok;
   if (threadIdx.x < 64) {
@@ -1266,19 +1269,17 @@ __device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, i
     if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return s_ok != 0;
 }
 
-// this block's global stores are out (each wave drained), then one count: the release that
-// wait_count's acquire pairs with
+// this block's global stores are out (each wave drained - they are write-through: the
+// producers of a multi-GPU step store their gradients system-scope), then one relaxed
+// count.  (An agent-scope release here is `buffer_wbl2 sc1`: a write-back of the XCD's
+// whole L2 per block.)
 __device__ __forceinline__ void count_done(int* cnt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T, int PXT, bool DA1X, bool WA1X, int GH, int GW, int GCI, int GCO, bool FRED, int CS = 1,
@@ -1330,7 +1331,9 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
       if (threadIdx.x == 0) {
         // the step's last work item advances the batch window (the fc role read it before
         // counting itself into fc_done, which every role block waited for)
-        const int old = __hip_atomic_fetch_add(xar.xar_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        // (relaxed: nothing is published through it - an agent-scope acq_rel is an L2
+        // write-back + invalidate of the XCD per block)
+        const int old = __hip_atomic_fetch_add(xar.xar_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == nx - 1 && xar.step_ctr) xar.step_ctr[0] += 1;
       }
       return;
