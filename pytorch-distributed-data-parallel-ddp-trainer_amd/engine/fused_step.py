@@ -119,8 +119,9 @@ class EngineOptions:
     dist_mode: int = 3
     # dist_mode 2: the most blocks of a bucket's xGMI channel (its role blocks wait at the
     # head of the conv backward grid; the engine takes the in-launch path while the channels'
-    # blocks total <= 192)
-    xar_blocks: int = 40
+    # blocks total <= 192).  Forced world 1: 40 -> 479k, 96 -> 535k, 128 -> 525k, 173 -> 499k
+    # img/s (profiles/r5_dist); dist_mode 3 698k
+    xar_blocks: int = 96
     # bucket plan as for this many ranks (None: the real world size) - forced all-reduces
     # at world size 1 (--force_allreduce) then run the multi-GPU plan's buckets
     plan_world: int | None = None
