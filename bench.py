@@ -52,6 +52,16 @@ METRIC = "images/sec MNIST SimpleCNN DDP at 1/2/4/8 MI355X; DDP scaling efficien
 BASELINE_IMG_S = {1: 2799.0, 2: 2665.0, 4: 3384.0, 8: 3670.0}
 
 
+def kernels_per_step(eng):
+    """Kernels per step of the chain a FusedSimpleCNNEngine ran (level 3 only): 2 on one GPU
+    and with the in-launch all-reduce, 3 with both buckets' all-reduces in one launch
+    (dist_mode 3); otherwise fc_bwd and one all-reduce kernel per bucket come on top."""
+    if not eng.eng.last_level3:
+        return None
+    nar = 0 if eng.eng.last_xar or eng.comm_kind == "none" else 1 if eng.eng.last_pair else len(eng.ranges)
+    return (2 if eng.eng.last_fc_role else 3) + nar
+
+
 def graph_chunk(k: int, cap: int = 100) -> int:
     for d in range(min(cap, k), 0, -1):
         if k % d == 0:
@@ -468,11 +478,7 @@ def main():
     plan = describe(eng.buckets, fs, eng.cost, ranges=eng.ranges) if (ws > 1 or force) else None
     finite = bool(torch.isfinite(fs.params).all().item())
     level3 = bool(eng.eng.last_level3)
-    # kernels per step of the chain that ran: 2 on one GPU and with the in-launch all-reduce,
-    # 3 with both buckets' all-reduces in one launch (dist_mode 3); otherwise fc_bwd and one
-    # all-reduce kernel per bucket come on top
-    nar = 0 if eng.eng.last_xar or eng.comm_kind == "none" else 1 if eng.eng.last_pair else len(eng.ranges)
-    kps = ((2 if eng.eng.last_fc_role else 3) + nar) if level3 else None
+    kps = kernels_per_step(eng)
     same = True
     if ws > 1:  # DDP invariant: every rank holds bit-identical parameters after the run
         pd = dev if args.backend == "nccl" else "cpu"
@@ -490,7 +496,7 @@ def main():
         fp32 = {"images_per_sec": round(ws * args.batch_size * args.steps / dt32, 1),
                 "ms_per_step": round(dt32 * 1000.0 / args.steps, 5),
                 "level3": bool(eng32.eng.last_level3),
-                "kernels_per_step": (2 if eng32.eng.last_fc_role else 3) if eng32.eng.last_level3 else None}
+                "kernels_per_step": kernels_per_step(eng32)}
         del eng32
     if rank == 0:
         base = BASELINE_IMG_S.get(ws)

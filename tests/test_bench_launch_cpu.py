@@ -115,3 +115,23 @@ def test_child_timeout_kills_the_whole_group(tmp_path):
         time.sleep(0.1)
     else:
         raise AssertionError("the grandchild survived the timeout")
+
+
+def test_kernels_per_step_record():
+    """config.kernels_per_step / fp32_kernels_per_step of the chain that ran: 2 on one GPU,
+    2 with the in-launch all-reduce, 3 with both buckets in one launch (dist_mode 3), fc_bwd +
+    one kernel per bucket otherwise; None off level 3."""
+    import types
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    def eng(l3=True, fc_role=True, xar=False, pair=False, comm="xgmi1", nb=2):
+        e = types.SimpleNamespace(last_level3=l3, last_fc_role=fc_role, last_xar=xar, last_pair=pair)
+        return types.SimpleNamespace(eng=e, comm_kind=comm, ranges=[(0, 1)] * nb)
+
+    assert bench.kernels_per_step(eng(comm="none")) == 2
+    assert bench.kernels_per_step(eng(xar=True)) == 2
+    assert bench.kernels_per_step(eng(pair=True)) == 3
+    assert bench.kernels_per_step(eng(fc_role=False, nb=2)) == 5
+    assert bench.kernels_per_step(eng(l3=False)) is None
