@@ -128,3 +128,26 @@ def test_replica_digest_detects_divergence():
     with torch.no_grad():
         fs.params[123] = torch.nextafter(fs.params[123], torch.tensor(1e9))  # one ulp
     assert replica_digest(fs, opt) != d0
+
+
+def test_no_agent_scope_fences_in_kernels():
+    """Round 5: on gfx950 an agent-scope release compiles to `buffer_wbl2 sc1` (a write-back
+    of the XCD's whole L2) and an acquire to `buffer_inv sc1` - one per block of an in-launch
+    completion count cost the multi-GPU step ~4 us (profiles/r5_dist).  Hand-offs in the
+    kernels are relaxed counts after write-through stores + a drain, read with system- or
+    agent-scope loads; no kernel source may carry an ordering atomic or a fence."""
+    import os
+    import re
+
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "kernels")
+    pat = re.compile(r"__ATOMIC_(ACQ_REL|RELEASE|ACQUIRE|SEQ_CST)|__threadfence|amdgcn_fence")
+    bad = []
+    for name in sorted(os.listdir(root)):
+        if not name.endswith((".hip", ".h")):
+            continue
+        with open(os.path.join(root, name)) as f:
+            for n, line in enumerate(f, 1):
+                code = line.split("//", 1)[0]
+                if pat.search(code):
+                    bad.append(f"{name}:{n}: {line.strip()}")
+    assert not bad, "\n".join(bad)
