@@ -294,7 +294,7 @@ def main():
                          "all-reduces on the --comm plane at world size 1) - times the dist chain on one GPU")
     ap.add_argument("--plan_world", type=int, default=None,
                     help="bucket plan as for this many ranks (default: the world size; --force_allreduce: 8)")
-    ap.add_argument("--dist_mode", type=int, default=None, choices=[0, 1, 2, 3],
+    ap.add_argument("--dist_mode", type=int, default=None, choices=[0, 1, 2, 3, 4],
                     help="N>1, level 3: 3 = both bucket all-reduces in one launch behind the conv backward "
                          "(xGMI, default); 2 = inside the conv backward launch; 1 = fc weight gradient + fc "
                          "bucket all-reduce on a graph branch forked after the forward; 0 = the round-4 serial order")
@@ -303,6 +303,9 @@ def main():
     ap.add_argument("--no_breakdown", action="store_true",
                     help="N>1 / --force_allreduce: skip the comm-free local run that splits the step into "
                          "local compute and exposed communication (config.step_breakdown)")
+    ap.add_argument("--no_placement", action="store_true",
+                    help="N>1 / --force_allreduce: do not time the placements (dist_mode 3 / 0 / 1) "
+                         "before the run; use --dist_mode or the engine default")
     ap.add_argument("--no_chain_check", action="store_true",
                     help="N>1: skip the start-up check that the production kernel chain gives the "
                          "conservative chain's bits across the ranks")
@@ -391,12 +394,59 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize()
 
-    def timed_run(dtype, local=False):
-        """Build the engine for ``dtype`` (fresh seeded model, rank-0 init broadcast), warm up,
-        time exactly ``args.steps`` steps between barrier + synchronize brackets; returns
-        (seconds = MAX over ranks, engine, flat space, model, graph chunk).  ``local``: the
-        same config as a comm-free one-rank engine on every rank at once (the step-breakdown
-        reference: what the step costs without any collective)."""
+    placement = {"source": "not applicable (one rank, no forced all-reduce)"}
+
+    def max_over_ranks(dt):
+        if ws > 1:
+            t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    def pick_placement(dtype):
+        """time every bitwise-equivalent placement (dist_mode) of the multi-GPU
+        chain on THIS node - a throwaway engine each, a few graph replays, untimed for the
+        metric - and agree on the fastest through the store (the slowest rank's time counts).
+        An explicit --dist_mode skips it."""
+        from ddp_amd.engine.fused_step import PLACEMENT_NAMES, agree_placement, placement_candidates
+
+        if args.dist_mode is not None:
+            return {"source": "fixed (--dist_mode)", "chosen": args.dist_mode}
+        # (an xGMI plane whose self-test fails runs RCCL: mode 3 then times as mode 0)
+        cands = placement_candidates("rccl" if args.comm == "rccl" else "xgmi", dtype)
+        if len(cands) < 2:
+            return {"source": "single candidate", "chosen": cands[0] if cands else None}
+        mine = {}
+        for mode in cands:
+            eng, *_ = build(dtype, False, mode)
+            try:
+                eng.refresh()
+                if not args.no_graph:
+                    eng.run_steps(0)
+                    eng._ensure_graph()
+                n = max(20, 2 * (args.graph_steps or graph_chunk(max(1, args.steps))))
+                eng.run_steps(min(n, 20))
+                eng.synchronize()
+                barrier()
+                t0 = time.perf_counter()
+                eng.run_steps(n)
+                barrier()
+                dt = time.perf_counter() - t0
+                eng.synchronize()
+                mine[mode] = round(dt * 1e6 / n, 3)
+            except RuntimeError as e:  # a placement that fails here simply does not compete
+                print(f"[bench] rank {rank}: placement dist_mode {mode} failed ({e})", file=sys.stderr)
+                mine[mode] = None
+            del eng
+        store = dist.distributed_c10d._get_default_store() if dist.is_initialized() else None
+        best, worst = agree_placement(store, f"ddp_amd/bench/placement/{dtype}", rank, ws, mine)
+        return {"source": "timed on this node (untimed for the metric)", "chosen": best,
+                "chosen_name": PLACEMENT_NAMES.get(best), "placement_us": {str(k): v for k, v in worst.items()},
+                "this_rank_us": {str(k): v for k, v in mine.items()}}
+
+    def build(dtype, local, mode=None):
+        """A fresh seeded model (rank-0 init broadcast) and its engine for ``dtype``;
+        ``mode``: the dist_mode to build with (None: args / placement / engine default)."""
         torch.manual_seed(0)
         model = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
         fs = flat_space(model)
@@ -429,10 +479,27 @@ def main():
         if not local:
             eo.plan_world = args.plan_world or (8 if force else None)
             eo.cost_fit = calib
+            if mode is not None:
+                eo.dist_mode = mode
+            elif placement.get("chosen") is not None:
+                eo.dist_mode = placement["chosen"]
         if local:
             eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, 1, 0, None, eo)
         else:
             eng = FusedSimpleCNNEngine(model, opt, data, args.batch_size, ws, rank, comm, eo)
+        return eng, fs, model, k, eo
+
+    def timed_run(dtype, local=False):
+        """Build the engine for ``dtype`` (fresh seeded model, rank-0 init broadcast), warm up,
+        time exactly ``args.steps`` steps between barrier + synchronize brackets; returns
+        (seconds = MAX over ranks, engine, flat space, model, graph chunk).  ``local``: the
+        same config as a comm-free one-rank engine on every rank at once (the step-breakdown
+        reference: what the step costs without any collective).  At N > 1 (or forced) the
+        placement is timed first (pick_placement)."""
+        nonlocal placement
+        if (ws > 1 or force) and not local and not args.no_placement:
+            placement = pick_placement(dtype)
+        eng, fs, model, k, eo = build(dtype, local)
         eng.refresh()
         if (ws > 1 or force) and not local and not args.no_chain_check:
             eng.verify_chain()  # untimed: production vs conservative chain, bitwise, all ranks
@@ -444,17 +511,14 @@ def main():
         eng.synchronize()
         barrier()
         t0 = time.perf_counter()
-        eng.run_steps(args.steps, head=head)
+        eng.run_steps(args.steps, head=args.graph_head_used)
         barrier()  # torch.cuda.synchronize() waits for the engine's streams too
         dt = time.perf_counter() - t0
         eng.synchronize()  # (idle by now) raises if an in-launch / cross-GPU wait timed out
-        if ws > 1:
-            t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return dt, eng, fs, model, k, eo
+        return max_over_ranks(dt), eng, fs, model, k, eo
 
     dt, eng, fs, model, k, eo = timed_run(args.dtype)
+    placement_main = dict(placement, dist_mode_run=eo.dist_mode)
     ms = dt * 1000.0 / args.steps
     img_s = ws * args.batch_size * args.steps / dt
     bucket_us = eng.measure_bucket_allreduce() if (ws > 1 or force) else None  # after the timed region
@@ -537,6 +601,7 @@ def main():
                        "force_allreduce": force, "step_breakdown": breakdown,
                        "inlaunch_allreduce": bool(eng.eng.last_xar),
                        "pair_allreduce": bool(eng.eng.last_pair),
+                       "placement": placement_main,
                        "comm_calibration": calib,
                        "fp32_images_per_sec": fp32["images_per_sec"] if fp32 else None,
                        "fp32_level3": fp32["level3"] if fp32 else None,

@@ -29,6 +29,7 @@
 //  * wgrad: split-K over image-row chunks, one fp32 slab row per block, bias
 //           gradient from an extra MFMA against a ones fragment; fixed-order
 //           reduction in grad_reduce (bitwise reproducible, no float atomics).
+#include <algorithm>
 #include <stdexcept>
 
 #include <cstdio>
@@ -140,15 +141,49 @@ constexpr bool F32_FC_PREFETCH = DDP_AMD_F32_FC_PREFETCH;
 #define DDP_AMD_FWD_PF_SPLIT 1
 #endif  // see conv3x3_fwd_kernel (DZ, fp32)
 
+// MRG (dist_mode 4, step_head_kernel): the forward runs in the SAME launch as the previous
+// step's bucket all-reduces, whose fused SGD writes this step's parameters.  Its blocks stage
+// the step's images first, wait for the conv bucket's all-reduce blocks (FwdMerge conv_done)
+// before they read conv1's weights, conv2's bf16 weight shadow and bias, and for the fc
+// bucket's (fc_done) before the fc epilogue reads the fc weight shadow and bias; every one of
+// those reads is an sc1 (agent-coherent) load, the writers store write-through (xgmi_body.h
+// WT) and drain before they count - the hand-off pattern of the fused slab reduction.  No fc
+// weight prefetch (the weights are not final before the wait).
+struct FwdMerge {
+  const int* conv_done = nullptr;
+  const int* fc_done = nullptr;
+  int conv_want = 0, fc_want = 0;
+  int* err = nullptr;
+};
+constexpr int MRG_ERR = 5;  // sync_err code of a timed-out merged-forward wait
+
+__device__ __forceinline__ bf16x8 ld16_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /* sc1 */));
+}
+__device__ __forceinline__ Conv1Group conv1_group_load_sc1(const float* w1, const float* b1, int g) {
+  Conv1Group r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+      r.w[j][k] = __hip_atomic_load(w1 + (8 * g + j) * 9 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.b[j] = __hip_atomic_load(b1 + 8 * g + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return r;
+}
+__device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, int code);
+
 template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
-          bool DZ = false, int OCC = 1>
-__global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  // 2nd: waves per SIMD
-    const T* __restrict__ X, const T* __restrict__ Wt, const float* __restrict__ bias,
+          bool DZ = false, int OCC = 1, bool MRG = false>
+__device__ __forceinline__ void fwd_body(
+    const int bx, const int by, const T* __restrict__ X, const T* __restrict__ Wt, const float* __restrict__ bias,
     T* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
-    const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1, FwdDz dzo) {
+    const T* __restrict__ wfc, float* __restrict__ fc_part, const C1Src& c1, const FwdDz& dzo, const FwdMerge& mg) {
   using P = Prec<T>;
   constexpr bool F32 = sizeof(T) == 4;
   static_assert(!DZ || (NOF == 10 && A1X), "level-3 dZ2 needs the fc epilogue and the conv1 recompute");
+  static_assert(!MRG || (DZ && !F32), "the merged forward is the bf16 level-3 forward");
   constexpr int CE = P::CE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DDP_STAMP(STAMP_K_CONV_FWD, 0);
@@ -157,23 +192,24 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long Ptot = (long)B * HW;
-  const int co0 = blockIdx.y * 64;
+  const int co0 = by * 64;
   // row strides = 8 mod 16 dwords: conflict-free b128 fragment reads
   const int KW = 9 * Cin, WS = KW + P::PAD, XS = Cin + P::PAD;
   const int XR = CH + 2 * W + 2;
   T* sW = reinterpret_cast<T*>(smem);
   T* sX = sW + 64 * WS;
-  const long P0 = (long)blockIdx.x * CH;
+  const long P0 = (long)bx * CH;
   const long Pbase = P0 - W - 1;
 
   const int wc = KW / CE;
   const int xc = Cin / CE;
   if (A1X && c1.zero_i32)  // the step's level-2 hand-off flags (see C1Src)
     for (int i = threadIdx.x; i < c1.zero_per_block; i += NT) {
-      const long z = (long)blockIdx.x * c1.zero_per_block + i;
+      const long z = (long)bx * c1.zero_per_block + i;
       if (z < c1.zero_total) c1.zero_i32[z] = 0;
     }
   Conv1Group cg;
+  if constexpr (!MRG) {
   if (A1X) cg = conv1_group_load(c1.w, c1.b, wave & 3);  // lands during the staging round
   // weights and (unless recomputed) the input rows in ONE round of loads
   stage2<(64 / NW) * (F32 ? 2 : 1), NT>(64 * wc,
@@ -186,6 +222,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
                return (Pq >= 0 && Pq < Ptot) ? ld16(X + Pq * Cin + c) : zero8();
              },
              [&](int i, bf16x8 v) { const int r = i / xc, c = (i - r * xc) * CE; st16(sX + r * XS + c, v); });
+  }
   if (A1X) {
     // x for the linear range [Pbase - W - 1, Pbase + XR + W + 1), then a1 (conv1 recompute).
     // The block also writes its own pixels (and the labels of images starting in them)
@@ -207,6 +244,17 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
         }
       }
       sxx[r] = v;
+    }
+    if constexpr (MRG) {
+      // the step's images are staged; now this step's conv parameters must be final
+      wait_count(mg.conv_done, mg.conv_want, mg.err, MRG_ERR);
+      cg = conv1_group_load_sc1(c1.w, c1.b, wave & 3);
+      const __amdgpu_buffer_rsrc_t rw =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Wt), (short)0, 0x7fffffff, 0x00020000);
+      stage2<64 / NW, NT>(64 * wc,
+          [&](int i) { const int r = i / wc, c = (i - r * wc) * CE; return ld16_sc1(rw, (int)(((co0 + r) * KW + c) * sizeof(T))); },
+          [&](int i, bf16x8 v) { const int r = i / wc, c = (i - r * wc) * CE; st16(sW + r * WS + c, v); },
+          0, [&](int) { return zero8(); }, [&](int, bf16x8) {});
     }
     __syncthreads();
     DDP_STAMP(STAMP_K_CONV_FWD, 1);
@@ -248,7 +296,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   // OCC 2 (level 3 at B > 32, two blocks per CU): no prefetch - the 80 VGPRs of bf16 weight
   // pairs would hold the kernel at one block per CU; they are read where used (L2 hits),
   // the other block of the CU hides that latency
-  constexpr bool PFW = NOF > 0 && !F32 && OCC == 1;
+  constexpr bool PFW = NOF > 0 && !F32 && OCC == 1 && !MRG;
   if constexpr (DZ) DDP_STAMP(STAMP_K_FWD_DZ, 6);  // (pixel index math done)
   // buffer loads: one per-lane VGPR offset per pixel tile and a uniform (o, t) SGPR offset
   // (flat loads: two 64-bit adds per load; without the prefetch (!PFW) the compiler kept 40
@@ -258,7 +306,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   auto fcw = [&](int pt, int t, int o) {
     const int vo = (((rem[pt] >> 4) * (Cout >> 4) + (co0 >> 4)) * 64 + lane) * 4 * (int)sizeof(T);
     const int so = ((o * (HW >> 4) * (Cout >> 4) + t) * 64) * 4 * (int)sizeof(T);
-    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwfc, vo, so, 0));
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rwfc, vo, so, MRG ? 16 : 0));
   };
   uint2 wv[PFW ? PXT : 1][4][PFW ? NOF : 1];
   // PF_SPLIT: the prefetch is issued in slices between the MFMA loop's taps instead of all
@@ -331,7 +379,9 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   // the start of the epilogue cost ~1-2 us per block)
   float4 bq[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) bq[t] = *reinterpret_cast<const float4*>(bias + co0 + 16 * t + 4 * (lane >> 4));
+  for (int t = 0; t < 4; ++t)
+    bq[t] = MRG ? slab_ld4_sc1(bias, co0 + 16 * t + 4 * (lane >> 4))
+                : *reinterpret_cast<const float4*>(bias + co0 + 16 * t + 4 * (lane >> 4));
 
   const T* wrow = sW + col * WS + kofs;
 #pragma unroll
@@ -363,6 +413,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
   }
 
   DDP_STAMP(STAMP_K_CONV_FWD, 3);
+  if constexpr (MRG) wait_count(mg.fc_done, mg.fc_want, mg.err, MRG_ERR);  // the fc weight shadow is final
   // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
   float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X, (int)sizeof(T)));
@@ -459,7 +510,7 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
           acc_o += in ? v : 0.f;
         }
       }
-      float* dst = fc_part + ((long)blockIdx.x * 2 + slot) * NOF + o;
+      float* dst = fc_part + ((long)bx * 2 + slot) * NOF + o;
       if constexpr (DZ) st_wt(dst, acc_o);  // read by the other blocks of the image in-launch
       else *dst = acc_o;
     }
@@ -530,7 +581,8 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
           const float a = xent_logit_acc(img0 + slot, o, HWi, CH, NOF, [&](int i) {
             return __hip_atomic_load(fc_part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           });
-          s_lg[lane] = dzo.fc_bias[o] + a;
+          s_lg[lane] = (MRG ? __hip_atomic_load(dzo.fc_bias + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : dzo.fc_bias[o]) + a;
         }
       }
       DDP_STAMP(STAMP_K_FWD_DZ, 4);
@@ -597,6 +649,16 @@ __global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  //
     DDP_STAMP(STAMP_K_CONV_FWD, 7);
     DDP_STAMP(STAMP_K_FWD_DZ, 5);
   }
+}
+
+template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
+          bool DZ = false, int OCC = 1>
+__global__ __launch_bounds__(NW * 64, OCC * NW / 4) void conv3x3_fwd_kernel(  // 2nd: waves per SIMD
+    const T* __restrict__ X, const T* __restrict__ Wt, const float* __restrict__ bias,
+    T* __restrict__ Y, int B, int H, int W, int Cin, int Cout,
+    const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1, FwdDz dzo) {
+  fwd_body<T, PXT, NW, RELU, NOF, A1X, GH, GW, GCI, GCO, DZ, OCC, false>(
+      (int)blockIdx.x, (int)blockIdx.y, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, c1, dzo, FwdMerge());
 }
 
 // ---------------------------------------------------------------- data gradient
@@ -1297,10 +1359,12 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 || CS == 2) ? 2 : 1) void conv
     // multi-GPU level-3 step (BwdXar): the bucket all-reduces run here, each as soon as its
     // gradients are final - the fc bucket while the conv roles still run (SURVEY.md §2.6 I6:
     // DDP's bucket 0 overlapping the rest of the backward), the conv bucket right behind the
-    // last fused reducer.  These blocks come first in the grid, so they are dispatched
-    // before every block they wait for (in-order dispatch: no deadlock whatever the grid's
-    // residency); each waits only for this launch's producers and for the same role block of
-    // its peers (which is at the head of their grids too).
+    // last fused reducer.  Each role block waits only for this launch's producers and for the
+    // same role block of its peers.  Deadlock freedom: the launcher takes this variant only
+    // when the WHOLE grid (role + fc + conv + reducer blocks) fits the GPU's resident slots of
+    // this instantiation (bwd_launch, hipOccupancy), so no block waits for an undispatched
+    // one; a larger grid relies on in-order workgroup dispatch (these blocks come first) and
+    // is opt-in, DDP_AMD_L3_INORDER=1, as for the level-3 forward.
     const int nx = xar.nblk0 + xar.nblk1;
     if (cb < nx) {
       unsigned* s_sh = reinterpret_cast<unsigned*>(smem);
@@ -1499,6 +1563,14 @@ static bool fwd_dz_occ2(unsigned grid) {
   return cus > 0 && grid > (unsigned)cus;
 }
 
+// DDP_AMD_L3_INORDER=1: launches whose spinning blocks would not all be resident at once may
+// rely on in-order workgroup dispatch (the hardware does not promise it) - the level-3
+// forward beyond one wave of blocks, and the in-launch all-reduce (dist_mode 2)
+static bool inorder_optin() {
+  const char* e = getenv("DDP_AMD_L3_INORDER");  // (read per call: launch-plan time only)
+  return e && e[0] == '1';
+}
+
 template <typename T>
 static bool fwd_dz_fits(int B, int H, int W, int pxt) {
   if (H != 28 || W != 28 || (pxt != 1 && pxt != 2) || B <= 0) return false;
@@ -1536,11 +1608,92 @@ static bool fwd_dz_fits(int B, int H, int W, int pxt) {
   // order and a concurrent stream's kernels can hold the slots; the failure mode is the
   // bounded wait (FWD_DZ_WAIT_TICKS) setting the step's error word - the engine's
   // synchronize() raises and the start-up chain check downgrades to level 1.
-  static const bool inorder = [] { const char* e = getenv("DDP_AMD_L3_INORDER"); return e && e[0] == '1'; }();
-  return inorder && (long)occ * cus >= 64;
+  return inorder_optin() && (long)occ * cus >= 64;
 }
 bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt, int es) {
   return es == 4 ? fwd_dz_fits<float>(B, H, W, pxt) : fwd_dz_fits<bf16_t>(B, H, W, pxt);
+}
+
+// ---------------------------------------------------------------- dist_mode 4 step head
+// Step k's two bucket all-reduces (+ fused SGD, stored write-through) and step k + 1's bf16
+// level-3 forward (256-thread blocks, pxt 1) in ONE launch: blocks [0, nblk0) all-reduce the
+// fc bucket, [nblk0, nblk0 + nblk1) the conv bucket (exactly xgmi_allreduce_pair's roles), the
+// rest are forward blocks (fwd_body<MRG>), which stage their images while the all-reduce runs
+// and wait for each bucket's blocks only where they first read its parameters.  The forward
+// needs the conv bucket at its staging and the fc bucket only at its fc epilogue, so the
+// fc bucket's 2 MB all-gather overlaps the staging, the conv1 recompute and the MFMA loop
+// (profiles/r5_dist: the step's last kernel and the next step's first used to run back to
+// back with a launch boundary between).  Deadlock freedom: the launcher requires the WHOLE
+// grid to be resident at once (hipOccupancy of this kernel x CUs >= grid), so no block waits
+// for an undispatched one; the all-reduce blocks wait only for their peers' same blocks.
+template <typename T>
+__global__ __launch_bounds__(256, 3) void step_head_kernel(
+    BwdXar x, int* done_fc, int* done_conv, const T* __restrict__ Wt, const float* __restrict__ bias,
+    T* __restrict__ Y, int B, const T* __restrict__ wfc, float* __restrict__ fc_part, C1Src c1, FwdDz dzo,
+    int* err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = x.nblk0 + x.nblk1;
+  if ((int)blockIdx.x < nx) {
+    const int k = (int)blockIdx.x < x.nblk0 ? 0 : 1;
+    unsigned* s_sh = reinterpret_cast<unsigned*>(smem);
+    XgmiArgs* s_xa = reinterpret_cast<XgmiArgs*>(smem + 64);
+    {  // the bucket's arguments into LDS (from global memory every field was re-loaded per store)
+      const int* src = reinterpret_cast<const int*>(x.args + k);
+      int* dst = reinterpret_cast<int*>(s_xa);
+      for (int i = threadIdx.x; i < (int)(sizeof(XgmiArgs) / 4); i += 256) dst[i] = src[i];
+    }
+    __syncthreads();
+    DDP_STAMP(STAMP_K_XGMI, 0);
+    if (k == 0) xgmi_allreduce_body<true>(*s_xa, (int)blockIdx.x, x.nblk0, s_sh);
+    else xgmi_allreduce_body<true>(*s_xa, (int)blockIdx.x - x.nblk0, x.nblk1, s_sh);
+    DDP_STAMP(STAMP_K_XGMI, 7);
+    count_done(k == 0 ? done_fc : done_conv);  // drain (write-through) + one relaxed count
+    return;
+  }
+  FwdMerge mg;
+  mg.conv_done = done_conv;
+  mg.fc_done = done_fc;
+  mg.conv_want = x.nblk1;
+  mg.fc_want = x.nblk0;
+  mg.err = err;
+  fwd_body<T, 1, 4, true, 10, true, 28, 28, 32, 64, true, 2, true>(
+      (int)blockIdx.x - nx, 0, static_cast<const T*>(nullptr), Wt, bias, Y, B, 28, 28, 32, 64, wfc, fc_part, c1,
+      dzo, mg);
+}
+
+static int step_head_occupancy(size_t lds) {
+  auto k = step_head_kernel<bf16_t>;
+  lds_optin(k, lds);
+  int dev = 0, cus = 0, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256, lds) != hipSuccess) return 0;
+  return occ * cus;
+}
+
+bool conv3x3_step_head_fits(int nx, int B) {
+  if (B <= 0 || nx <= 0) return false;
+  const long nf = ((long)B * 28 * 28 + 63) / 64;
+  const size_t lds = std::max(conv3x3_fwd_lds(28, 32, 1, true, 2), (size_t)64 + sizeof(XgmiArgs));
+  return (long)step_head_occupancy(lds) >= nx + nf;
+}
+
+bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16_t* Wt, const float* bias,
+                       bf16_t* Y, int B, const bf16_t* wfc, float* fc_part, const C1Src& c1, const FwdDz& dz,
+                       int* err, hipStream_t s) {
+  const int nx = x.nblk0 + x.nblk1;
+  if (!x.args || x.nblk0 <= 0 || x.nblk1 <= 0 || !done_fc || !done_conv || !dz.dz2 || !dz.img_cnt || !dz.fc_bias ||
+      !wfc || !c1.x)
+    throw std::runtime_error("conv3x3_step_head: needs both buckets' all-reduce arguments, their counters and the "
+                             "level-3 forward's buffers");
+  if (!conv3x3_step_head_fits(nx, B)) return false;
+  const long nf = ((long)B * 28 * 28 + 63) / 64;
+  const size_t lds = std::max(conv3x3_fwd_lds(28, 32, 1, true, 2), (size_t)64 + sizeof(XgmiArgs));
+  auto k = step_head_kernel<bf16_t>;
+  lds_optin(k, lds);
+  hipLaunchKernelGGL(k, dim3((unsigned)(nx + nf)), dim3(256), lds, s, x, done_fc, done_conv, Wt, bias, Y, B, wfc,
+                     fc_part, c1, dz, err);
+  return true;
 }
 
 template <typename T>
@@ -1918,8 +2071,22 @@ static bool bwd_launch(const T* dY, const T* WT, T* dX, float* w1slab, float* sl
   // this launch (its waits count their blocks); otherwise the caller runs the bucket kernels
   BwdXar xv;
   int nx = 0;
-  const bool use_xar = xar && fc && fused && pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, true) !=
-                                                pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, false);
+  bool use_xar = xar && fc && fused && pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, true) !=
+                                          pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, false);
+  if (use_xar) {
+    // residency of the exact instantiation that would run: the role blocks spin
+    // at the head of the grid, so either everything fits at once or in-order dispatch is
+    // opted into; otherwise the caller runs the bucket kernels
+    const BwdKFn<T> kx = pick_bwd<T>(pxt, da, wa, g, true, cs, true, dcs, true);
+    lds_optin(kx, lds);
+    int dev = 0, cus = 0, occ = 0;
+    const long total = (long)xar->nblk0 + xar->nblk1 + nd + nw + nfc;
+    const bool fits = hipGetDevice(&dev) == hipSuccess &&
+                      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kx, 256, lds) == hipSuccess &&
+                      (long)occ * cus >= total;
+    if (!fits && !inorder_optin()) use_xar = false;
+  }
   if (xar && !use_xar && std::getenv("DDP_AMD_XAR_DEBUG"))
     fprintf(stderr, "[ddp_amd] in-launch all-reduce not used: fc %d fused %d first_reducer %d nconv %d\n",
             fc != nullptr, fused != nullptr, red.first_reducer, nd + nw);

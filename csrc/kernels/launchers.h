@@ -411,5 +411,15 @@ constexpr int XAR_ERR = 4;
 // concurrently; the waits / expected counts of BwdXar are unused, the last block advances
 // step_ctr (xar_done).
 void xgmi_allreduce_pair(const BwdXar& x, hipStream_t s);
+// dist_mode 4: the pair's roles (fused SGD stored write-through, each block counted into
+// done_fc / done_conv - zeroed beforehand) and the NEXT step's bf16 level-3 forward
+// (pxt 1, B images; its blocks wait for the buckets' counts before reading their
+// parameters) in ONE launch (conv3x3.hip step_head_kernel).  Returns false without
+// launching when the whole grid does not fit the GPU at once (the caller then runs the pair
+// and the forward as two launches - the same bits).  err: sync_err (code 5 on a wait timeout).
+bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16_t* Wt, const float* bias,
+                       bf16_t* Y, int B, const bf16_t* wfc, float* fc_part, const C1Src& c1, const FwdDz& dz,
+                       int* err, hipStream_t s);
+bool conv3x3_step_head_fits(int nx, int B);
 
 }  // namespace ddp_amd

@@ -1,6 +1,32 @@
 // Device side of the direct xGMI all-reduce (see allreduce.hip for the algorithm): the
 // body runs as the standalone bucket kernel (xgmi_allreduce_kernel) or as an in-launch role
 // of the SimpleCNN conv backward (conv3x3.hip XAR), parameterised by its block index / count.
+//
+// Store policy of every buffer a PEER reads.  The barrier below has no
+// release / acquire fence, so each peer-read byte must be stored write-through at system
+// scope (sc0 sc1: the line goes to HBM, not only to the writer XCD's L2), drained by its
+// wave (s_waitcnt vmcnt(0)) before the block's flag store, and read with system-scope loads
+// (sc0 sc1: no L1 / L2 hit on a stale line).
+//
+//   buffer            written by (cache policy)                                   read by peers
+//   ----------------  -----------------------------------------------------------  ---------------
+//   data[r] bucket    engine producers with sys_store = 1: the fc role / fc_bwd dW    RS ld4_sys,
+//     (gradients)     (st_sys), the fused slab reducer / grad_reduce dst (st_sys),    one-shot: not
+//                     the fc bias (st_sys); module path: plain autograd stores, then   read (the
+//                     the publish pass re-stores them st4_sys (a.publish)              stage is)
+//   stage[r]          RS output / one-shot publish: st4_sys                         AG / one-shot
+//                                                                                   sum: ld4_sys
+//   sig[r]            flags: relaxed system-scope atomic stores into uncached        relaxed system
+//                     memory (hipDeviceMallocUncached)                              atomic loads
+//
+// The AG's reduced values land in data[rank] with PLAIN stores: peers read that range again
+// only in the next call's RS, after the next step's producers rewrote it write-through, and
+// at least one kernel boundary (which writes back this XCD's dirty L2 lines) lies between.
+// The one-shot publish reads the local bucket with system-scope loads (its producers may run
+// in the same launch on another XCD: dist_mode 2).  tests/test_hygiene_cpu.py checks the ISA
+// of the hot kernels for cache write-back / invalidate instructions; the start-up chain check
+// (engine/fused_step.py verify_chain) compares the reduced gradient with an oracle summed
+// outside this code.
 #pragma once
 
 #include "kernels/common.h"
@@ -101,13 +127,16 @@ __device__ __forceinline__ float4 rank_sum_tail(float* const* src, long q, long 
 
 // the fused optimizer on flat bucket element k with reduced gradient g: same update on
 // every rank, so parameters stay bitwise identical
+// WT (the dist_mode 4 launch): parameters and shadows stored write-through - the next step's
+// forward blocks of the same launch read them with sc1 loads (conv3x3.hip step_head_kernel)
+template <bool WT = false>
 __device__ __forceinline__ void sgd_elem(const XgmiArgs& a, long k, float g) {
   const long j = a.off + k;
   float m = a.mbuf ? a.mbuf[j] : 0.f;
   const float pn = sgd_one(a.params[j], g, &m, a.sgd);
-  a.params[j] = pn;
+  put_f<WT>(a.params + j, pn);
   if (a.mbuf) a.mbuf[j] = m;
-  shadow_one(a.sh, j, pn);
+  shadow_one<WT>(a.sh, j, pn);
 }
 // quad q (elements 4q.., below lim) of the reduced bucket times scale -> my gradient
 // buffer and, with the fused optimizer (a.sgd.update), the parameters / momentum / shadows.
@@ -116,6 +145,7 @@ __device__ __forceinline__ void sgd_elem(const XgmiArgs& a, long k, float g) {
 __device__ __forceinline__ float4 scale4(const XgmiArgs& a, float4 v) {
   return make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
 }
+template <bool WT = false>
 __device__ __forceinline__ void finish_quad(const XgmiArgs& a, long q, float4 v, long lim) {
   if (4 * q + 3 < lim && (a.off & 3) == 0) {
     const long j = a.off + 4 * q;
@@ -123,7 +153,7 @@ __device__ __forceinline__ void finish_quad(const XgmiArgs& a, long q, float4 v,
     if (a.sgd.update) {
       const float4 pm = ld_quad(a.params, j);
       const float4 mm = a.sgd.momentum != 0.f ? ld_quad(a.mbuf, j) : make_float4(0.f, 0.f, 0.f, 0.f);
-      sgd_quad_apply(a.params, a.mbuf, j, v, pm, mm, a.sgd, a.sh);
+      sgd_quad_apply<WT>(a.params, a.mbuf, j, v, pm, mm, a.sgd, a.sh);
     }
     return;
   }
@@ -133,11 +163,12 @@ __device__ __forceinline__ void finish_quad(const XgmiArgs& a, long q, float4 v,
   for (int j = 0; j < 4; ++j) {
     if (4 * q + j >= lim) continue;
     d[j] = e[j];
-    if (a.sgd.update) sgd_elem(a, 4 * q + j, e[j]);
+    if (a.sgd.update) sgd_elem<WT>(a, 4 * q + j, e[j]);
   }
 }
+template <bool WT = false>
 __device__ __forceinline__ void finish4(const XgmiArgs& a, long q, float4 v, long lim) {
-  finish_quad(a, q, scale4(a, v), lim);
+  finish_quad<WT>(a, q, scale4(a, v), lim);
 }
 
 // The all-reduce as block `blk` of `nblk` (the standalone kernel: blockIdx.x of gridDim.x;
@@ -145,6 +176,7 @@ __device__ __forceinline__ void finish4(const XgmiArgs& a, long q, float4 v, lon
 // Every call of a channel must use the same nblk on every rank (the per-block sequence
 // counters, barrier flags and quad mapping are per block index).  s_epoch / s_fail: two
 // words of the block's LDS.  Returns with the block's stores drained.
+template <bool WT = false>
 __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, int nblk, unsigned* s_sh) {
   unsigned& s_epoch = s_sh[0];
   unsigned& s_fail = s_sh[1];
@@ -173,15 +205,19 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
     const long par1 = (long)(e & 1u) * ((nq * 4 + 3) & ~3L);
     const float* mine = a.data[r] + a.off;
     const __amdgpu_buffer_rsrc_t mystage = sys_rsrc(a.stage[r] + par1);
+    // `mine` with system-scope loads: in the in-launch placement (dist_mode 2) the
+    // gradient was written in this same launch by blocks on other XCDs, and this XCD's L2 may
+    // still hold the previous step's lines - a plain load could read them
     for (long q = q0; q < nq; q += G) {
       float4 v;
       const float ps = a.prescale;
       if (q < fq) {
-        v = make_float4(mine[4 * q] * ps, mine[4 * q + 1] * ps, mine[4 * q + 2] * ps, mine[4 * q + 3] * ps);
+        v = make_float4(ld_sys(mine + 4 * q) * ps, ld_sys(mine + 4 * q + 1) * ps, ld_sys(mine + 4 * q + 2) * ps,
+                        ld_sys(mine + 4 * q + 3) * ps);
       } else {
         float t[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = 4 * q + j < n ? mine[4 * q + j] * ps : 0.f;
+        for (int j = 0; j < 4; ++j) t[j] = 4 * q + j < n ? ld_sys(mine + 4 * q + j) * ps : 0.f;
         v = make_float4(t[0], t[1], t[2], t[3]);
       }
       st4_sys(mystage, q, v);  // the stage holds whole quads (zero-padded tail)
@@ -197,10 +233,10 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
       long q = q0;
       for (; q + G < nq; q += 2 * G) {
         const float4 s0 = rank_sum4(src, q, N), s1 = rank_sum4(src, q + G, N);
-        finish4(a, q, s0, n);
-        finish4(a, q + G, s1, n);
+        finish4<WT>(a, q, s0, n);
+        finish4<WT>(a, q + G, s1, n);
       }
-      if (q < nq) finish4(a, q, rank_sum4(src, q, N), n);
+      if (q < nq) finish4<WT>(a, q, rank_sum4(src, q, N), n);
     }
     if (a.step_ctr && blk == 0 && threadIdx.x == 0) a.step_ctr[0] += 1;
     return;
@@ -341,9 +377,9 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
         if (vec && 4 * qq + 3 < a.n) {
           const long j = a.off + 4 * qq;
           *reinterpret_cast<float4*>(a.data[r] + j) = d;
-          if (a.sgd.update) sgd_quad_apply(a.params, a.mbuf, j, d, pq, mq, a.sgd, a.sh);
+          if (a.sgd.update) sgd_quad_apply<WT>(a.params, a.mbuf, j, d, pq, mq, a.sgd, a.sh);
         } else {
-          finish_quad(a, qq, d, a.n);
+          finish_quad<WT>(a, qq, d, a.n);
         }
       }
     }

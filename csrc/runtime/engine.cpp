@@ -108,7 +108,9 @@ void SimpleCNNEngine::synchronize() {
   DDP_HIP_CHECK(hipStreamSynchronize(cs_));
   if (const int e = sync_error()) {
     throw std::runtime_error(std::string("engine: an in-launch hand-off wait timed out (") +
-                             (e == 2 ? "fused slab reduction" : e == XAR_ERR ? "in-launch all-reduce" : "level-3 forward dZ2") +
+                             (e == 2 ? "fused slab reduction" : e == XAR_ERR ? "in-launch all-reduce"
+                                      : e == 5 ? "dist_mode 4 step head: forward waiting for the bucket all-reduce"
+                                               : "level-3 forward dZ2") +
                              "); results invalid");
   }
 }
@@ -123,6 +125,13 @@ bool SimpleCNNEngine::level3_active(int batch) {
     f = conv3x3_fwd_dz_fits(batch, cfg_.H, cfg_.W, cfg_.pxt_fwd, cfg_.f32 ? 4 : 2) && cfg_.C1 == 32 && cfg_.C2 == 64
             ? 1 : 0;
   return f == 1;
+}
+
+bool SimpleCNNEngine::overlap_active() {
+  const bool use_x = xgmi_ && (xgmi_->world() > 1 || cfg_.force_allreduce);
+  return cfg_.dist_mode == 4 && !cfg_.f32 && use_x && pair_plan_ok_ && cfg_.fuse_level >= 3 && cfg_.l3_fc_role &&
+         cfg_.pxt_fwd == 1 && level3_active(cfg_.max_batch) &&
+         conv3x3_bwd_fc_role_ok(cfg_.H, cfg_.W, cfg_.C1, cfg_.C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
 }
 
 void SimpleCNNEngine::refresh_shadows() {
@@ -149,8 +158,9 @@ void SimpleCNNEngine::refresh_shadows() {
   DDP_HIP_CHECK(hipGetLastError());
 }
 
-void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
+void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, unsigned parts) {
   if (cfg_.f32) {
+    if (parts != PART_ALL) throw std::runtime_error("engine: the fp32 step runs whole (no step-head merge)");
     launch_step_f32(B, stride, first_momentum_step);
     return;
   }
@@ -181,9 +191,12 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   const bool l3 = level3_active(B);
   const bool fred = f1 && cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
   const long n_fc = (long)NO * HW * C2;
-  if (fred || l3) {  // the forward resets the step's hand-off counters
+  // dist_mode 3 on any chain (level 1 too: the same-GPU multi-rank rehearsals run level 1):
+  // one stream, both buckets in one launch behind the conv backward
+  const bool pair_mode = dist && use_x && f1 && cfg_.dist_mode >= 3 && sync_ok_for_xar();
+  if (fred || l3 || pair_mode) {  // the forward resets the step's hand-off counters
     const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
-    const int nsync = SYNC_RED_INTS + (l3 ? L3_FC_INTS : 0);
+    const int nsync = SYNC_RED_INTS + ((l3 || pair_mode) ? L3_FC_INTS : 0);
     c1.zero_i32 = b_.sync_flags;
     c1.zero_per_block = (nsync + nfwd - 1) / nfwd;
     c1.zero_total = nsync;  // level 3: the per-image counters follow (L3_IMG_OFF)
@@ -211,9 +224,18 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // dist_mode 2 (xGMI): the same fc role inside the conv backward at world size > 1, its
   // gradient all-reduced in-launch (make_xar / BwdXar)
   const bool xar_mode = dist && use_x && l3 &&
-                        ((cfg_.dist_mode == 2 && xar_plan_ok_) || cfg_.dist_mode == 3);
+                        ((cfg_.dist_mode == 2 && xar_plan_ok_) || cfg_.dist_mode >= 3);
+  // the one-stream chains: fc weight gradient (role or kernel) -> conv backward -> the bucket
+  // all-reduces on cs_ (in-launch: dist_mode 2; one pair launch: dist_mode 3 / 4)
+  const bool one_stream = xar_mode || pair_mode;
   const bool fc_role = l3 && (!dist || xar_mode) && cfg_.l3_fc_role &&
                        conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
+  // dist_mode 4 (the step head): mode 3's chain, but the step counter advances in the conv
+  // backward's fc role (after it read the loss index) instead of the pair launch, so that the
+  // pair launch can carry the NEXT step's forward (which reads the counter for its batch)
+  const bool ov = dist && use_x && l3 && fc_role && cfg_.dist_mode == 4;
+  if ((parts & (PART_HEAD | PART_AR)) && !ov && parts != PART_ALL)
+    throw std::runtime_error("engine: a split step needs the dist_mode 4 chain");
   const C1Src* pc1 = f1 ? &c1 : nullptr;
   BatchIdx bid{nullptr, nullptr, 0, 0};
   bid.n_rows = B;
@@ -223,10 +245,37 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   c1b.w = c1.w;
   c1b.b = c1.b;
 
-  // ---- forward
-  if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
-  conv3x3_fwd(f1 ? nullptr : b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true,
-              b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1, l3 ? &dzo : nullptr);
+  // ---- forward (PART_HEAD: in one launch with the previous step's bucket all-reduces)
+  const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
+                   cfg_.maximize, first_momentum_step ? 1 : 0, 1};
+  float* M = b_.momentum;  // null when momentum == 0
+  bool head_used = false;
+  if (parts & PART_HEAD) {
+    // the previous step's pair (its fused SGD writes this step's parameters write-through)
+    // + this step's forward; two launches (same bits) when the merged grid does not fit
+    if (first_momentum_step) throw std::runtime_error("engine: the step head runs the steady-state SGD only");
+    ShadowSet sh3{};
+    sh3.r[0] = ShadowRegion{b_.off_w2, (long)C2 * 9 * C1, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
+    sh3.r[1] = ShadowRegion{b_.off_w2, (long)C2 * 9 * C1, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
+    sh3.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+    sh3.count = 3;
+    BwdXar hx;
+    if (!make_xar(hx, sa, M, sh3)) throw std::runtime_error("engine: the step head needs the pair plan");
+    hx.step_ctr = nullptr;  // (advanced by the fc role)
+    int* mc = b_.sync_flags + L3_IMG_OFF + (long)FWD_DZ_CNT_STRIDE * cfg_.max_batch;
+    head_used = cfg_.pxt_fwd == 1 && B == cfg_.max_batch &&
+                conv3x3_step_head(hx, mc, mc + FWD_DZ_CNT_STRIDE, b_.w2_bf16, P + b_.off_b2, b_.a2, B, b_.wfc_frag,
+                                  b_.fc_part, c1, dzo, b_.sync_err, cs_);
+    if (!head_used) xgmi_allreduce_pair(hx, cs_);
+    DDP_HIP_CHECK(hipGetLastError());
+  }
+  if ((parts & PART_FWD) || ((parts & PART_HEAD) && !head_used)) {
+    if (!f1) conv1_fwd(b_.images, true, bi, P + b_.off_w1, P + b_.off_b1, b_.a1, B, H, W, C1, cs_);
+    conv3x3_fwd(f1 ? nullptr : b_.a1, b_.w2_bf16, P + b_.off_b2, b_.a2, B, H, W, C1, C2, true,
+                b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1, l3 ? &dzo : nullptr);
+  }
+  if (parts & (PART_FWD | PART_HEAD)) last_head_ = head_used;
+  if (!(parts & (PART_BWD | PART_AR))) return;
   // ---- loss + fc backward (bucket 0)
   if (!f1)
     xent_rows(b_.fc_part, HW, 64 * cfg_.pxt_fwd, P + b_.off_bfc, NO, B, b_.labels, bi, b_.dlogits,
@@ -252,9 +301,6 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
   // fc_bwd; convs + fc bias: grad_reduce) and the separate SGD pass disappears
   const bool fopt = !dist && cfg_.fuse_opt;
   const long n_w2 = (long)C2 * 9 * C1, w2row = n_w2 + C2;
-  const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
-                   cfg_.maximize, first_momentum_step ? 1 : 0, 1};
-  float* M = b_.momentum;  // null when momentum == 0
   ex.sys_store = use_x ? 1 : 0;  // bucket 0 is read by the peers over xGMI
   if (fopt) {
     ex.sgd = sa;
@@ -273,7 +319,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     ex.part = nullptr;
     ex.loss_rows = b_.loss_rows;
     ex.zero_i32 = dzo.img_cnt;  // re-arm the forward's per-image counters for the next step
-    ex.n_zero = B;
+    // (dist_mode 4: and the step head's two bucket-done counters behind them)
+    ex.n_zero = ov ? cfg_.max_batch + 2 : B;
     ex.zero_stride = FWD_DZ_CNT_STRIDE;
     if (fc_role) {
       // inside the conv backward launch: block 0 of the fc role owns the fc bias, the loss
@@ -283,6 +330,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
         ex.m_b = M ? M + b_.off_bfc : nullptr;
         ex.step_inc = b_.step_ctr;
       }
+      if (ov) ex.step_inc = b_.step_ctr;
       ex.sh_plain = nullptr;  // level 3 never reads the plain bf16 fc shadow (stale until refreshed)
       fcr.a2 = b_.a2;
       fcr.dl = b_.dlogits;
@@ -353,7 +401,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
             (int)xar_plan_ok_, (int)fc_role, (int)fred, (int)buckets_.size());
   bool xar_used = false, pair_used = false;
   auto conv_launch = [&]() {
-    if (f1) {
+    if (!(parts & PART_BWD)) {  // (dist_mode 4: the last step's pair alone)
+    } else if (f1) {
       // dZ1 only feeds conv1's weight gradient, which the dgrad role computes in registers
       reduced = conv3x3_bwd(b_.dz2, b_.w2t_bf16, nullptr, b_.w1slab, b_.w2slab, B, H, W, C1, C2, cfg_.pxt_dgrad,
                             cfg_.wgrad_rows, c1b, cfg_.store_a1 ? b_.a1 : nullptr, cfg_.store_a1 == 2, cs_,
@@ -365,12 +414,13 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
                     b_.w1slab, cfg_.pxt_dgrad, cs_, nullptr);
       conv3x3_wgrad(b_.dz2, nullptr, b_.a1, b_.w2slab, B, H, W, C1, C2, cfg_.wgrad_rows, cs_, nullptr);
     }
-    if (!reduced) grad_reduce(ss, cs_);
-    if (xar_mode && !xar_used) {
-      // dist_mode 3 (or the in-launch all-reduce did not apply): the bucket all-reduces behind
-      // the conv backward on the compute stream - both in one launch when the plan allows
+    if (!reduced && (parts & PART_BWD)) grad_reduce(ss, cs_);
+    if (one_stream && !xar_used && (parts & PART_AR)) {
+      // dist_mode 3 / 4 (or the in-launch all-reduce did not apply): the bucket all-reduces
+      // behind the conv backward on the compute stream - both in one launch when the plan allows
       BwdXar pr;
-      if (cfg_.dist_mode == 3 && make_xar(pr, sa, M, sh_all)) {
+      if (cfg_.dist_mode >= 3 && make_xar(pr, sa, M, sh_all)) {
+        if (ov) pr.step_ctr = nullptr;  // (advanced by the fc role)
         xgmi_allreduce_pair(pr, cs_);
         pair_used = true;
         DDP_HIP_CHECK(hipGetLastError());
@@ -381,14 +431,23 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step) {
     }
   };
   // fc buckets overlap the conv backward: in-launch (dist_mode 2), or the fc weight gradient
-  // forks off the compute stream after the forward (dist_mode 1)
-  if (xar_mode) conv_launch();
-  else schedule_backward(dist, dist && l3 && cfg_.dist_mode == 1, use_x, fc_launch, conv_launch, sa, M, sh_all);
+  // forks off the compute stream after the forward (dist_mode 1); the one-stream chains run
+  // the fc weight-gradient kernel (when it is not a role of the conv backward) first
+  if (one_stream) {
+    if (fc_launch && (parts & PART_BWD)) fc_launch(cs_);
+    conv_launch();
+  } else {
+    schedule_backward(dist, dist && l3 && cfg_.dist_mode == 1, use_x, fc_launch, conv_launch, sa, M, sh_all);
+  }
+  if (!(parts & PART_BWD)) {  // (a lone pair: the step's other flags stay those of its backward)
+    last_pair_ = pair_used;
+    return;
+  }
   last_fused_reduce_ = reduced;
   last_level3_ = l3;
   last_fc_role_ = fc_role;
   last_xar_ = xar_used;
-  last_pair_ = pair_used;
+  last_pair_ = pair_used || head_used;
   if (fopt) return;
   if (dist && use_x) return;  // the optimizer ran inside the all-reduces
   // ---- optimizer + bf16 shadows + next batch window
@@ -417,7 +476,7 @@ void SimpleCNNEngine::enqueue_buckets(int stage, bool use_x, hipStream_t s, cons
 }
 
 bool SimpleCNNEngine::make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh) {
-  if (!xgmi_ || !(cfg_.dist_mode == 3 ? pair_plan_ok_ : xar_plan_ok_)) return false;
+  if (!xgmi_ || !(cfg_.dist_mode >= 3 ? pair_plan_ok_ : xar_plan_ok_)) return false;
   // the pair lives in device memory, one immutable copy per distinct content (a captured
   // graph keeps pointing at the copy it was captured with): the momentum-init step's and
   // the steady state's - both made on the first (eager) call, so a capture never needs a
@@ -561,9 +620,10 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
   c1b.b = c1.b;
   const bool l3 = level3_active(B);
   const bool fred = cfg_.fuse_reduce && b_.sync_flags;  // grad_reduce inside the conv bwd
-  if (fred || l3) {  // the forward resets the step's hand-off counters
+  const bool pair_mode = dist && use_x && cfg_.dist_mode >= 3 && sync_ok_for_xar();  // (see launch_step)
+  if (fred || l3 || pair_mode) {  // the forward resets the step's hand-off counters
     const int nfwd = conv3x3_dgrad_blocks(B, H, W, cfg_.pxt_fwd);
-    const int nsync = SYNC_RED_INTS + (l3 ? L3_FC_INTS : 0);
+    const int nsync = SYNC_RED_INTS + ((l3 || pair_mode) ? L3_FC_INTS : 0);
     c1.zero_i32 = b_.sync_flags;
     c1.zero_per_block = (nsync + nfwd - 1) / nfwd;
     c1.zero_total = nsync;
@@ -583,7 +643,8 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
     dzo.loss_rows = b_.loss_rows;
   }
   const bool xar_mode = dist && use_x && l3 &&
-                        ((cfg_.dist_mode == 2 && xar_plan_ok_) || cfg_.dist_mode == 3);
+                        ((cfg_.dist_mode == 2 && xar_plan_ok_) || cfg_.dist_mode >= 3);
+  const bool one_stream = xar_mode || pair_mode;  // (fp32: dist_mode 4 runs mode 3's chain)
   const bool fc_role = l3 && (!dist || xar_mode) && cfg_.l3_fc_role &&
                        conv3x3_bwd_fc_role_ok(H, W, C1, C2, cfg_.pxt_dgrad, cfg_.wgrad_split);
 
@@ -692,11 +753,11 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
                           fc_role ? &fcr : nullptr, !dist && cfg_.fuse_reduce == 2, want_xar ? &xa : nullptr,
                           &xar_used);
     if (!reduced) grad_reduce(ss, cs_);
-    if (xar_mode && !xar_used) {
+    if (one_stream && !xar_used) {
       // dist_mode 3 (or the in-launch all-reduce did not apply): the bucket all-reduces behind
       // the conv backward on the compute stream - both in one launch when the plan allows
       BwdXar pr;
-      if (cfg_.dist_mode == 3 && make_xar(pr, sa, M, sh1)) {
+      if (cfg_.dist_mode >= 3 && make_xar(pr, sa, M, sh1)) {
         xgmi_allreduce_pair(pr, cs_);
         pair_used = true;
         DDP_HIP_CHECK(hipGetLastError());
@@ -706,8 +767,12 @@ void SimpleCNNEngine::launch_step_f32(int B, int stride, bool first_momentum_ste
       }
     }
   };
-  if (xar_mode) conv_launch();
-  else schedule_backward(dist, dist && l3 && cfg_.dist_mode == 1, use_x, fc_launch, conv_launch, sa, M, sh1);
+  if (one_stream) {
+    if (fc_launch) fc_launch(cs_);
+    conv_launch();
+  } else {
+    schedule_backward(dist, dist && l3 && cfg_.dist_mode == 1, use_x, fc_launch, conv_launch, sa, M, sh1);
+  }
   last_fused_reduce_ = reduced;
   last_level3_ = l3;
   last_fc_role_ = fc_role;
@@ -765,7 +830,15 @@ void SimpleCNNEngine::capture(int nsteps) {
   destroy_graph();
   DDP_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
   try {
-    for (int i = 0; i < nsteps; ++i) launch_step(cfg_.max_batch, cfg_.max_batch, false);
+    if (overlap_active()) {
+      // dist_mode 4: [fwd 0] [bwd 0] [pair 0 + fwd 1] [bwd 1] ... [bwd n-1] [pair n-1] - the
+      // pair of every step but the last shares a launch with the next step's forward
+      for (int i = 0; i < nsteps; ++i)
+        launch_step(cfg_.max_batch, cfg_.max_batch, false, (i == 0 ? PART_FWD : PART_HEAD) | PART_BWD);
+      launch_step(cfg_.max_batch, cfg_.max_batch, false, PART_AR);
+    } else {
+      for (int i = 0; i < nsteps; ++i) launch_step(cfg_.max_batch, cfg_.max_batch, false);
+    }
   } catch (...) {
     hipGraph_t g = nullptr;
     hipStreamEndCapture(cs_, &g);

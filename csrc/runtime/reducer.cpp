@@ -11,6 +11,8 @@
 // stream ordered by hipEvents (capturable), and the collective is RCCL directly - or,
 // per bucket, the direct xGMI kernel (set_xgmi; two-shot with an in-kernel publish pass,
 // since autograd produced the gradients with plain stores).
+#include <cstdlib>
+
 #include "runtime/runtime.h"
 
 namespace ddp_amd {
@@ -74,13 +76,17 @@ void Reducer::launch_bucket(int b, hipStream_t compute) {
     xgmi_->all_reduce(xch_[b], comm_stream_, 1.f, true, prescale_ ? 1.f : inv);
     ++calls_;
   } else if (comm_ && comm_->world() > 1) {
-    // DDP's prescale by 1/world folded into the reduction (RCCL pre-multiplied SUM: no
-    // separate read + write pass over the bucket); producers that prescaled already SUM
+    // DDP's prescale by 1/world: scale pass + SUM (torch DDP's own order).  RCCL's
+    // pre-multiplied SUM folds the scale into the reduction (no extra pass) but is opt-in
+    // (DDP_AMD_RCCL_PREMUL=1, and only for 16-byte-aligned buckets of whole quads): it was seen
+    // leaving a non-multiple-of-4 tail unscaled at one rank, and no multi-rank run has pinned
+    // its bits against scale + SUM; producers that prescaled already SUM
+    static const bool premul = [] { const char* e = std::getenv("DDP_AMD_RCCL_PREMUL"); return e && e[0] == '1'; }();
     if (prescale_) {
       comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
-    } else if (bucket_num_[b] % 4 == 0) {
+    } else if (premul && bucket_num_[b] % 4 == 0 && bucket_off_[b] % 4 == 0) {
       comm_->all_reduce_premul(flat_ + bucket_off_[b], (size_t)bucket_num_[b], inv, comm_stream_);
-    } else {  // (RCCL's pre-multiplied SUM was seen skipping a non-multiple-of-4 tail at one rank)
+    } else {
       scale_copy(flat_ + bucket_off_[b], flat_ + bucket_off_[b], bucket_num_[b], inv, comm_stream_);
       comm_->all_reduce(flat_ + bucket_off_[b], (size_t)bucket_num_[b], 0, 0, comm_stream_);
     }

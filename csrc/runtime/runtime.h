@@ -97,6 +97,12 @@ class XgmiComm {
   // the conv backward runs the same body from them, with blocks(channel) blocks)
   XgmiArgs make_args(int channel, const SgdArgs& sgd, float* params, float* mbuf, const ShadowSet& sh,
                      int* step_ctr, float scale = 1.f, bool publish = false, float prescale = 1.f) const;
+  // Two channels' all-reduces in ONE launch - the engine's dist_mode 3 kernel
+  // (xgmi_allreduce_pair) as a standalone call: blocks [0, blocks(ch0)) run ch0, the rest
+  // ch1, side by side, each with the fused SGD of all_reduce_sgd; the launch's last block
+  // advances step_ctr.  (Multi-rank tests drive the production kernel through this.)
+  void all_reduce_pair(int ch0, int ch1, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
+                       const ShadowSet& sh, int* step_ctr);
   // != 0: a barrier timed out (result invalid) - the first failed channel's error word
   // (xgmi_error_code: block, peer, barrier)
   unsigned error_flags() const;
@@ -104,6 +110,7 @@ class XgmiComm {
   int rank() const { return rank_; }
   int world() const { return world_; }
   int channels() const { return (int)ch_.size(); }
+  long data_numel() const { return data_numel_; }
 
  private:
   struct Channel {
@@ -117,6 +124,7 @@ class XgmiComm {
   };
   int rank_, world_, device_;
   float* data_ = nullptr;
+  long data_numel_ = 0;
   char* data_base_ = nullptr;
   long data_off_ = 0;
   float* data_peer_[XGMI_MAX_RANKS] = {};
@@ -124,6 +132,12 @@ class XgmiComm {
   std::vector<void*> opened_;
   bool imported_ = false;
   double timeout_s_ = XGMI_DEFAULT_TIMEOUT_S;
+  struct PairArgs {  // all_reduce_pair: device copies of the argument pairs, one per content
+    XgmiArgs host[2];
+    XgmiArgs* dev = nullptr;
+  };
+  std::vector<PairArgs> pair_cache_;
+  int* pair_done_ = nullptr;  // the pair launch's last-block count (zeroed before each launch)
 };
 
 // ---------------------------------------------------------------- gradient reducer
@@ -268,6 +282,11 @@ struct EngineConfig {
   //      profiles/r5_dist/README.md): the in-launch roles get too few blocks, a graph
   //      branch costs two cross-stream edges
   //  0 = the round-4 order (fc_bwd in front of the conv backward, all-reduces on ms_)
+  //  4 = the step head (xGMI, bf16 level 3, pxt_fwd 1): mode 3's chain, but in a captured
+  //      graph the pair launch of step k also carries step k + 1's forward (conv3x3.hip
+  //      step_head_kernel: the forward blocks wait for each bucket's all-reduce blocks only
+  //      where they first read its parameters) - 2 launches per step instead of 3; the step
+  //      counter advances in the conv backward's fc role.  Same bits as mode 3.
   int dist_mode = 3;
 };
 
@@ -301,6 +320,8 @@ class SimpleCNNEngine {
   int sync_error() const { return err_host_ ? __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) : 0; }
   // whether a step of `batch` images runs the level-3 chain (fuse_level 3 and it applies)
   bool level3_active(int batch);
+  // whether dist_mode 4's step head applies to a captured full-batch step
+  bool overlap_active();
   // whether the last launched step reduced its weight-gradient slabs inside the conv
   // backward launch (false: separate grad_reduce kernel)
   bool last_fused_reduce() const { return last_fused_reduce_; }
@@ -312,6 +333,8 @@ class SimpleCNNEngine {
   bool last_xar() const { return last_xar_; }
   // ... or behind it in one launch for both buckets (dist_mode 3, xgmi_allreduce_pair)
   bool last_pair() const { return last_pair_; }
+  // ... and whether its forward shared a launch with the previous step's pair (dist_mode 4)
+  bool last_head() const { return last_head_; }
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
   // bucket b; set before capturing a graph
@@ -320,7 +343,11 @@ class SimpleCNNEngine {
   int bucket_stage(int b) const { return stage_.at(b); }
 
  private:
-  void launch_step(int batch, int batch_stride, bool first_momentum_step);
+  // parts of a step (dist_mode 4 splits steps inside a captured graph): the forward, the
+  // backward, the bucket all-reduce pair; PART_HEAD = the forward merged with the PREVIOUS
+  // step's pair (step_head_kernel)
+  enum : unsigned { PART_FWD = 1, PART_BWD = 2, PART_AR = 4, PART_HEAD = 8, PART_ALL = 7 };
+  void launch_step(int batch, int batch_stride, bool first_momentum_step, unsigned parts = PART_ALL);
   void launch_step_f32(int batch, int batch_stride, bool first_momentum_step);
   // enqueue the all-reduces of the buckets of `stage` (0: after fc_bwd, 1: after
   // grad_reduce) on the comm stream behind an event of the compute stream; with xGMI the
@@ -362,6 +389,7 @@ class SimpleCNNEngine {
   bool last_fc_role_ = false;
   bool last_xar_ = false;
   bool last_pair_ = false;
+  bool last_head_ = false;
   bool xar_plan_ok_ = false;  // set_xgmi: the bucket plan fits the in-launch all-reduce
   bool pair_plan_ok_ = false;  // ... and the one-launch pair of bucket kernels (dist_mode 3)
   struct XarArgs {

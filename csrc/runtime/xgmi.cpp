@@ -39,6 +39,8 @@ XgmiComm::XgmiComm(int rank, int world, int device) : rank_(rank), world_(world)
 XgmiComm::~XgmiComm() {
   if (process_exiting()) return;
   for (void* p : opened_) hipIpcCloseMemHandle(p);
+  for (PairArgs& e : pair_cache_) hipFree(e.dev);
+  if (pair_done_) hipFree(pair_done_);
   for (auto& c : ch_) {
     if (c.stage_local) hipFree(c.stage_local);
     if (c.sig_local) hipFree(c.sig_local);
@@ -75,6 +77,7 @@ void XgmiComm::set_data(float* data, long numel) {
   for (auto& c : ch_)
     if (c.off < 0 || c.off + c.n > numel) throw std::runtime_error("xgmi: channel outside the data buffer");
   data_ = data;
+  data_numel_ = numel;
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   DDP_HIP_CHECK(hipMemGetAddressRange(&base, &size, data));
@@ -181,6 +184,36 @@ void XgmiComm::all_reduce_sgd(int channel, hipStream_t s, const SgdArgs& sgd, fl
                               float prescale) {
   const XgmiArgs a = make_args(channel, sgd, params, mbuf, sh, step_ctr, scale, publish, prescale);
   xgmi_allreduce(a, ch_[channel].blocks, s);
+  DDP_HIP_CHECK(hipGetLastError());
+}
+
+void XgmiComm::all_reduce_pair(int ch0, int ch1, hipStream_t s, const SgdArgs& sgd, float* params, float* mbuf,
+                               const ShadowSet& sh, int* step_ctr) {
+  if (ch0 == ch1) throw std::runtime_error("xgmi: all_reduce_pair needs two distinct channels");
+  XgmiArgs pair[2];
+  std::memset(static_cast<void*>(pair), 0, sizeof(pair));  // (compared bytewise below)
+  pair[0] = make_args(ch0, sgd, params, mbuf, sh, nullptr);
+  pair[1] = make_args(ch1, sgd, params, mbuf, sh, nullptr);
+  const XgmiArgs* dev = nullptr;
+  for (const PairArgs& e : pair_cache_)
+    if (std::memcmp(e.host, pair, sizeof(pair)) == 0) dev = e.dev;
+  if (!dev) {
+    PairArgs e;
+    std::memcpy(static_cast<void*>(e.host), pair, sizeof(pair));
+    DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&e.dev), sizeof(pair)));
+    DDP_HIP_CHECK(hipMemcpy(e.dev, pair, sizeof(pair), hipMemcpyHostToDevice));
+    pair_cache_.push_back(e);
+    dev = e.dev;
+  }
+  if (!pair_done_) DDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&pair_done_), sizeof(int)));
+  DDP_HIP_CHECK(hipMemsetAsync(pair_done_, 0, sizeof(int), s));
+  BwdXar x;
+  x.args = dev;
+  x.nblk0 = ch_[ch0].blocks;
+  x.nblk1 = ch_[ch1].blocks;
+  x.xar_done = pair_done_;
+  x.step_ctr = step_ctr;
+  xgmi_allreduce_pair(x, s);
   DDP_HIP_CHECK(hipGetLastError());
 }
 

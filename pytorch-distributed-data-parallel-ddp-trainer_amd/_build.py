@@ -19,11 +19,21 @@ Layout of the native sources (``<repo>/csrc``):
 Objects are rebuilt only when their source (or any header under ``csrc``) is
 newer than the object; the link step is skipped when the ``.so`` is newer than
 every object.
+
+The binary is tied to its sources: every build embeds
+:func:`source_hash` - a SHA-256 over every file under ``csrc`` (relative path +
+bytes) and the compile flags - as the string ``DDP_AMD_SRC_HASH=<hex>`` in ``_C.so``.
+``native.require()`` recomputes the hash of the tree it runs from and refuses a
+binary built from other sources (:func:`binary_hash` reads the marker without loading
+the library), so a forgotten rebuild cannot silently test old kernels.
 """
 from __future__ import annotations
 
 import concurrent.futures as _cf
 import glob
+import hashlib
+import json
+import mmap
 import os
 import shutil
 import subprocess
@@ -79,27 +89,82 @@ def _needs(obj: str, src: str, hdr_mtime: float, cmd=None) -> bool:
 # v_mov 0 + v_mov_dpp + add (the conv1 weight-gradient reduction of the dgrad role: 750 ->
 # 400 VALU instructions with the adds folded into v_add_f32_dpp)
 KERNEL_FLAGS = {"conv3x3.hip": ["-fno-slp-vectorize"]}
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__"]
+DEVICE_FLAGS = ["-munsafe-fp-atomics"]
+BIND_FLAGS = ["-O2", "-DUSE_ROCM", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H"]
+SOURCE_EXTS = (".hip", ".cpp", ".h", ".cuh", ".hpp")
+HASH_MARKER = b"DDP_AMD_SRC_HASH="
+HASH_LEN = 40
+
+
+def source_hash(csrc: str = CSRC) -> str:
+    """Hash of everything the binary is built from: each source file under ``csrc``
+    (relative path + bytes, sorted) and the path-independent compile flags (the repo sits
+    at another path on the GPU box, so absolute include paths are left out)."""
+    h = hashlib.sha256()
+    files = sorted(p for p in glob.glob(os.path.join(csrc, "**", "*"), recursive=True)
+                   if os.path.isfile(p) and p.endswith(SOURCE_EXTS))
+    for p in files:
+        h.update(os.path.relpath(p, csrc).replace(os.sep, "/").encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    sig = dict(arch=ARCH, common=COMMON_FLAGS, device=DEVICE_FLAGS, kernel=KERNEL_FLAGS, bind=BIND_FLAGS)
+    h.update(json.dumps(sig, sort_keys=True).encode())
+    return h.hexdigest()[:HASH_LEN]
+
+
+def binary_hash(so_path: str = SO_PATH) -> str | None:
+    """The source hash embedded in a built ``_C.so`` (None: no marker - a binary from
+    before round 6, or not ours).  Reads the file; does not load it."""
+    try:
+        with open(so_path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as mm:
+            i = mm.find(HASH_MARKER)
+            if i < 0:
+                return None
+            return mm[i + len(HASH_MARKER):i + len(HASH_MARKER) + HASH_LEN].decode("ascii", "replace")
+    except (OSError, ValueError):
+        return None
+
+
+def _hash_source_file() -> str:
+    """(Re)write the generated TU that embeds the source hash; untouched when unchanged,
+    so an unchanged tree relinks nothing."""
+    path = os.path.join(BUILD_DIR, "source_hash.cpp")
+    text = ("// generated by _build.py: the sources this binary was built from\n"
+            f'extern "C" const char ddp_amd_source_hash_str[] = "{HASH_MARKER.decode()}{source_hash()}";\n')
+    try:
+        with open(path) as f:
+            if f.read() == text:
+                return path
+    except OSError:
+        pass
+    with open(path, "w") as f:
+        f.write(text)
+    return path
 
 
 def _compile_cmds():
     hipcc = _hipcc()
     _, tinc, _ = _torch_dirs()
     rocm_inc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "include")
-    common = ["-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I", rocm_inc, "-I", CSRC]
+    common = [*COMMON_FLAGS, "-I", rocm_inc, "-I", CSRC]
     cmds = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(BUILD_DIR, "k_" + os.path.basename(src) + ".o")
         cmds.append((src, obj, [hipcc, f"--offload-arch={ARCH}", *common, *KERNEL_FLAGS.get(os.path.basename(src), []),
-                                "-munsafe-fp-atomics", "-c", src, "-o", obj]))
+                                *DEVICE_FLAGS, "-c", src, "-o", obj]))
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD_DIR, "r_" + os.path.basename(src) + ".o")
         # host-only TUs: still driven by hipcc so hip_runtime.h resolves, but no device code
         cmds.append((src, obj, [hipcc, *common, "-x", "c++", "-c", src, "-o", obj]))
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(BUILD_DIR, "bindings.o")
+    hsrc = _hash_source_file()
+    cmds.append((hsrc, os.path.join(BUILD_DIR, "source_hash.o"), ["g++", "-fPIC", "-c", hsrc, "-o",
+                                                                  os.path.join(BUILD_DIR, "source_hash.o")]))
     cmds.append((bsrc, bobj, [
-        hipcc, *common[:-2], "-O2", "-x", "c++", "-I", CSRC,
-        "-DUSE_ROCM", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+        hipcc, *common[:-2], "-x", "c++", "-I", CSRC, *BIND_FLAGS,
         f"-D_GLIBCXX_USE_CXX11_ABI={int(_cxx11_abi())}",
         "-I", tinc, "-I", os.path.join(tinc, "torch", "csrc", "api", "include"),
         "-I", sysconfig.get_paths()["include"], "-w", "-c", bsrc, "-o", bobj]))

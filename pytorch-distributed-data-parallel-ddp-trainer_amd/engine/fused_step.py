@@ -115,7 +115,10 @@ class EngineOptions:
     # soon as it is final - 2 kernels per step, as on one GPU (engine.cpp make_xar, conv3x3.hip
     # XAR); 1 = fc_bwd + the fc buckets' all-reduces on a graph branch forked after the
     # forward (schedule_backward); 3 = one stream: the fc role inside the conv backward, the
-    # bucket kernels behind it (no cross-stream edge); 0 = the round-4 serial order
+    # bucket kernels behind it (no cross-stream edge); 0 = the round-4 serial order;
+    # 4 = the step head (bf16, xGMI; forces pxt_fwd 1): mode 3's chain, but in a captured graph
+    # step k's bucket-pair launch also runs step k + 1's forward (2 launches per step instead
+    # of 3; conv3x3.hip step_head_kernel) - same bits as mode 3
     dist_mode: int = 3
     # dist_mode 2: the most blocks of a bucket's xGMI channel (its role blocks wait at the
     # head of the conv backward grid; the engine takes the in-launch path while the channels'
@@ -138,11 +141,107 @@ def agree(store, key: str, rank: int, world: int, ok: bool) -> bool:
     return all(store.get(f"{key}/{r}") == b"1" for r in range(world))
 
 
+# ---------------------------------------------------------------------- reduction oracle
+# the start-up check compares the production chain's reduced gradient with a
+# sum computed WITHOUT the xGMI code - every rank's local (prescaled) gradient gathered over
+# the process group and added in rank order on the host - so a stale or misplaced read in
+# the fence-free cross-GPU protocol cannot pass by being shared with the reference chain.
+
+def gather_rank_sum(local: torch.Tensor, world: int) -> torch.Tensor:
+    """Every rank's ``local`` (same shape, fp32) summed in rank order 0..world-1 on the host
+    (``acc = g0; acc += g1; ...`` - IEEE fp32 adds in the order the xGMI kernels use),
+    gathered over the default process group (gloo: host tensors, nccl: device tensors).
+    Collective."""
+    import torch.distributed as dist
+
+    src = local.detach().float().contiguous()
+    if world <= 1 or not dist.is_initialized():
+        return src.cpu().clone()
+    if dist.get_backend() == "gloo":
+        src = src.cpu()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src)
+    acc = parts[0].cpu().clone()
+    for p in parts[1:]:
+        acc += p.cpu()
+    return acc
+
+
+def oracle_mismatches(reduced: torch.Tensor, oracle: torch.Tensor, ranges) -> int:
+    """Elements of the bucket ranges where ``reduced`` differs from ``oracle`` bit for bit."""
+    r = reduced.detach().float().cpu().contiguous()
+    o = oracle.detach().float().cpu().contiguous()
+    bad = 0
+    for off, n in ranges:
+        bad += int((r[off:off + n].view(torch.int32) != o[off:off + n].view(torch.int32)).sum())
+    return bad
+
+
+# ---------------------------------------------------------------------- placement choice
+# VERDICT r5 #5: at N > 1 the multi-GPU placement (EngineOptions.dist_mode) is timed on the
+# node it runs on instead of being fixed by a world-1 measurement.  Only placements that give
+# the same bits compete (all of them sum in the plane's fixed order), so the choice never
+# changes the trained parameters, only the speed.
+PLACEMENT_NAMES = {0: "serial", 1: "fork", 3: "pair", 4: "step head"}
+
+
+def placement_candidates(comm_kind: str, dtype: str = "bf16") -> tuple:
+    """dist_modes worth timing on a data plane: xGMI - the step head (4: the pair launch
+    carrying the next step's forward; bf16 only), the pair launch (3), the serial bucket
+    kernels (0) and the forked fc branch (1); RCCL - 0 and 1 (its calls never share a launch).
+    dist_mode 2 (in-launch) needs the in-order-dispatch opt-in and is not a candidate."""
+    if comm_kind.startswith("xgmi"):
+        return (4, 3, 0, 1) if dtype == "bf16" else (3, 0, 1)
+    if comm_kind.startswith("rccl"):
+        return (0, 1)
+    return ()
+
+
+def choose_placement(all_times) -> tuple:
+    """``all_times``: every rank's {dist_mode: us per step, or None when it failed there}.  A
+    step is as slow as its slowest rank, so each mode counts with its max over ranks; the
+    fastest such mode wins (ties: the lower mode).  Returns (mode or None, {mode: max us})."""
+    modes = sorted(set().union(*[set(t) for t in all_times]))
+    worst = {}
+    for m in modes:
+        vals = [t.get(m) for t in all_times]
+        worst[m] = None if any(v is None for v in vals) else max(vals)
+    ok = {m: v for m, v in worst.items() if v is not None}
+    if not ok:
+        return None, worst
+    return min(ok, key=lambda m: (ok[m], m)), worst
+
+
+def agree_placement(store, key: str, rank: int, world: int, mine: dict) -> tuple:
+    """Every rank publishes its timings under ``key`` (c10d store) and computes
+    :func:`choose_placement` over all of them - the same answer on every rank."""
+    import json
+
+    if store is None or world <= 1:
+        return choose_placement([mine])
+    store.set(f"{key}/{rank}", json.dumps({str(k): v for k, v in mine.items()}).encode())
+    allt = [{int(k): v for k, v in json.loads(store.get(f"{key}/{r}").decode()).items()} for r in range(world)]
+    return choose_placement(allt)
+
+
+def chain_decision(same_all: bool, xgmi_ok_all: bool, oracle_ok_all: bool, have_rccl: bool) -> str:
+    """What every rank does after the start-up check (all inputs already agreed across ranks):
+    "keep" the production chain; "conservative" chain on the same plane (the production
+    chain's bits differ from it); "rccl" (an xGMI wait timed out, or the xGMI reduction
+    differs from the host oracle: the direct plane itself is not trusted); "fail" (that, with
+    no RCCL plane to fall back to - a gloo control plane)."""
+    if not xgmi_ok_all or not oracle_ok_all:
+        return "rccl" if have_rccl else "fail"
+    return "keep" if same_all else "conservative"
+
+
 class FusedSimpleCNNEngine:
     def __init__(self, model, optimizer, data: DeviceMNIST, batch_size: int, world_size: int,
                  rank: int, comm=None, opts: EngineOptions | None = None, seed: int = 0):
         self.C = native.require()
-        self.opts = opts or EngineOptions()
+        self.opts = dataclasses.replace(opts) if opts is not None else EngineOptions()
+        if self.opts.dist_mode == 4 and self.opts.dtype == "bf16":
+            self.opts.pxt_fwd = 1  # the step head runs the 256-thread forward in the all-reduce's blocks
         self.model, self.opt, self.data = model, optimizer, data
         self.B = int(batch_size)
         self.world_size, self.rank = world_size, rank
@@ -219,7 +318,8 @@ class FusedSimpleCNNEngine:
         # step's forward, and their wait-timeout word
         # (level 3: [256] the fc side kernel's last-block counter, [288, 288 + B) the
         # forward's per-image arrival counters - engine.cpp L3_IMG_OFF)
-        nfl = 256 + 32 + 64 * B  # (counters 64 ints apart: FWD_DZ_CNT_STRIDE)
+        # (+ 2 rows: dist_mode 4's bucket-done counters behind the image counters)
+        nfl = 256 + 32 + 64 * (B + 2)  # (counters 64 ints apart: FWD_DZ_CNT_STRIDE)
         self.t["sync_flags"] = torch.zeros(nfl, dtype=torch.int32, device=dev)
         # (the engine replaces it by a coherent host word: eng.sync_error)
         self.t["sync_err"] = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -305,21 +405,32 @@ class FusedSimpleCNNEngine:
         ref = dict(self.cfg, fuse_level=min(int(self.cfg["fuse_level"]), 1), fuse_reduce=0)
         return None if ref == self.cfg else ref
 
-    def verify_chain(self, nsteps: int = 2, store=None, _corrupt_rank: int | None = None) -> bool:
+    def verify_chain(self, nsteps: int = 2, store=None, _corrupt_rank: int | None = None,
+                     _corrupt_oracle_rank: int | None = None) -> bool:
         """VERDICT r3 #3a: before training commits to the production chain (level 3 + the
         fused slab reduction + the chosen data plane), run ``nsteps`` eager steps on it, then
         the same steps from the same snapshot on the conservative chain (level 1, separate
         grad_reduce, same plane), and compare parameters, momentum and losses bitwise.
-        Every rank publishes its verdict through the store (:func:`agree`); if any rank saw
-        a mismatch or an in-launch / cross-GPU wait timeout, EVERY rank switches to the
-        conservative chain (and, after an xGMI timeout, to RCCL), deterministically, and logs
-        it.  The snapshot (parameters, momentum, step counter, loss history, momentum state)
-        is restored afterwards, so training starts exactly where it would have.  Collective
-        at world size > 1.  Returns True when the production chain was kept."""
+
+        On the xGMI plane both chains share the all-reduce code, so step 1 is
+        also checked against an oracle that does not use it: a comm-free engine computes this
+        rank's local gradient from the same snapshot, every rank's local gradient is gathered
+        over the process group and summed in rank order on the host (:func:`gather_rank_sum`),
+        and the production chain's reduced gradient must equal it bit for bit on every bucket.
+
+        Every rank publishes its verdicts through the store (:func:`agree`) and acts on the
+        agreed ones (:func:`chain_decision`): a mismatch with the conservative chain -> every
+        rank takes the conservative chain; an xGMI wait timeout or an oracle mismatch -> every
+        rank takes RCCL (without an RCCL plane: a RuntimeError).  The snapshot (parameters,
+        momentum, step counter, loss history, momentum state) is restored afterwards, so
+        training starts exactly where it would have.  Collective at world size > 1.  Returns
+        True when the production chain was kept."""
         ref_cfg = self.conservative_cfg()
-        if ref_cfg is None:
+        if ref_cfg is None and self.xgmi is None:
             self.chain_check = {"ran": False, "reason": "production chain is the conservative one"}
             return True
+        if ref_cfg is None:  # (the oracle still runs; the "conservative" chain is this one)
+            ref_cfg = dict(self.cfg)
         import torch.distributed as dist
 
         if store is None and dist.is_initialized() and self.world_size > 1:
@@ -368,21 +479,33 @@ class FusedSimpleCNNEngine:
         got, err_p = run(self.eng)
         if got is not None and _corrupt_rank == self.rank:  # test hook: a one-ulp disagreement
             got[0][0] = torch.nextafter(got[0][0], torch.tensor(float("inf"), device=got[0].device))
+        pair_ran = bool(self.eng.last_pair)
         want, err_r = run(ref)
         same = got is not None and want is not None and all(torch.equal(a, b) for a, b in zip(got, want))
         xgmi_bad = (err_p or "").startswith("xgmi") or (err_r or "").startswith("xgmi")
+        # ---- the independent oracle (xGMI plane: its sum order is fixed, so bits must match)
+        oracle = {"ran": False}
+        oracle_ok = True
+        if self.xgmi is not None and not xgmi_bad:
+            oracle_ok, oracle = self._reduce_oracle(restore, _corrupt_oracle_rank)
+            xgmi_bad = xgmi_bad or oracle.get("xgmi_error") is not None
         key = f"ddp_amd/chain/{FusedSimpleCNNEngine._chain_gen}"
         FusedSimpleCNNEngine._chain_gen += 1
         ok_all = agree(store, key + "/same", self.rank, self.world_size, same)
         x_ok_all = agree(store, key + "/xgmi", self.rank, self.world_size, not xgmi_bad)
+        o_ok_all = agree(store, key + "/oracle", self.rank, self.world_size, oracle_ok)
+        action = chain_decision(ok_all, x_ok_all, o_ok_all, self.comm is not None)
         chosen = self.eng
-        if not x_ok_all:
-            if self.comm is None:
-                raise RuntimeError("start-up chain check: the xGMI data plane timed out and there is no RCCL plane")
+        if action == "fail":
+            raise RuntimeError("start-up chain check: the xGMI data plane "
+                               f"{'timed out' if not x_ok_all else 'disagrees with the host oracle'} "
+                               f"({oracle}) and there is no RCCL plane")
+        if action == "rccl":
             self.xgmi, self.xgmi_plan, self.comm_kind = None, "rccl", "rccl"
             chosen = self.C.SimpleCNNEngine(ref_cfg, t, self.offs, self.comm)
-            self._log_downgrade("start-up chain check: xGMI wait timed out -> conservative chain over RCCL")
-        elif not ok_all:
+            why = "xGMI wait timed out" if not x_ok_all else "xGMI reduction differs from the host oracle"
+            self._log_downgrade(f"start-up chain check: {why} -> conservative chain over RCCL")
+        elif action == "conservative":
             chosen = ref
             self._log_downgrade("start-up chain check: production chain differs from the conservative one "
                                 f"(here: {'same' if same else err_p or err_r or 'bits differ'}) -> conservative chain")
@@ -396,11 +519,49 @@ class FusedSimpleCNNEngine:
         restore(self.eng)
         torch.cuda.synchronize()
         self.chain_check = {"ran": True, "steps": nsteps, "identical_here": same, "identical_all": ok_all,
-                            "xgmi_ok_all": x_ok_all, "kept_production": chosen is not ref and x_ok_all,
+                            "xgmi_ok_all": x_ok_all, "oracle_ok_all": o_ok_all, "oracle": oracle,
+                            "pair": pair_ran, "kept_production": action == "keep",
                             "error": err_p or err_r}
         return self.chain_check["kept_production"]
 
     _chain_gen = 0
+
+    def _reduce_oracle(self, restore, corrupt_rank=None):
+        """Step 1 of the production chain vs the host oracle (see :meth:`verify_chain`):
+        (ok_here, info).  ``restore(e)`` resets the snapshot for engine ``e``.  Collective."""
+        t, B = self.t, self.B
+        # this rank's local gradient, prescaled by 1 / world exactly as the production
+        # producers write it: the same chain without any data plane and without the fused
+        # optimizer (the gradient buffer keeps the gradient; its SGD pass is undone by restore)
+        loc_cfg = dict(self.cfg, force_allreduce=False, fuse_opt=False)
+        loc = self.C.SimpleCNNEngine(loc_cfg, t, self.offs, None)
+        self.start_epoch(0)
+        restore(loc)
+        loc.step(B, B)
+        loc.synchronize()
+        torch.cuda.synchronize()
+        local = t["grads"].detach().clone()
+        self.start_epoch(0)
+        restore(self.eng)
+        self.eng.step(B, B)
+        info = {"ran": True, "buckets": len(self.ranges)}
+        try:
+            self.eng.synchronize()
+        except RuntimeError as ex:
+            info["xgmi_error"] = f"in-launch wait: {ex}"
+        if self.xgmi.error_flags():
+            from ..parallel.xgmi import describe_xgmi_error
+
+            info["xgmi_error"] = describe_xgmi_error(self.xgmi.error_flags())
+        torch.cuda.synchronize()
+        reduced = t["grads"].detach().clone()
+        if corrupt_rank == self.rank:  # test hook: one ulp off in this rank's reduced bucket
+            off = int(self.ranges[0][0])
+            reduced[off] = torch.nextafter(reduced[off], torch.tensor(float("inf"), device=reduced.device))
+        want = gather_rank_sum(local, self.world_size)
+        bad = oracle_mismatches(reduced, want, self.ranges)
+        info["mismatches"] = bad
+        return bad == 0 and "xgmi_error" not in info, info
 
     # ------------------------------------------------------------------ helpers
     def _device_shared(self, world_size: int) -> bool:

@@ -432,9 +432,52 @@ def test_verify_chain_world1_forced(corrupt, stall):
                 assert kept == (not corrupt), e.chain_check
                 assert e.chain_check["identical_here"] == (not corrupt)
                 assert e.level3 == (not corrupt) and (e.cfg["fuse_level"] == (3 if not corrupt else 1))
+                # the independent host oracle ran on the production chain's step 1 and agreed
+                assert e.chain_check["oracle"]["ran"] and e.chain_check["oracle"]["mismatches"] == 0, e.chain_check
+                assert e.chain_check["pair"], e.chain_check  # the dist_mode 3 pair launch was checked
             e.run_steps(12)
             e.synchronize()
             assert e.eng.sync_error == 0
+            out.append((e.fs.params.clone(), e.opt.momentum_buffer.clone()))
+        assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_verify_chain_oracle_downgrades_to_rccl():
+    """a one-ulp error in the xGMI-reduced gradient (injected into the bucket
+    the production chain reduced) is caught by the host oracle - not by the conservative
+    chain, which shares the xGMI code - and the engine moves to RCCL, then trains to the
+    comm-free chain's bits (world size 1: RCCL's one-rank sum is exact)."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+    from ddp_amd.parallel import native_comm
+
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(),
+                            device_id=torch.device("cuda", 0))
+    try:
+        imgs, labels = synthetic_mnist(2048)
+        data = DeviceMNIST(imgs, labels, dev)
+        out = []
+        for force in (False, True):
+            torch.manual_seed(0)
+            m = SimpleCNN().to(dev)
+            e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, native_comm(),
+                                     EngineOptions(graph_steps=5, force_allreduce=force, comm="xgmi"))
+            e.refresh()
+            if force:
+                assert e.comm_kind.startswith("xgmi")
+                kept = e.verify_chain(_corrupt_oracle_rank=0)
+                cc = e.chain_check
+                assert not kept and cc["identical_all"] and not cc["oracle_ok_all"], cc
+                assert cc["oracle"]["mismatches"] == 1, cc
+                assert e.comm_kind == "rccl" and e.xgmi is None
+            e.run_steps(12)
+            e.synchronize()
             out.append((e.fs.params.clone(), e.opt.momentum_buffer.clone()))
         assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     finally:
@@ -486,15 +529,17 @@ def test_comm_tune_rccl_candidates_world1():
 
 
 @pytest.mark.parametrize("plane,dtype", [("xgmi", "bf16"), ("xgmi", "fp32"), ("rccl", "bf16")])
-def test_dist_chains_bitwise_world1(plane, dtype):
+def test_dist_chains_bitwise_world1(plane, dtype, monkeypatch):
     """every multi-GPU step chain trains to the same bits as the comm-free
     one-GPU chain, at world size 1 with the all-reduces forced and the 8-rank bucket plan (fc
     bucket two-shot, conv bucket one-shot), graph-replayed, with momentum (the fused SGD of
     the xGMI all-gather updates the momentum buffer too) and a ragged last batch:
     dist_mode 3 (default) - both buckets' all-reduces in one launch behind the conv backward
     (xGMI; 3 kernels per step, xgmi_allreduce_pair), 2 - the in-launch all-reduce (xGMI; 2
-    kernels per step, engine.cpp make_xar), 1 - fc_bwd + the fc bucket forked beside the conv
-    backward, 0 - the round-4 serial order."""
+    kernels per step, engine.cpp make_xar; its grid does not fit the GPU at once, so it needs
+    the in-order-dispatch opt-in DDP_AMD_L3_INORDER=1 - without it the bucket kernels run,
+    "inlaunch_fb"), 1 - fc_bwd + the fc bucket forked beside the conv backward, 0 - the
+    round-4 serial order."""
     import torch.distributed as dist
 
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -515,8 +560,12 @@ def test_dist_chains_bitwise_world1(plane, dtype):
         data = DeviceMNIST(imgs, labels, dev)
         out = {}
         modes = (("local", False, 3), ("serial", True, 0), ("fork", True, 1), ("inlaunch", True, 2),
-                 ("pair", True, 3))
+                 ("inlaunch_fb", True, 2), ("pair", True, 3))
         for tag, force, mode in modes:
+            if tag == "inlaunch":
+                monkeypatch.setenv("DDP_AMD_L3_INORDER", "1")
+            else:
+                monkeypatch.delenv("DDP_AMD_L3_INORDER", raising=False)
             torch.manual_seed(0)
             m = SimpleCNN(compute_dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(dev)
             e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, comm,
@@ -532,7 +581,8 @@ def test_dist_chains_bitwise_world1(plane, dtype):
             e.run_steps(3)  # full batches again: the in-launch all-reduce runs
             e.synchronize()
             assert e.eng.sync_error == 0 and e.eng.last_level3
-            assert e.eng.last_xar == (tag == "inlaunch" and plane == "xgmi"), tag
+            if tag != "inlaunch_fb":  # (in-launch iff its whole grid fits this GPU at once)
+                assert e.eng.last_xar == (tag == "inlaunch" and plane == "xgmi"), tag
             assert e.eng.last_pair == (tag == "pair" and plane == "xgmi"), tag
             out[tag] = (e.fs.params.clone(), e.opt.momentum_buffer.clone())
         for tag, _, _ in modes[1:]:
@@ -548,8 +598,9 @@ def test_rccl_premul_sum_world1_eager_and_graph():
     scale pass; at world size 1 the result is exactly x * scale (fp32 multiply), eagerly and
     replayed from a captured graph (the host-immediate scalar is captured by value).
     (RCCL 2.26's one-rank path leaves the last n % 4 elements of a large buffer unscaled -
-    scripts/premul_probe.py, profiles/r5_dist; the reducer's buckets are whole 64-element
-    parameter slots, and it takes the pre-multiplied SUM only for counts % 4 == 0.)"""
+    scripts/premul_probe.py, profiles/r5_dist; since round 6 the reducer takes the
+    pre-multiplied SUM only when opted in, DDP_AMD_RCCL_PREMUL=1, and only for 16-byte-aligned
+    buckets of whole quads - no multi-rank run has pinned it against scale + SUM)"""
     import torch.distributed as dist
 
     from ddp_amd.parallel import free_port, native_comm

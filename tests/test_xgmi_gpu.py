@@ -118,6 +118,10 @@ def _engine_worker(rank, world, port, q, comm="xgmi2"):
         p_one = fs.params.detach().cpu().clone()
         eng.run_steps(15)
         eng.synchronize()
+        # the default multi-GPU chain's all-reduce launch (dist_mode 3: both buckets in one
+        # xgmi_allreduce_pair launch) ran with a real second rank - on the level-1 chain that
+        # ranks sharing a GPU run
+        assert eng.eng.last_pair, "the dist_mode 3 pair launch did not run"
         p = fs.params.detach().cpu()
         allp = [None] * world
         dist.all_gather_object(allp, p)
@@ -220,6 +224,79 @@ def test_engine_two_ranks_xgmi_identical_params(comm):
 
     res = _run(_engine_worker, 2, free_port(), comm)
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
+
+
+def _pair_worker(rank, world, port, q, ncalls):
+    """The production dist_mode 3 launch (xgmi_allreduce_pair: the fc bucket two-shot and the
+    conv bucket one-shot side by side, SGD + momentum fused into the all-gathers) with real
+    peer ranks, against an oracle that does not use the xGMI code: every rank's bucket
+    gathered over gloo and added in rank order on the host, then the plain SGD kernel."""
+    try:
+        _init(rank, world, port)
+        from ddp_amd import native
+        from ddp_amd.parallel import create_xgmi
+
+        C = native.require()
+        dev = torch.device("cuda", 0)
+        n_fc, n_conv = 501_770, 18_816  # SimpleCNN's two buckets (SURVEY.md §2.6 I6 / I7)
+        n = n_fc + n_conv
+        grads = torch.zeros(n, device=dev)
+        x = create_xgmi(grads, [(0, n_fc), (n_fc, n_conv)], rank, world, oneshot=(1,))
+        assert x is not None, "self-test failed"
+        assert x.oneshot(2) and not x.oneshot(1)
+        params = torch.randn(n, generator=torch.Generator().manual_seed(7)).to(dev)  # same on every rank
+        mom = torch.zeros_like(params)
+        ref_p, ref_m = params.clone(), mom.clone()
+        step = torch.zeros(1, dtype=torch.int32, device=dev)
+        lr, mu = 0.05, 0.9
+        pairs_run = set()
+        for it in range(ncalls):
+            # mostly the production pairing (fc two-shot + conv one-shot); every third call both
+            # two-shot - each channel sees both stage parities
+            ch1 = 1 if it % 3 == 0 else 2
+            pairs_run.add(ch1)
+            g = torch.Generator().manual_seed(1000 * it + rank)
+            mine = torch.randn(n, generator=g) * (1.0 / world)  # prescaled, as the producers write it
+            grads.copy_(mine.to(dev))
+            torch.cuda.synchronize()
+            x.all_reduce_pair(0, ch1, params, mom, lr=lr, momentum=mu, first_step=it == 0, step_ctr=step)
+            torch.cuda.synchronize()
+            assert x.error_flags() == 0, x.error_flags()
+            allin = [None] * world
+            dist.all_gather_object(allin, mine)
+            want = allin[0].clone()
+            for r in range(1, world):
+                want += allin[r]  # rank order 0..world-1, fp32
+            got = grads.cpu()
+            if not torch.equal(got, want):
+                bad = (got != want).nonzero().flatten()
+                raise AssertionError(f"call {it} (ch {ch1}): {bad.numel()} elements differ, first {bad[:4].tolist()}")
+            C.sgd(ref_p, want.to(dev), ref_m, lr, mu, 0.0, 0.0, False, False, it == 0, True, [])
+            torch.cuda.synchronize()
+            assert torch.equal(params, ref_p) and torch.equal(mom, ref_m), f"call {it}: fused SGD differs"
+        assert int(step.item()) == ncalls, int(step.item())
+        assert pairs_run == {1, 2}
+        allp = [None] * world
+        dist.all_gather_object(allp, torch.cat([params.cpu(), mom.cpu()]))
+        assert all(torch.equal(a, allp[0]) for a in allp), "replicas differ"
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc()[-800:]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pair_launch_multirank_oracle(world):
+    """the default multi-GPU all-reduce launch with 2 and 3 real ranks on one
+    GPU, 50 calls each (both stage parities of every channel), bitwise against the rank-order
+    host sum and the SGD kernel, replicas identical, the step counter advanced once per call."""
+    from ddp_amd.parallel import free_port
+
+    res = _run(_pair_worker, world, free_port(), 50)
+    assert all(r[1] == "ok" for r in res), res
 
 
 def _calib_worker(rank, world, port, q, out):
