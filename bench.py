@@ -59,7 +59,11 @@ def kernels_per_step(eng):
     if not eng.eng.last_level3:
         return None
     nar = 0 if eng.eng.last_xar or eng.comm_kind == "none" else 1 if eng.eng.last_pair else len(eng.ranges)
-    return (2 if eng.eng.last_fc_role else 3) + nar
+    k = (2 if eng.eng.last_fc_role else 3) + nar
+    gs, heads = eng.eng.graph_steps, eng.eng.graph_heads
+    if heads and gs:  # dist_mode 4 graph: every step head saves a launch (per-step average)
+        k = round(k - heads / gs, 3)
+    return k
 
 
 def graph_chunk(k: int, cap: int = 100) -> int:

@@ -172,7 +172,11 @@ __device__ __forceinline__ Conv1Group conv1_group_load_sc1(const float* w1, cons
   }
   return r;
 }
+template <int SLEEP = 2>
 __device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, int code);
+// the merged forward's waits: hundreds of blocks poll one counter while the all-reduce they
+// wait for moves megabytes - poll ~10x less often than the conv backward's waits
+constexpr int MRG_SLEEP = 16;
 
 template <typename T, int PXT, int NW, bool RELU, int NOF, bool A1X, int GH, int GW, int GCI, int GCO,
           bool DZ = false, int OCC = 1, bool MRG = false>
@@ -247,7 +251,8 @@ __device__ __forceinline__ void fwd_body(
     }
     if constexpr (MRG) {
       // the step's images are staged; now this step's conv parameters must be final
-      wait_count(mg.conv_done, mg.conv_want, mg.err, MRG_ERR);
+      wait_count<MRG_SLEEP>(mg.conv_done, mg.conv_want, mg.err, MRG_ERR);
+      DDP_STAMP(STAMP_K_HEAD, 5);
       cg = conv1_group_load_sc1(c1.w, c1.b, wave & 3);
       const __amdgpu_buffer_rsrc_t rw =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Wt), (short)0, 0x7fffffff, 0x00020000);
@@ -413,7 +418,10 @@ __device__ __forceinline__ void fwd_body(
   }
 
   DDP_STAMP(STAMP_K_CONV_FWD, 3);
-  if constexpr (MRG) wait_count(mg.fc_done, mg.fc_want, mg.err, MRG_ERR);  // the fc weight shadow is final
+  if constexpr (MRG) {  // the fc weight shadow is final
+    wait_count<MRG_SLEEP>(mg.fc_done, mg.fc_want, mg.err, MRG_ERR);
+    DDP_STAMP(STAMP_K_HEAD, 6);
+  }
   // epilogue: bias + ReLU + bf16 store (+ fc partial logits: per block and image,
   // layout [block][2][NOF], see FC_BLOCK_PARTIALS in launchers.h)
   float* s_fc = reinterpret_cast<float*>(smem + fwd_stage_lds(W, Cin, CH / 64, A1X, (int)sizeof(T)));
@@ -1315,6 +1323,7 @@ __device__ __forceinline__ void fc_role_chunk(const BwdFc& fcr, const float* s_d
 // the wait was stored write-through by its producers and is read with system-scope loads
 // (an agent-scope acquire is `buffer_inv sc1`, invalidating the XCD's L2 under the conv
 // roles sharing it).
+template <int SLEEP>
 __device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, int code) {
   __shared__ int s_ok;
   if (threadIdx.x < 64) {
@@ -1326,7 +1335,7 @@ __device__ __forceinline__ bool wait_count(const int* cnt, int want, int* err, i
         ok = false;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(SLEEP);
     }
     if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
   }
@@ -1634,7 +1643,11 @@ __global__ __launch_bounds__(256, 3) void step_head_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nx = x.nblk0 + x.nblk1;
   if ((int)blockIdx.x < nx) {
-    const int k = (int)blockIdx.x < x.nblk0 ? 0 : 1;
+    // the conv bucket's blocks FIRST (every forward block waits for them before its staging),
+    // then the fc bucket's; both at raised issue priority over the forward blocks beside them
+    const int k = (int)blockIdx.x < x.nblk1 ? 1 : 0;
+    const int rb = k == 1 ? (int)blockIdx.x : (int)blockIdx.x - x.nblk1;  // block within its channel
+    __builtin_amdgcn_s_setprio(2);
     unsigned* s_sh = reinterpret_cast<unsigned*>(smem);
     XgmiArgs* s_xa = reinterpret_cast<XgmiArgs*>(smem + 64);
     {  // the bucket's arguments into LDS (from global memory every field was re-loaded per store)
@@ -1643,10 +1656,9 @@ __global__ __launch_bounds__(256, 3) void step_head_kernel(
       for (int i = threadIdx.x; i < (int)(sizeof(XgmiArgs) / 4); i += 256) dst[i] = src[i];
     }
     __syncthreads();
-    DDP_STAMP(STAMP_K_XGMI, 0);
-    if (k == 0) xgmi_allreduce_body<true>(*s_xa, (int)blockIdx.x, x.nblk0, s_sh);
-    else xgmi_allreduce_body<true>(*s_xa, (int)blockIdx.x - x.nblk0, x.nblk1, s_sh);
-    DDP_STAMP(STAMP_K_XGMI, 7);
+    DDP_STAMP(STAMP_K_HEAD, 0);
+    xgmi_allreduce_body<true>(*s_xa, rb, k == 0 ? x.nblk0 : x.nblk1, s_sh, STAMP_K_HEAD);
+    DDP_STAMP(STAMP_K_HEAD, 7);
     count_done(k == 0 ? done_fc : done_conv);  // drain (write-through) + one relaxed count
     return;
   }
@@ -1671,11 +1683,18 @@ static int step_head_occupancy(size_t lds) {
   return occ * cus;
 }
 
+int conv3x3_step_head_slots() {
+  return step_head_occupancy(std::max(conv3x3_fwd_lds(28, 32, 1, true, 2), (size_t)64 + sizeof(XgmiArgs)));
+}
+
 bool conv3x3_step_head_fits(int nx, int B) {
   if (B <= 0 || nx <= 0) return false;
   const long nf = ((long)B * 28 * 28 + 63) / 64;
-  const size_t lds = std::max(conv3x3_fwd_lds(28, 32, 1, true, 2), (size_t)64 + sizeof(XgmiArgs));
-  return (long)step_head_occupancy(lds) >= nx + nf;
+  const bool ok = (long)conv3x3_step_head_slots() >= nx + nf;
+  if (!ok && std::getenv("DDP_AMD_XAR_DEBUG"))
+    fprintf(stderr, "[ddp_amd] step head does not fit: %d resident slots < %ld blocks\n", conv3x3_step_head_slots(),
+            nx + nf);
+  return ok;
 }
 
 bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16_t* Wt, const float* bias,

@@ -421,5 +421,6 @@ bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16
                        bf16_t* Y, int B, const bf16_t* wfc, float* fc_part, const C1Src& c1, const FwdDz& dz,
                        int* err, hipStream_t s);
 bool conv3x3_step_head_fits(int nx, int B);
+int conv3x3_step_head_slots();  // resident blocks of the step-head kernel on this GPU
 
 }  // namespace ddp_amd

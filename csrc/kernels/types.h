@@ -70,7 +70,7 @@ struct SgdArgs {
 // diagnostic phase-stamp kernel ids / buffer geometry (common.h DDP_STAMP)
 enum { STAMP_K_CONV_FWD = 0, STAMP_K_FC_BWD = 1, STAMP_K_DGRAD = 2, STAMP_K_WGRAD = 3,
        STAMP_K_GRAD_REDUCE = 4, STAMP_K_SGD = 5, STAMP_K_XENT = 6, STAMP_K_CONV1 = 7,
-       STAMP_K_FWD_DZ = 8, STAMP_K_XGMI = 9, STAMP_K_COUNT = 10 };
+       STAMP_K_FWD_DZ = 8, STAMP_K_XGMI = 9, STAMP_K_HEAD = 10, STAMP_K_COUNT = 11 };
 constexpr int STAMP_SLOTS = 8, STAMP_KSTRIDE = 4096 * STAMP_SLOTS;
 
 }  // namespace ddp_amd

@@ -176,8 +176,10 @@ __device__ __forceinline__ void finish4(const XgmiArgs& a, long q, float4 v, lon
 // Every call of a channel must use the same nblk on every rank (the per-block sequence
 // counters, barrier flags and quad mapping are per block index).  s_epoch / s_fail: two
 // words of the block's LDS.  Returns with the block's stores drained.
+// skid: the phase-stamp kernel id (scripts/stamps.py; the dist_mode 4 step head stamps apart)
 template <bool WT = false>
-__device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, int nblk, unsigned* s_sh) {
+__device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, int nblk, unsigned* s_sh,
+                                                    int skid = STAMP_K_XGMI) {
   unsigned& s_epoch = s_sh[0];
   unsigned& s_fail = s_sh[1];
   const int N = a.world, r = a.rank;
@@ -223,9 +225,9 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
       st4_sys(mystage, q, v);  // the stage holds whole quads (zero-padded tail)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    DDP_STAMP(STAMP_K_XGMI, 1);
+    DDP_STAMP(skid, 1);
     xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_ONESHOT, blk);
-    DDP_STAMP(STAMP_K_XGMI, 2);
+    DDP_STAMP(skid, 2);
     if (!s_fail) {
       __amdgpu_buffer_rsrc_t src[XGMI_MAX_RANKS];
 #pragma unroll
@@ -267,9 +269,9 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  DDP_STAMP(STAMP_K_XGMI, 1);
+  DDP_STAMP(skid, 1);
   xgmi_barrier(a, 2u * e, &s_fail, XGMI_PHASE_B0, blk);  // B0
-  DDP_STAMP(STAMP_K_XGMI, 2);
+  DDP_STAMP(skid, 2);
   if (!s_fail) {
     // ---- RS: quads of my slice, fixed-order sum over ranks 0..N-1
     float* srcp[XGMI_MAX_RANKS];
@@ -314,7 +316,7 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
     (void)src;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  DDP_STAMP(STAMP_K_XGMI, 3);
+  DDP_STAMP(skid, 3);
   // ---- AG: quad q of every rank's reduced slice into my gradient buffer
   // the thread's quads q0, q0 + G, ... of every rank's reduced slice as (quad j, rank p)
   // items in order, XGMI_BATCH per batch: every load of a batch (reduced quads over xGMI,
@@ -340,7 +342,7 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
   };
   load_pm(0);
   xgmi_barrier(a, 2u * e + 1u, &s_fail, XGMI_PHASE_B1, blk);  // B1
-  DDP_STAMP(STAMP_K_XGMI, 4);
+  DDP_STAMP(skid, 4);
   if (!s_fail) {
     const long items = items_g;
     for (long i0 = 0; i0 < items; i0 += XGMI_BATCH) {

@@ -275,6 +275,7 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, u
                 b_.wfc_frag, b_.fc_part, NO, cfg_.pxt_fwd, cs_, pc1, l3 ? &dzo : nullptr);
   }
   if (parts & (PART_FWD | PART_HEAD)) last_head_ = head_used;
+  if (head_used && capturing_) graph_heads_ += 1;
   if (!(parts & (PART_BWD | PART_AR))) return;
   // ---- loss + fc backward (bucket 0)
   if (!f1)
@@ -828,6 +829,8 @@ void SimpleCNNEngine::capture(int nsteps) {
   if (cfg_.momentum != 0.f && !momentum_started_)
     throw std::runtime_error("engine: run one eager step before capturing (momentum init)");
   destroy_graph();
+  graph_heads_ = 0;
+  capturing_ = true;
   DDP_HIP_CHECK(hipStreamBeginCapture(cs_, hipStreamCaptureModeRelaxed));
   try {
     if (overlap_active()) {
@@ -840,11 +843,13 @@ void SimpleCNNEngine::capture(int nsteps) {
       for (int i = 0; i < nsteps; ++i) launch_step(cfg_.max_batch, cfg_.max_batch, false);
     }
   } catch (...) {
+    capturing_ = false;
     hipGraph_t g = nullptr;
     hipStreamEndCapture(cs_, &g);
     if (g) hipGraphDestroy(g);
     throw;
   }
+  capturing_ = false;
   DDP_HIP_CHECK(hipStreamEndCapture(cs_, &graph_));
   DDP_HIP_CHECK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
   // upload the exec's kernel-argument / node state now, on the engine stream, so its

@@ -335,6 +335,8 @@ class SimpleCNNEngine {
   bool last_pair() const { return last_pair_; }
   // ... and whether its forward shared a launch with the previous step's pair (dist_mode 4)
   bool last_head() const { return last_head_; }
+  // step-head launches (pair + next forward in one launch) in the captured graph
+  int graph_heads() const { return graph_heads_; }
   void set_momentum_started(bool v) { momentum_started_ = v; }
   // bucket all-reduces over the direct xGMI kernel instead of RCCL: channels[b] serves
   // bucket b; set before capturing a graph
@@ -390,6 +392,8 @@ class SimpleCNNEngine {
   bool last_xar_ = false;
   bool last_pair_ = false;
   bool last_head_ = false;
+  bool capturing_ = false;
+  int graph_heads_ = 0;  // step-head launches in the captured graph (dist_mode 4)
   bool xar_plan_ok_ = false;  // set_xgmi: the bucket plan fits the in-launch all-reduce
   bool pair_plan_ok_ = false;  // ... and the one-launch pair of bucket kernels (dist_mode 3)
   struct XarArgs {

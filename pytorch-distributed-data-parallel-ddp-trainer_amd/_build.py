@@ -16,9 +16,9 @@ Layout of the native sources (``<repo>/csrc``):
 * ``bindings.cpp``   - the only TU that includes ``torch/extension.h``; converts
   ``at::Tensor`` to raw pointers / streams and exposes everything via pybind11.
 
-Objects are rebuilt only when their source (or any header under ``csrc``) is
-newer than the object; the link step is skipped when the ``.so`` is newer than
-every object.
+Objects are rebuilt only when their source or a ``csrc`` header they include (their
+``-MD`` depfile) is newer than the object, or their command line changed; the link step
+is skipped when the ``.so`` is newer than every object.
 
 The binary is tied to its sources: every build embeds
 :func:`source_hash` - a SHA-256 over every file under ``csrc`` (relative path +
@@ -68,9 +68,21 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def _deps(obj: str):
+    """The csrc headers an object was built from (its ``-MD`` depfile), or None."""
+    try:
+        with open(obj + ".d") as f:
+            text = f.read().replace("\\\n", " ")
+    except OSError:
+        return None
+    files = text.split(":", 1)[1].split() if ":" in text else []
+    return [f for f in files if os.path.abspath(f).startswith(CSRC + os.sep)]
+
+
 def _needs(obj: str, src: str, hdr_mtime: float, cmd=None) -> bool:
-    """Rebuild when the object is missing, older than its source or any header, or was
-    built by a different command line (flags change: the ``.cmd`` sidecar differs)."""
+    """Rebuild when the object is missing, older than its source or any csrc header it
+    includes (its depfile; without one: any csrc header), or was built by a different command
+    line (flags change: the ``.cmd`` sidecar differs)."""
     if not os.path.exists(obj):
         return True
     if cmd is not None:
@@ -81,6 +93,9 @@ def _needs(obj: str, src: str, hdr_mtime: float, cmd=None) -> bool:
         except OSError:
             return True
     t = os.path.getmtime(obj)
+    deps = _deps(obj)
+    if deps is not None:
+        return any(not os.path.exists(d) or os.path.getmtime(d) > t for d in [src, *deps])
     return os.path.getmtime(src) > t or hdr_mtime > t
 
 
@@ -153,11 +168,11 @@ def _compile_cmds():
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(BUILD_DIR, "k_" + os.path.basename(src) + ".o")
         cmds.append((src, obj, [hipcc, f"--offload-arch={ARCH}", *common, *KERNEL_FLAGS.get(os.path.basename(src), []),
-                                *DEVICE_FLAGS, "-c", src, "-o", obj]))
+                                *DEVICE_FLAGS, "-MD", "-MF", obj + ".d", "-c", src, "-o", obj]))
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(BUILD_DIR, "r_" + os.path.basename(src) + ".o")
         # host-only TUs: still driven by hipcc so hip_runtime.h resolves, but no device code
-        cmds.append((src, obj, [hipcc, *common, "-x", "c++", "-c", src, "-o", obj]))
+        cmds.append((src, obj, [hipcc, *common, "-x", "c++", "-MD", "-MF", obj + ".d", "-c", src, "-o", obj]))
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(BUILD_DIR, "bindings.o")
     hsrc = _hash_source_file()
@@ -167,7 +182,7 @@ def _compile_cmds():
         hipcc, *common[:-2], "-x", "c++", "-I", CSRC, *BIND_FLAGS,
         f"-D_GLIBCXX_USE_CXX11_ABI={int(_cxx11_abi())}",
         "-I", tinc, "-I", os.path.join(tinc, "torch", "csrc", "api", "include"),
-        "-I", sysconfig.get_paths()["include"], "-w", "-c", bsrc, "-o", bobj]))
+        "-I", sysconfig.get_paths()["include"], "-w", "-MD", "-MF", bobj + ".d", "-c", bsrc, "-o", bobj]))
     return cmds
 
 

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 NAMES = {0: "conv3x3_fwd", 1: "fc_bwd", 2: "conv3x3_dgrad", 3: "conv3x3_wgrad",
-         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging", 8: "fwd-dZ2", 9: "xgmi"}
+         4: "grad_reduce", 5: "sgd", 6: "xent", 7: "dgrad-staging", 8: "fwd-dZ2", 9: "xgmi",
+         10: "step-head"}
 
 
 def main():
@@ -35,6 +36,12 @@ def main():
     ap.add_argument("--comm", default="xgmi", help="with --force_allreduce: xgmi | rccl")
     ap.add_argument("--dist_mode", type=int, default=None)
     ap.add_argument("--xgmi_blocks", action="store_true", help="print every xgmi block's stamps")
+    ap.add_argument("--head_split", default=None,
+                    help="dist_mode 4: 'a,b' - summarise the step head's blocks [0,a) (conv bucket), "
+                         "[a,b) (fc bucket) and [b,...) (forward waits) separately")
+    ap.add_argument("--min_block", type=int, default=0,
+                    help="ignore blocks below this index (dist_mode 4 --graph: the step head's forward "
+                         "blocks follow its all-reduce blocks; lower indices hold the graph's first forward)")
     a = ap.parse_args()
     from ddp_amd import native
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -83,13 +90,30 @@ def main():
     st = buf.view(C.STAMP_K_COUNT, 4096, 8).cpu().double()
     t0 = None
     rows = []
+    if a.head_split:
+        ca, cb = (int(v) for v in a.head_split.split(","))
+        hs = st[10]
+        t00 = hs[:cb, 0][hs[:cb, 0] > 0].min()
+        for name, lo, hi in (("head conv AR", 0, ca), ("head fc AR", ca, cb), ("head fwd", cb, 4096)):
+            blk = hs[lo:hi]
+            blk = blk[(blk > 0).any(dim=1)]
+            parts = []
+            for slot in range(8):
+                v = blk[:, slot]
+                v = v[v > 0]
+                if v.numel():
+                    d = (v - t00) / 100.0
+                    parts.append(f"s{slot} med {d.median().item():6.2f} max {d.max().item():6.2f}")
+            print(f"{name:14s} blocks {blk.shape[0]:4d} | " + " ".join(parts))
     for k in range(C.STAMP_K_COUNT):
         s = st[k]
-        live = s[:, 0] > 0
+        if a.min_block and NAMES.get(k) in ("conv3x3_fwd", "fwd-dZ2"):
+            s = s[a.min_block:]
+        live = (s > 0).any(dim=1)  # (step-head forward blocks stamp only their two waits)
         if not live.any():
             continue
         s = s[live]
-        kstart = s[:, 0].min()
+        kstart = s[:, 0][s[:, 0] > 0].min() if (s[:, 0] > 0).any() else s[s > 0].min()
         t0 = kstart if t0 is None else min(t0, kstart)
         rows.append((kstart, k, s))
     rows.sort(key=lambda r: r[0])
@@ -110,7 +134,7 @@ def main():
                 print(f"    xgmi block {bi:3d}: {vals}")
         # per-block durations (first -> last stamp)
         last = s.max(dim=1).values
-        dur = (last - s[:, 0]) / 100.0
+        dur = ((last - s[:, 0]) / 100.0)[s[:, 0] > 0]
         line.append(f" | blk dur med {dur.median().item():.2f} max {dur.max().item():.2f}")
         print("".join(line))
 

@@ -539,7 +539,8 @@ def test_dist_chains_bitwise_world1(plane, dtype, monkeypatch):
     kernels per step, engine.cpp make_xar; its grid does not fit the GPU at once, so it needs
     the in-order-dispatch opt-in DDP_AMD_L3_INORDER=1 - without it the bucket kernels run,
     "inlaunch_fb"), 1 - fc_bwd + the fc bucket forked beside the conv backward, 0 - the
-    round-4 serial order."""
+    round-4 serial order, 4 - the step head (bf16: the pair launch of step k also runs step
+    k + 1's forward, conv3x3.hip step_head_kernel; fp32: mode 3's chain)."""
     import torch.distributed as dist
 
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -559,8 +560,11 @@ def test_dist_chains_bitwise_world1(plane, dtype, monkeypatch):
         imgs, labels = synthetic_mnist(1000)  # 31 full batches + a ragged one of 8
         data = DeviceMNIST(imgs, labels, dev)
         out = {}
+        # (dist_mode 4 runs the 256-thread forward, pxt_fwd 1, whose per-block partial logits
+        # group the fc sum differently: it is compared with the comm-free chain at pxt 1)
         modes = (("local", False, 3), ("serial", True, 0), ("fork", True, 1), ("inlaunch", True, 2),
-                 ("inlaunch_fb", True, 2), ("pair", True, 3))
+                 ("inlaunch_fb", True, 2), ("pair", True, 3)) + \
+            ((("local_pf1", False, 3),) if dtype == "bf16" else ()) + (("head", True, 4),)
         for tag, force, mode in modes:
             if tag == "inlaunch":
                 monkeypatch.setenv("DDP_AMD_L3_INORDER", "1")
@@ -571,7 +575,7 @@ def test_dist_chains_bitwise_world1(plane, dtype, monkeypatch):
             e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), data, 32, 1, 0, comm,
                                      EngineOptions(graph_steps=5, force_allreduce=force, comm=plane,
                                                    dist_mode=mode, plan_world=8 if force else None,
-                                                   dtype=dtype))
+                                                   dtype=dtype, pxt_fwd=1 if tag == "local_pf1" else 2))
             if force:
                 assert e.comm_kind.startswith(plane), e.comm_kind
                 assert len(e.ranges) == 2  # the 8-rank plan: [fc], [conv]
@@ -583,11 +587,21 @@ def test_dist_chains_bitwise_world1(plane, dtype, monkeypatch):
             assert e.eng.sync_error == 0 and e.eng.last_level3
             if tag != "inlaunch_fb":  # (in-launch iff its whole grid fits this GPU at once)
                 assert e.eng.last_xar == (tag == "inlaunch" and plane == "xgmi"), tag
-            assert e.eng.last_pair == (tag == "pair" and plane == "xgmi"), tag
+            assert e.eng.last_pair == (tag in ("pair", "head") and plane == "xgmi"), tag
+            # dist_mode 4 (bf16): the captured graph's pair launches carried the next forward
+            head = tag == "head" and plane == "xgmi" and dtype == "bf16"
+            assert e.eng.overlap_active() == head, tag
+            e.run_steps(5)  # one whole graph replay (dist_mode 4: its pair launches carry forwards)
+            e.synchronize()
+            # a 5-step graph: 4 step heads ([fwd 0] [bwd 0] [pair 0 + fwd 1] ... [bwd 4] [pair 4])
+            assert e.eng.graph_heads == (4 if head else 0) and e.eng.sync_error == 0, (tag, e.eng.graph_heads)
             out[tag] = (e.fs.params.clone(), e.opt.momentum_buffer.clone())
-        for tag, _, _ in modes[1:]:
-            assert torch.equal(out[tag][0], out["local"][0]), tag
-            assert torch.equal(out[tag][1], out["local"][1]), tag
+        for tag, _, mode in modes[1:]:
+            if tag == "local_pf1":
+                continue
+            ref = "local_pf1" if (mode == 4 and dtype == "bf16") else "local"
+            assert torch.equal(out[tag][0], out[ref][0]), tag
+            assert torch.equal(out[tag][1], out[ref][1]), tag
     finally:
         dist.destroy_process_group()
 
