@@ -151,6 +151,7 @@ void scale_copy(float* dst, const float* src, long n, float scale, hipStream_t s
 DDP_STAMPS_SETTER(stamps_set_optim)
 void stamps_set_conv1(void*);
 void stamps_set_conv3x3(void*);
+void stamps_set_conv3x3_bwd(void*);
 void stamps_set_linear(void*);
 void stamps_set_xent(void*);
 void stamps_set_allreduce(void*);
@@ -158,6 +159,7 @@ void stamps_set(void* p) {
   stamps_set_optim(p);
   stamps_set_conv1(p);
   stamps_set_conv3x3(p);
+  stamps_set_conv3x3_bwd(p);
   stamps_set_linear(p);
   stamps_set_xent(p);
   stamps_set_allreduce(p);

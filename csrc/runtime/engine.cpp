@@ -245,6 +245,15 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, u
   c1b.w = c1.w;
   c1b.b = c1.b;
 
+  // every bf16 shadow the chain reads; a bucket's fused SGD refreshes the ones inside its
+  // range (level 3 never reads the plain fc shadow: plain_stale_ re-derives it on a switch)
+  const long n_w2s = (long)C2 * 9 * C1;
+  ShadowSet sh_all{};
+  sh_all.r[0] = ShadowRegion{b_.off_w2, n_w2s, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
+  sh_all.r[1] = ShadowRegion{b_.off_w2, n_w2s, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
+  sh_all.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
+  sh_all.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
+  sh_all.count = l3 ? 3 : 4;
   // ---- forward (PART_HEAD: in one launch with the previous step's bucket all-reduces)
   const SgdArgs sa{cfg_.lr, cfg_.momentum, cfg_.dampening, cfg_.weight_decay, cfg_.nesterov,
                    cfg_.maximize, first_momentum_step ? 1 : 0, 1};
@@ -254,13 +263,8 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, u
     // the previous step's pair (its fused SGD writes this step's parameters write-through)
     // + this step's forward; two launches (same bits) when the merged grid does not fit
     if (first_momentum_step) throw std::runtime_error("engine: the step head runs the steady-state SGD only");
-    ShadowSet sh3{};
-    sh3.r[0] = ShadowRegion{b_.off_w2, (long)C2 * 9 * C1, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
-    sh3.r[1] = ShadowRegion{b_.off_w2, (long)C2 * 9 * C1, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
-    sh3.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
-    sh3.count = 3;
     BwdXar hx;
-    if (!make_xar(hx, sa, M, sh3)) throw std::runtime_error("engine: the step head needs the pair plan");
+    if (!make_xar(hx, sa, M, sh_all)) throw std::runtime_error("engine: the step head needs the pair plan");
     hx.step_ctr = nullptr;  // (advanced by the fc role)
     int* mc = b_.sync_flags + L3_IMG_OFF + (long)FWD_DZ_CNT_STRIDE * cfg_.max_batch;
     head_used = cfg_.pxt_fwd == 1 && B == cfg_.max_batch &&
@@ -353,14 +357,6 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, u
              (long)HW * C2, NO, /*mask=*/true, s, ex);
     };
   }
-  // every bf16 shadow the chain reads; a bucket's fused SGD refreshes the ones inside its
-  // range (level 3 never reads the plain fc shadow: plain_stale_ re-derives it on a switch)
-  ShadowSet sh_all{};
-  sh_all.r[0] = ShadowRegion{b_.off_w2, n_w2, b_.w2_bf16, SHADOW_BF16, 0, 0, 0};
-  sh_all.r[1] = ShadowRegion{b_.off_w2, n_w2, b_.w2t_bf16, SHADOW_BF16_TAPT, C2, 9, C1};
-  sh_all.r[2] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_frag, SHADOW_BF16_FCFRAG, HW, C2, 0};
-  sh_all.r[3] = ShadowRegion{b_.off_wfc, n_fc, b_.wfc_bf16, SHADOW_BF16, 0, 0, 0};
-  sh_all.count = l3 ? 3 : 4;
   // ---- conv backward (bucket 1) + the slab reduction (fused into it, or grad_reduce)
   SlabSet ss{};
   const int wblk = conv3x3_wgrad_blocks(B, H, cfg_.wgrad_rows);

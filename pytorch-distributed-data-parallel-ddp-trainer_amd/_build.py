@@ -103,7 +103,7 @@ def _needs(obj: str, src: str, hdr_mtime: float, cmd=None) -> bool:
 # reductions' adds into v_pk_add_f32, which cannot take a DPP operand, so every step became
 # v_mov 0 + v_mov_dpp + add (the conv1 weight-gradient reduction of the dgrad role: 750 ->
 # 400 VALU instructions with the adds folded into v_add_f32_dpp)
-KERNEL_FLAGS = {"conv3x3.hip": ["-fno-slp-vectorize"]}
+KERNEL_FLAGS = {"conv3x3.hip": ["-fno-slp-vectorize"], "conv3x3_bwd.hip": ["-fno-slp-vectorize"]}
 COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__"]
 DEVICE_FLAGS = ["-munsafe-fp-atomics"]
 BIND_FLAGS = ["-O2", "-DUSE_ROCM", "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H"]

@@ -456,13 +456,28 @@ class FusedSimpleCNNEngine:
             e.refresh_shadows()
             torch.cuda.synchronize()
 
-        def run(e):
+        # dist_mode 4: the step head (a pair launch carrying the next forward) exists only in a
+        # captured graph, so the production chain runs its steps as one (momentum-init step
+        # eager) - with at least one step head in it
+        head = bool(self.eng.overlap_active())
+        if head:
+            nsteps = max(nsteps, 3)
+
+        def run(e, graph=False):
             """nsteps on engine e from the snapshot -> (params, momentum, losses) or an error."""
             self.start_epoch(0)
             restore(e)
             try:
-                for _ in range(nsteps):
-                    e.step(B, B)
+                if graph:
+                    left = nsteps
+                    if self.opt.momentum_buffer is not None and not started:
+                        e.step(B, B)  # (the momentum buffer's initialising step is eager)
+                        left -= 1
+                    e.capture(left)
+                    e.replay()
+                else:
+                    for _ in range(nsteps):
+                        e.step(B, B)
                 e.synchronize()
             except RuntimeError as ex:  # an in-launch wait timed out
                 return None, f"in-launch wait: {ex}"
@@ -476,7 +491,11 @@ class FusedSimpleCNNEngine:
         ref = self.C.SimpleCNNEngine(ref_cfg, t, self.offs, self.comm)
         if self.xgmi is not None:
             ref.set_xgmi(self.xgmi, self.xch)
-        got, err_p = run(self.eng)
+        got, err_p = run(self.eng, graph=head)
+        heads_checked = int(self.eng.graph_heads) if head else 0
+        if head:
+            self.eng.destroy_graph()
+            self._captured = 0
         if got is not None and _corrupt_rank == self.rank:  # test hook: a one-ulp disagreement
             got[0][0] = torch.nextafter(got[0][0], torch.tensor(float("inf"), device=got[0].device))
         pair_ran = bool(self.eng.last_pair)
@@ -520,7 +539,8 @@ class FusedSimpleCNNEngine:
         torch.cuda.synchronize()
         self.chain_check = {"ran": True, "steps": nsteps, "identical_here": same, "identical_all": ok_all,
                             "xgmi_ok_all": x_ok_all, "oracle_ok_all": o_ok_all, "oracle": oracle,
-                            "pair": pair_ran, "kept_production": action == "keep",
+                            "pair": pair_ran, "step_heads_checked": heads_checked,
+                            "kept_production": action == "keep",
                             "error": err_p or err_r}
         return self.chain_check["kept_production"]
 

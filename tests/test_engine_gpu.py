@@ -444,6 +444,35 @@ def test_verify_chain_world1_forced(corrupt, stall):
         dist.destroy_process_group()
 
 
+def test_verify_chain_covers_the_step_head():
+    """dist_mode 4's step head exists only in captured graphs: the start-up check runs the
+    production chain's steps as a graph (momentum-init step eager), so at least one step head
+    is compared with the conservative chain before training commits to it."""
+    import torch.distributed as dist
+
+    from ddp_amd.data import DeviceMNIST, synthetic_mnist
+    from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+    from ddp_amd.models import SimpleCNN
+    from ddp_amd.ops import FusedSGD
+
+    dist.init_process_group("gloo", rank=0, world_size=1, store=dist.HashStore())
+    try:
+        imgs, labels = synthetic_mnist(2048)
+        torch.manual_seed(0)
+        m = SimpleCNN().to(dev)
+        e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), DeviceMNIST(imgs, labels, dev), 32, 1, 0,
+                                 None, EngineOptions(graph_steps=5, force_allreduce=True, comm="xgmi", dist_mode=4))
+        e.refresh()
+        assert e.eng.overlap_active()
+        assert e.verify_chain(), e.chain_check
+        assert e.chain_check["step_heads_checked"] >= 1 and e.chain_check["oracle"]["mismatches"] == 0, e.chain_check
+        e.run_steps(10)
+        e.synchronize()
+        assert e.eng.graph_heads == 4 and e.eng.sync_error == 0
+    finally:
+        dist.destroy_process_group()
+
+
 def test_verify_chain_oracle_downgrades_to_rccl():
     """a one-ulp error in the xGMI-reduced gradient (injected into the bucket
     the production chain reduced) is caught by the host oracle - not by the conservative

@@ -135,7 +135,8 @@ def test_replica_digest_detects_divergence():
 # checked.
 HOT_KERNELS = {
     "k_allreduce.hip.o": ("xgmi_allreduce_kernel", "xgmi_allreduce_pair_kernel"),
-    "k_conv3x3.hip.o": ("conv3x3_bwd_kernel", "conv3x3_fwd", "fwd_dz"),
+    "k_conv3x3.hip.o": ("conv3x3_fwd", "step_head_kernel"),
+    "k_conv3x3_bwd.hip.o": ("conv3x3_bwd_kernel",),
     "k_linear.hip.o": ("fc_bwd",),
     "k_optim.hip.o": ("sgd_kernel", "grad_reduce"),
 }
