@@ -35,7 +35,7 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "kernels/conv3x3_body.h"
+#include "kernels/conv3x3_fwd.h"
 
 namespace ddp_amd {
 

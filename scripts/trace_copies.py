@@ -7,8 +7,10 @@ step), takes the last n steps (steady state: graph replays) and lists, per step,
 HIP runtime blit kernel (``__amd_rocclr_copyBuffer*`` / ``__amd_rocclr_fillBuffer*``) with
 its grid size (threads; the runtime's blit kernels move 16 B per thread in the aligned
 path, so grid x 16 ~ bytes) and duration, plus their share of the step's kernel time.
-VERDICT r5 #4: attribute the ResNet-18 step's copies and fills.
+VERDICT r5 #4: attribute the ResNet-18 step's copies and fills.  Then the per-step kernel
+time by kernel family over the same steps, and the BatchNorm share (kernels named bn_*).
 """
+import collections
 import csv
 import glob
 import os
@@ -50,6 +52,18 @@ def main(d, marker="sgd_kernel", n=10):
                  if r[2].startswith("__amd_rocclr"))
     print(f"blit kernels in the whole trace: {len(allb)}; in the last {n} steps: {inside} "
           f"(the rest: set-up, data generation, warm-up / capture)")
+    fam, cnt, tot = collections.Counter(), collections.Counter(), 0
+    for j in range(len(ends) - n, len(ends)):
+        for r in rows[ends[j - 1] + 1:ends[j] + 1]:
+            k = r[2].split("(")[0].split("<")[0].replace("void ", "").replace("ddp_amd::", "")
+            fam[k] += r[1] - r[0]
+            cnt[k] += 1
+            tot += r[1] - r[0]
+    bn = sum(v for k, v in fam.items() if k.startswith("bn_"))
+    print(f"\n| kernel | launches/step | us/step | share |\n|---|---|---|---|")
+    for k, v in fam.most_common():
+        print(f"| {k} | {cnt[k] / n:.1f} | {v / n / 1000.0:.1f} | {100.0 * v / tot:.1f} % |")
+    print(f"\nkernel time per step {tot / n / 1000.0:.1f} us; BatchNorm (bn_*) {100.0 * bn / tot:.1f} %")
 
 
 if __name__ == "__main__":
