@@ -58,7 +58,7 @@ bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt, int es) {
 // Step k's two bucket all-reduces (+ fused SGD, stored write-through) and step k + 1's bf16
 // level-3 forward (256-thread blocks, pxt 1) in ONE launch: blocks [0, nblk1) all-reduce the
 // conv bucket, the next nblk0 the fc bucket (xgmi_allreduce_pair's roles), the rest are
-// forward blocks (conv3x3_fwd_kernel<MRG>), which stage their images while the all-reduce runs
+// forward blocks (fwd_body<MRG>), which stage their images while the all-reduce runs
 // and wait for each bucket's blocks only where they first read its parameters.  The forward
 // needs the conv bucket at its staging and the fc bucket only at its fc epilogue, so the
 // fc bucket's 2 MB all-gather overlaps the staging, the conv1 recompute and the MFMA loop
@@ -67,10 +67,23 @@ bool conv3x3_fwd_dz_fits(int B, int H, int W, int pxt, int es) {
 // grid to be resident at once (hipOccupancy of this kernel x CUs >= grid), so no block waits
 // for an undispatched one; the all-reduce blocks wait only for their peers' same blocks.
 // bf16, pxt 1 (256-thread blocks), level 3, three blocks per CU (next to the role blocks)
-static auto step_head_kernel() { return conv3x3_fwd_kernel<bf16_t, 1, 4, true, 10, true, 28, 28, 32, 64, true, 3, true>; }
+template <typename T>
+__global__ __launch_bounds__(256, 3) void step_head_kernel(
+    const T* __restrict__ Wt, const float* __restrict__ bias, T* __restrict__ Y, int B, const T* __restrict__ wfc,
+    float* __restrict__ fc_part, C1Src c1, FwdDz dzo, FwdMerge mg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nx = mg.nblk0 + mg.nblk1;
+  if ((int)blockIdx.x < nx) {
+    merge_allreduce_role(mg, smem);
+    return;
+  }
+  fwd_body<T, 1, 4, true, 10, true, 28, 28, 32, 64, true, 2, true>(
+      (int)blockIdx.x - nx, 0, static_cast<const T*>(nullptr), Wt, bias, Y, B, 28, 28, 32, 64, wfc, fc_part, c1,
+      dzo, mg);
+}
 
 static int step_head_occupancy(size_t lds) {
-  auto k = step_head_kernel();
+  auto k = step_head_kernel<bf16_t>;
   lds_optin(k, lds);
   int dev = 0, cus = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -111,10 +124,9 @@ bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16
   mg.fc_done = done_fc;
   mg.conv_done = done_conv;
   mg.err = err;
-  auto k = step_head_kernel();
+  auto k = step_head_kernel<bf16_t>;
   lds_optin(k, lds);
-  hipLaunchKernelGGL(k, dim3((unsigned)(nx + nf)), dim3(256), lds, s, static_cast<const bf16_t*>(nullptr), Wt, bias,
-                     Y, B, 28, 28, 32, 64, wfc, fc_part, c1, dz, mg);
+  hipLaunchKernelGGL(k, dim3((unsigned)(nx + nf)), dim3(256), lds, s, Wt, bias, Y, B, wfc, fc_part, c1, dz, mg);
   return true;
 }
 
@@ -140,13 +152,13 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
       if (pxt == 2 && fwd_dz_occ2(grid.x)) {
         auto k = fwd_dz_kernel<T, 2, 2>();
         lds_optin(k, lds);
-        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo, FwdMerge());
+        hipLaunchKernelGGL(k, grid, dim3(512), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo);
         return;
       }
     }
     auto k = pxt == 2 ? fwd_dz_kernel<T, 2>() : fwd_dz_kernel<T, 1>();
     lds_optin(k, lds);
-    hipLaunchKernelGGL(k, grid, dim3(256 * pxt), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo, FwdMerge());
+    hipLaunchKernelGGL(k, grid, dim3(256 * pxt), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc, fc_part, cs, dzo);
     return;
   }
   // one 16-pixel tile per wave: pxt 2 -> 8 waves (2 per SIMD), pxt 1 -> 4 waves
@@ -156,12 +168,12 @@ static void fwd_launch(const T* X, const T* Wt, const float* bias, T* Y, int B, 
       auto k = conv3x3_fwd_kernel<T, 1, 4 * PX, RL, NF, AX, 28, 28, 32, 64>;                        \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, grid, dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,  \
-                         fc_part, cs, dzo, FwdMerge());                                                         \
+                         fc_part, cs, dzo);                                                         \
     } else {                                                                                        \
       auto k = conv3x3_fwd_kernel<T, 1, 4 * PX, RL, NF, AX, 0, 0, 0, 0>;                            \
       lds_optin(k, lds);                                                                            \
       hipLaunchKernelGGL(k, grid, dim3(256 * PX), lds, s, X, Wt, bias, Y, B, H, W, Cin, Cout, wfc,  \
-                         fc_part, cs, dzo, FwdMerge());                                                         \
+                         fc_part, cs, dzo);                                                         \
     }                                                                                               \
   } while (0)
   if (pxt == 2) {
