@@ -587,7 +587,7 @@ def main():
                        "engine": "fused hipGraph" if not args.no_graph else "fused eager",
                        "graph_steps": k, "graph_head": getattr(args, "graph_head_used", 0), "fuse_level": eo.fuse_level, "level3": level3,
                        "kernels_per_step": kps,
-                       "tiling": {"pxt_fwd": eo.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
+                       "tiling": {"pxt_fwd": eng.opts.pxt_fwd, "pxt_dgrad": eo.pxt_dgrad,
                                   "wgrad_rows": eng.wgrad_rows, "store_a1": eng.store_a1,
                                   "wgrad_split": eo.wgrad_split},
                        "params_finite": finite,

@@ -45,7 +45,12 @@ BF16 = torch.bfloat16
 class EngineOptions:
     graph_steps: int = 100     # steps per captured graph (one loss readback per chunk)
     use_graph: bool = True
-    pxt_fwd: int = 2
+    # forward pixel tiles per wave: 1 = 256-thread blocks, 2 = 512-thread blocks.  None: 1 for
+    # bf16 when its level-3 grid fits the GPU at once (B <= ~41: the step head's forward, and
+    # equal in-call / +1 % driver-shaped at B = 32, profiles/r5_pxt_fwd), else 2 (bf16 B = 64:
+    # the OCC 2 forward; exact fp32).  The two group the fc partial logits differently, so
+    # chains compared bit for bit must run the same value.
+    pxt_fwd: int | None = None
     pxt_dgrad: int = 2
     wgrad_rows: int | None = None
     bucket_cap_mb: float = 25.0
@@ -116,10 +121,13 @@ class EngineOptions:
     # XAR); 1 = fc_bwd + the fc buckets' all-reduces on a graph branch forked after the
     # forward (schedule_backward); 3 = one stream: the fc role inside the conv backward, the
     # bucket kernels behind it (no cross-stream edge); 0 = the round-4 serial order;
-    # 4 = the step head (bf16, xGMI; forces pxt_fwd 1): mode 3's chain, but in a captured graph
-    # step k's bucket-pair launch also runs step k + 1's forward (2 launches per step instead
-    # of 3; conv3x3.hip step_head_kernel) - same bits as mode 3
-    dist_mode: int = 3
+    # 4 = the step head (bf16, xGMI; forces pxt_fwd 1 when the step all-reduces): mode 3's
+    # chain, but in a captured graph step k's bucket-pair launch also runs step k + 1's
+    # forward (2 launches per step instead of 3; conv3x3.hip step_head_kernel) - same bits as
+    # mode 3 at pxt 1.  The default (round 6: forced world 1 716-724k vs mode 3 692-700k
+    # img/s, profiles/r6_dist); fp32, the RCCL plane and a head grid that does not fit the
+    # GPU run mode 3's launches.  bench.py times the placements on the node at N > 1.
+    dist_mode: int = 4
     # dist_mode 2: the most blocks of a bucket's xGMI channel (its role blocks wait at the
     # head of the conv backward grid; the engine takes the in-launch path while the channels'
     # blocks total <= 192).  Forced world 1: 40 -> 479k, 96 -> 535k, 128 -> 525k, 173 -> 499k
@@ -240,10 +248,13 @@ class FusedSimpleCNNEngine:
                  rank: int, comm=None, opts: EngineOptions | None = None, seed: int = 0):
         self.C = native.require()
         self.opts = dataclasses.replace(opts) if opts is not None else EngineOptions()
-        if self.opts.dist_mode == 4 and self.opts.dtype == "bf16":
-            self.opts.pxt_fwd = 1  # the step head runs the 256-thread forward in the all-reduce's blocks
         self.model, self.opt, self.data = model, optimizer, data
         self.B = int(batch_size)
+        pf1 = self.opts.dtype == "bf16" and bool(self.C.conv3x3_fwd_dz_fits(self.B, 28, 28, 1))
+        if self.opts.pxt_fwd is None:
+            self.opts.pxt_fwd = 1 if pf1 else 2
+        if self.opts.dist_mode == 4 and pf1 and (world_size > 1 or self.opts.force_allreduce):
+            self.opts.pxt_fwd = 1  # the step head runs the 256-thread forward in the all-reduce's blocks
         self.world_size, self.rank = world_size, rank
         self.fs = fs = flat_space(model)
         dev = fs.params.device
