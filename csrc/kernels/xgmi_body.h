@@ -188,6 +188,17 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
   // (the host raises on the error word; a broken run must not cost timeouts per step)
   const bool failed_before = __hip_atomic_load(my + XGMI_ERR_OFF, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+  const long q0 = (long)blk * XGMI_THREADS + threadIdx.x;
+  // one-shot: this thread's first quad of the local bucket, requested before the call
+  // counter's round trip (only the stage store needs the counter's parity) - the two
+  // latencies overlap instead of adding up on the conv bucket's path into the step head
+  float4 first = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool first_ok = a.oneshot && q0 < a.n / 4;
+  if (first_ok) {
+    const float* mine = a.data[r] + a.off;
+    first = make_float4(ld_sys(mine + 4 * q0), ld_sys(mine + 4 * q0 + 1), ld_sys(mine + 4 * q0 + 2),
+                        ld_sys(mine + 4 * q0 + 3));
+  }
   if (threadIdx.x == 0) {
     // per-block call counter (only this block of this rank touches it); every call of a
     // channel uses the same grid, so the counters of all blocks stay equal
@@ -199,7 +210,6 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
   __syncthreads();
   const unsigned e = s_epoch;
   const long G = (long)nblk * XGMI_THREADS;     // quads per grid stride
-  const long q0 = (long)blk * XGMI_THREADS + threadIdx.x;
 
   if (a.oneshot) {
     // ---- publish my whole bucket, one barrier, sum every rank's copy in rank order
@@ -213,7 +223,9 @@ __device__ __forceinline__ void xgmi_allreduce_body(const XgmiArgs& a, int blk, 
     for (long q = q0; q < nq; q += G) {
       float4 v;
       const float ps = a.prescale;
-      if (q < fq) {
+      if (q == q0 && first_ok) {
+        v = make_float4(first.x * ps, first.y * ps, first.z * ps, first.w * ps);
+      } else if (q < fq) {
         v = make_float4(ld_sys(mine + 4 * q) * ps, ld_sys(mine + 4 * q + 1) * ps, ld_sys(mine + 4 * q + 2) * ps,
                         ld_sys(mine + 4 * q + 3) * ps);
       } else {

@@ -263,6 +263,19 @@ class _AvgPool(torch.autograd.Function):
         return dx
 
 
+_ONES: dict = {}
+
+
+def _ones(n: int, device) -> torch.Tensor:
+    """A persistent all-ones fp32 vector (the bias gradient's 1^T operand): a fresh
+    ``torch.ones`` was a fill kernel inside every captured ResNet step (profiles/r6_resnet)."""
+    key = (n, str(device))
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones(n, device=device)
+    return t
+
+
 class _LinearHead(torch.autograd.Function):
     """fp32 classifier head ([B,512] x [512,classes]) on the in-tree GEMM (``sgemm``): the
     forward with the bias folded in; the backward as dx = dl.W, dW += dl^T.x and
@@ -300,7 +313,7 @@ class _LinearHead(torch.autograd.Function):
             C.sgemm(N, K, B, dl, 1, N, x, K, 1, rw, None, 1.0)
         rb = None
         if b is not None:
-            ones = torch.ones(B, device=dl.device)
+            ones = _ones(B, dl.device)
             gb = direct_grad.grad_dst(b)
             if gb is not None:
                 C.sgemm(1, N, B, ones, 0, 1, dl, N, 1, gb, None, 1.0, True)    # db += 1^T . dl
