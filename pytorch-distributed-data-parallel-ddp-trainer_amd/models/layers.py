@@ -317,9 +317,22 @@ class FlatSpace:
                 g.copy_(p.grad)
                 p.grad = g
 
-    def zero_grad(self):
+    def zero_grad(self, lazy: bool = False):
+        """Zero every gradient.  ``lazy`` (FusedSGD): skip the memset when every parameter's
+        gradient was written by a direct producer last step (ops/direct_grad.py lazy_zero)."""
+        from ..ops import direct_grad
+
+        if lazy:
+            self.reattach_grads()
+            if direct_grad.lazy_zero(p for p, _ in self._pairs):
+                return
+            self.grads.zero_()
+            return
         self.grads.zero_()
         self.reattach_grads()
+        for p, _ in self._pairs:  # (zeroed for real: nothing fresh, nothing written yet)
+            direct_grad._fresh.discard(p)
+            direct_grad._written.discard(p)
 
 
 class BufferSpace:

@@ -184,8 +184,13 @@ class _ConvBNAct(torch.autograd.Function):
         # BatchNorm backward; dgamma / dbeta straight into the parameter gradients if allowed
         gg, gb = direct_grad.grad_dst(gamma), direct_grad.grad_dst(beta)
         direct_bn = gg is not None and gb is not None
+        acc_bn = False
         if direct_bn:
             dgamma, dbeta = gg, gb
+            ag, ab = direct_grad.accumulate(gamma), direct_grad.accumulate(beta)
+            if ag != ab:  # (one of the pair fresh: clear it, then both add)
+                (dbeta if ag else dgamma).zero_()
+            acc_bn = ag or ab
         else:
             dgamma, dbeta = torch.empty(Cout, device=dev), torch.empty(Cout, device=dev)
         ws = torch.empty(C.bn_bwd_rows(P, Cout), 2, Cout, device=dev)
@@ -194,7 +199,7 @@ class _ConvBNAct(torch.autograd.Function):
         dres = torch.empty_like(y) if has_res else None
         mask_beta = beta.detach() if (relu and out is None) else None
         C.bn_bwd(dout, out if relu else None, y, mean, invstd, gamma.detach(), float(P), ws, sums,
-                 dgamma, dbeta, direct_bn, dy, dres, _take_stash(ctx), mask_beta)
+                 dgamma, dbeta, acc_bn, dy, dres, _take_stash(ctx), mask_beta)
         # data gradient (the stem's input is the image: none)
         dx = None
         if ctx.needs_input_grad[0] and not stem:
@@ -204,16 +209,17 @@ class _ConvBNAct(torch.autograd.Function):
             C.conv_gemm_dgrad(dy, wb, None, dx, KH, KW, stride, pad, part)
         # weight gradient
         gw = direct_grad.grad_dst(w)
+        acc_w = gw is not None and direct_grad.accumulate(w)
         ppc = C.conv_gemm_wgrad_ppc(x, dy, KH, KW, stride, pad)
         chunks = C.conv_gemm_wgrad_chunks(x, dy, KH, KW, stride, pad, ppc)
         row = w.numel()
         dw = gw if gw is not None else torch.empty(w.shape, device=dev)
         if chunks == 1:
-            C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, gw is not None, bn=ctx.xbn)
+            C.conv_gemm_wgrad(dy, x, dw, KH, KW, stride, pad, ppc, acc_w, bn=ctx.xbn)
         else:
             slab = torch.empty(chunks, row, device=dev)
             C.conv_gemm_wgrad(dy, x, slab, KH, KW, stride, pad, ppc, False, bn=ctx.xbn)
-            C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, gw is not None)])
+            C.grad_reduce([(slab, row, 0, row, chunks, dw.view(-1), 1.0, acc_w)])
         rw = None if gw is not None else dw
         rg, rb = (None, None) if direct_bn else (dgamma, dbeta)
         if ctx.stash is not None:  # residual branch: hand the block-input gradient over
@@ -307,7 +313,7 @@ class _LinearHead(torch.autograd.Function):
         gw = direct_grad.grad_dst(w)
         rw = None
         if gw is not None:
-            C.sgemm(N, K, B, dl, 1, N, x, K, 1, gw, None, 1.0, True)           # dW += dl^T . x
+            C.sgemm(N, K, B, dl, 1, N, x, K, 1, gw, None, 1.0, direct_grad.accumulate(w))  # dW (+)= dl^T . x
         else:
             rw = torch.empty(N, K, device=dl.device)
             C.sgemm(N, K, B, dl, 1, N, x, K, 1, rw, None, 1.0)
@@ -316,7 +322,7 @@ class _LinearHead(torch.autograd.Function):
             ones = _ones(B, dl.device)
             gb = direct_grad.grad_dst(b)
             if gb is not None:
-                C.sgemm(1, N, B, ones, 0, 1, dl, N, 1, gb, None, 1.0, True)    # db += 1^T . dl
+                C.sgemm(1, N, B, ones, 0, 1, dl, N, 1, gb, None, 1.0, direct_grad.accumulate(b))  # db (+)= 1^T . dl
             else:
                 rb = torch.empty(N, device=dl.device)
                 C.sgemm(1, N, B, ones, 0, 1, dl, N, 1, rb, None, 1.0)

@@ -46,14 +46,18 @@ class FusedSGD:
         return self.param_groups[0]["lr"]
 
     def zero_grad(self, set_to_none: bool = True):
-        # grads are views of the flat buffer: "none" is a memset that keeps the views
-        self.flat.zero_grad()
+        # grads are views of the flat buffer: "none" is a memset that keeps the views - or no
+        # memset at all when every gradient's producer overwrites it (direct_grad lazy zeroing)
+        self.flat.zero_grad(lazy=True)
 
     @torch.no_grad()
     def step(self):
         g = self.param_groups[0]
         fs = self.flat
         fs.reattach_grads()
+        from . import direct_grad
+
+        direct_grad.flush_fresh(p for p, _ in fs._pairs)
         first = self.momentum_buffer is None
         if g["momentum"] != 0 and first:
             self.momentum_buffer = torch.zeros_like(fs.params)
