@@ -38,6 +38,15 @@ namespace ddp_amd {
 // loads in flight per thread in the reduce-scatter / all-gather loops (XgmiArgs items)
 constexpr int XGMI_BATCH = 8;
 
+// DDP_AMD_XGMI_FENCED=1 (a build switch): put a system-scope release fence before
+// each barrier flag store and an acquire fence after the wait - the conservative protocol,
+// for a node where the write-through + drain argument above is in doubt.  Off by default:
+// on gfx950 each fence is a whole-L2 write-back / invalidate (profiles/r5_dist: ~4 us per
+// multi-GPU step), and the hot kernels' ISA is checked to contain neither.
+#ifndef DDP_AMD_XGMI_FENCED
+#define DDP_AMD_XGMI_FENCED 0
+#endif
+
 // Signal all peers (lane p of wave 0 -> peer p) and wait until every peer's block b
 // has signalled `target` to us.  Caller guarantees every wave drained its stores.
 // On a timeout the FIRST stalled wait is recorded in the error word (xgmi_error_code:
@@ -53,6 +62,7 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
     // release (write-back of the whole L2) and an acquire (invalidation of L1 / L2, after
     // which this block's own parameter loads missed) only cost time.  Producers with plain
     // stores go through the publish pass (a.publish), which re-stores write-through.
+    if constexpr (DDP_AMD_XGMI_FENCED) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store(dst, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned* src = a.sig[a.rank] + XGMI_FLAG_OFF + blk * XGMI_MAX_RANKS + t;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -67,6 +77,7 @@ __device__ __forceinline__ void xgmi_barrier(const XgmiArgs& a, unsigned target,
         break;
       }
     }
+    if constexpr (DDP_AMD_XGMI_FENCED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
 }
