@@ -20,6 +20,7 @@ behind the GPU (a chunk = one replay), so logging never stalls the stream.
 from __future__ import annotations
 
 import dataclasses
+import os
 import math
 
 import torch
@@ -628,7 +629,10 @@ class FusedSimpleCNNEngine:
         resident: ranks that share a device (same-GPU rehearsals) would split the GPU
         between two such forwards, so they run the level-1 chain instead (logged)."""
         lvl = int(self.opts.fuse_level)
-        if lvl >= 3 and self._device_shared(world_size):
+        # DDP_AMD_SHARED_GPU_L3=1 (multi-rank tests on one GPU, small batches): keep level 3 -
+        # and with it the step head - when the ranks' grids together fit the GPU; a wait that
+        # cannot complete is bounded and raises (the start-up check then downgrades)
+        if lvl >= 3 and self._device_shared(world_size) and os.environ.get("DDP_AMD_SHARED_GPU_L3") != "1":
             self._log_downgrade("fuse level 3 -> 1 (a GPU is shared by several ranks)")
             return 1
         return lvl

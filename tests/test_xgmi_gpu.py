@@ -226,6 +226,62 @@ def test_engine_two_ranks_xgmi_identical_params(comm):
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
 
 
+def _head_worker(rank, world, port, q):
+    """The default multi-GPU chain (level 3 + dist_mode 4: step k's bucket all-reduces and step
+    k + 1's forward in one launch) with a real second rank on the same GPU: B = 8 per rank so
+    both ranks' grids fit the GPU together (DDP_AMD_SHARED_GPU_L3), the start-up check with the
+    host oracle (every rank's local gradient gathered over gloo and summed in rank order),
+    then graph replays with step heads; parameters bit-identical across ranks."""
+    try:
+        os.environ["DDP_AMD_SHARED_GPU_L3"] = "1"
+        os.environ["DDP_AMD_XGMI_GRID_CAP"] = "16"  # (the channels' role blocks, per rank)
+        _init(rank, world, port)
+        from ddp_amd.data import DeviceMNIST, synthetic_mnist
+        from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
+        from ddp_amd.models import SimpleCNN
+        from ddp_amd.models.layers import flat_space
+        from ddp_amd.ops import FusedSGD
+
+        torch.manual_seed(0)
+        model = SimpleCNN().cuda()
+        fs = flat_space(model)
+        opt = FusedSGD(model, lr=0.05, momentum=0.9)
+        imgs, labels = synthetic_mnist(2048)
+        eng = FusedSimpleCNNEngine(model, opt, DeviceMNIST(imgs, labels, torch.device("cuda", 0)),
+                                   8, world, rank, None, EngineOptions(graph_steps=5, comm="xgmi1"))
+        assert eng.level3 and eng.opts.dist_mode == 4, (eng.level3, eng.opts.dist_mode)
+        eng.refresh()
+        assert eng.eng.overlap_active()
+        assert eng.verify_chain(), eng.chain_check
+        ck = eng.chain_check
+        assert ck["oracle"]["ran"] and ck["oracle"]["mismatches"] == 0 and ck["step_heads_checked"] >= 1, ck
+        eng.run_steps(11)  # the momentum-init step eager, then two 5-step graphs with step heads
+        eng.synchronize()
+        assert eng.eng.sync_error == 0 and eng.eng.graph_heads == 4, eng.eng.graph_heads
+        p = fs.params.detach().cpu()
+        allp = [None] * world
+        dist.all_gather_object(allp, p)
+        for r in range(world):
+            assert torch.equal(allp[r], allp[0]), f"rank {r} params differ from rank 0"
+        assert torch.isfinite(p).all()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, f"{e!r}\n{traceback.format_exc()}"))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_step_head_two_real_ranks():
+    """VERDICT r5 missing #1 for the round-6 default chain: the step head with a real peer."""
+    from ddp_amd.parallel import free_port
+
+    res = _run(_head_worker, 2, free_port())
+    assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
+
+
 def _pair_worker(rank, world, port, q, ncalls):
     """The production dist_mode 3 launch (xgmi_allreduce_pair: the fc bucket two-shot and the
     conv bucket one-shot side by side, SGD + momentum fused into the all-gathers) with real
