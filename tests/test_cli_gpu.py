@@ -93,11 +93,12 @@ def test_cli_fault_resume_byte_identical(tmp_path, momentum):
 @pytest.mark.parametrize("comm", ["xgmi", "rccl"])
 def test_cli_fault_resume_dist_chain_byte_identical(tmp_path, comm):
     """VERDICT r4 missing #3 (BASELINE config 4 on the production multi-GPU chain): the
-    default ws > 1 step chain (dist_mode 3) - the level-3 forward, the conv backward with the
+    default ws > 1 step chain (dist_mode 4) - the level-3 forward, the conv backward with the
     fc weight gradient as its third role and the fused slab reduction (reducers stop short of
     the SGD), then ONE launch all-reducing both buckets of the 8-rank plan side by side with
-    the optimizer fused into its all-gather (xGMI: xgmi_allreduce_pair) or RCCL + one SGD
-    pass; plus the start-up chain check - rehearsed at world size 1 (--force_allreduce): a
+    the optimizer fused into its all-gather and carrying the next step's forward (xGMI: the
+    step head) or RCCL + one SGD pass; plus the start-up chain check - rehearsed at world
+    size 1 (--force_allreduce): a
     crash at epoch 1 step 20 and an auto-resume give the uninterrupted run's epoch_2.pt byte
     for byte, and that equals the one-GPU chain's.  (The same chain at 2 ranks on one GPU, on
     the level-1 forward that ranks sharing a device run:
