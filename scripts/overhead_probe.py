@@ -1,9 +1,9 @@
 """Fixed per-run overhead of a short timed region (the driver's ``--steps 20 --warmup 5``).
 
-For a few graph chunk sizes and the eager path it times, on the host, the launch call
-alone, launch + stream sync, and the device span (events on the engine stream) of a
-K-step run.  wall - device = host launch latency + sync wake-up (what a short run pays
-on top of K * step time)."""
+For a few graph chunk sizes and the eager path it times, on the host, from a synchronized
+device: ``pre_launch_us`` - run_steps' Python before the graph launch call, ``launch_us`` -
+until run_steps returns (hipGraphLaunch submits the graph's nodes), ``wall_us`` - until
+torch.cuda.synchronize() returns (what a short run pays on top of K * step time)."""
 import argparse
 import json
 import os
@@ -38,23 +38,36 @@ def make(k, use_graph=True):
     return eng
 
 
+class _Timed:
+    """The engine's native handle with replay() timestamped on entry (host time spent in
+    run_steps before the graph launch call)."""
+
+    def __init__(self, inner):
+        self._inner, self.t_replay = inner, None
+
+    def replay(self):
+        self.t_replay = time.perf_counter()
+        return self._inner.replay()
+
+    def __getattr__(self, name):
+        return getattr(self._inner, name)
+
+
 def probe(eng, nsteps, trials):
     rows = []
     first = None
+    timed = _Timed(eng.eng)
+    eng.eng = timed
     for t in range(trials):
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        timed.t_replay = None
         t0 = time.perf_counter()
-        e0.record(eng.stream)
         eng.run_steps(nsteps)
         t1 = time.perf_counter()
-        e1.record(eng.stream)
-        eng.synchronize()
-        t2 = time.perf_counter()
         torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        rows.append({"launch_us": (t1 - t0) * 1e6, "wall_us": (t2 - t0) * 1e6,
-                     "dev_us": e0.elapsed_time(e1) * 1e3, "resync_us": (t3 - t2) * 1e6})
+        t2 = time.perf_counter()
+        rows.append({"pre_launch_us": ((timed.t_replay or t1) - t0) * 1e6, "launch_us": (t1 - t0) * 1e6,
+                     "wall_us": (t2 - t0) * 1e6})
         if t == 0:
             first = {k: round(v, 1) for k, v in rows[0].items()}
     rows.sort(key=lambda r: r["wall_us"])
@@ -70,7 +83,7 @@ def main():
     args = ap.parse_args()
     native.require()
     out = {}
-    for k, n in ((20, 20), (20, 1000), (10, 20)):
+    for k, n in ((20, 20), (20, 1000), (5, 20)):
         eng = make(k)
         out[f"graph{k}_steps{n}"] = probe(eng, n, args.trials)
         print(json.dumps({f"graph{k}_steps{n}": out[f"graph{k}_steps{n}"]}), flush=True)
