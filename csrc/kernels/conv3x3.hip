@@ -108,7 +108,7 @@ bool conv3x3_step_head_fits(int nx, int B) {
 
 bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16_t* Wt, const float* bias,
                        bf16_t* Y, int B, const bf16_t* wfc, float* fc_part, const C1Src& c1, const FwdDz& dz,
-                       int* err, hipStream_t s) {
+                       int* err, hipStream_t s, const ShadowSet* late) {
   const int nx = x.nblk0 + x.nblk1;
   const char* bad = !x.args ? "all-reduce arguments" : x.nblk0 < 0 || x.nblk1 <= 0 ? "the conv bucket's blocks"
                    : !done_fc || !done_conv ? "bucket-done counters" : !dz.dz2 || !dz.img_cnt || !dz.fc_bias
@@ -124,6 +124,7 @@ bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16
   mg.fc_done = done_fc;
   mg.conv_done = done_conv;
   mg.err = err;
+  if (late) mg.late = *late;
   auto k = step_head_kernel<bf16_t>;
   lds_optin(k, lds);
   hipLaunchKernelGGL(k, dim3((unsigned)(nx + nf)), dim3(256), lds, s, Wt, bias, Y, B, wfc, fc_part, c1, dz, mg);

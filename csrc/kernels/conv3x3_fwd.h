@@ -44,6 +44,7 @@ struct FwdMerge {
   int* fc_done = nullptr;          // per-bucket block counts, zeroed by the previous fc role
   int* conv_done = nullptr;
   int* err = nullptr;
+  ShadowSet late{};                // conv bucket shadows written after the count (see below)
 };
 constexpr int MRG_ERR = 5;  // sync_err code of a timed-out merged-forward wait
 
@@ -84,6 +85,25 @@ __device__ __forceinline__ void merge_allreduce_role(FwdMerge mg, char* smem) {
   DDP_STAMP(STAMP_K_HEAD, 7);
   count_done(k == 0 ? mg.fc_done : mg.conv_done);  // drain (write-through) + one relaxed count
   DDP_STAMP(STAMP_K_HEAD, 6);
+  if (k == 1 && mg.late.count) {
+    // the shadows no forward block reads (conv2's [tap][ci][co] copy, 4 scattered 2-byte
+    // stores per quad): refreshed after the count, from the parameters this block just
+    // stored (system-scope loads: no stale cached line) - out of the drain the forward
+    // waited for (stamps: conv bucket counted 9.2 -> 6.3 us, profiles/r6_dist).  Plain
+    // stores: the next launch (the conv backward) reads them.
+    const XgmiArgs& a = *s_xa;
+    const ShadowSet late = mg.late;
+    const long n = a.n, G = (long)mg.nblk1 * XGMI_THREADS;
+    const float* pb = a.params + a.off;
+    const __amdgpu_buffer_rsrc_t rp = sys_rsrc(pb);
+    for (long q = (long)rb * XGMI_THREADS + threadIdx.x; 4 * q < n; q += G) {
+      if (4 * q + 3 < n) {
+        shadow_quad<false>(late, a.off + 4 * q, ld4_sys(rp, q));
+      } else {
+        for (long e = 4 * q; e < n; ++e) shadow_one<false>(late, a.off + e, ld_sys(pb + e));
+      }
+    }
+  }
 }
 
 // The forward conv (+ fc partials, + level-3 dZ2): the plain kernel ...

@@ -417,9 +417,12 @@ void xgmi_allreduce_pair(const BwdXar& x, hipStream_t s);
 // parameters) in ONE launch (conv3x3.hip step_head_kernel).  Returns false without
 // launching when the whole grid does not fit the GPU at once (the caller then runs the pair
 // and the forward as two launches - the same bits).  err: sync_err (code 5 on a wait timeout).
+// late: shadows of the conv bucket the forward does not read (the conv2 weight's [tap][ci][co]
+// copy for the next backward), written by the conv bucket's blocks AFTER their count - their
+// scattered write-through stores no longer sit in the drain the forward waits for
 bool conv3x3_step_head(const BwdXar& x, int* done_fc, int* done_conv, const bf16_t* Wt, const float* bias,
                        bf16_t* Y, int B, const bf16_t* wfc, float* fc_part, const C1Src& c1, const FwdDz& dz,
-                       int* err, hipStream_t s);
+                       int* err, hipStream_t s, const ShadowSet* late = nullptr);
 bool conv3x3_step_head_fits(int nx, int B);
 int conv3x3_step_head_slots();  // resident blocks of the step-head kernel on this GPU
 

@@ -263,14 +263,27 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, u
     // the previous step's pair (its fused SGD writes this step's parameters write-through)
     // + this step's forward; two launches (same bits) when the merged grid does not fit
     if (first_momentum_step) throw std::runtime_error("engine: the step head runs the steady-state SGD only");
+    // the head's fused SGD refreshes the shadows its forward reads (conv2 bf16, fc fragment
+    // order); the conv2 [tap][ci][co] copy (the next backward's) is written after the conv
+    // bucket's count (FwdMerge late).  The same bytes as sh_all, in two passes.
+    ShadowSet sh_head = sh_all, late{};
+    sh_head.r[1] = sh_all.r[2];
+    sh_head.count = 2;
+    late.r[0] = sh_all.r[1];
+    late.count = 1;
     BwdXar hx;
-    if (!make_xar(hx, sa, M, sh_all)) throw std::runtime_error("engine: the step head needs the pair plan");
-    hx.step_ctr = nullptr;  // (advanced by the fc role)
     int* mc = b_.sync_flags + L3_IMG_OFF + (long)FWD_DZ_CNT_STRIDE * cfg_.max_batch;
-    head_used = cfg_.pxt_fwd == 1 && B == cfg_.max_batch &&
-                conv3x3_step_head(hx, mc, mc + FWD_DZ_CNT_STRIDE, b_.w2_bf16, P + b_.off_b2, b_.a2, B, b_.wfc_frag,
-                                  b_.fc_part, c1, dzo, b_.sync_err, cs_);
-    if (!head_used) xgmi_allreduce_pair(hx, cs_);
+    if (cfg_.pxt_fwd == 1 && B == cfg_.max_batch) {
+      if (!make_xar(hx, sa, M, sh_head)) throw std::runtime_error("engine: the step head needs the pair plan");
+      hx.step_ctr = nullptr;  // (advanced by the fc role)
+      head_used = conv3x3_step_head(hx, mc, mc + FWD_DZ_CNT_STRIDE, b_.w2_bf16, P + b_.off_b2, b_.a2, B,
+                                    b_.wfc_frag, b_.fc_part, c1, dzo, b_.sync_err, cs_, &late);
+    }
+    if (!head_used) {
+      if (!make_xar(hx, sa, M, sh_all)) throw std::runtime_error("engine: the step head needs the pair plan");
+      hx.step_ctr = nullptr;
+      xgmi_allreduce_pair(hx, cs_);
+    }
     DDP_HIP_CHECK(hipGetLastError());
   }
   if ((parts & PART_FWD) || ((parts & PART_HEAD) && !head_used)) {
