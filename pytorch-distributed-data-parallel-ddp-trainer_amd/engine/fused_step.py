@@ -125,7 +125,7 @@ class EngineOptions:
     # 4 = the step head (bf16, xGMI; forces pxt_fwd 1 when the step all-reduces): mode 3's
     # chain, but in a captured graph step k's bucket-pair launch also runs step k + 1's
     # forward (2 launches per step instead of 3; conv3x3.hip step_head_kernel) - same bits as
-    # mode 3 at pxt 1.  The default (round 6: forced world 1 716-724k vs mode 3 692-700k
+    # mode 3 at pxt 1.  The default (round 6: forced world 1 751-756k vs mode 3 692-700k
     # img/s, profiles/r6_dist); fp32, the RCCL plane and a head grid that does not fit the
     # GPU run mode 3's launches.  bench.py times the placements on the node at N > 1.
     dist_mode: int = 4
