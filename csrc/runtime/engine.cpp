@@ -266,11 +266,16 @@ void SimpleCNNEngine::launch_step(int B, int stride, bool first_momentum_step, u
     // the head's fused SGD refreshes the shadows its forward reads (conv2 bf16, fc fragment
     // order); the conv2 [tap][ci][co] copy (the next backward's) is written after the conv
     // bucket's count (FwdMerge late).  The same bytes as sh_all, in two passes.
+    // Only when the whole conv2 weight lies in the one-shot conv-stage bucket: its blocks
+    // then rewrite exactly the quads they updated (no wait on another block); any other plan
+    // refreshes every shadow in the SGD pass as before.
     ShadowSet sh_head = sh_all, late{};
-    sh_head.r[1] = sh_all.r[2];
-    sh_head.count = 2;
-    late.r[0] = sh_all.r[1];
-    late.count = 1;
+    if (late_shadow_ok(b_.off_w2, n_w2s)) {
+      sh_head.r[1] = sh_all.r[2];
+      sh_head.count = 2;
+      late.r[0] = sh_all.r[1];
+      late.count = 1;
+    }
     BwdXar hx;
     int* mc = b_.sync_flags + L3_IMG_OFF + (long)FWD_DZ_CNT_STRIDE * cfg_.max_batch;
     if (cfg_.pxt_fwd == 1 && B == cfg_.max_batch) {
@@ -483,6 +488,19 @@ void SimpleCNNEngine::enqueue_buckets(int stage, bool use_x, hipStream_t s, cons
       comm_->all_reduce(b_.grads + buckets_[b].off, (size_t)buckets_[b].n, 0, 0, s);
     }
   }
+}
+
+bool SimpleCNNEngine::late_shadow_ok(long off, long n) const {
+  if (!xgmi_) return false;
+  bool inside = false;
+  for (int b = 0; b < (int)buckets_.size(); ++b) {
+    const long b0 = buckets_[b].off, b1 = b0 + (long)buckets_[b].n;
+    const bool overlaps = b0 < off + n && off < b1;
+    if (!overlaps) continue;
+    if (stage_[b] != 1 || !xgmi_->oneshot(xch_[b]) || b0 > off || b1 < off + n) return false;
+    inside = true;
+  }
+  return inside;
 }
 
 bool SimpleCNNEngine::make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh) {

@@ -368,6 +368,8 @@ class SimpleCNNEngine {
                          const std::function<void()>& conv, const SgdArgs& sa, float* M, const ShadowSet& sh);
   // dist_mode 2 with this bucket plan / data plane: the in-launch all-reduce's arguments for
   // this step (false: not applicable - the caller uses the bucket kernels)
+  // the step head may defer a shadow of [off, off + n) to after the conv bucket's count
+  bool late_shadow_ok(long off, long n) const;
   bool make_xar(BwdXar& xa, const SgdArgs& sa, float* M, const ShadowSet& sh);
   bool sync_ok_for_xar() const;
   EngineConfig cfg_;

@@ -444,10 +444,13 @@ def test_verify_chain_world1_forced(corrupt, stall):
         dist.destroy_process_group()
 
 
-def test_verify_chain_covers_the_step_head():
+@pytest.mark.parametrize("comm", ["xgmi", "xgmi2"])
+def test_verify_chain_covers_the_step_head(comm):
     """dist_mode 4's step head exists only in captured graphs: the start-up check runs the
     production chain's steps as a graph (momentum-init step eager), so at least one step head
-    is compared with the conservative chain before training commits to it."""
+    is compared with the conservative chain before training commits to it.  "xgmi": the conv
+    bucket one-shot (conv2's tap-transposed shadow written after its count); "xgmi2": both
+    buckets two-shot (every shadow in the SGD pass)."""
     import torch.distributed as dist
 
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
@@ -461,7 +464,7 @@ def test_verify_chain_covers_the_step_head():
         torch.manual_seed(0)
         m = SimpleCNN().to(dev)
         e = FusedSimpleCNNEngine(m, FusedSGD(m, lr=0.01, momentum=0.9), DeviceMNIST(imgs, labels, dev), 32, 1, 0,
-                                 None, EngineOptions(graph_steps=5, force_allreduce=True, comm="xgmi", dist_mode=4))
+                                 None, EngineOptions(graph_steps=5, force_allreduce=True, comm=comm, dist_mode=4))
         e.refresh()
         assert e.eng.overlap_active()
         assert e.verify_chain(), e.chain_check
