@@ -274,11 +274,13 @@ def _head_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def test_step_head_two_real_ranks():
-    """VERDICT r5 missing #1 for the round-6 default chain: the step head with a real peer."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_step_head_two_real_ranks(world):
+    """VERDICT r5 missing #1 for the round-6 default chain: the step head with real peers
+    (2 and 3 ranks on one GPU, B = 8 each)."""
     from ddp_amd.parallel import free_port
 
-    res = _run(_head_worker, 2, free_port())
+    res = _run(_head_worker, world, free_port())
     assert all(r[1] == "ok" for r in res), [r[:2] for r in res]
 
 
