@@ -55,11 +55,13 @@ BASELINE_IMG_S = {1: 2799.0, 2: 2665.0, 4: 3384.0, 8: 3670.0}
 def kernels_per_step(eng):
     """Kernels per step of the chain a FusedSimpleCNNEngine ran (level 3 only): 2 on one GPU
     and with the in-launch all-reduce, 3 with both buckets' all-reduces in one launch
-    (dist_mode 3); otherwise fc_bwd and one all-reduce kernel per bucket come on top."""
+    (dist_mode 3); otherwise fc_bwd and one all-reduce kernel per bucket come on top, and the
+    separate grad_reduce kernel when the conv backward did not fuse the slab reduction (the
+    exact-fp32 default)."""
     if not eng.eng.last_level3:
         return None
     nar = 0 if eng.eng.last_xar or eng.comm_kind == "none" else 1 if eng.eng.last_pair else len(eng.ranges)
-    k = (2 if eng.eng.last_fc_role else 3) + nar
+    k = (2 if eng.eng.last_fc_role else 3) + nar + (0 if getattr(eng.eng, "last_fused_reduce", True) else 1)
     gs, heads = eng.eng.graph_steps, eng.eng.graph_heads
     if heads and gs:  # dist_mode 4 graph: every step head saves a launch (per-step average)
         k = round(k - heads / gs, 3)
@@ -538,7 +540,7 @@ def main():
         breakdown = {"step_us": round(step_us, 2), "local_step_us": round(loc_us, 2),
                      "exposed_comm_us": round(step_us - loc_us, 2),
                      "dist_over_local": round(step_us / loc_us, 4),
-                     "local_kernels_per_step": (2 if engl.eng.last_fc_role else 3) if engl.eng.last_level3 else None,
+                     "local_kernels_per_step": kernels_per_step(engl),
                      "bucket_allreduce_isolated_us": bucket_us}
         del engl
     from ddp_amd.parallel.bucket_model import describe

@@ -87,8 +87,13 @@ class EngineOptions:
     # resident capacity; 2: the whole capacity when nothing else runs (single process) -
     # lets the exact-fp32 step fuse, measured slower there (385-386k vs 389-391k img/s,
     # profiles/r3_fp32: its 224 waiting reducers hold the CUs the one-block-per-CU dgrad /
-    # wgrad roles need); 0: the separate grad_reduce kernel
-    fuse_reduce: int = 1
+    # wgrad roles need); 0: the separate grad_reduce kernel.  None: 1 for bf16, 0 for fp32 -
+    # the exact-fp32 level-3 step at two blocks per CU fuses under rule 1 but runs faster
+    # with the separate kernel (B = 32: 438k -> 459k img/s in-call, 408k -> 426k driver-
+    # shaped; forced dist 362k -> 378k; B = 64 on par; bitwise the same -
+    # profiles/r6_rebuilt/fp32_fuse_reduce.md); bf16 keeps the fused one (973k vs 816k), and
+    # so does dist_mode 2, whose in-launch all-reduce counts the fused reducers
+    fuse_reduce: int | None = None
     # level 1: 0 = the conv backward recomputes conv1 from the compact uint8 batch;
     # 1 = the forward stores a1 and the dgrad role reads its ReLU mask from it; 2 = the
     # wgrad role reads a1 tiles too.  None = 1 for bf16 (with the wgrad role split over
@@ -641,12 +646,15 @@ class FusedSimpleCNNEngine:
         """The fused reduction's waiting blocks are sized against ONE launch's share of the
         GPU; ranks that share a device (same-GPU rehearsals) each hold waiting blocks at
         once, so they keep the separate grad_reduce kernel (logged)."""
-        if not self.opts.fuse_reduce:
+        fr = self.opts.fuse_reduce
+        if fr is None:  # (the in-launch all-reduce, dist_mode 2, needs the fused reduction)
+            fr = 0 if self.opts.dtype == "fp32" and self.opts.dist_mode != 2 else 1
+        if not fr:
             return 0
         if self._device_shared(world_size):
             self._log_downgrade("fused slab reduction off (a GPU is shared by several ranks)")
             return 0
-        return int(self.opts.fuse_reduce)
+        return int(fr)
 
     def _log_downgrade(self, what: str):
         self.downgrades = getattr(self, "downgrades", []) + [what]

@@ -126,9 +126,9 @@ def test_kernels_per_step_record():
     sys.path.insert(0, REPO)
     import bench
 
-    def eng(l3=True, fc_role=True, xar=False, pair=False, comm="xgmi1", nb=2, steps=0, heads=0):
+    def eng(l3=True, fc_role=True, xar=False, pair=False, comm="xgmi1", nb=2, steps=0, heads=0, fred=True):
         e = types.SimpleNamespace(last_level3=l3, last_fc_role=fc_role, last_xar=xar, last_pair=pair,
-                                  graph_steps=steps, graph_heads=heads)
+                                  graph_steps=steps, graph_heads=heads, last_fused_reduce=fred)
         return types.SimpleNamespace(eng=e, comm_kind=comm, ranges=[(0, 1)] * nb)
 
     assert bench.kernels_per_step(eng(comm="none")) == 2
@@ -136,6 +136,8 @@ def test_kernels_per_step_record():
     assert bench.kernels_per_step(eng(pair=True)) == 3
     assert bench.kernels_per_step(eng(fc_role=False, nb=2)) == 5
     assert bench.kernels_per_step(eng(l3=False)) is None
+    # the exact-fp32 default: the slab reduction in its own grad_reduce kernel
+    assert bench.kernels_per_step(eng(comm="none", fred=False)) == 3
     # dist_mode 4: a graph of 5 steps with 4 step heads (the first step's forward stands alone)
     assert bench.kernels_per_step(eng(pair=True, steps=5, heads=4)) == 2.2
     assert bench.kernels_per_step(eng(pair=True, steps=100, heads=99)) == 2.01

@@ -175,7 +175,7 @@ def test_simple_cnn_fp32_module_path_matches_stock_fp32_model():
 
 
 def _engine(B=32, momentum=0.0, fuse_opt=True, use_graph=False, graph_steps=5, dtype="fp32", seed=0,
-            fuse_level=1, wgrad_split=1, weight_decay=0.0, l3_fc_role=1):
+            fuse_level=1, wgrad_split=1, weight_decay=0.0, l3_fc_role=1, fuse_reduce=None):
     from ddp_amd.data import DeviceMNIST, synthetic_mnist
     from ddp_amd.engine import EngineOptions, FusedSimpleCNNEngine
     from ddp_amd.models import SimpleCNN
@@ -189,7 +189,8 @@ def _engine(B=32, momentum=0.0, fuse_opt=True, use_graph=False, graph_steps=5, d
     eng = FusedSimpleCNNEngine(model, opt, data, B, 1, 0,
                                opts=EngineOptions(graph_steps=graph_steps, use_graph=use_graph,
                                                   fuse_level=fuse_level, fuse_opt=fuse_opt, dtype=dtype,
-                                                  wgrad_split=wgrad_split, l3_fc_role=l3_fc_role))
+                                                  wgrad_split=wgrad_split, l3_fc_role=l3_fc_role,
+                                                  fuse_reduce=fuse_reduce))
     eng.refresh()
     return model, opt, eng, imgs, labels
 
@@ -259,27 +260,30 @@ def test_fp32_engine_batch_sweep_nan_poisoned():
             assert relerr(delta, g[k]) < 1e-3, (B, k)  # lr-division of an fp32 update: ~1e-4 noise
 
 
-@pytest.mark.parametrize("B,momentum,role,fuse_opt", [(32, 0.9, 1, True), (32, 0.0, 1, True), (20, 0.9, 1, True),
-                                                      (1, 0.9, 1, True), (40, 0.9, 1, True), (32, 0.9, 0, True),
-                                                      (32, 0.9, 1, False)])
-def test_fp32_level3_bitwise_equals_round3_level1(B, momentum, role, fuse_opt):
+@pytest.mark.parametrize("B,momentum,role,fuse_opt,fred", [(32, 0.9, 1, True, 1), (32, 0.0, 1, True, 1),
+                                                           (20, 0.9, 1, True, 1), (1, 0.9, 1, True, 1),
+                                                           (40, 0.9, 1, True, 1), (32, 0.9, 0, True, 1),
+                                                           (32, 0.9, 1, False, 1), (32, 0.9, 1, True, None),
+                                                           (32, 0.9, 1, False, None)])
+def test_fp32_level3_bitwise_equals_round3_level1(B, momentum, role, fuse_opt, fred):
     """the exact-fp32 step on the level-3 structure - dL and dZ2 in the
     forward, the fc weight gradient + SGD as a role of the conv backward launch (role 1) or
     its own kernel (role 0), both conv backward roles split over input-channel halves at two
     blocks per CU, the fused slab reduction - gives parameters, momentum, losses, the fp32
     weight copies and the step counter bit-identical to round 3's fp32 level-1 chain (one
-    conv backward block per row / chunk) after 12 graph-captured steps."""
+    conv backward block per row / chunk) after 12 graph-captured steps.  fred None: the fp32
+    default, the slab reduction in the separate grad_reduce kernel (faster for fp32, round 6)."""
     kw = dict(B=B, momentum=momentum, weight_decay=1e-4, use_graph=True, graph_steps=4, fuse_opt=fuse_opt)
     m1, o1, e1, _, _ = _engine(fuse_level=1, wgrad_split=1, **kw)
-    m3, o3, e3, _, _ = _engine(fuse_level=3, wgrad_split=2, l3_fc_role=role, **kw)
+    m3, o3, e3, _, _ = _engine(fuse_level=3, wgrad_split=2, l3_fc_role=role, fuse_reduce=fred, **kw)
     assert e3.level3 and not e1.level3
     e1.run_steps(12)
     e1.synchronize()
     e3.run_steps(12)
     e3.synchronize()
     assert e3.eng.last_level3 and e3.eng.last_fc_role == (role == 1)
-    if B == 32:
-        assert e3.eng.last_fused_reduce  # two blocks per CU: the 224 wgrad rows fit the reducer budget
+    if B == 32:  # two blocks per CU: the 224 wgrad rows fit the reducer budget (fred 1)
+        assert e3.eng.last_fused_reduce == (fred == 1)
     for (n, a), (_, b) in zip(m1.named_parameters(), m3.named_parameters()):
         assert torch.equal(a, b), n
     if momentum:
